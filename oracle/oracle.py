@@ -1,0 +1,246 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+
+ctypes front-ends to
+  * ``liboracle.so``        -- the clean-room C restatement in ``kmer_oracle.c``
+  * ``_ref/libkmh_ref.so``  -- the reference's own index core (src/kmer_pos.c,
+                               src/kmer_util.c, klib) compiled by ``oracle/Makefile``
+                               behind the R-free harness ``ref_harness.c``.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module.  Arrays follow the reference's R layouts (column-major 2 x N / 3 x P,
+i.e. row-interleaved) so they compare 1:1 with what ``kmer.pos`` / ``seq.kmer.pos`` return.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ORC = None
+_REF = None
+
+i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+i64p = np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS")
+u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+
+
+def build(force: bool = False) -> None:
+    """Compile liboracle.so (and _ref/ when /root/reference is present)."""
+    if force or not os.path.exists(os.path.join(_HERE, "liboracle.so")):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def _orc():
+    global _ORC
+    if _ORC is None:
+        build()
+        lib = C.CDLL(os.path.join(_HERE, "liboracle.so"))
+        lib.orc_windows.restype = C.c_long
+        lib.orc_windows.argtypes = [C.c_char_p, C.c_long, C.c_int, u64p, i32p, i32p]
+        lib.orc_index_build.restype = C.c_long
+        lib.orc_index_build.argtypes = [C.c_char_p, C.c_long, C.c_int, u64p, i32p, i64p, i32p,
+                                        C.POINTER(C.c_long), C.POINTER(C.c_int64),
+                                        C.POINTER(C.c_int32)]
+        lib.orc_query.restype = C.c_int64
+        lib.orc_query.argtypes = [u64p, i32p, i64p, i32p, C.c_long, C.c_char_p, C.c_long, C.c_int,
+                                  C.c_void_p]
+        lib.orc_pairs.restype = C.c_int64
+        lib.orc_pairs.argtypes = [i32p, i64p, i32p, C.c_long, C.c_void_p, i32p]
+        lib.orc_khash_order.restype = C.c_long
+        lib.orc_khash_order.argtypes = [u64p, C.c_long, i64p]
+        _ORC = lib
+    return _ORC
+
+
+def ref_available() -> bool:
+    return os.path.exists(os.path.join(_HERE, "_ref", "libkmh_ref.so"))
+
+
+class _RefPos(C.Structure):
+    _fields_ = [("n_kmers", C.c_long), ("kmers", C.c_void_p),
+                ("n_pos", C.c_long), ("pos", C.c_void_p),
+                ("n_pairs", C.c_long), ("pairs", C.c_void_p),
+                ("n_counts", C.c_long), ("counts", C.c_void_p)]
+
+
+def _ref():
+    global _REF
+    if _REF is None:
+        lib = C.CDLL(os.path.join(_HERE, "_ref", "libkmh_ref.so"))
+        lib.ref_build.restype = C.c_void_p
+        lib.ref_build.argtypes = [C.c_char_p, C.c_int, C.c_int, C.POINTER(C.c_long),
+                                  C.POINTER(C.c_int)]
+        lib.ref_size.restype = C.c_long
+        lib.ref_size.argtypes = [C.c_void_p]
+        lib.ref_free_index.argtypes = [C.c_void_p]
+        lib.ref_free.argtypes = [C.c_void_p]
+        lib.ref_positions.argtypes = [C.c_void_p, C.c_uint, C.POINTER(_RefPos)]
+        lib.ref_query.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(C.c_long),
+                                  C.POINTER(C.POINTER(C.c_int))]
+        _REF = lib
+    return _REF
+
+
+def _as_bytes(seq) -> bytes:
+    if isinstance(seq, str):
+        return seq.encode("latin-1")
+    if isinstance(seq, np.ndarray):
+        return seq.astype(np.uint8, copy=False).tobytes()
+    return bytes(seq)
+
+
+# --------------------------------------------------------------------------- restatement
+def windows(seq, k: int):
+    """(keys u64, start1 i32, end1 i32) of every window the reference visits."""
+    b = _as_bytes(seq)
+    L = len(b)
+    keys = np.empty(L + 1, np.uint64)
+    s = np.empty(L + 1, np.int32)
+    e = np.empty(L + 1, np.int32)
+    n = _orc().orc_windows(b, L, k, keys, s, e)
+    return keys[:n], s[:n], e[:n]
+
+
+class OracleIndex:
+    """Canonical CSR: key ids rank distinct keys by first position; positions ascend."""
+
+    def __init__(self, seq, k: int):
+        b = _as_bytes(seq)
+        L = len(b)
+        self.k = k
+        cap = L + 1
+        keys = np.empty(cap, np.uint64)
+        counts = np.empty(cap, np.int32)
+        offs = np.empty(cap + 1, np.int64)
+        pos = np.empty(cap, np.int32)
+        n = C.c_long(0)
+        p = C.c_int64(0)
+        mx = C.c_int32(0)
+        U = _orc().orc_index_build(b, L, k, keys, counts, offs, pos, C.byref(n), C.byref(p),
+                                   C.byref(mx))
+        if U < 0:
+            raise MemoryError("oracle allocation failed")
+        self.U, self.N, self.P, self.max_n = int(U), int(n.value), int(p.value), int(mx.value)
+        self.keys = keys[:U].copy()
+        self.counts = counts[:U].copy()
+        self.offsets = offs[:U + 1].copy()
+        self.positions = pos[:self.N].copy()
+
+    # kmer.pos pieces in canonical order -----------------------------------------------
+    def pos_rows(self) -> np.ndarray:
+        """2 x N data (i, pos) interleaved, i 1-based in canonical order."""
+        out = np.empty((self.N, 2), np.int32)
+        out[:, 0] = np.repeat(np.arange(1, self.U + 1, dtype=np.int32), self.counts)
+        out[:, 1] = self.positions
+        return out.reshape(-1)
+
+    def pair_rows(self, order=None) -> np.ndarray:
+        out = np.empty(3 * self.P + 1, np.int32)
+        o = None if order is None else np.ascontiguousarray(order, np.int64)
+        n = _orc().orc_pairs(self.counts, self.offsets, self.positions, self.U,
+                             None if o is None else o.ctypes.data, out)
+        assert n == self.P
+        return out[:3 * self.P]
+
+    def kmer_strings(self) -> list[str]:
+        return [decode(int(x), self.k) for x in self.keys]
+
+    def khash_order(self) -> np.ndarray:
+        """ids in the bucket order khash 0.2.8 gives the reference (kmer_positions' row order)."""
+        out = np.empty(self.U, np.int64)
+        r = _orc().orc_khash_order(self.keys, self.U, out)
+        assert r == self.U
+        return out
+
+    def query(self, seq, kq: int) -> np.ndarray:
+        b = _as_bytes(seq)
+        lib = _orc()
+        h = lib.orc_query(self.keys, self.counts, self.offsets, self.positions, self.U, b, len(b),
+                          kq, None)
+        rows = np.empty(2 * h + 1, np.int32)
+        h2 = lib.orc_query(self.keys, self.counts, self.offsets, self.positions, self.U, b, len(b),
+                           kq, rows.ctypes.data)
+        assert h2 == h
+        return rows[:2 * h]
+
+
+_NUC = "ACTG"
+
+
+def decode(key: int, k: int) -> str:
+    """kmer_seq (reference src/kmer_hash.c:123-133): LSB pair is the last base."""
+    out = []
+    for _ in range(k):
+        out.append(_NUC[key & 3])
+        key >>= 2
+    return "".join(reversed(out))
+
+
+# --------------------------------------------------------------------------- reference
+class RefIndex:
+    """The compiled reference index (khash order, exactly what the R API would return)."""
+
+    def __init__(self, seq, k: int, do_sort: int = 0):
+        lib = _ref()
+        self._b = _as_bytes(seq)
+        cnt = C.c_long(0)
+        err = C.c_int(0)
+        self.k = k
+        self.h = lib.ref_build(self._b, k, do_sort, C.byref(cnt), C.byref(err))
+        if err.value == 1:
+            raise ValueError("k must be a positive integer less than 1+MAX_K")
+        if err.value == 2:
+            raise ValueError("the length of the sequence must be at least k")
+        self.kmer_count = int(cnt.value)
+
+    def positions(self, opt: int) -> dict:
+        lib = _ref()
+        r = _RefPos()
+        lib.ref_positions(self.h, opt, C.byref(r))
+        out = {"kmer": None, "pos": None, "pair.pos": None, "count": None}
+
+        def take(ptr, n, dt):
+            a = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int32)), shape=(n,)).copy() \
+                if n else np.empty(0, dt)
+            lib.ref_free(ptr)
+            return a
+
+        if opt & 1:
+            raw = C.string_at(r.kmers, r.n_kmers * (self.k + 1)) if r.n_kmers else b""
+            lib.ref_free(r.kmers)
+            out["kmer"] = [raw[i * (self.k + 1):i * (self.k + 1) + self.k].decode()
+                           for i in range(r.n_kmers)]
+        if opt & 2:
+            out["pos"] = take(r.pos, 2 * r.n_pos, np.int32)
+        if opt & 4:
+            out["pair.pos"] = take(r.pairs, 3 * r.n_pairs, np.int32)
+        if opt & 8:
+            out["count"] = take(r.counts, r.n_counts, np.int32)
+        return out
+
+    def query(self, seq, kq: int) -> np.ndarray:
+        lib = _ref()
+        n = C.c_long(0)
+        rows = C.POINTER(C.c_int)()
+        rc = lib.ref_query(self.h, _as_bytes(seq), kq, C.byref(n), C.byref(rows))
+        if rc:
+            raise ValueError("the sequence should be longer than k and k should not be longer "
+                             "than 31")
+        a = np.ctypeslib.as_array(rows, shape=(2 * n.value,)).copy() if n.value else \
+            np.empty(0, np.int32)
+        lib.ref_free(rows)
+        return a
+
+    def close(self):
+        if self.h:
+            _ref().ref_free_index(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
