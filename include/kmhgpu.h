@@ -1,0 +1,133 @@
+/*
+ * kmhgpu.h -- C-ABI of the MI355X k-mer position index (libkmhgpu.so).
+ *
+ * Drop-in boundary for the hot path of lmjakt/kmer_hasheR.  Plain pointers and sizes only; no
+ * torch or HIP types in the signatures (streams are passed as `void*` = hipStream_t, NULL = the
+ * library's own stream).  Every function returns KMHG_OK (0) or an error code; the message is
+ * in kmhg_last_error() (thread-local).  Where the reference raises an R error() the message is
+ * the reference's own text.
+ *
+ * Reference interfaces replaced (paths relative to the reference checkout):
+ *   kmhg_build / kmhg_build_device
+ *        <- .Call("make_kmer_h_index", seq, k, do.sort)      src/kmer_hash.c:506-540
+ *           (+ seq_to_hash, src/kmer_pos.c:66-98; sort_kmer_pos, src/kmer_pos.c:21-33)
+ *   kmhg_free
+ *        <- finalise_khash_ptr (externalptr finaliser)       src/kmer_hash.c:56-66
+ *           (+ clear_kmer_h, src/kmer_pos.c:10-19)
+ *   kmhg_positions_size / kmhg_positions_fill / kmhg_positions_fill_device
+ *        <- .Call("kmer_positions", ptr, opt.flag)           src/kmer_hash.c:1054-1147
+ *           (+ kmer_seq decode, src/kmer_hash.c:123-133)
+ *   kmhg_query_run / kmhg_query_run_device / kmhg_query_fill / kmhg_query_rows_device
+ *        <- .Call("sequence_kmer_positions", ptr, seq, k)    src/kmer_hash.c:1151-1172
+ *           (+ seq_kmer_positions, src/kmer_pos.c:110-136)
+ *   registration of the three symbols with arities 3/2/3    src/kmer_hash.c:1205-1224
+ *           is done by the R glue (kmer_hasher_amd/R/kmer_hash_glue.c) over this ABI.
+ *
+ * Output layouts are the R matrices' column-major data, exactly what the reference memcpy's:
+ *   pos      2 x N int32   (i, pos)      i = 1-based k-mer index, pos = 1-based window start
+ *   pair.pos 3 x P int32   (i, x, y)     x < y, j-outer / k-inner inside a k-mer
+ *   count    N_kmers int32
+ *   kmer     N_kmers strings of k chars, each followed by a NUL (stride k+1)
+ *   query    2 x H int32   (i, j)        i = 1-based END of the query window, j = index pos
+ * K-mer order (the `i` labels): distinct k-mers ranked by first occurrence.  The reference
+ * labels them in khash bucket order; the sets, counts, position lists and pairs per k-mer are
+ * identical, and seq.kmer.pos rows are identical including order (DESIGN.md "Parity").
+ */
+#ifndef KMHGPU_H
+#define KMHGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMHG_OK 0
+#define KMHG_EINVAL 1     /* argument rejected (message = the reference's R error text) */
+#define KMHG_ENOMEM 2     /* device or host allocation failed */
+#define KMHG_EDEVICE 3    /* HIP runtime error */
+#define KMHG_EOVERFLOW 4  /* result exceeds int32 / R matrix limits */
+
+/* opt.flag bits of kmer.pos (src/kmer_hash.c:17; src/kmer_pos.h:8-12) */
+#define KMHG_OPT_KMER 1u
+#define KMHG_OPT_POS 2u
+#define KMHG_OPT_PAIRS 4u
+#define KMHG_OPT_COUNT 8u
+
+typedef struct kmhg_index kmhg_index;
+typedef struct kmhg_query kmhg_query;
+
+typedef struct {
+  int32_t k;             /* index k-mer length */
+  int32_t device;        /* HIP device ordinal holding the index */
+  int64_t seq_len;       /* L */
+  int64_t n_kmers;       /* distinct k-mers (kh_size) */
+  int64_t n_positions;   /* windows indexed (rows of kmer.pos $pos) */
+  int64_t n_pairs;       /* sum C(n,2) (rows of kmer.pos $pair.pos) */
+  int64_t max_count;     /* largest position list */
+  int64_t table_slots;   /* hash-table capacity */
+  int64_t device_bytes;  /* device memory held by the index */
+} kmhg_info;
+
+const char *kmhg_last_error(void);
+int kmhg_version(void);
+
+/* make.kmer.hash.  seq: host chars, L = its length (the sequence ends at L or at the first NUL,
+ * as a C string does).  Errors: "k must be a positive integer less than 1+MAX_K",
+ * "the length of the sequence must be at least k".  do_sort is accepted for API identity; the
+ * engine always stores positions ascending, which is what sort_kmer_pos would produce. */
+int kmhg_build(const char *seq, size_t L, int k, int do_sort, kmhg_index **out);
+/* Same, for a device-resident sequence (no NULs assumed) on `stream`. */
+int kmhg_build_device(const void *d_seq, size_t L, int k, int do_sort, void *stream,
+                      kmhg_index **out);
+int kmhg_free(kmhg_index *idx);
+int kmhg_index_info(const kmhg_index *idx, kmhg_info *info);
+
+/* kmer.pos, two-phase: sizes first so the caller (R's allocMatrix) can allocate, then fill.
+ * Unset opt bits give 0 sizes and the corresponding pointers may be NULL. */
+int kmhg_positions_size(kmhg_index *idx, uint32_t opt, int64_t *n_kmers, int64_t *n_pos_rows,
+                        int64_t *n_pair_rows, int64_t *n_counts);
+int kmhg_positions_fill(kmhg_index *idx, uint32_t opt, char *kmers, int32_t *pos,
+                        int32_t *pairs, int32_t *counts);
+int kmhg_positions_fill_device(kmhg_index *idx, uint32_t opt, char *d_kmers, int32_t *d_pos,
+                               int32_t *d_pairs, int32_t *d_counts, void *stream);
+
+/* seq.kmer.pos.  Errors: "the sequence should be longer than k and k should not be longer than
+ * 31" (also for k < 1, where the reference's behaviour is undefined). */
+int kmhg_query_run(kmhg_index *idx, const char *seq, size_t L, int k, kmhg_query **q,
+                   int64_t *n_rows);
+int kmhg_query_run_device(kmhg_index *idx, const void *d_seq, size_t L, int k, void *stream,
+                          kmhg_query **q, int64_t *n_rows);
+int kmhg_query_fill(kmhg_query *q, int32_t *rows);               /* host, 2 * n_rows int32 */
+int kmhg_query_rows_device(kmhg_query *q, const int32_t **d_rows); /* owned by q */
+/* Device-to-device copy of the 2 x n_rows int32 rows into caller memory on `stream`. */
+int kmhg_query_copy_device(kmhg_query *q, void *d_dst, void *stream);
+int kmhg_query_free(kmhg_query *q);
+
+/* Index replication for the multi-GPU query (the index is broadcast once over RCCL/xGMI by the
+ * caller): export the device image into caller buffers, import on another device. */
+typedef struct {
+  int64_t table_bytes, positions_bytes, keys_bytes, counts_bytes, offsets_bytes;
+} kmhg_image_sizes;
+int kmhg_image_sizes_get(const kmhg_index *idx, kmhg_image_sizes *sz, int64_t header[8]);
+int kmhg_image_export(const kmhg_index *idx, void *d_table, void *d_positions, void *d_keys,
+                      void *d_counts, void *d_offsets, void *stream);
+int kmhg_image_import(const int64_t header[8], const void *d_table, const void *d_positions,
+                      const void *d_keys, const void *d_counts, const void *d_offsets,
+                      void *stream, kmhg_index **out);
+
+/* Per-kernel HIP-event timing (KMHG_TIMING=1 also enables it).  The report is JSON:
+ * {"kernel": [launches, total_ms], ...}; events are recorded on the kernels' own stream. */
+int kmhg_timing_enable(int on);
+int kmhg_timing_reset(void);
+int kmhg_timing_report(char *buf, size_t cap);
+
+/* Device memory pool (caching allocator). */
+int kmhg_pool_trim(void);
+int64_t kmhg_pool_cached_bytes(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMHGPU_H */

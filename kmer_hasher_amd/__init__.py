@@ -1,0 +1,10 @@
+"""MI355X-native k-mer position index: the make.kmer.hash / kmer.pos / seq.kmer.pos hot path
+of lmjakt/kmer_hasheR as hand-written HIP (gfx950) kernels behind a C-ABI (include/kmhgpu.h).
+
+    from kmer_hasher_amd import make_kmer_hash, kmer_pos, seq_kmer_pos
+"""
+from .api import (FIELDS, KMER_HASH_TAG, ExtPtr, KmerHashError, kmer_pos, make_kmer_hash,
+                  seq_kmer_pos)
+
+__all__ = ["make_kmer_hash", "kmer_pos", "seq_kmer_pos", "ExtPtr", "KmerHashError",
+           "KMER_HASH_TAG", "FIELDS"]

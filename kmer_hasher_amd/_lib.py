@@ -1,0 +1,99 @@
+"""ctypes binding of libkmhgpu.so (the C-ABI declared in include/kmhgpu.h).
+
+The product path has exactly one implementation: the HIP kernels in this shared library.  If the
+library is missing or cannot be loaded, every entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkmhgpu.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "kmhgpu.h")
+
+KMHG_OK, KMHG_EINVAL, KMHG_ENOMEM, KMHG_EDEVICE, KMHG_EOVERFLOW = 0, 1, 2, 3, 4
+
+
+class KmhgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+class Info(C.Structure):
+    _fields_ = [("k", C.c_int32), ("device", C.c_int32), ("seq_len", C.c_int64),
+                ("n_kmers", C.c_int64), ("n_positions", C.c_int64), ("n_pairs", C.c_int64),
+                ("max_count", C.c_int64), ("table_slots", C.c_int64), ("device_bytes", C.c_int64)]
+
+
+class ImageSizes(C.Structure):
+    _fields_ = [("table_bytes", C.c_int64), ("positions_bytes", C.c_int64),
+                ("keys_bytes", C.c_int64), ("counts_bytes", C.c_int64),
+                ("offsets_bytes", C.c_int64)]
+
+
+_LIB = None
+vp = C.c_void_p
+i64p = C.POINTER(C.c_int64)
+
+_PROTOS = {
+    "kmhg_last_error": (C.c_char_p, []),
+    "kmhg_version": (C.c_int, []),
+    "kmhg_build": (C.c_int, [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(vp)]),
+    "kmhg_build_device": (C.c_int, [vp, C.c_size_t, C.c_int, C.c_int, vp, C.POINTER(vp)]),
+    "kmhg_free": (C.c_int, [vp]),
+    "kmhg_index_info": (C.c_int, [vp, C.POINTER(Info)]),
+    "kmhg_positions_size": (C.c_int, [vp, C.c_uint32, i64p, i64p, i64p, i64p]),
+    "kmhg_positions_fill": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp]),
+    "kmhg_positions_fill_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, vp]),
+    "kmhg_query_run": (C.c_int, [vp, C.c_char_p, C.c_size_t, C.c_int, C.POINTER(vp), i64p]),
+    "kmhg_query_run_device": (C.c_int, [vp, vp, C.c_size_t, C.c_int, vp, C.POINTER(vp), i64p]),
+    "kmhg_query_fill": (C.c_int, [vp, vp]),
+    "kmhg_query_rows_device": (C.c_int, [vp, C.POINTER(vp)]),
+    "kmhg_query_copy_device": (C.c_int, [vp, vp, vp]),
+    "kmhg_query_free": (C.c_int, [vp]),
+    "kmhg_image_sizes_get": (C.c_int, [vp, C.POINTER(ImageSizes), i64p]),
+    "kmhg_image_export": (C.c_int, [vp, vp, vp, vp, vp, vp, vp]),
+    "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, vp, vp, vp, C.POINTER(vp)]),
+    "kmhg_timing_enable": (C.c_int, [C.c_int]),
+    "kmhg_timing_reset": (C.c_int, []),
+    "kmhg_timing_report": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "kmhg_pool_trim": (C.c_int, []),
+    "kmhg_pool_cached_bytes": (C.c_int64, []),
+}
+
+
+def header_symbols() -> list[str]:
+    """Every function declared in include/kmhgpu.h."""
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(kmhg_[a-z_]+)\s*\(", txt)))
+
+
+def lib():
+    """Load libkmhgpu.so (raises if absent: the HIP path is the only path)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+        # Load after torch (if present) so both share one HIP runtime (soname libamdhip64.so.7).
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _PROTOS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(rc: int) -> None:
+    if rc != KMHG_OK:
+        msg = lib().kmhg_last_error().decode(errors="replace")
+        raise KmhgError(rc, msg)

@@ -1,0 +1,179 @@
+"""Host-side mirror of the reference's R API for the index hot path (reference kmer_hash.R:5-28).
+
+    make_kmer_hash(seq, k, do_sort=False)  <- make.kmer.hash  (kmer_hash.R:5-8)
+    kmer_pos(ex_ptr, opt_flag)             <- kmer.pos        (kmer_hash.R:10-21)
+    seq_kmer_pos(ex_ptr, seq, k)           <- seq.kmer.pos    (kmer_hash.R:23-28)
+
+Same argument meaning, same validation order and the reference's own error messages (raised as
+``KmerHashError``, the analogue of R's error()).  Results follow the R wrappers after their
+``t()``: ``pos`` is an (N, 2) int32 matrix with columns (i, pos), ``pair.pos`` (P, 3) with
+(i, x, y), the query an (H, 2) matrix with (i, j).  Everything runs through libkmhgpu.so on the
+GPU; nothing here computes a result on the CPU.
+
+The external pointer is an ``ExtPtr`` carrying the reference's tag "kmer_hash_250930"
+(src/kmer_hash.c:22) and a finaliser that frees the device index (finalise_khash_ptr,
+src/kmer_hash.c:56-66).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import weakref
+
+import numpy as np
+
+from . import _lib
+
+KMER_HASH_TAG = "kmer_hash_250930"
+OPT_KMER, OPT_POS, OPT_PAIRS, OPT_COUNT = 1, 2, 4, 8
+FIELDS = ("kmer", "pos", "pair.pos", "count")          # src/kmer_hash.c:18
+INT_MAX = 2**31 - 1
+
+
+class KmerHashError(ValueError):
+    """R error() raised by the .Call bridge."""
+
+
+class ExtPtr:
+    """Analogue of the EXTPTRSXP returned by make_kmer_h_index."""
+
+    def __init__(self, handle: int, tag: str = KMER_HASH_TAG):
+        self._h = C.c_void_p(handle)
+        self.tag = tag
+        self._fin = weakref.finalize(self, ExtPtr._finalise, handle)
+
+    @staticmethod
+    def _finalise(handle):
+        if handle:
+            _lib.lib().kmhg_free(C.c_void_p(handle))
+
+    @property
+    def handle(self) -> C.c_void_p:
+        if not self._h:
+            raise KmerHashError("external pointer has been freed")
+        return self._h
+
+    def info(self) -> _lib.Info:
+        inf = _lib.Info()
+        _lib.check(_lib.lib().kmhg_index_info(self.handle, C.byref(inf)))
+        return inf
+
+    def free(self):
+        if self._h:
+            self._fin()
+            self._h = C.c_void_p(0)
+
+
+def _as_seq_bytes(seq, what: str) -> bytes:
+    # as.character(seq); STRING_ELT(seq_r, 0) -- only the first element is used
+    if isinstance(seq, (list, tuple)):
+        if len(seq) < 1:
+            raise KmerHashError(what)
+        seq = seq[0]
+    if isinstance(seq, str):
+        return seq.encode("latin-1")
+    if isinstance(seq, (bytes, bytearray)):
+        return bytes(seq)
+    if isinstance(seq, np.ndarray) and seq.dtype == np.uint8:
+        return seq.tobytes()
+    raise KmerHashError(what)
+
+
+def _as_int(x, what: str) -> int:
+    if isinstance(x, (list, tuple, np.ndarray)):
+        if len(x) < 1:
+            raise KmerHashError(what)
+        x = x[0]
+    try:
+        return int(x)
+    except (TypeError, ValueError):
+        raise KmerHashError(what) from None
+
+
+def make_kmer_hash(seq, k, do_sort=False) -> ExtPtr:
+    """make.kmer.hash -> .Call("make_kmer_h_index", ...)  (src/kmer_hash.c:506-540)."""
+    b = _as_seq_bytes(seq, "seq_r should be a character vector of length at least one")
+    kk = _as_int(k, "k_r must be an integer vector of length at least one")
+    ds = _as_int(do_sort, "sort_pos_r must be an integer vector of length at least one")
+    out = C.c_void_p()
+    rc = _lib.lib().kmhg_build(b, len(b), kk, ds, C.byref(out))
+    if rc == _lib.KMHG_EINVAL:
+        raise KmerHashError(_lib.lib().kmhg_last_error().decode())
+    _lib.check(rc)
+    return ExtPtr(out.value)
+
+
+def _extract(ptr) -> ExtPtr:
+    # extract_khash_ptr, src/kmer_hash.c:491-503
+    if not isinstance(ptr, ExtPtr):
+        raise KmerHashError("ptr_r should be an external pointer")
+    if ptr.tag != KMER_HASH_TAG:
+        raise KmerHashError("External pointer has incorrect tag")
+    return ptr
+
+
+def kmer_pos(ex_ptr, opt_flag) -> dict:
+    """kmer.pos -> .Call("kmer_positions", ...)  (src/kmer_hash.c:1054-1147).
+
+    Returns {"kmer", "pos", "pair.pos", "count"}; unset flags give None (R's NULL)."""
+    p = _extract(ex_ptr)
+    if isinstance(opt_flag, (list, tuple, np.ndarray)) and len(opt_flag) != 1:
+        raise KmerHashError("opt_flag_r should be an integer vector of length 1")
+    opt = _as_int(opt_flag, "opt_flag_r should be an integer vector of length 1") & 0xFFFFFFFF
+    L = _lib.lib()
+    nk, npos, npair, ncnt = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+    _lib.check(L.kmhg_positions_size(p.handle, opt, C.byref(nk), C.byref(npos), C.byref(npair),
+                                     C.byref(ncnt)))
+    # R's allocMatrix takes an int ncol: the reference overflows silently; we refuse cleanly.
+    if npair.value > INT_MAX or npos.value > INT_MAX:
+        raise KmerHashError("result has more than 2^31-1 columns (R matrix limit)")
+    k = p.info().k
+    kb = np.empty(nk.value * (k + 1), np.uint8) if opt & OPT_KMER else None
+    pos = np.empty(2 * npos.value, np.int32) if opt & OPT_POS else None
+    pairs = np.empty(3 * npair.value, np.int32) if opt & OPT_PAIRS else None
+    cnt = np.empty(ncnt.value, np.int32) if opt & OPT_COUNT else None
+
+    def ptr(a):
+        return a.ctypes.data if a is not None and a.size else None
+
+    _lib.check(L.kmhg_positions_fill(p.handle, opt, ptr(kb), ptr(pos), ptr(pairs), ptr(cnt)))
+    out = dict.fromkeys(FIELDS)
+    if kb is not None:
+        out["kmer"] = [x.decode() for x in kb.reshape(-1, k + 1)[:, :k].view(f"S{k}").ravel()] \
+            if nk.value else []
+    if pos is not None:
+        out["pos"] = pos.reshape(-1, 2)          # t(tmp$pos): columns i, pos
+    if pairs is not None:
+        out["pair.pos"] = pairs.reshape(-1, 3)   # t(tmp$pair.pos): columns i, x, y
+    if cnt is not None:
+        out["count"] = cnt
+    return out
+
+
+def seq_kmer_pos(ex_ptr, seq, k) -> np.ndarray:
+    """seq.kmer.pos -> .Call("sequence_kmer_positions", ...)  (src/kmer_hash.c:1151-1172).
+
+    Returns an (H, 2) int32 matrix with columns (i, j): i = 1-based end of the query window,
+    j = 1-based start of the indexed occurrence; rows ordered by i then j."""
+    p = _extract(ex_ptr)
+    if isinstance(seq, (list, tuple)) and len(seq) != 1:
+        raise KmerHashError("seq_r should be a single sequence")
+    b = _as_seq_bytes(seq, "seq_r should be a single sequence")
+    if isinstance(k, (list, tuple, np.ndarray)) and len(k) != 1:
+        raise KmerHashError("k should be an integer of length 1")
+    kk = _as_int(k, "k should be an integer of length 1")
+    L = _lib.lib()
+    q = C.c_void_p()
+    h = C.c_int64()
+    rc = L.kmhg_query_run(p.handle, b, len(b), kk, C.byref(q), C.byref(h))
+    if rc == _lib.KMHG_EINVAL:
+        raise KmerHashError(L.kmhg_last_error().decode())
+    _lib.check(rc)
+    try:
+        if h.value > INT_MAX:
+            raise KmerHashError("result has more than 2^31-1 columns (R matrix limit)")
+        rows = np.empty(2 * h.value, np.int32)
+        if h.value:
+            _lib.check(L.kmhg_query_fill(q, rows.ctypes.data))
+    finally:
+        L.kmhg_query_free(q)
+    return rows.reshape(-1, 2)

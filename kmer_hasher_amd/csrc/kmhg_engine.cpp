@@ -1,0 +1,748 @@
+// kmhg_engine.cpp -- host orchestrator of the MI355X k-mer position index + the C-ABI.
+//
+// Runtime pieces (native, as the reference's C core is native):
+//   * DevicePool   caching device allocator (size-classed free lists per device)
+//   * Timing       per-kernel HIP-event pairs on the launch stream (kmhg_timing_*)
+//   * Index/Query  build -> query -> readout pipelines over kmhg_kernels.hip
+// Reference entry points each C function replaces are listed in include/kmhgpu.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kmhg_common.h"
+#include "kmhg_kernels.h"
+#include "../../include/kmhgpu.h"
+
+using namespace kmhg;
+
+// ============================================================================ errors
+static thread_local std::string g_err;
+
+namespace {
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+[[noreturn]] void fail(int code, const std::string& msg) { throw Error{code, msg}; }
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    if (e == hipErrorOutOfMemory) fail(KMHG_ENOMEM, std::string(what) + ": out of device memory");
+    fail(KMHG_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+  }
+}
+#define HIPC(x) hip_check((x), #x)
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return KMHG_OK;
+  } catch (const Error& e) {
+    g_err = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "host allocation failed";
+    return KMHG_ENOMEM;
+  }
+}
+
+// ============================================================================ device pool
+// Caching allocator: blocks are kept per (device, rounded size) and reused, so repeated builds
+// and queries (bench steps, many queries against one index) pay hipMalloc once.
+class DevicePool {
+ public:
+  static DevicePool& get() {
+    static DevicePool p;
+    return p;
+  }
+  void* alloc(size_t bytes) {
+    if (bytes == 0) bytes = 256;
+    size_t sz = round(bytes);
+    int dev = 0;
+    HIPC(hipGetDevice(&dev));
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      poll_pending();
+      auto& fl = free_[{dev, sz}];
+      if (!fl.empty()) {
+        void* p = fl.back();
+        fl.pop_back();
+        cached_ -= sz;
+        live_[p] = {dev, sz};
+        return p;
+      }
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, sz);
+    if (e == hipErrorOutOfMemory) {   // release the cache and retry once
+      (void)hipGetLastError();
+      trim();
+      e = hipMalloc(&p, sz);
+    }
+    hip_check(e, "hipMalloc");
+    std::lock_guard<std::mutex> g(mu_);
+    live_[p] = {dev, sz};
+    return p;
+  }
+  // Stream-ordered release: the block returns to the free list once the work queued on
+  // `stream` up to now has completed (an event is recorded and polled on later allocations).
+  void release(void* p, hipStream_t stream = nullptr, bool ordered = false) {
+    if (!p) return;
+    hipEvent_t ev = nullptr;
+    if (ordered) {
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+          hipEventRecord(ev, stream) != hipSuccess) {
+        (void)hipStreamSynchronize(stream);
+        if (ev) (void)hipEventDestroy(ev);
+        ev = nullptr;
+      }
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = live_.find(p);
+    if (it == live_.end()) return;
+    if (ev) {
+      pending_.push_back({p, it->second, ev});
+    } else {
+      free_[it->second].push_back(p);
+      cached_ += it->second.second;
+    }
+    live_.erase(it);
+  }
+  void trim() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& pd : pending_) {
+      (void)hipEventSynchronize(pd.ev);
+      (void)hipEventDestroy(pd.ev);
+      free_[pd.key].push_back(pd.p);
+    }
+    pending_.clear();
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto& kv : free_) {
+      (void)hipSetDevice(kv.first.first);
+      for (void* p : kv.second) (void)hipFree(p);
+      kv.second.clear();
+    }
+    (void)hipSetDevice(cur);
+    cached_ = 0;
+  }
+  int64_t cached() {
+    std::lock_guard<std::mutex> g(mu_);
+    return (int64_t)cached_;
+  }
+
+ private:
+  struct Pending { void* p; std::pair<int, size_t> key; hipEvent_t ev; };
+  void poll_pending() {
+    for (size_t i = 0; i < pending_.size();) {
+      if (hipEventQuery(pending_[i].ev) == hipSuccess) {
+        (void)hipEventDestroy(pending_[i].ev);
+        free_[pending_[i].key].push_back(pending_[i].p);
+        cached_ += pending_[i].key.second;
+        pending_[i] = pending_.back();
+        pending_.pop_back();
+      } else {
+        ++i;
+      }
+    }
+  }
+  static size_t round(size_t b) {
+    if (b <= (1u << 20)) {           // small: power of two >= 256 B
+      size_t r = 256;
+      while (r < b) r <<= 1;
+      return r;
+    }
+    const size_t g = 2u << 20;       // large: 2 MiB granules
+    return (b + g - 1) / g * g;
+  }
+  std::mutex mu_;
+  std::map<std::pair<int, size_t>, std::vector<void*>> free_;
+  std::map<void*, std::pair<int, size_t>> live_;
+  std::vector<Pending> pending_;
+  size_t cached_ = 0;
+};
+
+// RAII device buffer from the pool.  A buffer bound to a stream is released stream-ordered
+// (kernels still queued on that stream may use it after the C++ object dies).
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipStream_t s = nullptr;
+  bool ordered = false;
+  DBuf() = default;
+  explicit DBuf(size_t count) { reset(count); }
+  DBuf(size_t count, hipStream_t stream) { reset(count); bind(stream); }
+  ~DBuf() { free(); }
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  void bind(hipStream_t stream) { s = stream; ordered = true; }
+  void reset(size_t count) {
+    free();
+    n = count;
+    p = static_cast<T*>(DevicePool::get().alloc(std::max<size_t>(count, 1) * sizeof(T)));
+  }
+  void free() {
+    if (p) DevicePool::get().release(p, s, ordered);
+    p = nullptr; n = 0;
+  }
+  size_t bytes() const { return n * sizeof(T); }
+};
+
+// ============================================================================ timing
+struct Timing {
+  static Timing& get() {
+    static Timing t;
+    return t;
+  }
+  bool on = false;
+  struct Rec { std::string name; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+  std::map<std::string, std::pair<int64_t, double>> acc;
+  std::mutex mu;
+
+  Timing() {
+    const char* e = std::getenv("KMHG_TIMING");
+    on = e && e[0] == '1';
+  }
+  template <class F>
+  void run(const char* name, hipStream_t s, F&& launch) {
+    if (!on) { launch(); HIPC(hipGetLastError()); return; }
+    hipEvent_t a, b;
+    HIPC(hipEventCreate(&a));
+    HIPC(hipEventCreate(&b));
+    HIPC(hipEventRecord(a, s));
+    launch();
+    HIPC(hipGetLastError());
+    HIPC(hipEventRecord(b, s));
+    std::lock_guard<std::mutex> g(mu);
+    recs.push_back({name, a, b});
+  }
+  void collect() {   // resolve recorded events (synchronises on them)
+    std::lock_guard<std::mutex> g(mu);
+    for (auto& r : recs) {
+      (void)hipEventSynchronize(r.b);
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, r.a, r.b);
+      auto& x = acc[r.name];
+      x.first += 1;
+      x.second += ms;
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    recs.clear();
+  }
+};
+#define LAUNCH(name, stream, ...) Timing::get().run(name, stream, [&] { __VA_ARGS__; })
+
+// One library stream per device for host-pointer entry points.
+hipStream_t lib_stream() {
+  static std::mutex mu;
+  static std::map<int, hipStream_t> streams;
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  hipStream_t s;
+  HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  streams[dev] = s;
+  return s;
+}
+
+// The hash table is sized from the number of windows (an upper bound on distinct k-mers) for a
+// load factor <= 0.7; capacity is not a power of two (slot = mulhi(hash, cap)).
+uint64_t table_capacity(int64_t Nw) {
+  uint64_t cap = (uint64_t)((double)Nw / 0.7) + 16;
+  return (cap + 7) & ~7ull;
+}
+
+struct Canon {              // canonical (first-occurrence) readout order, built on first use
+  bool ready = false;
+  DBuf<uint32_t> perm, canon_off, pkeys;
+  DBuf<uint64_t> pair_off;
+  uint64_t n_multi = 0;
+};
+
+}  // namespace
+
+// ============================================================================ objects
+struct kmhg_index {
+  int k = 0;
+  int device = 0;
+  int64_t L = 0;
+  uint64_t cap = 0;
+  uint64_t U = 0, N = 0, P = 0;
+  uint32_t max_n = 0;
+  DBuf<Slot> table;
+  DBuf<uint64_t> ukeys;
+  DBuf<uint32_t> counts, offsets;
+  DBuf<int32_t> positions;
+  Canon canon;
+};
+
+struct kmhg_query {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t H = 0;
+  DBuf<int2> rows;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = 0;
+  explicit DeviceGuard(int dev) {
+    HIPC(hipGetDevice(&prev));
+    if (dev != prev) HIPC(hipSetDevice(dev));
+  }
+  ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+size_t effective_len(const char* seq, size_t L) {   // a C string ends at its first NUL
+  const void* z = memchr(seq, 0, L);
+  return z ? (size_t)((const char*)z - seq) : L;
+}
+
+void check_build_args(size_t L, int k) {
+  // make_kmer_h_index, src/kmer_hash.c:514-520
+  if (k < 1 || k > 32) fail(KMHG_EINVAL, "k must be a positive integer less than 1+MAX_K");
+  if ((int64_t)L <= k) fail(KMHG_EINVAL, "the length of the sequence must be at least k");
+  if (L >= (size_t)INT32_MAX) fail(KMHG_EOVERFLOW, "sequence longer than 2^31-1 (int positions)");
+}
+
+void check_query_args(size_t L, int k) {
+  // sequence_kmer_positions, src/kmer_hash.c:1163-1164
+  if ((int64_t)L <= k || k > 31 || k < 1)
+    fail(KMHG_EINVAL,
+         "the sequence should be longer than k and k should not be longer than 31");
+  if (L >= (size_t)INT32_MAX) fail(KMHG_EOVERFLOW, "sequence longer than 2^31-1 (int positions)");
+}
+
+// ---------------------------------------------------------------------------- build
+kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
+  auto idx = std::make_unique<kmhg_index>();
+  HIPC(hipGetDevice(&idx->device));
+  idx->k = k;
+  idx->L = L;
+  const int64_t Nw = L - k + 1;
+  const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
+  idx->cap = table_capacity(Nw);
+  const uint64_t nslots = idx->cap + 1;
+  idx->table.reset(nslots);
+  DBuf<uint32_t> win_slot(Nw, s);
+  LAUNCH("k_table_init", s, launch_table_init(idx->table.p, nslots, s));
+  LAUNCH("k_build_insert", s,
+         launch_build_insert(d_seq, L, k, idx->table.p, idx->cap, win_slot.p, Nw, aligned, s));
+  // compaction scratch: look-back status + ticket + meta in one zeroed block
+  const uint32_t nt = tiles_for(nslots);
+  const size_t scratch_bytes = (size_t)nt * 8 + 64 + sizeof(BuildMeta);
+  DBuf<uint8_t> scratch(scratch_bytes, s);
+  HIPC(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
+  uint64_t* status = reinterpret_cast<uint64_t*>(scratch.p);
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(scratch.p + (size_t)nt * 8);
+  BuildMeta* meta = reinterpret_cast<BuildMeta*>(scratch.p + (size_t)nt * 8 + 64);
+  idx->ukeys.reset(Nw);
+  idx->counts.reset(Nw);
+  idx->offsets.reset(Nw + 1);
+  DBuf<uint32_t> small_ids(Nw / 2 + 1, s), large_ids(Nw / LARGE_MIN + 1, s);
+  LAUNCH("k_build_compact", s,
+         launch_build_compact(idx->table.p, nslots, status, ticket, idx->ukeys.p, idx->counts.p,
+                              idx->offsets.p, small_ids.p, large_ids.p, meta, s));
+  idx->positions.reset(Nw);
+  LAUNCH("k_build_scatter", s, launch_build_scatter(win_slot.p, Nw, idx->table.p,
+                                                    idx->positions.p, s));
+  LAUNCH("k_sort_small", s, launch_sort_small(small_ids.p, meta, idx->counts.p, idx->offsets.p,
+                                              idx->positions.p, s));
+  LAUNCH("k_sort_large", s,
+         launch_sort_large(large_ids.p, meta, idx->counts.p, idx->offsets.p, idx->positions.p,
+                           reinterpret_cast<int32_t*>(win_slot.p), s));
+  BuildMeta hm;
+  HIPC(hipMemcpyAsync(&hm, meta, sizeof(hm), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  idx->U = hm.n_kmers;
+  idx->N = hm.n_positions;
+  idx->P = hm.n_pairs;
+  idx->max_n = hm.max_count;
+  return idx.release();
+}
+
+// ---------------------------------------------------------------------------- query
+kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int kq, hipStream_t s) {
+  auto q = std::make_unique<kmhg_query>();
+  q->device = idx->device;
+  q->stream = s;
+  const int64_t Nw = L - kq + 1;
+  const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
+  const uint32_t nt = tiles_for(Nw);
+  DBuf<uint2> qinfo(Nw, s);
+  const size_t scratch_bytes = (size_t)nt * 16 + 64 + 16;
+  DBuf<uint8_t> scratch(scratch_bytes, s);
+  HIPC(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
+  uint64_t* status = reinterpret_cast<uint64_t*>(scratch.p);
+  uint64_t* tile_row0 = reinterpret_cast<uint64_t*>(scratch.p + (size_t)nt * 8);
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(scratch.p + (size_t)nt * 16);
+  uint64_t* total = reinterpret_cast<uint64_t*>(scratch.p + (size_t)nt * 16 + 64);
+  LAUNCH("k_query_probe", s,
+         launch_query_probe(d_seq, L, kq, idx->table.p, idx->cap, qinfo.p, Nw, aligned, status,
+                            ticket, tile_row0, total, s));
+  uint64_t H = 0;
+  HIPC(hipMemcpyAsync(&H, total, sizeof(H), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  q->H = (int64_t)H;
+  q->rows.reset(H);
+  if (H)
+    LAUNCH("k_query_emit", s,
+           launch_query_emit(qinfo.p, Nw, kq, idx->positions.p, tile_row0, q->rows.p, s));
+  return q.release();
+}
+
+// ---------------------------------------------------------------------------- readout
+void prepare_canon(kmhg_index* idx, hipStream_t s) {
+  Canon& c = idx->canon;
+  if (c.ready) return;
+  const int64_t L = idx->L;
+  const uint32_t U = (uint32_t)idx->U;
+  DBuf<uint32_t> F(L, s);
+  HIPC(hipMemsetAsync(F.p, 0xFF, (size_t)L * 4, s));
+  if (U) LAUNCH("k_read_first", s, launch_read_first(idx->offsets.p, idx->positions.p, U, F.p, s));
+  const uint32_t nt = tiles_for(L);
+  const size_t scratch_bytes = (size_t)nt * 24 + 64 + sizeof(ReadMeta);
+  DBuf<uint8_t> scratch(scratch_bytes, s);
+  HIPC(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
+  uint64_t* st_a = reinterpret_cast<uint64_t*>(scratch.p);
+  uint64_t* st_b = st_a + nt;
+  uint64_t* st_c = st_b + nt;
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(scratch.p + (size_t)nt * 24);
+  ReadMeta* rm = reinterpret_cast<ReadMeta*>(scratch.p + (size_t)nt * 24 + 64);
+  c.perm.reset(U);
+  c.canon_off.reset(U + 1);
+  // keys with >= 2 positions: at most N/2
+  c.pkeys.reset(idx->N / 2 + 1);
+  c.pair_off.reset(idx->N / 2 + 1);
+  LAUNCH("k_read_order", s,
+         launch_read_order(F.p, L, idx->counts.p, st_a, st_b, st_c, ticket, c.perm.p,
+                           c.canon_off.p, c.pkeys.p, c.pair_off.p, rm, s));
+  ReadMeta h;
+  HIPC(hipMemcpyAsync(&h, rm, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  if (h.n_keys != idx->U || h.n_rows != idx->N || h.n_pairs != idx->P)
+    fail(KMHG_EDEVICE, "readout order inconsistent with the index (internal error)");
+  c.n_multi = h.n_multi;
+  c.ready = true;
+}
+
+void positions_sizes(kmhg_index* idx, uint32_t opt, int64_t* nk, int64_t* np, int64_t* npp,
+                     int64_t* nc) {
+  if (nk) *nk = (opt & KMHG_OPT_KMER) ? (int64_t)idx->U : 0;
+  if (np) *np = (opt & KMHG_OPT_POS) ? (int64_t)idx->N : 0;
+  if (npp) *npp = (opt & KMHG_OPT_PAIRS) ? (int64_t)idx->P : 0;
+  if (nc) *nc = (opt & KMHG_OPT_COUNT) ? (int64_t)idx->U : 0;
+}
+
+void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, int32_t* pairs,
+                      int32_t* counts, hipStream_t s) {
+  prepare_canon(idx, s);
+  Canon& c = idx->canon;
+  const uint32_t U = (uint32_t)idx->U;
+  if ((opt & (KMHG_OPT_KMER | KMHG_OPT_COUNT)) && U)
+    LAUNCH("k_read_keys", s,
+           launch_read_keys(c.perm.p, U, idx->ukeys.p, idx->counts.p, idx->k,
+                            (opt & KMHG_OPT_COUNT) ? counts : nullptr,
+                            (opt & KMHG_OPT_KMER) ? kmers : nullptr, s));
+  if ((opt & KMHG_OPT_POS) && idx->N)
+    LAUNCH("k_read_pos", s,
+           launch_read_pos(c.perm.p, c.canon_off.p, U, idx->N, idx->offsets.p, idx->positions.p,
+                           reinterpret_cast<int2*>(pos), s));
+  if ((opt & KMHG_OPT_PAIRS) && idx->P)
+    LAUNCH("k_read_pairs", s,
+           launch_read_pairs(c.pkeys.p, c.pair_off.p, (uint32_t)c.n_multi, idx->P, c.perm.p,
+                             idx->counts.p, idx->offsets.p, idx->positions.p, pairs, s));
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI
+extern "C" {
+
+const char* kmhg_last_error(void) { return g_err.c_str(); }
+int kmhg_version(void) { return 1; }
+
+int kmhg_build(const char* seq, size_t L, int k, int do_sort, kmhg_index** out) {
+  (void)do_sort;
+  return guarded([&] {
+    if (!seq || !out) fail(KMHG_EINVAL, "null argument");
+    L = effective_len(seq, L);
+    check_build_args(L, k);
+    hipStream_t s = lib_stream();
+    DBuf<uint8_t> d(L + 16, s);
+    HIPC(hipMemcpyAsync(d.p, seq, L, hipMemcpyHostToDevice, s));
+    *out = build_device(d.p, (int64_t)L, k, s);
+  });
+}
+
+int kmhg_build_device(const void* d_seq, size_t L, int k, int do_sort, void* stream,
+                      kmhg_index** out) {
+  (void)do_sort;
+  return guarded([&] {
+    if (!d_seq || !out) fail(KMHG_EINVAL, "null argument");
+    check_build_args(L, k);
+    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    *out = build_device((const uint8_t*)d_seq, (int64_t)L, k, s);
+  });
+}
+
+int kmhg_free(kmhg_index* idx) {
+  return guarded([&] {
+    if (!idx) return;
+    DeviceGuard g(idx->device);
+    HIPC(hipDeviceSynchronize());            // queued readouts/queries may still read it
+    delete idx;
+  });
+}
+
+int kmhg_index_info(const kmhg_index* idx, kmhg_info* info) {
+  return guarded([&] {
+    if (!idx || !info) fail(KMHG_EINVAL, "null argument");
+    info->k = idx->k;
+    info->device = idx->device;
+    info->seq_len = idx->L;
+    info->n_kmers = (int64_t)idx->U;
+    info->n_positions = (int64_t)idx->N;
+    info->n_pairs = (int64_t)idx->P;
+    info->max_count = idx->max_n;
+    info->table_slots = (int64_t)idx->cap;
+    info->device_bytes = (int64_t)(idx->table.bytes() + idx->ukeys.bytes() + idx->counts.bytes() +
+                                   idx->offsets.bytes() + idx->positions.bytes());
+  });
+}
+
+int kmhg_positions_size(kmhg_index* idx, uint32_t opt, int64_t* n_kmers, int64_t* n_pos_rows,
+                        int64_t* n_pair_rows, int64_t* n_counts) {
+  return guarded([&] {
+    if (!idx) fail(KMHG_EINVAL, "null index");
+    positions_sizes(idx, opt, n_kmers, n_pos_rows, n_pair_rows, n_counts);
+  });
+}
+
+int kmhg_positions_fill_device(kmhg_index* idx, uint32_t opt, char* d_kmers, int32_t* d_pos,
+                               int32_t* d_pairs, int32_t* d_counts, void* stream) {
+  return guarded([&] {
+    if (!idx) fail(KMHG_EINVAL, "null index");
+    DeviceGuard g(idx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    positions_device(idx, opt, d_kmers, d_pos, d_pairs, d_counts, s);
+  });
+}
+
+int kmhg_positions_fill(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, int32_t* pairs,
+                        int32_t* counts) {
+  return guarded([&] {
+    if (!idx) fail(KMHG_EINVAL, "null index");
+    DeviceGuard g(idx->device);
+    hipStream_t s = lib_stream();
+    const size_t U = idx->U;
+    DBuf<char> dk((opt & KMHG_OPT_KMER) ? U * (idx->k + 1) : 0, s);
+    DBuf<int32_t> dp((opt & KMHG_OPT_POS) ? 2 * idx->N : 0, s);
+    DBuf<int32_t> dpp((opt & KMHG_OPT_PAIRS) ? 3 * idx->P : 0, s);
+    DBuf<int32_t> dc((opt & KMHG_OPT_COUNT) ? U : 0, s);
+    positions_device(idx, opt, dk.p, dp.p, dpp.p, dc.p, s);
+    if ((opt & KMHG_OPT_KMER) && U && kmers)
+      HIPC(hipMemcpyAsync(kmers, dk.p, dk.bytes(), hipMemcpyDeviceToHost, s));
+    if ((opt & KMHG_OPT_POS) && idx->N && pos)
+      HIPC(hipMemcpyAsync(pos, dp.p, dp.bytes(), hipMemcpyDeviceToHost, s));
+    if ((opt & KMHG_OPT_PAIRS) && idx->P && pairs)
+      HIPC(hipMemcpyAsync(pairs, dpp.p, dpp.bytes(), hipMemcpyDeviceToHost, s));
+    if ((opt & KMHG_OPT_COUNT) && U && counts)
+      HIPC(hipMemcpyAsync(counts, dc.p, dc.bytes(), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+  });
+}
+
+int kmhg_query_run(kmhg_index* idx, const char* seq, size_t L, int k, kmhg_query** q,
+                   int64_t* n_rows) {
+  return guarded([&] {
+    if (!idx || !seq || !q) fail(KMHG_EINVAL, "null argument");
+    L = effective_len(seq, L);
+    check_query_args(L, k);
+    DeviceGuard g(idx->device);
+    hipStream_t s = lib_stream();
+    DBuf<uint8_t> d(L + 16, s);
+    HIPC(hipMemcpyAsync(d.p, seq, L, hipMemcpyHostToDevice, s));
+    *q = query_device(idx, d.p, (int64_t)L, k, s);
+    HIPC(hipStreamSynchronize(s));
+    if (n_rows) *n_rows = (*q)->H;
+  });
+}
+
+int kmhg_query_run_device(kmhg_index* idx, const void* d_seq, size_t L, int k, void* stream,
+                          kmhg_query** q, int64_t* n_rows) {
+  return guarded([&] {
+    if (!idx || !d_seq || !q) fail(KMHG_EINVAL, "null argument");
+    check_query_args(L, k);
+    DeviceGuard g(idx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    *q = query_device(idx, (const uint8_t*)d_seq, (int64_t)L, k, s);
+    if (n_rows) *n_rows = (*q)->H;
+  });
+}
+
+int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
+  return guarded([&] {
+    if (!q) fail(KMHG_EINVAL, "null query");
+    if (!q->H) return;
+    if (!rows) fail(KMHG_EINVAL, "null output");
+    DeviceGuard g(q->device);
+    hipStream_t s = lib_stream();
+    HIPC(hipMemcpyAsync(rows, q->rows.p, (size_t)q->H * 8, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+  });
+}
+
+int kmhg_query_rows_device(kmhg_query* q, const int32_t** d_rows) {
+  return guarded([&] {
+    if (!q || !d_rows) fail(KMHG_EINVAL, "null argument");
+    *d_rows = reinterpret_cast<const int32_t*>(q->rows.p);
+  });
+}
+
+int kmhg_query_copy_device(kmhg_query* q, void* d_dst, void* stream) {
+  return guarded([&] {
+    if (!q) fail(KMHG_EINVAL, "null query");
+    if (!q->H) return;
+    if (!d_dst) fail(KMHG_EINVAL, "null output");
+    DeviceGuard g(q->device);
+    hipStream_t s = stream ? (hipStream_t)stream : q->stream;
+    if (s != q->stream) {   // order after the emit kernel queued on q->stream
+      hipEvent_t ev;
+      HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      HIPC(hipEventRecord(ev, q->stream));
+      HIPC(hipStreamWaitEvent(s, ev, 0));
+      HIPC(hipEventDestroy(ev));
+    }
+    HIPC(hipMemcpyAsync(d_dst, q->rows.p, (size_t)q->H * 8, hipMemcpyDeviceToDevice, s));
+  });
+}
+
+int kmhg_query_free(kmhg_query* q) {
+  return guarded([&] {
+    if (!q) return;
+    DeviceGuard g(q->device);
+    HIPC(hipStreamSynchronize(q->stream));   // the caller keeps its stream alive until here
+    delete q;
+  });
+}
+
+int kmhg_image_sizes_get(const kmhg_index* idx, kmhg_image_sizes* sz, int64_t header[8]) {
+  return guarded([&] {
+    if (!idx || !sz || !header) fail(KMHG_EINVAL, "null argument");
+    sz->table_bytes = (int64_t)((idx->cap + 1) * sizeof(Slot));
+    sz->positions_bytes = (int64_t)(idx->N * 4);
+    sz->keys_bytes = (int64_t)(idx->U * 8);
+    sz->counts_bytes = (int64_t)(idx->U * 4);
+    sz->offsets_bytes = (int64_t)((idx->U + 1) * 4);
+    header[0] = idx->k; header[1] = idx->L; header[2] = (int64_t)idx->cap;
+    header[3] = (int64_t)idx->U; header[4] = (int64_t)idx->N; header[5] = (int64_t)idx->P;
+    header[6] = idx->max_n; header[7] = 0x6B6D6867;   // 'kmhg'
+  });
+}
+
+int kmhg_image_export(const kmhg_index* idx, void* d_table, void* d_positions, void* d_keys,
+                      void* d_counts, void* d_offsets, void* stream) {
+  return guarded([&] {
+    if (!idx) fail(KMHG_EINVAL, "null index");
+    DeviceGuard g(idx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    auto cp = [&](void* dst, const void* src, size_t b) {
+      if (dst && b) HIPC(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToDevice, s));
+    };
+    cp(d_table, idx->table.p, (idx->cap + 1) * sizeof(Slot));
+    cp(d_positions, idx->positions.p, idx->N * 4);
+    cp(d_keys, idx->ukeys.p, idx->U * 8);
+    cp(d_counts, idx->counts.p, idx->U * 4);
+    cp(d_offsets, idx->offsets.p, (idx->U + 1) * 4);
+    if (!stream) HIPC(hipStreamSynchronize(s));
+  });
+}
+
+int kmhg_image_import(const int64_t header[8], const void* d_table, const void* d_positions,
+                      const void* d_keys, const void* d_counts, const void* d_offsets,
+                      void* stream, kmhg_index** out) {
+  return guarded([&] {
+    if (!header || !out || header[7] != 0x6B6D6867) fail(KMHG_EINVAL, "bad index image header");
+    auto idx = std::make_unique<kmhg_index>();
+    HIPC(hipGetDevice(&idx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    idx->k = (int)header[0]; idx->L = header[1]; idx->cap = (uint64_t)header[2];
+    idx->U = (uint64_t)header[3]; idx->N = (uint64_t)header[4]; idx->P = (uint64_t)header[5];
+    idx->max_n = (uint32_t)header[6];
+    idx->table.reset(idx->cap + 1);
+    idx->positions.reset(idx->N);
+    idx->ukeys.reset(idx->U);
+    idx->counts.reset(idx->U);
+    idx->offsets.reset(idx->U + 1);
+    auto cp = [&](void* dst, const void* src, size_t b) {
+      if (b) {
+        if (!src) fail(KMHG_EINVAL, "null image buffer");
+        HIPC(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToDevice, s));
+      }
+    };
+    cp(idx->table.p, d_table, (idx->cap + 1) * sizeof(Slot));
+    cp(idx->positions.p, d_positions, idx->N * 4);
+    cp(idx->ukeys.p, d_keys, idx->U * 8);
+    cp(idx->counts.p, d_counts, idx->U * 4);
+    cp(idx->offsets.p, d_offsets, (idx->U + 1) * 4);
+    HIPC(hipStreamSynchronize(s));
+    *out = idx.release();
+  });
+}
+
+int kmhg_timing_enable(int on) {
+  Timing::get().on = on != 0;
+  return KMHG_OK;
+}
+
+int kmhg_timing_reset(void) {
+  return guarded([&] {
+    Timing::get().collect();
+    Timing::get().acc.clear();
+  });
+}
+
+int kmhg_timing_report(char* buf, size_t cap) {
+  return guarded([&] {
+    Timing& t = Timing::get();
+    t.collect();
+    std::string js = "{";
+    bool first = true;
+    for (auto& kv : t.acc) {
+      char tmp[256];
+      snprintf(tmp, sizeof tmp, "%s\"%s\": [%lld, %.6f]", first ? "" : ", ", kv.first.c_str(),
+               (long long)kv.second.first, kv.second.second);
+      js += tmp;
+      first = false;
+    }
+    js += "}";
+    if (!buf || cap < js.size() + 1) fail(KMHG_EINVAL, "timing report buffer too small");
+    memcpy(buf, js.c_str(), js.size() + 1);
+  });
+}
+
+int kmhg_pool_trim(void) {
+  return guarded([&] { DevicePool::get().trim(); });
+}
+
+int64_t kmhg_pool_cached_bytes(void) { return DevicePool::get().cached(); }
+
+}  // extern "C"

@@ -1,0 +1,801 @@
+// kmhg_kernels.hip -- CDNA4 (gfx950) kernels of the k-mer position index.
+//
+// Reference hot loops replaced (lmjakt/kmer_hasheR):
+//   K_insert   seq_to_hash window walk + kmer_h_insert  (src/kmer_pos.c:36-50, 66-98;
+//              init_kmer src/kmer_util.c:18-32; UPDATE_OFFSET/LC src/kmer_util.h:8,10)
+//   K_compact  kvec sizing -> CSR offsets                (kvec growth, src/kvec.h:74-80)
+//   K_scatter  kv_push(pos)                               (src/kmer_pos.c:47)
+//   K_sort     sort_kmer_pos / ascending order            (src/kmer_pos.c:21-33)
+//   Q_probe,
+//   Q_emit     seq_kmer_positions + pair_positions_push   (src/kmer_pos.c:101-136)
+//   R_*        kmer_positions bucket walk                 (src/kmer_hash.c:1054-1147)
+//              and kmer_seq decode                        (src/kmer_hash.c:123-133)
+//
+// Integer/byte work only: every kernel is bounded by HBM (or by random-access latency on the
+// table), none by arithmetic; nothing here is matmul-shaped.
+#include <hip/hip_runtime.h>
+#include "kmhg_common.h"
+#include "kmhg_kernels.h"
+
+namespace kmhg {
+
+// ------------------------------------------------------------------ small wave/block helpers
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Inclusive wave scan (64 lanes).
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t t = __shfl_up(v, d);
+    if (lane_id() >= d) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan over the 256 threads of a block (one value per thread).  `lds` needs 5 u64.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* lds, uint64_t& total) {
+  const int wid = threadIdx.x >> 6;
+  uint64_t inc = wave_incl_scan(v);
+  if (lane_id() == 63) lds[wid] = inc;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / 64; ++w) {
+    uint64_t x = lds[w];
+    if (w < wid) off += x;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return off + inc - v;
+}
+
+// ------------------------------------------------------------------ decoupled look-back
+// status word: [63:62] = 0 not ready / 1 aggregate / 2 inclusive prefix, [61:0] payload.
+// Each word is a self-describing 8-B granule written by ONE relaxed agent-scope store and read
+// by relaxed agent-scope loads (sc1), so no separate flag, fence or payload hand-off exists.
+// Tiles come from a ticket counter so every tile a block waits on is already running.
+constexpr uint64_t LB_MASK = (1ull << 62) - 1;
+
+__device__ uint64_t lookback_excl(uint64_t* status, uint32_t tile, uint64_t agg) {
+  if (tile == 0) { st_relaxed(&status[0], (2ull << 62) | agg); return 0; }
+  st_relaxed(&status[tile], (1ull << 62) | agg);
+  uint64_t excl = 0;
+  int64_t j = (int64_t)tile - 1;
+  for (;;) {
+    uint64_t w = ld_relaxed(&status[j]);
+    uint64_t f = w >> 62;
+    if (f == 0) { __builtin_amdgcn_s_sleep(1); continue; }
+    excl += w & LB_MASK;
+    if (f == 2) break;
+    --j;
+  }
+  st_relaxed(&status[tile], (2ull << 62) | (excl + agg));
+  return excl;
+}
+
+// Grab a tile ticket (thread 0) and broadcast it.
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* counter, uint32_t* lds) {
+  if (threadIdx.x == 0) *lds = atomicAdd(counter, 1u);
+  __syncthreads();
+  uint32_t t = *lds;
+  __syncthreads();
+  return t;
+}
+
+// ------------------------------------------------------------------ LDS staging of a tile
+// Chars [base, base + STAGE) are loaded coalesced (16 B per lane when the sequence is 16-B
+// aligned) and packed into 2-bit codes (MSB-first, 16 chars per u32) and N flags (16 chars per
+// u16 kept in a u32).  Chars outside [0, L) are flagged N: a window that touches them is never
+// valid, and position -1 acting as N gives the reference's "start of sequence" rule.
+struct Stage {
+  uint32_t code[STAGE_W16];
+  uint32_t nbit[STAGE_W16];
+};
+
+__device__ __forceinline__ void pack16(const uint8_t* c, uint32_t& code, uint32_t& nb) {
+  uint32_t cd = 0, n = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    uint32_t ch = c[i];
+    cd = (cd << 2) | ((ch >> 1) & 3u);       // UPDATE_OFFSET, src/kmer_util.h:8
+    n = (n << 1) | (((ch | 0x20u) == 'n') ? 1u : 0u);   // LC(c)=='n', src/kmer_util.h:10
+  }
+  code = cd; nb = n;
+}
+
+__device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ seq, int64_t L,
+                                           int64_t base, Stage& st, bool aligned) {
+  for (int w = threadIdx.x; w < STAGE_W16; w += BLOCK) {
+    int64_t c0 = base + 16 * (int64_t)w;
+    uint8_t buf[16];
+    if (aligned && c0 >= 0 && c0 + 16 <= L) {
+      uint4 v = *reinterpret_cast<const uint4*>(seq + c0);
+      *reinterpret_cast<uint4*>(buf) = v;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        int64_t p = c0 + i;
+        buf[i] = (p >= 0 && p < L) ? seq[p] : (uint8_t)'N';
+      }
+    }
+    uint32_t cd, nb;
+    pack16(buf, cd, nb);
+    st.code[w] = cd;
+    st.nbit[w] = nb;
+  }
+}
+
+// Window whose first char is stage offset o (global start s).  Returns validity per the
+// reference walk: no N in [s, s+k), s+k <= L, and NOT (s+k == L and the char
+// before s is N or s == 0) -- the end-drop quirk of init_kmer (src/kmer_pos.c:81-83).
+__device__ __forceinline__ bool window_key(const Stage& st, int o, int64_t s, int64_t L, int k,
+                                           uint64_t& key) {
+  if (s + k > L) return false;
+  // N flags of chars [o-1, o+k): k+1 <= 33 bits out of a 48-bit window of three u16 words
+  int p = o - 1;
+  int q = p >> 4, c = p & 15;
+  uint64_t x48 = ((uint64_t)st.nbit[q] << 32) | ((uint64_t)st.nbit[q + 1] << 16) |
+                 (uint64_t)st.nbit[q + 2];
+  uint64_t m = (x48 << (16 + c)) >> (63 - k);          // top k+1 bits
+  uint64_t winN = m & ((2ull << (k - 1)) - 1ull);      // low k bits (k <= 32)
+  if (winN) return false;
+  if (s + k == L && ((m >> k) & 1ull)) return false;
+  // 2k code bits of chars [o, o+k)
+  int qw = o >> 4, b = (o & 15) * 2;
+  uint64_t x = ((uint64_t)st.code[qw] << 32) | st.code[qw + 1];
+  uint64_t y = st.code[qw + 2];
+  uint64_t t = (x << b) | ((y << b) >> 32);
+  key = t >> (64 - 2 * k);
+  return true;
+}
+
+// ------------------------------------------------------------------ hash table primitives
+__device__ __forceinline__ uint64_t home_slot(uint64_t key, uint64_t cap) {
+  return __umul64hi(mix64(key), cap);
+}
+
+// Find-or-insert (atomicCAS on the 64-bit key word).  Keys only move EMPTY -> key, so a stale
+// plain read can only show EMPTY, which the CAS then corrects.
+__device__ __forceinline__ uint32_t table_insert(Slot* __restrict__ T, uint64_t cap, uint64_t key) {
+  if (key == EMPTY_KEY) return (uint32_t)cap;          // side slot (k = 32, all G)
+  uint64_t i = home_slot(key, cap);
+  for (;;) {
+    uint64_t cur = T[i].key;
+    if (cur == key) return (uint32_t)i;
+    if (cur == EMPTY_KEY) {
+      uint64_t prev = atomicCAS((unsigned long long*)&T[i].key, (unsigned long long)EMPTY_KEY,
+                                (unsigned long long)key);
+      if (prev == EMPTY_KEY || prev == key) return (uint32_t)i;
+    }
+    if (++i == cap) i = 0;
+  }
+}
+
+// Read-only probe: returns the slot or NONE.
+__device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, uint64_t cap,
+                                               uint64_t key, uint32_t& count, uint32_t& end) {
+  if (key == EMPTY_KEY) {
+    uint4 v = *reinterpret_cast<const uint4*>(&T[cap]);
+    count = v.z; end = v.w;
+    return count ? (uint32_t)cap : NONE;
+  }
+  uint64_t i = home_slot(key, cap);
+  for (;;) {
+    uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+    uint64_t cur = ((uint64_t)v.y << 32) | v.x;
+    if (cur == key) { count = v.z; end = v.w; return (uint32_t)i; }
+    if (cur == EMPTY_KEY) { count = 0; end = 0; return NONE; }
+    if (++i == cap) i = 0;
+  }
+}
+
+// Wave-aggregated atomicAdd on a per-slot u32 counter.  Lanes that hold the same slot are
+// grouped behind the first active lane (readfirstlane + ballot); one atomic per group.  The
+// loop stops as soon as a group of one appears (i.i.d. data: one iteration), leaving the rest
+// to plain per-lane atomics; periodic (tandem-repeat) waves collapse to one atomic per key.
+// Returns the old value + this lane's rank inside its group (ranks follow lane order).
+__device__ __forceinline__ uint32_t wave_agg_add(uint32_t* base_ptr_of_slot0, bool act,
+                                                 uint32_t slot, size_t stride_u32) {
+  uint64_t active = __ballot(act);
+  uint32_t result = 0;
+  bool done = false;
+  while (active) {
+    int leader = __ffsll((unsigned long long)active) - 1;
+    uint32_t lslot = __shfl(slot, leader);
+    uint64_t grp = __ballot(act && !done && slot == lslot) & active;
+    int gsz = __popcll(grp);
+    if (gsz == 1) break;
+    uint32_t old = 0;
+    if (lane_id() == leader)
+      old = atomicAdd(base_ptr_of_slot0 + (size_t)lslot * stride_u32, (uint32_t)gsz);
+    old = __shfl(old, leader);
+    if ((grp >> lane_id()) & 1ull) {
+      result = old + (uint32_t)__popcll(grp & lanemask_lt());
+      done = true;
+    }
+    active &= ~grp;
+  }
+  if (act && !done) result = atomicAdd(base_ptr_of_slot0 + (size_t)slot * stride_u32, 1u);
+  return result;
+}
+
+// ================================================================== build kernels
+__global__ void __launch_bounds__(BLOCK) k_table_init(Slot* __restrict__ T, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (; i < n; i += stride) {
+    uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+    *reinterpret_cast<uint4*>(&T[i]) = v;
+  }
+}
+
+// K_insert: encode + N-mask + find-or-insert + count.  One lane per window, TILE windows per
+// workgroup, lane-consecutive windows so the win_slot stores are coalesced.
+__global__ void __launch_bounds__(BLOCK)
+k_build_insert(const uint8_t* __restrict__ seq, int64_t L, int k, Slot* __restrict__ T,
+               uint64_t cap, uint32_t* __restrict__ win_slot, int64_t Nw, int aligned) {
+  __shared__ Stage st;
+  const int64_t tile0 = (int64_t)blockIdx.x * TILE;
+  stage_tile(seq, L, tile0 - HALO, st, aligned != 0);
+  __syncthreads();
+  uint32_t* cnt0 = &T[0].count;
+  const size_t stride = sizeof(Slot) / sizeof(uint32_t);
+#pragma unroll 2
+  for (int j = 0; j < WPT; ++j) {
+    const int w = j * BLOCK + threadIdx.x;
+    const int64_t s = tile0 + w;
+    uint64_t key = 0;
+    bool valid = (s < Nw) && window_key(st, HALO + w, s, L, k, key);
+    uint32_t slot = NONE;
+    if (valid) slot = table_insert(T, cap, key);
+    wave_agg_add(cnt0, valid, slot, stride);
+    if (s < Nw) win_slot[s] = slot;
+  }
+}
+
+// K_compact: one pass over the table (ticketed tiles, look-back scan of {occupied, count}).
+// Occupied slot -> dense id (slot order), CSR offset; slot.end := offset (K_scatter advances it).
+// Also collects ids of keys with count >= 2 into the small/large sort lists, sum C(n,2), max n.
+__global__ void __launch_bounds__(BLOCK)
+k_build_compact(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ status,
+                uint32_t* __restrict__ ticket, uint64_t* __restrict__ ukeys,
+                uint32_t* __restrict__ counts, uint32_t* __restrict__ offsets,
+                uint32_t* __restrict__ small_ids, uint32_t* __restrict__ large_ids,
+                BuildMeta* __restrict__ meta, uint32_t ntiles, uint32_t large_min) {
+  __shared__ uint64_t sh[8];
+  __shared__ uint32_t tk;
+  __shared__ uint32_t sh_smallbase, sh_largebase;
+  const uint32_t tile = take_ticket(ticket, &tk);
+  const uint64_t t0 = (uint64_t)tile * TILE;
+  uint64_t keyv[WPT];
+  uint32_t cnt[WPT];
+  uint64_t lane_excl[WPT];
+  // pass 1: load (coalesced 16-B slots), per-j block scans
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    cnt[j] = 0; keyv[j] = EMPTY_KEY;
+    if (i < nslots) {
+      uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+      keyv[j] = ((uint64_t)v.y << 32) | v.x;
+      cnt[j] = v.z;
+    }
+  }
+  // packed value: occupied in the high 32 bits, count in the low 32 (no carry inside a tile)
+  uint64_t row_tot[WPT];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    uint64_t v = cnt[j] ? ((1ull << 32) | cnt[j]) : 0ull;
+    lane_excl[j] = block_excl_scan(v, sh, row_tot[j]);
+  }
+  uint64_t tile_tot = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    uint64_t base = tile_tot;
+    tile_tot += row_tot[j];
+    lane_excl[j] += base;
+  }
+  // global prefix: payload = occupied << 31 | count (each < 2^31 overall)
+  if (threadIdx.x == 0) {
+    uint64_t agg = ((tile_tot >> 32) << 31) | (tile_tot & 0xFFFFFFFFull);
+    uint64_t ex = lookback_excl(status, tile, agg);
+    sh[6] = ex;
+    if (tile == ntiles - 1) {
+      uint64_t inc = ex + agg;
+      meta->n_kmers = inc >> 31;
+      meta->n_positions = inc & ((1ull << 31) - 1);
+      offsets[meta->n_kmers] = (uint32_t)meta->n_positions;
+    }
+  }
+  __syncthreads();
+  const uint64_t gex = sh[6];
+  const uint64_t g_occ = gex >> 31, g_cnt = gex & ((1ull << 31) - 1);
+  uint64_t pairs = 0;
+  uint32_t mx = 0, nsmall = 0, nlarge = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (!cnt[j]) continue;
+    uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    uint32_t id = (uint32_t)(g_occ + (lane_excl[j] >> 32));
+    uint32_t off = (uint32_t)(g_cnt + (lane_excl[j] & 0xFFFFFFFFull));
+    ukeys[id] = keyv[j];
+    counts[id] = cnt[j];
+    offsets[id] = off;
+    T[i].end = off;
+    uint64_t n = cnt[j];
+    pairs += n * (n - 1) / 2;
+    mx = max(mx, cnt[j]);
+    if (cnt[j] >= 2) { if (cnt[j] >= large_min) ++nlarge; else ++nsmall; }
+  }
+  // list appends: per-thread count -> block scan -> one atomic per block per list
+  uint64_t tot_s, tot_l;
+  uint64_t ex_s = block_excl_scan(nsmall, sh, tot_s);
+  uint64_t ex_l = block_excl_scan(nlarge, sh, tot_l);
+  if (threadIdx.x == 0) {
+    sh_smallbase = tot_s ? atomicAdd(&meta->n_small, (uint32_t)tot_s) : 0;
+    sh_largebase = tot_l ? atomicAdd(&meta->n_large, (uint32_t)tot_l) : 0;
+  }
+  __syncthreads();
+  uint32_t ps = sh_smallbase + (uint32_t)ex_s, pl = sh_largebase + (uint32_t)ex_l;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (cnt[j] < 2) continue;
+    uint32_t id = (uint32_t)(g_occ + (lane_excl[j] >> 32));
+    if (cnt[j] >= large_min) large_ids[pl++] = id; else small_ids[ps++] = id;
+  }
+  // tile reductions for P and max n
+  for (int d = 32; d >= 1; d >>= 1) {
+    pairs += __shfl_xor(pairs, d);
+    mx = max(mx, (uint32_t)__shfl_xor(mx, d));
+  }
+  if (lane_id() == 0) {
+    if (pairs) atomicAdd((unsigned long long*)&meta->n_pairs, (unsigned long long)pairs);
+    if (mx) atomicMax(&meta->max_count, mx);
+  }
+}
+
+// K_scatter: positions[slot.end++] = s + 1 for every valid window (wave-aggregated, lane-order
+// ranks inside a group).  Order across waves is arbitrary; K_sort restores ascending order.
+__global__ void __launch_bounds__(BLOCK)
+k_build_scatter(const uint32_t* __restrict__ win_slot, int64_t Nw, Slot* __restrict__ T,
+                int32_t* __restrict__ positions) {
+  uint32_t* end0 = &T[0].end;
+  const size_t stride = sizeof(Slot) / sizeof(uint32_t);
+  const int64_t tile0 = (int64_t)blockIdx.x * TILE;
+#pragma unroll 2
+  for (int j = 0; j < WPT; ++j) {
+    const int64_t s = tile0 + j * BLOCK + threadIdx.x;
+    uint32_t slot = (s < Nw) ? win_slot[s] : NONE;
+    bool act = slot != NONE;
+    uint32_t r = wave_agg_add(end0, act, slot, stride);
+    if (act) positions[r] = (int32_t)(s + 1);
+  }
+}
+
+// K_sort (small): one lane per key with 2 <= n < large_min; insertion sort in place.
+__global__ void __launch_bounds__(BLOCK)
+k_sort_small(const uint32_t* __restrict__ ids, const BuildMeta* __restrict__ meta,
+             const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
+             int32_t* __restrict__ positions) {
+  const uint32_t n_ids = meta->n_small;
+  for (uint32_t t = blockIdx.x * BLOCK + threadIdx.x; t < n_ids; t += gridDim.x * BLOCK) {
+    uint32_t id = ids[t];
+    int32_t* a = positions + offsets[id];
+    uint32_t n = counts[id];
+    for (uint32_t i = 1; i < n; ++i) {
+      int32_t x = a[i];
+      int32_t j = (int32_t)i - 1;
+      while (j >= 0 && a[j] > x) { a[j + 1] = a[j]; --j; }
+      a[j + 1] = x;
+    }
+  }
+}
+
+// Block bitonic sort of a segment of up to SORT_CHUNK ints held in LDS (padded with INT_MAX).
+__device__ void lds_bitonic(int32_t* s, uint32_t pow2) {
+  for (uint32_t size = 2; size <= pow2; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t t = threadIdx.x; t < pow2 / 2; t += BLOCK) {
+        uint32_t lo = 2 * t - (t & (stride - 1));
+        uint32_t hi = lo + stride;
+        bool up = ((lo & size) == 0);
+        int32_t a = s[lo], b = s[hi];
+        if ((a > b) == up) { s[lo] = b; s[hi] = a; }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// K_sort (large): one workgroup per key with n >= large_min.  Chunks of SORT_CHUNK are sorted
+// in LDS; longer segments are then merged pairwise (each element finds its rank in the partner
+// run by binary search -- positions are unique) ping-ponging with `tmp`.
+__global__ void __launch_bounds__(BLOCK)
+k_sort_large(const uint32_t* __restrict__ ids, const BuildMeta* __restrict__ meta,
+             const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
+             int32_t* __restrict__ positions, int32_t* __restrict__ tmp) {
+  __shared__ int32_t s[SORT_CHUNK];
+  const uint32_t n_ids = meta->n_large;
+  for (uint32_t t = blockIdx.x; t < n_ids; t += gridDim.x) {
+    const uint32_t id = ids[t];
+    const uint32_t n = counts[id];
+    int32_t* a = positions + offsets[id];
+    int32_t* b = tmp + offsets[id];
+    for (uint32_t c0 = 0; c0 < n; c0 += SORT_CHUNK) {
+      uint32_t m = min((uint32_t)SORT_CHUNK, n - c0);
+      uint32_t p2 = 1;
+      while (p2 < m) p2 <<= 1;
+      for (uint32_t i = threadIdx.x; i < p2; i += BLOCK) s[i] = (i < m) ? a[c0 + i] : INT32_MAX;
+      __syncthreads();
+      lds_bitonic(s, p2);
+      for (uint32_t i = threadIdx.x; i < m; i += BLOCK) a[c0 + i] = s[i];
+      __syncthreads();
+    }
+    int32_t* src = a;
+    int32_t* dst = b;
+    for (uint32_t w = SORT_CHUNK; w < n; w <<= 1) {
+      for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+        uint32_t run = i / (2 * w), r0 = run * 2 * w;
+        uint32_t a0 = r0, a1 = min(r0 + w, n), b1 = min(r0 + 2 * w, n);
+        int32_t x = src[i];
+        uint32_t lo, hi, out;
+        if (i < a1) {           // element of run A: rank in B = #B < x
+          lo = a1; hi = b1;
+          while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (src[mid] < x) lo = mid + 1; else hi = mid; }
+          out = r0 + (i - a0) + (lo - a1);
+        } else {                // element of run B: rank in A = #A < x
+          lo = a0; hi = a1;
+          while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (src[mid] < x) lo = mid + 1; else hi = mid; }
+          out = r0 + (i - a1) + (lo - a0);
+        }
+        dst[out] = x;
+      }
+      __syncthreads();
+      int32_t* tp = src; src = dst; dst = tp;
+    }
+    if (src != a)
+      for (uint32_t i = threadIdx.x; i < n; i += BLOCK) a[i] = src[i];
+    __syncthreads();
+  }
+}
+
+// ================================================================== query kernels
+// Q_probe: per query window (query k) probe the table; qinfo[s] = {count, start}; per-tile row
+// totals go through the look-back so each tile learns its first output row.
+__global__ void __launch_bounds__(BLOCK)
+k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
+              uint64_t cap, uint2* __restrict__ qinfo, int64_t Nw, int aligned,
+              uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
+              uint64_t* __restrict__ tile_row0, uint64_t* __restrict__ total_rows,
+              uint32_t ntiles) {
+  __shared__ Stage st;
+  __shared__ uint64_t sh[8];
+  __shared__ uint32_t tk;
+  const uint32_t tile = take_ticket(ticket, &tk);
+  const int64_t tile0 = (int64_t)tile * TILE;
+  stage_tile(seq, L, tile0 - HALO, st, aligned != 0);
+  __syncthreads();
+  uint64_t rows = 0;
+#pragma unroll 2
+  for (int j = 0; j < WPT; ++j) {
+    const int w = j * BLOCK + threadIdx.x;
+    const int64_t s = tile0 + w;
+    uint64_t key = 0;
+    uint32_t count = 0, end = 0;
+    if (s < Nw && window_key(st, HALO + w, s, L, kq, key))
+      table_find(T, cap, key, count, end);
+    if (s < Nw) qinfo[s] = make_uint2(count, end - count);
+    rows += count;
+  }
+  uint64_t tot;
+  block_excl_scan(rows, sh, tot);
+  if (threadIdx.x == 0) {
+    uint64_t ex = lookback_excl(status, tile, tot);
+    tile_row0[tile] = ex;
+    if (tile == ntiles - 1) *total_rows = ex + tot;
+  }
+}
+
+// Q_emit: per tile, rows are dealt to lanes evenly (binary search over the tile's LDS prefix of
+// hit counts), so a window with thousands of hits does not serialise one lane.  Output rows are
+// (i = 1-based window end, j = 1-based index position), ordered by i then j as in the reference.
+__global__ void __launch_bounds__(BLOCK)
+k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int kq,
+             const int32_t* __restrict__ positions, const uint64_t* __restrict__ tile_row0,
+             int2* __restrict__ out) {
+  __shared__ uint64_t incl[TILE];
+  __shared__ uint32_t start[TILE];
+  __shared__ uint64_t sh[8];
+  const int64_t tile0 = (int64_t)blockIdx.x * TILE;
+  // load counts / starts (coalesced), then thread-contiguous prefix over WPT entries
+  for (int j = 0; j < WPT; ++j) {
+    int w = j * BLOCK + threadIdx.x;
+    int64_t s = tile0 + w;
+    uint2 v = (s < Nw) ? qinfo[s] : make_uint2(0u, 0u);
+    incl[w] = v.x;
+    start[w] = v.y;
+  }
+  __syncthreads();
+  uint64_t run = 0;
+  uint64_t loc[WPT];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) { run += incl[threadIdx.x * WPT + j]; loc[j] = run; }
+  uint64_t tot;
+  uint64_t ex = block_excl_scan(run, sh, tot);
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) incl[threadIdx.x * WPT + j] = loc[j] + ex;
+  __syncthreads();
+  if (tot == 0) return;
+  const uint64_t r0 = tile_row0[blockIdx.x];
+  for (uint64_t r = threadIdx.x; r < tot; r += BLOCK) {
+    // first w with incl[w] > r
+    int lo = 0, hi = TILE - 1;
+    while (lo < hi) { int mid = (lo + hi) >> 1; if (incl[mid] > r) hi = mid; else lo = mid + 1; }
+    uint64_t before = lo ? incl[lo - 1] : 0;
+    int32_t j = positions[start[lo] + (uint32_t)(r - before)];
+    out[r0 + r] = make_int2((int32_t)(tile0 + lo + kq), j);
+  }
+}
+
+// ================================================================== readout kernels
+// R_first: F[first position - 1] = id (first position = positions[offsets[id]] after K_sort).
+__global__ void __launch_bounds__(BLOCK)
+k_read_first(const uint32_t* __restrict__ offsets, const int32_t* __restrict__ positions,
+             uint32_t U, uint32_t* __restrict__ F) {
+  for (uint32_t id = blockIdx.x * BLOCK + threadIdx.x; id < U; id += gridDim.x * BLOCK)
+    F[positions[offsets[id]] - 1] = id;
+}
+
+// R_order: compact F in position order -> perm (canonical order = first occurrence), with the
+// canonical pos-row offsets, and the list of keys that own pair rows with their pair offsets.
+// Three look-back chains: {keys, pos rows} packed 31|31, {multi keys}, {pair rows}.
+__global__ void __launch_bounds__(BLOCK)
+k_read_order(const uint32_t* __restrict__ F, int64_t L, const uint32_t* __restrict__ counts,
+             uint64_t* __restrict__ st_a, uint64_t* __restrict__ st_b, uint64_t* __restrict__ st_c,
+             uint32_t* __restrict__ ticket, uint32_t* __restrict__ perm,
+             uint32_t* __restrict__ canon_off, uint32_t* __restrict__ pkeys,
+             uint64_t* __restrict__ pair_off, uint32_t ntiles, ReadMeta* __restrict__ rmeta) {
+  __shared__ uint64_t sh[8];
+  __shared__ uint64_t ex_sh[3];
+  __shared__ uint32_t tk;
+  const uint32_t tile = take_ticket(ticket, &tk);
+  const int64_t t0 = (int64_t)tile * TILE;
+  uint32_t id[WPT];
+  uint64_t va[WPT], vb[WPT], vc[WPT];
+  uint64_t suma = 0, sumb = 0, sumc = 0;
+  // thread-contiguous WPT entries keep the compaction order == position order
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    int64_t p = t0 + (int64_t)threadIdx.x * WPT + j;
+    id[j] = (p < L) ? F[p] : NONE;
+    uint64_t n = (id[j] != NONE) ? counts[id[j]] : 0;
+    va[j] = (id[j] != NONE) ? ((1ull << 32) | n) : 0;
+    vb[j] = (n >= 2) ? 1 : 0;
+    vc[j] = n * (n - (n ? 1 : 0)) / 2;
+    suma += va[j]; sumb += vb[j]; sumc += vc[j];
+  }
+  uint64_t ta, tb, tc;
+  uint64_t ea = block_excl_scan(suma, sh, ta);
+  uint64_t eb = block_excl_scan(sumb, sh, tb);
+  uint64_t ec = block_excl_scan(sumc, sh, tc);
+  if (threadIdx.x == 0) {
+    uint64_t agga = ((ta >> 32) << 31) | (ta & 0xFFFFFFFFull);
+    uint64_t xa = lookback_excl(st_a, tile, agga);
+    uint64_t xb = lookback_excl(st_b, tile, tb);
+    uint64_t xc = lookback_excl(st_c, tile, tc);
+    ex_sh[0] = xa; ex_sh[1] = xb; ex_sh[2] = xc;
+    if (tile == ntiles - 1) {
+      rmeta->n_keys = (xa + agga) >> 31;
+      rmeta->n_rows = (xa + agga) & ((1ull << 31) - 1);
+      rmeta->n_multi = xb + tb;
+      rmeta->n_pairs = xc + tc;
+    }
+  }
+  __syncthreads();
+  uint64_t ga = ex_sh[0], gb = ex_sh[1], gc = ex_sh[2];
+  uint64_t ca = (ga >> 31) + (ea >> 32), ra = (ga & ((1ull << 31) - 1)) + (ea & 0xFFFFFFFFull);
+  uint64_t cb = gb + eb, cc = gc + ec;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (id[j] == NONE) continue;
+    perm[ca] = id[j];
+    canon_off[ca] = (uint32_t)ra;
+    if (vb[j]) { pkeys[cb] = (uint32_t)ca; pair_off[cb] = cc; ++cb; }
+    ++ca; ra += va[j] & 0xFFFFFFFFull; cc += vc[j];
+  }
+}
+
+// R_keys: counts (opt 8) and k-mer strings (opt 1) in canonical order.
+__global__ void __launch_bounds__(BLOCK)
+k_read_keys(const uint32_t* __restrict__ perm, uint32_t U, const uint64_t* __restrict__ ukeys,
+            const uint32_t* __restrict__ counts, int k, int32_t* __restrict__ out_counts,
+            char* __restrict__ out_kmers) {
+  const char NUC[4] = {'A', 'C', 'T', 'G'};             // src/kmer_hash.c:21
+  for (uint32_t c = blockIdx.x * BLOCK + threadIdx.x; c < U; c += gridDim.x * BLOCK) {
+    uint32_t id = perm[c];
+    if (out_counts) out_counts[c] = (int32_t)counts[id];
+    if (out_kmers) {
+      uint64_t key = ukeys[id];
+      char* o = out_kmers + (size_t)c * (k + 1);
+      for (int i = k - 1; i >= 0; --i) { o[i] = NUC[key & 3]; key >>= 2; }
+      o[k] = 0;
+    }
+  }
+}
+
+// R_pos: rows (i, pos) in canonical order.  Each workgroup owns RROWS output rows; every key
+// owns >= 1 row so its key range fits the LDS copy of the canonical offsets.
+__global__ void __launch_bounds__(BLOCK)
+k_read_pos(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ canon_off, uint32_t U,
+           uint64_t nrows, const uint32_t* __restrict__ offsets,
+           const int32_t* __restrict__ positions, int2* __restrict__ out) {
+  __shared__ uint32_t off[TILE + 1];
+  __shared__ uint32_t cr[2];
+  const uint64_t r0 = (uint64_t)blockIdx.x * TILE;
+  if (r0 >= nrows) return;
+  const uint64_t r1 = min(nrows, r0 + TILE);
+  if (threadIdx.x < 2) {            // key holding row r0 / row r1-1: last c with off[c] <= r
+    uint64_t r = threadIdx.x == 0 ? r0 : r1 - 1;
+    uint32_t lo = 0, hi = U - 1;
+    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (canon_off[mid] <= r) lo = mid; else hi = mid - 1; }
+    cr[threadIdx.x] = lo;
+  }
+  __syncthreads();
+  const uint32_t c0 = cr[0], nk = cr[1] - cr[0] + 1;
+  for (uint32_t i = threadIdx.x; i < nk; i += BLOCK) off[i] = canon_off[c0 + i];
+  __syncthreads();
+  for (uint64_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
+    uint32_t lo = 0, hi = nk - 1;
+    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (off[mid] <= r) lo = mid; else hi = mid - 1; }
+    uint32_t c = c0 + lo;
+    uint32_t id = perm[c];
+    int32_t p = positions[offsets[id] + (uint32_t)(r - off[lo])];
+    out[r] = make_int2((int32_t)(c + 1), p);
+  }
+}
+
+// R_pairs: rows (i, x, y), x < y, j-outer / k-inner inside a key (src/kmer_hash.c:1113-1121).
+// Keys without pairs are excluded from pkeys, so again every listed key owns >= 1 row.
+__global__ void __launch_bounds__(BLOCK)
+k_read_pairs(const uint32_t* __restrict__ pkeys, const uint64_t* __restrict__ pair_off,
+             uint32_t M, uint64_t nrows, const uint32_t* __restrict__ perm,
+             const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
+             const int32_t* __restrict__ positions, int32_t* __restrict__ out) {
+  __shared__ uint64_t off[TILE + 1];
+  __shared__ uint32_t cr[2];
+  const uint64_t r0 = (uint64_t)blockIdx.x * TILE;
+  if (r0 >= nrows) return;
+  const uint64_t r1 = min(nrows, r0 + TILE);
+  if (threadIdx.x < 2) {
+    uint64_t r = threadIdx.x == 0 ? r0 : r1 - 1;
+    uint32_t lo = 0, hi = M - 1;
+    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (pair_off[mid] <= r) lo = mid; else hi = mid - 1; }
+    cr[threadIdx.x] = lo;
+  }
+  __syncthreads();
+  const uint32_t m0 = cr[0], nk = cr[1] - cr[0] + 1;
+  for (uint32_t i = threadIdx.x; i < nk; i += BLOCK) off[i] = pair_off[m0 + i];
+  __syncthreads();
+  for (uint64_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
+    uint32_t lo = 0, hi = nk - 1;
+    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (off[mid] <= r) lo = mid; else hi = mid - 1; }
+    uint32_t c = pkeys[m0 + lo];
+    uint32_t id = perm[c];
+    uint64_t n = counts[id];
+    uint64_t t = r - off[lo];
+    // largest j with S(j) = j*(2n-j-1)/2 <= t
+    double dn = (double)(2 * n - 1);
+    double disc = dn * dn - 8.0 * (double)t;
+    int64_t j = (int64_t)((dn - sqrt(disc > 0 ? disc : 0)) * 0.5);
+    if (j < 0) j = 0;
+    if (j > (int64_t)n - 2) j = (int64_t)n - 2;
+    auto S = [n](int64_t jj) -> uint64_t { return (uint64_t)jj * (2 * n - (uint64_t)jj - 1) / 2; };
+    while (j > 0 && S(j) > t) --j;
+    while (j + 1 <= (int64_t)n - 2 && S(j + 1) <= t) ++j;
+    uint64_t q = (uint64_t)j + 1 + (t - S(j));
+    const int32_t* a = positions + offsets[id];
+    int32_t* o = out + 3 * r;
+    o[0] = (int32_t)(c + 1); o[1] = a[j]; o[2] = a[q];
+  }
+}
+
+// ================================================================== launchers
+static inline unsigned grid_for(uint64_t n, unsigned per) {
+  uint64_t g = (n + per - 1) / per;
+  return (unsigned)(g ? g : 1);
+}
+
+void launch_table_init(Slot* T, uint64_t n, hipStream_t s) {
+  unsigned g = grid_for(n, BLOCK);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(k_table_init, dim3(g), dim3(BLOCK), 0, s, T, n);
+}
+void launch_build_insert(const uint8_t* seq, int64_t L, int k, Slot* T, uint64_t cap,
+                         uint32_t* win_slot, int64_t Nw, bool aligned, hipStream_t s) {
+  hipLaunchKernelGGL(k_build_insert, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, seq, L, k, T,
+                     cap, win_slot, Nw, aligned ? 1 : 0);
+}
+void launch_build_compact(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket,
+                          uint64_t* ukeys, uint32_t* counts, uint32_t* offsets,
+                          uint32_t* small_ids, uint32_t* large_ids, BuildMeta* meta,
+                          hipStream_t s) {
+  uint32_t nt = grid_for(nslots, TILE);
+  hipLaunchKernelGGL(k_build_compact, dim3(nt), dim3(BLOCK), 0, s, T, nslots, status, ticket,
+                     ukeys, counts, offsets, small_ids, large_ids, meta, nt,
+                     (uint32_t)LARGE_MIN);
+}
+void launch_build_scatter(const uint32_t* win_slot, int64_t Nw, Slot* T, int32_t* positions,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(k_build_scatter, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, win_slot, Nw,
+                     T, positions);
+}
+void launch_sort_small(const uint32_t* small_ids, const BuildMeta* meta, const uint32_t* counts,
+                       const uint32_t* offsets, int32_t* positions, hipStream_t s) {
+  hipLaunchKernelGGL(k_sort_small, dim3(2048), dim3(BLOCK), 0, s, small_ids, meta, counts,
+                     offsets, positions);
+}
+void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const uint32_t* counts,
+                       const uint32_t* offsets, int32_t* positions, int32_t* tmp, hipStream_t s) {
+  hipLaunchKernelGGL(k_sort_large, dim3(1024), dim3(BLOCK), 0, s, large_ids, meta, counts,
+                     offsets, positions, tmp);
+}
+void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, uint64_t cap,
+                        uint2* qinfo, int64_t Nw, bool aligned, uint64_t* status,
+                        uint32_t* ticket, uint64_t* tile_row0, uint64_t* total_rows,
+                        hipStream_t s) {
+  uint32_t nt = grid_for(Nw, TILE);
+  hipLaunchKernelGGL(k_query_probe, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, cap, qinfo, Nw,
+                     aligned ? 1 : 0, status, ticket, tile_row0, total_rows, nt);
+}
+void launch_query_emit(const uint2* qinfo, int64_t Nw, int kq, const int32_t* positions,
+                       const uint64_t* tile_row0, int2* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qinfo, Nw, kq,
+                     positions, tile_row0, out);
+}
+void launch_read_first(const uint32_t* offsets, const int32_t* positions, uint32_t U, uint32_t* F,
+                       hipStream_t s) {
+  unsigned g = grid_for(U, BLOCK);
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_read_first, dim3(g), dim3(BLOCK), 0, s, offsets, positions, U, F);
+}
+void launch_read_order(const uint32_t* F, int64_t L, const uint32_t* counts, uint64_t* st_a,
+                       uint64_t* st_b, uint64_t* st_c, uint32_t* ticket, uint32_t* perm,
+                       uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
+                       ReadMeta* rmeta, hipStream_t s) {
+  uint32_t nt = grid_for(L, TILE);
+  hipLaunchKernelGGL(k_read_order, dim3(nt), dim3(BLOCK), 0, s, F, L, counts, st_a, st_b, st_c,
+                     ticket, perm, canon_off, pkeys, pair_off, nt, rmeta);
+}
+void launch_read_keys(const uint32_t* perm, uint32_t U, const uint64_t* ukeys,
+                      const uint32_t* counts, int k, int32_t* out_counts, char* out_kmers,
+                      hipStream_t s) {
+  unsigned g = grid_for(U, BLOCK);
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_read_keys, dim3(g), dim3(BLOCK), 0, s, perm, U, ukeys, counts, k,
+                     out_counts, out_kmers);
+}
+void launch_read_pos(const uint32_t* perm, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
+                     const uint32_t* offsets, const int32_t* positions, int2* out, hipStream_t s) {
+  if (!nrows) return;
+  hipLaunchKernelGGL(k_read_pos, dim3(grid_for(nrows, TILE)), dim3(BLOCK), 0, s, perm, canon_off,
+                     U, nrows, offsets, positions, out);
+}
+void launch_read_pairs(const uint32_t* pkeys, const uint64_t* pair_off, uint32_t M,
+                       uint64_t nrows, const uint32_t* perm, const uint32_t* counts,
+                       const uint32_t* offsets, const int32_t* positions, int32_t* out,
+                       hipStream_t s) {
+  if (!nrows) return;
+  hipLaunchKernelGGL(k_read_pairs, dim3(grid_for(nrows, TILE)), dim3(BLOCK), 0, s, pkeys,
+                     pair_off, M, nrows, perm, counts, offsets, positions, out);
+}
+
+}  // namespace kmhg

@@ -1,0 +1,170 @@
+"""Device-resident entry points (inputs already in HBM as torch uint8 tensors).
+
+These drive the same C-ABI as ``api`` (kmhg_*_device variants) on the caller's current torch
+stream, so bench.py can time the hot path with inputs resident in HBM and the multi-GPU layer
+(``dist``) can move index images and hit rows with RCCL.  torch is plumbing here (device memory,
+streams, torch.distributed); every result is computed by the HIP kernels in libkmhgpu.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+
+import torch
+
+from . import _lib
+
+
+def _stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _check_seq(t: torch.Tensor):
+    if not (t.is_cuda and t.dtype == torch.uint8 and t.dim() == 1 and t.is_contiguous()):
+        raise TypeError("sequence must be a contiguous 1-D torch.uint8 CUDA tensor")
+
+
+class DeviceIndex:
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+
+    @classmethod
+    def build(cls, seq: torch.Tensor, k: int, stream=None) -> "DeviceIndex":
+        _check_seq(seq)
+        with torch.cuda.device(seq.device):
+            out = C.c_void_p()
+            _lib.check(_lib.lib().kmhg_build_device(C.c_void_p(seq.data_ptr()), seq.numel(), k, 0,
+                                                    _stream_ptr(stream), C.byref(out)))
+        return cls(out.value)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> dict:
+        inf = _lib.Info()
+        _lib.check(_lib.lib().kmhg_index_info(self._h, C.byref(inf)))
+        return {f: getattr(inf, f) for f, _ in _lib.Info._fields_}
+
+    def query(self, seq: torch.Tensor, k: int, stream=None) -> "DeviceQuery":
+        _check_seq(seq)
+        q = C.c_void_p()
+        h = C.c_int64()
+        with torch.cuda.device(seq.device):
+            _lib.check(_lib.lib().kmhg_query_run_device(self._h, C.c_void_p(seq.data_ptr()),
+                                                        seq.numel(), k, _stream_ptr(stream),
+                                                        C.byref(q), C.byref(h)))
+        return DeviceQuery(q.value, h.value)
+
+    def positions(self, opt: int, stream=None) -> dict:
+        """kmer.pos into device tensors: {'kmer': uint8 (U, k+1), 'pos': int32 (N, 2),
+        'pair.pos': int32 (P, 3), 'count': int32 (U,)} for the requested bits."""
+        L = _lib.lib()
+        nk, npos, npair, ncnt = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+        _lib.check(L.kmhg_positions_size(self._h, opt, C.byref(nk), C.byref(npos),
+                                         C.byref(npair), C.byref(ncnt)))
+        inf = self.info()
+        dev = torch.device("cuda", inf["device"])
+        out = {"kmer": None, "pos": None, "pair.pos": None, "count": None}
+        if opt & 1:
+            out["kmer"] = torch.empty((nk.value, inf["k"] + 1), dtype=torch.uint8, device=dev)
+        if opt & 2:
+            out["pos"] = torch.empty((npos.value, 2), dtype=torch.int32, device=dev)
+        if opt & 4:
+            out["pair.pos"] = torch.empty((npair.value, 3), dtype=torch.int32, device=dev)
+        if opt & 8:
+            out["count"] = torch.empty((ncnt.value,), dtype=torch.int32, device=dev)
+
+        def p(t):
+            return C.c_void_p(t.data_ptr()) if t is not None and t.numel() else None
+
+        with torch.cuda.device(dev):
+            _lib.check(L.kmhg_positions_fill_device(self._h, opt, p(out["kmer"]), p(out["pos"]),
+                                                    p(out["pair.pos"]), p(out["count"]),
+                                                    _stream_ptr(stream)))
+        return out
+
+    # ---- index image (multi-GPU replication) ---------------------------------------------
+    def export_image(self, stream=None) -> tuple[torch.Tensor, list[torch.Tensor]]:
+        sz = _lib.ImageSizes()
+        hdr = (C.c_int64 * 8)()
+        _lib.check(_lib.lib().kmhg_image_sizes_get(self._h, C.byref(sz), hdr))
+        dev = torch.device("cuda", self.info()["device"])
+        bufs = [torch.empty(max(1, getattr(sz, f)), dtype=torch.uint8, device=dev)
+                for f, _ in _lib.ImageSizes._fields_]
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().kmhg_image_export(self._h,
+                                                    *[C.c_void_p(b.data_ptr()) for b in bufs],
+                                                    _stream_ptr(stream)))
+        header = torch.tensor(list(hdr), dtype=torch.int64)
+        sizes = torch.tensor([getattr(sz, f) for f, _ in _lib.ImageSizes._fields_],
+                             dtype=torch.int64)
+        return torch.cat([header, sizes]), bufs
+
+    @classmethod
+    def import_image(cls, meta: torch.Tensor, bufs: list[torch.Tensor], stream=None):
+        hdr = (C.c_int64 * 8)(*[int(x) for x in meta[:8].tolist()])
+        out = C.c_void_p()
+        with torch.cuda.device(bufs[0].device):
+            _lib.check(_lib.lib().kmhg_image_import(hdr, *[C.c_void_p(b.data_ptr()) for b in bufs],
+                                                    _stream_ptr(stream), C.byref(out)))
+        return cls(out.value)
+
+    def free(self):
+        if self._h:
+            _lib.lib().kmhg_free(self._h)
+            self._h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DeviceQuery:
+    def __init__(self, handle: int, n_rows: int):
+        self._h = C.c_void_p(handle)
+        self.n_rows = n_rows
+
+    def copy_to(self, dst: torch.Tensor, stream=None) -> torch.Tensor:
+        """Copy the (H, 2) int32 rows into `dst` (device, >= 2*H int32)."""
+        if dst.numel() < 2 * self.n_rows or dst.dtype != torch.int32 or not dst.is_cuda:
+            raise ValueError("destination too small or not an int32 CUDA tensor")
+        with torch.cuda.device(dst.device):
+            _lib.check(_lib.lib().kmhg_query_copy_device(self._h, C.c_void_p(dst.data_ptr()),
+                                                         _stream_ptr(stream)))
+        return dst
+
+    def rows(self, device=None) -> torch.Tensor:
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        t = torch.empty((self.n_rows, 2), dtype=torch.int32, device=dev)
+        if self.n_rows:
+            self.copy_to(t)
+        return t
+
+    def free(self):
+        if self._h:
+            _lib.lib().kmhg_query_free(self._h)
+            self._h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def timing_enable(on: bool = True):
+    _lib.check(_lib.lib().kmhg_timing_enable(1 if on else 0))
+
+
+def timing_reset():
+    _lib.check(_lib.lib().kmhg_timing_reset())
+
+
+def timing_report() -> dict:
+    buf = C.create_string_buffer(1 << 16)
+    _lib.check(_lib.lib().kmhg_timing_report(buf, len(buf)))
+    return json.loads(buf.value.decode())

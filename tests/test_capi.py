@@ -1,0 +1,68 @@
+"""C-ABI library: loads, exports every symbol include/kmhgpu.h declares, and validates
+arguments with the reference's error messages before touching a device (CPU-safe)."""
+import ctypes as C
+import subprocess
+
+import pytest
+
+from kmer_hasher_amd import _lib, api
+
+
+def test_library_loads_and_exports_header_symbols():
+    L = _lib.lib()
+    declared = _lib.header_symbols()
+    assert len(declared) >= 20
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(declared) == set(_lib._PROTOS), "ctypes prototypes out of sync with the header"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert set(declared) <= exported
+
+
+def test_lib_is_gfx950_code_object():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob     # the .hip_fatbin holds a gfx950 object
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob
+
+
+@pytest.mark.parametrize("k", [0, -1, 33])
+def test_build_rejects_k(k):
+    out = C.c_void_p()
+    rc = _lib.lib().kmhg_build(b"ACGTACGTACGT" * 4, 48, k, 0, C.byref(out))
+    assert rc == _lib.KMHG_EINVAL
+    assert _lib.lib().kmhg_last_error() == b"k must be a positive integer less than 1+MAX_K"
+
+
+def test_build_rejects_short_sequence():
+    out = C.c_void_p()
+    rc = _lib.lib().kmhg_build(b"ACGTA", 5, 5, 0, C.byref(out))
+    assert rc == _lib.KMHG_EINVAL
+    assert _lib.lib().kmhg_last_error() == b"the length of the sequence must be at least k"
+    # a NUL ends the sequence like a C string does (R strings never hold one)
+    rc = _lib.lib().kmhg_build(b"ACG\0TACGT", 9, 4, 0, C.byref(out))
+    assert rc == _lib.KMHG_EINVAL
+
+
+def test_python_api_validation_messages():
+    with pytest.raises(api.KmerHashError, match="the length of the sequence must be at least k"):
+        api.make_kmer_hash("ACGT", 4)
+    with pytest.raises(api.KmerHashError, match="k must be a positive integer less than 1"):
+        api.make_kmer_hash("ACGTACGT", 40)
+    with pytest.raises(api.KmerHashError, match="seq_r should be a character vector"):
+        api.make_kmer_hash([], 4)
+    with pytest.raises(api.KmerHashError, match="ptr_r should be an external pointer"):
+        api.kmer_pos("not a pointer", 15)
+    with pytest.raises(api.KmerHashError, match="ptr_r should be an external pointer"):
+        api.seq_kmer_pos(None, "ACGT", 3)
+    bad = api.ExtPtr(0, tag="kmer_tree_250930")
+    with pytest.raises(api.KmerHashError, match="External pointer has incorrect tag"):
+        api.kmer_pos(bad, 15)
+
+
+def test_timing_report_is_json_without_device():
+    import json
+    buf = C.create_string_buffer(4096)
+    assert _lib.lib().kmhg_timing_report(buf, len(buf)) == 0
+    assert isinstance(json.loads(buf.value.decode()), dict)

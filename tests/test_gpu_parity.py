@@ -1,0 +1,151 @@
+"""Parity of the HIP path (through the C-ABI) with the reference's golden vectors and with the
+oracle on seeded inputs.  Integer work: everything is compared bit-exactly."""
+import numpy as np
+import pytest
+
+from kmh_canon import sha
+from oracle import oracle as O
+from synth_inputs import sequence
+
+pytestmark = pytest.mark.gpu
+
+
+def _api():
+    from kmer_hasher_amd import kmer_pos, make_kmer_hash, seq_kmer_pos
+    return make_kmer_hash, kmer_pos, seq_kmer_pos
+
+
+def _check_against_oracle(s, k, qks=None, pairs=True):
+    make, kpos, sqk = _api()
+    ptr = make(s, k)
+    oi = O.OracleIndex(s, k)
+    res = kpos(ptr, 15 if pairs else 11)
+    assert np.array_equal(res["count"], oi.counts)
+    assert np.array_equal(res["pos"].reshape(-1), oi.pos_rows())
+    assert res["kmer"] == oi.kmer_strings()
+    if pairs:
+        assert np.array_equal(res["pair.pos"].reshape(-1), oi.pair_rows())
+    inf = ptr.info()
+    assert (inf.n_kmers, inf.n_positions, inf.n_pairs, inf.max_count) == \
+        (oi.U, oi.N, oi.P, oi.max_n)
+    for kq in (qks or [min(k, 31)]):
+        if len(s) > kq:
+            q = sqk(ptr, s, kq)
+            assert np.array_equal(q.reshape(-1), oi.query(s, kq)), kq
+    ptr.free()
+
+
+def test_golden_digests(gpu, golden, testfa):
+    make, kpos, sqk = _api()
+    for r in golden[0]["records"]:
+        s = sequence(r["name"], testfa)
+        ptr = make(s, r["k"])
+        res = kpos(ptr, 15)
+        assert len(res["count"]) == r["U"], r["name"]
+        assert sha(res["count"]) == r["canon_sha"]["count"], (r["name"], r["k"])
+        assert sha(res["pos"].reshape(-1)) == r["canon_sha"]["pos"], (r["name"], r["k"])
+        assert sha(res["pair.pos"].reshape(-1)) == r["canon_sha"]["pair.pos"], (r["name"], r["k"])
+        assert sha(res["kmer"]) == r["canon_sha"]["kmer"], (r["name"], r["k"])
+        for kq, qv in r["query"].items():
+            q = sqk(ptr, s, int(kq))
+            assert q.shape[0] == qv["H"]
+            assert sha(q.reshape(-1)) == qv["sha"], (r["name"], r["k"], kq)
+        ptr.free()
+
+
+def test_edge_cases_exact(gpu, golden):
+    make, kpos, sqk = _api()
+    for r in golden[1]:
+        s, k = r["name"], r["k"]
+        ptr = make(s, k)
+        res = kpos(ptr, 15)
+        a = r["arrays"]["canon"]
+        assert res["count"].tolist() == a["count"], (s, k)
+        assert res["pos"].reshape(-1).tolist() == a["pos"], (s, k)
+        assert res["pair.pos"].reshape(-1).tolist() == a["pair.pos"], (s, k)
+        assert res["kmer"] == a["kmer"], (s, k)
+        for kq, rows in r["arrays"]["query"].items():
+            assert sqk(ptr, s, int(kq)).reshape(-1).tolist() == rows, (s, k, kq)
+        ptr.free()
+
+
+def test_testfa_arrays(gpu, testfa):
+    import os
+    make, kpos, _ = _api()
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    for k in (15, 31):
+        g = np.load(os.path.join(here, f"testfa_k{k}.npz"))
+        res = kpos(make(testfa, k), 15)
+        assert np.array_equal(res["count"], g["count"])
+        assert np.array_equal(res["pos"].reshape(-1), g["pos"])
+        assert res["kmer"] == [x.decode() for x in g["kmer"]]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_strings_vs_oracle(gpu, seed):
+    rng = np.random.default_rng(100 + seed)
+    L = int(rng.integers(33, 20000))
+    alphabet = np.frombuffer(b"ACGTacgtNnRYKM-.", np.uint8)
+    p = np.array([4, 4, 4, 4, 1, 1, 1, 1, .3, .1, .1, .1, .1, .1, .05, .05])
+    s = alphabet[rng.choice(alphabet.size, L, p=p / p.sum())].tobytes().decode()
+    for k in (1, 3, 8, 16, 21, 31, 32):
+        if L > k:
+            _check_against_oracle(s, k, qks=[min(k, 31), max(1, k - 2)])
+
+
+def test_k32_all_g_side_slot(gpu):
+    # GGG...G at k = 32 is the empty-sentinel key ~0 (SURVEY.md §7 "k=32 sentinel")
+    for s in ("G" * 40, "G" * 33, "G" * 32 + "A" + "G" * 40, "ACGT" * 20 + "G" * 50):
+        _check_against_oracle(s, 32, qks=[31, 16])
+
+
+def test_all_n_and_no_valid_window(gpu):
+    make, kpos, sqk = _api()
+    for s, k in (("N" * 100, 5), ("ACGTNACGTNACGTN", 5), ("ACGTNACG", 4)):
+        ptr = make(s, k)
+        res = kpos(ptr, 15)
+        assert res["count"].size == 0 and res["pos"].size == 0 and res["pair.pos"].size == 0
+        assert res["kmer"] == []
+        assert sqk(ptr, s, 3).shape == (O.OracleIndex(s, k).query(s, 3).size // 2, 2)
+
+
+def test_tandem_repeats_heavy_keys(gpu):
+    # period-1/2/3 arrays: heavy keys (n >> LARGE_MIN, > SORT_CHUNK) exercise the aggregated
+    # atomics and the large-segment sort with merge passes
+    s = "A" * 20000 + "ACGT" * 100 + "AC" * 9000 + "N" * 7 + "ACG" * 7000 + "T"
+    for k in (5, 15, 31):
+        _check_against_oracle(s, k, qks=[k, 4], pairs=(k != 5))
+
+
+def test_repeat_rich_medium(gpu):
+    from kmer_hasher_amd import synth
+    s = synth.add_n_runs(synth.repeat_rich(1_000_000, 9, n_gap_every=200_000), 0.001, 3)
+    s = s.tobytes().decode("latin-1")
+    _check_against_oracle(s, 31, qks=[31, 25], pairs=True)
+
+
+def test_determinism(gpu):
+    from kmer_hasher_amd import synth
+    make, kpos, sqk = _api()
+    s = synth.repeat_rich(500_000, 4, n_gap_every=100_000).tobytes().decode()
+    a = kpos(make(s, 21), 15)
+    b = kpos(make(s, 21), 15)
+    for f in ("count", "pos", "pair.pos"):
+        assert np.array_equal(a[f], b[f])
+    assert a["kmer"] == b["kmer"]
+
+
+@pytest.mark.slow
+def test_10mbp_k31_vs_oracle(gpu):
+    """Config 2 (BASELINE.json configs[1]) at full size: bit-exact vs the oracle."""
+    from kmer_hasher_amd import synth
+    s = synth.iid(10_000_000, 1).tobytes().decode()
+    make, kpos, sqk = _api()
+    ptr = make(s, 31)
+    oi = O.OracleIndex(s, 31)
+    res = kpos(ptr, 11)
+    assert np.array_equal(res["count"], oi.counts)
+    assert np.array_equal(res["pos"].reshape(-1), oi.pos_rows())
+    assert sha(res["kmer"]) == sha(oi.kmer_strings())
+    q = sqk(ptr, s, 31)
+    assert np.array_equal(q.reshape(-1), oi.query(s, 31))
