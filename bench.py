@@ -1,0 +1,231 @@
+"""bench.py -- the headline benchmark of BASELINE.json on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3]
+
+metric: "Mbp/s indexed (make.kmer.hash k=31) at 1/2/4/8 GPUs; seq.kmer.pos query Mbp/s".
+A step is one make.kmer.hash build (kmhg_build_device: table init, encode/insert, compact,
+scatter, sort, meta read-back) of one synthetic sequence already resident in HBM, and the index
+is freed again.  Config 2 (default, BASELINE.json configs[1]): 10 Mbp iid ACGT, k = 31.  The
+seq.kmer.pos self-query of the same sequence is timed the same way and reported in `query`.
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): every rank indexes its own
+sequence (seed = 1 + rank), no data-path collective -> weak scaling; value = all ranks' Mbp
+divided by the max-over-ranks time.
+
+`roofline` prices the dominant build kernel from per-kernel HIP events recorded on the stream
+the kernels run on; `traffic` comes from profiles/pmc_<config>.json (rocprofv3 --pmc passes made
+by tools/profile.sh) when present.  `cpu_baseline` times the reference's own C core
+(oracle/_ref/libkmh_ref.so, 1 thread) on rank 0 over a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    2: dict(workload="configs[1]: synthetic 10 Mbp iid ACGT (splitmix64 seed 1+rank), k=31, "
+                     "make.kmer.hash index build; self seq.kmer.pos query timed alongside",
+            L=10_000_000, k=31),
+    3: dict(workload="configs[2]: synthetic 100 Mbp iid ACGT (splitmix64 seed 2+rank), k=21, "
+                     "index build + seq.kmer.pos self-query", L=100_000_000, k=21),
+}
+
+
+def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) -> int | None:
+    """Minimal bytes each kernel must move (DESIGN.md "Roofline accounting")."""
+    if kernel == "k_build_insert":      # read L chars; key+count per distinct key; slot id/window
+        return L + 12 * U + 4 * Nw
+    if kernel == "k_build_compact":     # key+count read, key+count+offset written per key
+        return 12 * U + 16 * U
+    if kernel == "k_build_scatter":     # slot id read + position write per window
+        return 8 * N
+    if kernel == "k_query_probe":       # read L chars; 8-B slot probe + 8-B window record
+        return L + 16 * Nw
+    if kernel == "k_query_emit":        # window record read + 8-B row write + 4-B position read
+        return 8 * Nw + 12 * H
+    return None
+
+
+def cpu_baseline(seq_bytes: bytes, k: int, budget_s: float = 20.0) -> dict | None:
+    """Reference C core (compiled from the reference's own sources into oracle/_ref) timed on
+    the host, single-threaded, on a bounded prefix sample of the workload."""
+    try:
+        from oracle import oracle as O
+        if not O.ref_available():
+            return None
+        sample = seq_bytes[: min(len(seq_bytes), 10_000_000)]
+        t_build, t_query, reps, n = 0.0, 0.0, 0, 0
+        t_start = time.perf_counter()
+        while time.perf_counter() - t_start < budget_s / 2 or reps == 0:
+            t0 = time.perf_counter()
+            r = O.RefIndex(sample, k)
+            t1 = time.perf_counter()
+            q = r.query(sample, k)
+            t2 = time.perf_counter()
+            r.close()
+            t_build += t1 - t0
+            t_query += t2 - t1
+            reps += 1
+            n = q.size // 2
+            if reps >= 3:
+                break
+        mbp = len(sample) / 1e6
+        return {"value": round(mbp * reps / t_build, 3), "unit": "Mbp/s", "cores": 1,
+                "kind": "reference",
+                "sample": f"{mbp:.1f} Mbp prefix of the same sequence, k={k}, {reps} build(s) "
+                          f"of src/kmer_pos.c seq_to_hash via oracle/_ref (gcc -O2, 1 thread)",
+                "query_value": round(mbp * reps / t_query, 3), "query_rows": n}
+    except Exception as e:  # the baseline is reported, never required
+        return {"value": None, "unit": "Mbp/s", "cores": 1, "kind": "reference",
+                "sample": f"unavailable: {e}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--profile", action="store_true",
+                    help="short run for rocprofv3 (no CPU leg, no JSON extras)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from kmer_hasher_amd import device as D
+    from kmer_hasher_amd import synth
+
+    cfg = CONFIGS[args.config]
+    L, k = cfg["L"], cfg["k"]
+    seed = (1 if args.config == 2 else 2) + rank
+    host_seq = synth.iid(L, seed)
+    seq = torch.from_numpy(host_seq).to(dev)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def build_step():
+        idx = D.DeviceIndex.build(seq, k, stream)
+        info = idx.info()
+        idx.free()
+        return info
+
+    # ---------------- build: warmup, then exactly K timed steps
+    for _ in range(args.warmup):
+        info = build_step()
+    D.timing_enable(True)     # events only around the timed steps' kernels
+    D.timing_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        info = build_step()
+    barrier()
+    t_build = time.perf_counter() - t0
+    ktimes = D.timing_report()
+    D.timing_enable(False)
+
+    # ---------------- query: self seq.kmer.pos against one resident index
+    idx = D.DeviceIndex.build(seq, k, stream)
+    for _ in range(max(1, args.warmup)):
+        q = idx.query(seq, k, stream)
+        H = q.n_rows
+        q.free()
+    D.timing_enable(True)
+    D.timing_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        q = idx.query(seq, k, stream)
+        q.free()
+    barrier()
+    t_query = time.perf_counter() - t0
+    qtimes = D.timing_report()
+    D.timing_enable(False)
+    idx.free()
+
+    tb = torch.tensor([t_build, t_query], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+    t_build, t_query = tb.tolist()
+
+    if rank == 0:
+        Nw = L - k + 1
+        U, N = info["n_kmers"], info["n_positions"]
+        mbp_total = L * world / 1e6
+        value = mbp_total * args.steps / t_build
+        qvalue = mbp_total * args.steps / t_query
+        # dominant build kernel and its roofline
+        per = {n: v[1] / v[0] for n, v in ktimes.items() if v[0]}
+        dom = max(per, key=per.get)
+        ab = algorithmic_bytes(dom, L, Nw, U, N)
+        achieved = ab / (per[dom] * 1e-3) / 1e9 if ab else None
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", f"pmc_config{args.config}.json")
+        if os.path.exists(pmc_path):
+            try:
+                traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        qper = {n: v[1] / v[0] for n, v in qtimes.items() if v[0]}
+        out = {
+            "metric": "Mbp/s indexed (make.kmer.hash k=31) at 1/2/4/8 GPUs; "
+                      "seq.kmer.pos query Mbp/s",
+            "value": round(value, 2),
+            "unit": "Mbp/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_build / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": cfg["workload"], "seq_len": L, "k": k,
+                       "distinct_kmers": U, "positions": N, "parallelism": f"replicas{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom,
+                         "achieved": round(achieved, 2) if achieved else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": traffic, "algorithmic_bytes": ab,
+                         "avg_ms": round(per[dom], 5)},
+            "query": {"value": round(qvalue, 2), "unit": "Mbp/s", "rows": H,
+                      "ms_per_step": round(t_query / args.steps * 1e3, 4),
+                      "kernels_ms": {n: round(v, 5) for n, v in qper.items()}},
+            "kernels_ms": {n: round(v, 5) for n, v in per.items()},
+        }
+        if not args.no_cpu and not args.profile:
+            out["cpu_baseline"] = cpu_baseline(host_seq.tobytes(), k)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

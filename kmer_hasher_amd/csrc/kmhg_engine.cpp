@@ -216,12 +216,22 @@ struct Timing {
     const char* e = std::getenv("KMHG_TIMING");
     on = e && e[0] == '1';
   }
+  std::vector<hipEvent_t> pool;       // recycled events: no create/destroy per launch
+  hipEvent_t take() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e;
+    HIPC(hipEventCreate(&e));
+    return e;
+  }
   template <class F>
   void run(const char* name, hipStream_t s, F&& launch) {
     if (!on) { launch(); HIPC(hipGetLastError()); return; }
     hipEvent_t a, b;
-    HIPC(hipEventCreate(&a));
-    HIPC(hipEventCreate(&b));
+    {
+      std::lock_guard<std::mutex> g(mu);
+      a = take();
+      b = take();
+    }
     HIPC(hipEventRecord(a, s));
     launch();
     HIPC(hipGetLastError());
@@ -238,8 +248,8 @@ struct Timing {
       auto& x = acc[r.name];
       x.first += 1;
       x.second += ms;
-      (void)hipEventDestroy(r.a);
-      (void)hipEventDestroy(r.b);
+      pool.push_back(r.a);
+      pool.push_back(r.b);
     }
     recs.clear();
   }

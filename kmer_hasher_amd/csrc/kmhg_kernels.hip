@@ -65,20 +65,34 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* lds, u
 // Tiles come from a ticket counter so every tile a block waits on is already running.
 constexpr uint64_t LB_MASK = (1ull << 62) - 1;
 
+// Wave-parallel look-back: called by ALL 64 lanes of one wave (same tile/agg in every lane).
+// Each round the 64 lanes read the 64 nearest predecessors at once; the window is consumed up
+// to (and including) the nearest inclusive prefix once every word in front of it is ready.
 __device__ uint64_t lookback_excl(uint64_t* status, uint32_t tile, uint64_t agg) {
-  if (tile == 0) { st_relaxed(&status[0], (2ull << 62) | agg); return 0; }
-  st_relaxed(&status[tile], (1ull << 62) | agg);
-  uint64_t excl = 0;
-  int64_t j = (int64_t)tile - 1;
-  for (;;) {
-    uint64_t w = ld_relaxed(&status[j]);
-    uint64_t f = w >> 62;
-    if (f == 0) { __builtin_amdgcn_s_sleep(1); continue; }
-    excl += w & LB_MASK;
-    if (f == 2) break;
-    --j;
+  const int lane = lane_id();
+  if (tile == 0) {
+    if (lane == 0) st_relaxed(&status[0], (2ull << 62) | agg);
+    return 0;
   }
-  st_relaxed(&status[tile], (2ull << 62) | (excl + agg));
+  if (lane == 0) st_relaxed(&status[tile], (1ull << 62) | agg);
+  uint64_t excl = 0;
+  int64_t base = (int64_t)tile - 1;
+  for (;;) {
+    int64_t j = base - lane;
+    uint64_t w = (j >= 0) ? ld_relaxed(&status[j]) : (2ull << 62);   // before tile 0: prefix 0
+    uint64_t f = w >> 62;
+    uint64_t m0 = __ballot(f == 0), m2 = __ballot(f == 2);
+    int first2 = m2 ? __ffsll((unsigned long long)m2) - 1 : 64;
+    uint64_t need = first2 == 64 ? ~0ull : ((2ull << first2) - 1ull);   // lanes 0..first2
+    if (m0 & need) { __builtin_amdgcn_s_sleep(1); continue; }
+    uint64_t v = (lane <= first2) ? (w & LB_MASK) : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    excl += v;
+    if (first2 < 64) break;
+    base -= 64;
+  }
+  if (lane == 0) st_relaxed(&status[tile], (2ull << 62) | (excl + agg));
   return excl;
 }
 
@@ -305,11 +319,11 @@ k_build_compact(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ st
     lane_excl[j] += base;
   }
   // global prefix: payload = occupied << 31 | count (each < 2^31 overall)
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
     uint64_t agg = ((tile_tot >> 32) << 31) | (tile_tot & 0xFFFFFFFFull);
     uint64_t ex = lookback_excl(status, tile, agg);
-    sh[6] = ex;
-    if (tile == ntiles - 1) {
+    if (threadIdx.x == 0) sh[6] = ex;
+    if (threadIdx.x == 0 && tile == ntiles - 1) {
       uint64_t inc = ex + agg;
       meta->n_kmers = inc >> 31;
       meta->n_positions = inc & ((1ull << 31) - 1);
@@ -498,10 +512,12 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   }
   uint64_t tot;
   block_excl_scan(rows, sh, tot);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
     uint64_t ex = lookback_excl(status, tile, tot);
-    tile_row0[tile] = ex;
-    if (tile == ntiles - 1) *total_rows = ex + tot;
+    if (threadIdx.x == 0) {
+      tile_row0[tile] = ex;
+      if (tile == ntiles - 1) *total_rows = ex + tot;
+    }
   }
 }
 
@@ -587,13 +603,13 @@ k_read_order(const uint32_t* __restrict__ F, int64_t L, const uint32_t* __restri
   uint64_t ea = block_excl_scan(suma, sh, ta);
   uint64_t eb = block_excl_scan(sumb, sh, tb);
   uint64_t ec = block_excl_scan(sumc, sh, tc);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
     uint64_t agga = ((ta >> 32) << 31) | (ta & 0xFFFFFFFFull);
     uint64_t xa = lookback_excl(st_a, tile, agga);
     uint64_t xb = lookback_excl(st_b, tile, tb);
     uint64_t xc = lookback_excl(st_c, tile, tc);
-    ex_sh[0] = xa; ex_sh[1] = xb; ex_sh[2] = xc;
-    if (tile == ntiles - 1) {
+    if (threadIdx.x == 0) { ex_sh[0] = xa; ex_sh[1] = xb; ex_sh[2] = xc; }
+    if (threadIdx.x == 0 && tile == ntiles - 1) {
       rmeta->n_keys = (xa + agga) >> 31;
       rmeta->n_rows = (xa + agga) & ((1ull << 31) - 1);
       rmeta->n_multi = xb + tb;

@@ -101,12 +101,15 @@ def test_k32_all_g_side_slot(gpu):
 
 def test_all_n_and_no_valid_window(gpu):
     make, kpos, sqk = _api()
-    for s, k in (("N" * 100, 5), ("ACGTNACGTNACGTN", 5), ("ACGTNACG", 4)):
+    for s, k in (("N" * 100, 5), ("ACGTNACGTNACGTN", 5), ("nnnnACGTnnnnACGTN", 5)):
         ptr = make(s, k)
         res = kpos(ptr, 15)
         assert res["count"].size == 0 and res["pos"].size == 0 and res["pair.pos"].size == 0
         assert res["kmer"] == []
-        assert sqk(ptr, s, 3).shape == (O.OracleIndex(s, k).query(s, 3).size // 2, 2)
+        assert sqk(ptr, s, 3).shape == (0, 2)
+    # a run of exactly k followed by N is indexed; at the very end it is dropped
+    _check_against_oracle("ACGTNACG", 4, qks=[4, 3])
+    _check_against_oracle("NACGTN", 4, qks=[4])
 
 
 def test_tandem_repeats_heavy_keys(gpu):
