@@ -99,6 +99,13 @@ int kmhg_query_run(kmhg_index *idx, const char *seq, size_t L, int k, kmhg_query
                    int64_t *n_rows);
 int kmhg_query_run_device(kmhg_index *idx, const void *d_seq, size_t L, int k, void *stream,
                           kmhg_query **q, int64_t *n_rows);
+/* Windows [w_begin, w_end) (0-based window starts, w_end <= L - k + 1) of a device-resident
+ * query: the unit of the multi-GPU query shard.  Window validity still sees the whole sequence
+ * (the char before a window, the true sequence end), so consecutive ranges concatenate to the
+ * unsharded result row for row. */
+int kmhg_query_run_device_range(kmhg_index *idx, const void *d_seq, size_t L, int k,
+                                int64_t w_begin, int64_t w_end, void *stream, kmhg_query **q,
+                                int64_t *n_rows);
 int kmhg_query_fill(kmhg_query *q, int32_t *rows);               /* host, 2 * n_rows int32 */
 int kmhg_query_rows_device(kmhg_query *q, const int32_t **d_rows); /* owned by q */
 /* Device-to-device copy of the 2 x n_rows int32 rows into caller memory on `stream`. */

@@ -1,0 +1,147 @@
+/*
+ * kmer_hash_glue.c -- R .Call bridge over the libkmhgpu C-ABI (include/kmhgpu.h).
+ *
+ * Drop-in for the index half of the reference's src/kmer_hash.c: the same three .Call
+ * symbols with the same arities (registration as in src/kmer_hash.c:1205-1224), the same
+ * argument validation and error() texts, the same externalptr tag "kmer_hash_250930"
+ * (src/kmer_hash.c:22) and return shapes:
+ *
+ *   make_kmer_h_index(seq, k, do_sort)      src/kmer_hash.c:506-540   -> EXTPTRSXP
+ *   kmer_positions(ptr, opt_flag)           src/kmer_hash.c:1054-1147 -> named VECSXP[4]
+ *   sequence_kmer_positions(ptr, seq, k)    src/kmer_hash.c:1151-1172 -> INTSXP 2 x H
+ *
+ * Differences, all deliberate: the finaliser frees the whole payload (the reference leaks the
+ * 32-B khash_ptr, src/kmer_hash.c:56-66); a freed pointer is detected instead of dereferenced;
+ * result sizes are checked against R's int ncol before allocMatrix (the reference overflows at
+ * 2^31 pair rows, README.md:80-89).  Results are written by the GPU library straight into the
+ * R-allocated INTSXP buffers (one D2H copy, no kvec temporaries).
+ *
+ * Build (R headers required; R is not installed in the development image, so this file is
+ * compiled by R CMD SHLIB on the user's machine -- see INTEGRATION.md):
+ *   R CMD SHLIB -o kmer_hash.so kmer_hash_glue.c -I../../include -L.. -lkmhgpu \
+ *       -Wl,-rpath,'$ORIGIN/..'
+ */
+#include <R.h>
+#include <Rinternals.h>
+#include <R_ext/Rdynload.h>
+#include <limits.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "kmhgpu.h"
+
+static const char *kmer_hash_tag = "kmer_hash_250930";
+static const char *pos_fields[4] = {"kmer", "pos", "pair.pos", "count"};
+
+static void finalise_gpu_index(SEXP ptr_r) {
+  kmhg_index *idx = (kmhg_index *)R_ExternalPtrAddr(ptr_r);
+  if (idx) {
+    kmhg_free(idx);
+    R_ClearExternalPtr(ptr_r);
+  }
+}
+
+/* extract_khash_ptr, src/kmer_hash.c:491-503 (same messages) */
+static kmhg_index *gpu_index_of(SEXP ptr_r) {
+  if (TYPEOF(ptr_r) != EXTPTRSXP) error("ptr_r should be an external pointer");
+  SEXP tag = R_ExternalPtrTag(ptr_r);
+  if (TYPEOF(tag) != STRSXP || length(tag) != 1 || strcmp(CHAR(STRING_ELT(tag, 0)), kmer_hash_tag))
+    error("External pointer has incorrect tag");
+  kmhg_index *idx = (kmhg_index *)R_ExternalPtrAddr(ptr_r);
+  if (!idx) error("external pointer has been finalised");
+  return idx;
+}
+
+SEXP make_kmer_h_index(SEXP seq_r, SEXP k_r, SEXP sort_pos_r) {
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) < 1)
+    error("seq_r should be a character vector of length at least one");
+  if (TYPEOF(k_r) != INTSXP || length(k_r) < 1)
+    error("k_r must be an integer vector of length at least one");
+  if (TYPEOF(sort_pos_r) != INTSXP || length(k_r) < 1)
+    error("sort_pos_r must be an integer vector of length at least one");
+  int k = INTEGER(k_r)[0];
+  int do_sort = asInteger(sort_pos_r);
+  SEXP s = STRING_ELT(seq_r, 0);
+  kmhg_index *idx = NULL;
+  int rc = kmhg_build(CHAR(s), (size_t)length(s), k, do_sort, &idx);
+  if (rc != KMHG_OK) error("%s", kmhg_last_error());
+  SEXP tag = PROTECT(allocVector(STRSXP, 1));
+  SET_STRING_ELT(tag, 0, mkChar(kmer_hash_tag));
+  SEXP ptr = PROTECT(R_MakeExternalPtr(idx, tag, R_NilValue));
+  R_RegisterCFinalizerEx(ptr, finalise_gpu_index, TRUE);
+  UNPROTECT(2);
+  return ptr;
+}
+
+SEXP kmer_positions(SEXP ptr_r, SEXP opt_flag_r) {
+  kmhg_index *idx = gpu_index_of(ptr_r);
+  if (TYPEOF(opt_flag_r) != INTSXP || length(opt_flag_r) != 1)
+    error("opt_flag_r should be an integer vector of length 1");
+  uint32_t opt = (uint32_t)asInteger(opt_flag_r);
+  int64_t nk = 0, np = 0, npp = 0, nc = 0;
+  if (kmhg_positions_size(idx, opt, &nk, &np, &npp, &nc) != KMHG_OK)
+    error("%s", kmhg_last_error());
+  if (np > INT_MAX || npp > INT_MAX || nk > INT_MAX)
+    error("result has more than 2^31-1 columns (R matrix limit)");
+  kmhg_info info;
+  kmhg_index_info(idx, &info);
+  SEXP ret = PROTECT(allocVector(VECSXP, 4));
+  SEXP nm = PROTECT(allocVector(STRSXP, 4));
+  for (int i = 0; i < 4; ++i) SET_STRING_ELT(nm, i, mkChar(pos_fields[i]));
+  setAttrib(ret, R_NamesSymbol, nm);
+  int *pos = NULL, *pairs = NULL, *counts = NULL;
+  char *kmers = NULL;
+  if (opt & KMHG_OPT_POS) {
+    SET_VECTOR_ELT(ret, 1, allocMatrix(INTSXP, 2, (int)np));
+    pos = INTEGER(VECTOR_ELT(ret, 1));
+  }
+  if (opt & KMHG_OPT_PAIRS) {
+    SET_VECTOR_ELT(ret, 2, allocMatrix(INTSXP, 3, (int)npp));
+    pairs = INTEGER(VECTOR_ELT(ret, 2));
+  }
+  if (opt & KMHG_OPT_COUNT) {
+    SET_VECTOR_ELT(ret, 3, allocVector(INTSXP, (R_xlen_t)nc));
+    counts = INTEGER(VECTOR_ELT(ret, 3));
+  }
+  if ((opt & KMHG_OPT_KMER) && nk) kmers = (char *)R_alloc((size_t)nk, info.k + 1);
+  if (kmhg_positions_fill(idx, opt, kmers, pos, pairs, counts) != KMHG_OK)
+    error("%s", kmhg_last_error());
+  if (opt & KMHG_OPT_KMER) {
+    SET_VECTOR_ELT(ret, 0, allocVector(STRSXP, (R_xlen_t)nk));
+    SEXP kr = VECTOR_ELT(ret, 0);
+    for (int64_t i = 0; i < nk; ++i)
+      SET_STRING_ELT(kr, (R_xlen_t)i, mkChar(kmers + (size_t)i * (info.k + 1)));
+  }
+  UNPROTECT(2);
+  return ret;
+}
+
+SEXP sequence_kmer_positions(SEXP ptr_r, SEXP seq_r, SEXP k_r) {
+  kmhg_index *idx = gpu_index_of(ptr_r);
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) != 1) error("seq_r should be a single sequence");
+  if (TYPEOF(k_r) != INTSXP || length(k_r) != 1) error("k should be an integer of length 1");
+  int k = INTEGER(k_r)[0];
+  SEXP s = STRING_ELT(seq_r, 0);
+  kmhg_query *q = NULL;
+  int64_t h = 0;
+  if (kmhg_query_run(idx, CHAR(s), (size_t)length(s), k, &q, &h) != KMHG_OK)
+    error("%s", kmhg_last_error());
+  if (h > INT_MAX) {
+    kmhg_query_free(q);
+    error("result has more than 2^31-1 columns (R matrix limit)");
+  }
+  SEXP ret = PROTECT(allocMatrix(INTSXP, 2, (int)h));
+  int rc = h ? kmhg_query_fill(q, INTEGER(ret)) : KMHG_OK;
+  kmhg_query_free(q);
+  if (rc != KMHG_OK) error("%s", kmhg_last_error());
+  UNPROTECT(1);
+  return ret;
+}
+
+static const R_CallMethodDef gpu_call_methods[] = {
+    {"make_kmer_h_index", (DL_FUNC)&make_kmer_h_index, 3},
+    {"kmer_positions", (DL_FUNC)&kmer_positions, 2},
+    {"sequence_kmer_positions", (DL_FUNC)&sequence_kmer_positions, 3},
+    {NULL, NULL, 0}};
+
+void R_init_kmer_hash(DllInfo *info) { R_registerRoutines(info, NULL, gpu_call_methods, NULL, NULL); }

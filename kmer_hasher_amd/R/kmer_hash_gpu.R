@@ -1,0 +1,34 @@
+## R front-end of the MI355X k-mer position index.
+## Same three functions, arguments and results as the reference's index API
+## (reference kmer_hash.R:5-28); only the shared object changes: kmer_hash.so is built from
+## kmer_hash_glue.c over libkmhgpu.so (see INTEGRATION.md).
+local({
+    here <- dirname(sys.frame(1)$ofile)
+    dyn.load(file.path(here, "kmer_hash.so"))
+})
+
+## build the index; positions come back ascending per k-mer whatever do.sort says
+make.kmer.hash <- function(seq, k, do.sort=FALSE){
+    .Call("make_kmer_h_index", as.character(seq), as.integer(k), as.integer(do.sort))
+}
+
+## opt.flag bits: 1 k-mer strings, 2 (i, pos) rows, 4 (i, x, y) pair rows, 8 counts
+kmer.pos <- function(ex.ptr, opt.flag){
+    res <- .Call("kmer_positions", ex.ptr, as.integer(opt.flag))
+    if(!is.null(res$pos)){
+        res$pos <- t(res$pos)
+        colnames(res$pos) <- c("i", "pos")
+    }
+    if(!is.null(res$pair.pos)){
+        res$pair.pos <- t(res$pair.pos)
+        colnames(res$pair.pos) <- c("i", "x", "y")
+    }
+    res
+}
+
+## dot-plot rows: i = end of the query window, j = start of the indexed occurrence
+seq.kmer.pos <- function(ex.ptr, seq, k){
+    m <- .Call("sequence_kmer_positions", ex.ptr, as.character(seq), as.integer(k))
+    rownames(m) <- c("i", "j")
+    t(m)
+}

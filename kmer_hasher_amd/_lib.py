@@ -50,6 +50,8 @@ _PROTOS = {
     "kmhg_positions_fill_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, vp]),
     "kmhg_query_run": (C.c_int, [vp, C.c_char_p, C.c_size_t, C.c_int, C.POINTER(vp), i64p]),
     "kmhg_query_run_device": (C.c_int, [vp, vp, C.c_size_t, C.c_int, vp, C.POINTER(vp), i64p]),
+    "kmhg_query_run_device_range": (C.c_int, [vp, vp, C.c_size_t, C.c_int, C.c_int64, C.c_int64,
+                                              vp, C.POINTER(vp), i64p]),
     "kmhg_query_fill": (C.c_int, [vp, vp]),
     "kmhg_query_rows_device": (C.c_int, [vp, C.POINTER(vp)]),
     "kmhg_query_copy_device": (C.c_int, [vp, vp, vp]),

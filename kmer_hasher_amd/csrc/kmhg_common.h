@@ -29,7 +29,7 @@ constexpr int BLOCK = 256;
 constexpr int WPT = 8;
 constexpr int TILE = BLOCK * WPT;          // windows per workgroup
 constexpr int HALO = 32;                   // chars staged before/after the tile (k <= 32)
-constexpr int STAGE = TILE + 2 * HALO;     // chars staged per workgroup
+constexpr int STAGE = TILE + 2 * HALO + 16;  // chars staged per workgroup (+16: base aligned down)
 constexpr int STAGE_W16 = STAGE / 16;      // 16-char words staged
 
 // murmur3 fmix64: keys are structured (2-bit packed DNA); khash's (key>>33)^key^(key<<11)

@@ -389,11 +389,15 @@ kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) 
 }
 
 // ---------------------------------------------------------------------------- query
-kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int kq, hipStream_t s) {
+// Windows [w0, w1) of the query (default: all L - kq + 1).  Rows come out ordered by window
+// end, so shards of consecutive window ranges concatenate to the unsharded result.
+kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int kq, int64_t w0,
+                         int64_t w1, hipStream_t s) {
   auto q = std::make_unique<kmhg_query>();
   q->device = idx->device;
   q->stream = s;
-  const int64_t Nw = L - kq + 1;
+  const int64_t Nw = w1 - w0;
+  if (Nw <= 0) return q.release();
   const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
   const uint32_t nt = tiles_for(Nw);
   DBuf<uint2> qinfo(Nw, s);
@@ -405,8 +409,8 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   uint32_t* ticket = reinterpret_cast<uint32_t*>(scratch.p + (size_t)nt * 16);
   uint64_t* total = reinterpret_cast<uint64_t*>(scratch.p + (size_t)nt * 16 + 64);
   LAUNCH("k_query_probe", s,
-         launch_query_probe(d_seq, L, kq, idx->table.p, idx->cap, qinfo.p, Nw, aligned, status,
-                            ticket, tile_row0, total, s));
+         launch_query_probe(d_seq, L, kq, idx->table.p, idx->cap, qinfo.p, w0, w1, aligned,
+                            status, ticket, tile_row0, total, s));
   uint64_t H = 0;
   HIPC(hipMemcpyAsync(&H, total, sizeof(H), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -414,7 +418,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   q->rows.reset(H);
   if (H)
     LAUNCH("k_query_emit", s,
-           launch_query_emit(qinfo.p, Nw, kq, idx->positions.p, tile_row0, q->rows.p, s));
+           launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, s));
   return q.release();
 }
 
@@ -590,7 +594,7 @@ int kmhg_query_run(kmhg_index* idx, const char* seq, size_t L, int k, kmhg_query
     hipStream_t s = lib_stream();
     DBuf<uint8_t> d(L + 16, s);
     HIPC(hipMemcpyAsync(d.p, seq, L, hipMemcpyHostToDevice, s));
-    *q = query_device(idx, d.p, (int64_t)L, k, s);
+    *q = query_device(idx, d.p, (int64_t)L, k, 0, (int64_t)L - k + 1, s);
     HIPC(hipStreamSynchronize(s));
     if (n_rows) *n_rows = (*q)->H;
   });
@@ -603,7 +607,22 @@ int kmhg_query_run_device(kmhg_index* idx, const void* d_seq, size_t L, int k, v
     check_query_args(L, k);
     DeviceGuard g(idx->device);
     hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
-    *q = query_device(idx, (const uint8_t*)d_seq, (int64_t)L, k, s);
+    *q = query_device(idx, (const uint8_t*)d_seq, (int64_t)L, k, 0, (int64_t)L - k + 1, s);
+    if (n_rows) *n_rows = (*q)->H;
+  });
+}
+
+int kmhg_query_run_device_range(kmhg_index* idx, const void* d_seq, size_t L, int k,
+                                int64_t w_begin, int64_t w_end, void* stream, kmhg_query** q,
+                                int64_t* n_rows) {
+  return guarded([&] {
+    if (!idx || !d_seq || !q) fail(KMHG_EINVAL, "null argument");
+    check_query_args(L, k);
+    const int64_t Nw = (int64_t)L - k + 1;
+    if (w_begin < 0 || w_end > Nw || w_begin > w_end) fail(KMHG_EINVAL, "window range out of bounds");
+    DeviceGuard g(idx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    *q = query_device(idx, (const uint8_t*)d_seq, (int64_t)L, k, w_begin, w_end, s);
     if (n_rows) *n_rows = (*q)->H;
   });
 }

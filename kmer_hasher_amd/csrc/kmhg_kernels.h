@@ -36,11 +36,12 @@ void launch_sort_small(const uint32_t* small_ids, const BuildMeta* meta, const u
 void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const uint32_t* counts,
                        const uint32_t* offsets, int32_t* positions, int32_t* tmp, hipStream_t s);
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, uint64_t cap,
-                        uint2* qinfo, int64_t Nw, bool aligned, uint64_t* status,
+                        uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* status,
                         uint32_t* ticket, uint64_t* tile_row0, uint64_t* total_rows,
                         hipStream_t s);
-void launch_query_emit(const uint2* qinfo, int64_t Nw, int kq, const int32_t* positions,
-                       const uint64_t* tile_row0, int2* out, hipStream_t s);
+void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
+                       const int32_t* positions, const uint64_t* tile_row0, int2* out,
+                       hipStream_t s);
 void launch_read_first(const uint32_t* offsets, const int32_t* positions, uint32_t U, uint32_t* F,
                        hipStream_t s);
 void launch_read_order(const uint32_t* F, int64_t L, const uint32_t* counts, uint64_t* st_a,

@@ -259,7 +259,7 @@ k_build_insert(const uint8_t* __restrict__ seq, int64_t L, int k, Slot* __restri
                uint64_t cap, uint32_t* __restrict__ win_slot, int64_t Nw, int aligned) {
   __shared__ Stage st;
   const int64_t tile0 = (int64_t)blockIdx.x * TILE;
-  stage_tile(seq, L, tile0 - HALO, st, aligned != 0);
+  stage_tile(seq, L, tile0 - HALO, st, aligned != 0);   // tile0 % 16 == 0: window o = HALO + w
   __syncthreads();
   uint32_t* cnt0 = &T[0].count;
   const size_t stride = sizeof(Slot) / sizeof(uint32_t);
@@ -487,7 +487,7 @@ k_sort_large(const uint32_t* __restrict__ ids, const BuildMeta* __restrict__ met
 // totals go through the look-back so each tile learns its first output row.
 __global__ void __launch_bounds__(BLOCK)
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
-              uint64_t cap, uint2* __restrict__ qinfo, int64_t Nw, int aligned,
+              uint64_t cap, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
               uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
               uint64_t* __restrict__ tile_row0, uint64_t* __restrict__ total_rows,
               uint32_t ntiles) {
@@ -495,19 +495,23 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   __shared__ uint64_t sh[8];
   __shared__ uint32_t tk;
   const uint32_t tile = take_ticket(ticket, &tk);
-  const int64_t tile0 = (int64_t)tile * TILE;
-  stage_tile(seq, L, tile0 - HALO, st, aligned != 0);
+  // windows [w0, w1) of the FULL sequence: halo chars come from the real neighbours, so the
+  // N / end-of-sequence rules at a shard boundary are those of the unsharded walk
+  const int64_t t_start = w0 + (int64_t)tile * TILE;
+  const int64_t base = (t_start & ~15ll) - HALO;
+  const int o0 = (int)(t_start - base);
+  stage_tile(seq, L, base, st, aligned != 0);
   __syncthreads();
   uint64_t rows = 0;
 #pragma unroll 2
   for (int j = 0; j < WPT; ++j) {
     const int w = j * BLOCK + threadIdx.x;
-    const int64_t s = tile0 + w;
+    const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, end = 0;
-    if (s < Nw && window_key(st, HALO + w, s, L, kq, key))
+    if (s < w1 && window_key(st, o0 + w, s, L, kq, key))
       table_find(T, cap, key, count, end);
-    if (s < Nw) qinfo[s] = make_uint2(count, end - count);
+    if (s < w1) qinfo[s - w0] = make_uint2(count, end - count);
     rows += count;
   }
   uint64_t tot;
@@ -525,7 +529,7 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
 // hit counts), so a window with thousands of hits does not serialise one lane.  Output rows are
 // (i = 1-based window end, j = 1-based index position), ordered by i then j as in the reference.
 __global__ void __launch_bounds__(BLOCK)
-k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int kq,
+k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
              const int32_t* __restrict__ positions, const uint64_t* __restrict__ tile_row0,
              int2* __restrict__ out) {
   __shared__ uint64_t incl[TILE];
@@ -558,7 +562,7 @@ k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int kq,
     while (lo < hi) { int mid = (lo + hi) >> 1; if (incl[mid] > r) hi = mid; else lo = mid + 1; }
     uint64_t before = lo ? incl[lo - 1] : 0;
     int32_t j = positions[start[lo] + (uint32_t)(r - before)];
-    out[r0 + r] = make_int2((int32_t)(tile0 + lo + kq), j);
+    out[r0 + r] = make_int2((int32_t)(w0 + tile0 + lo + kq), j);
   }
 }
 
@@ -765,17 +769,18 @@ void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const u
                      offsets, positions, tmp);
 }
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, uint64_t cap,
-                        uint2* qinfo, int64_t Nw, bool aligned, uint64_t* status,
+                        uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* status,
                         uint32_t* ticket, uint64_t* tile_row0, uint64_t* total_rows,
                         hipStream_t s) {
-  uint32_t nt = grid_for(Nw, TILE);
-  hipLaunchKernelGGL(k_query_probe, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, cap, qinfo, Nw,
-                     aligned ? 1 : 0, status, ticket, tile_row0, total_rows, nt);
+  uint32_t nt = grid_for(w1 - w0, TILE);
+  hipLaunchKernelGGL(k_query_probe, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, cap, qinfo, w0,
+                     w1, aligned ? 1 : 0, status, ticket, tile_row0, total_rows, nt);
 }
-void launch_query_emit(const uint2* qinfo, int64_t Nw, int kq, const int32_t* positions,
-                       const uint64_t* tile_row0, int2* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qinfo, Nw, kq,
-                     positions, tile_row0, out);
+void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
+                       const int32_t* positions, const uint64_t* tile_row0, int2* out,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qinfo, Nw, w0,
+                     kq, positions, tile_row0, out);
 }
 void launch_read_first(const uint32_t* offsets, const int32_t* positions, uint32_t U, uint32_t* F,
                        hipStream_t s) {

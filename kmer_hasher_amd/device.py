@@ -57,6 +57,17 @@ class DeviceIndex:
                                                         C.byref(q), C.byref(h)))
         return DeviceQuery(q.value, h.value)
 
+    def query_range(self, seq: torch.Tensor, k: int, w0: int, w1: int, stream=None) -> "DeviceQuery":
+        """Windows [w0, w1) of `seq` (the multi-GPU shard unit, see dist.py)."""
+        _check_seq(seq)
+        q = C.c_void_p()
+        h = C.c_int64()
+        with torch.cuda.device(seq.device):
+            _lib.check(_lib.lib().kmhg_query_run_device_range(
+                self._h, C.c_void_p(seq.data_ptr()), seq.numel(), k, w0, w1, _stream_ptr(stream),
+                C.byref(q), C.byref(h)))
+        return DeviceQuery(q.value, h.value)
+
     def positions(self, opt: int, stream=None) -> dict:
         """kmer.pos into device tensors: {'kmer': uint8 (U, k+1), 'pos': int32 (N, 2),
         'pair.pos': int32 (P, 3), 'count': int32 (U,)} for the requested bits."""

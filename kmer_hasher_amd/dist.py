@@ -1,0 +1,116 @@
+"""Multi-GPU seq.kmer.pos: one process per GPU over torch.distributed
+(backend "nccl" = RCCL over xGMI on MI355X).
+
+  * the index is built once (rank 0) and its device image is broadcast to every rank
+    (five ncclBroadcast calls: table, positions, keys, counts, offsets);
+  * the query's windows are split into `world` contiguous ranges; each rank runs the HIP query
+    on its range of the (replicated) query sequence -- validity at a range edge is decided on
+    the full sequence, so no halo logic leaks into the result;
+  * per-rank row counts are all-gathered (8 B each) and the rows are gathered to the root with
+    point-to-point send/recv (RCCL has no gatherv); concatenation in rank order is exactly the
+    reference's row order (window end ascending, then index position ascending).
+
+The collective layer is engine-agnostic: anything with ``query_range(seq, k, w0, w1) -> (h, 2)
+int32 tensor`` works, which is how tests exercise the sharding + gather logic with gloo on CPU.
+The product engine is ``HipQueryEngine`` (libkmhgpu.so).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_ranges(n: int, world: int) -> list[tuple[int, int]]:
+    """Balanced contiguous [w0, w1) ranges covering [0, n)."""
+    q, r = divmod(max(n, 0), world)
+    out, a = [], 0
+    for i in range(world):
+        b = a + q + (1 if i < r else 0)
+        out.append((a, b))
+        a = b
+    return out
+
+
+def broadcast_buffers(meta: torch.Tensor | None, bufs: list[torch.Tensor] | None, src: int,
+                      device: torch.device, group=None) -> tuple[torch.Tensor, list[torch.Tensor]]:
+    """Broadcast an int64 meta vector (last 5 entries = buffer byte sizes) and the byte buffers
+    it describes from `src`.  Non-src ranks pass None and receive freshly allocated tensors."""
+    rank = dist.get_rank(group)
+    n_meta = torch.zeros(1, dtype=torch.int64, device=device)
+    if rank == src:
+        n_meta[0] = meta.numel()
+    dist.broadcast(n_meta, src, group=group)
+    m = meta.to(device) if rank == src else torch.empty(int(n_meta.item()), dtype=torch.int64,
+                                                        device=device)
+    dist.broadcast(m, src, group=group)
+    sizes = [int(x) for x in m[-5:].tolist()]
+    if rank != src:
+        bufs = [torch.empty(max(1, s), dtype=torch.uint8, device=device) for s in sizes]
+    for b in bufs:
+        dist.broadcast(b, src, group=group)
+    return m, bufs
+
+
+def gather_rows(local: torch.Tensor, dst: int = 0, group=None) -> torch.Tensor | None:
+    """Concatenate every rank's (h_r, 2) int32 rows on `dst` in rank order."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = local.device
+    cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    if rank == dst:
+        out = torch.empty((sum(counts), 2), dtype=torch.int32, device=dev)
+        offs = [0]
+        for c in counts:
+            offs.append(offs[-1] + c)
+        out[offs[rank]:offs[rank + 1]] = local
+        ops = [dist.P2POp(dist.irecv, out[offs[r]:offs[r + 1]], r, group=group)
+               for r in range(world) if r != dst and counts[r]]
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        return out
+    if counts[rank]:
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), dst,
+                                                    group=group)]):
+            w.wait()
+    return None
+
+
+def sharded_query(engine, seq: torch.Tensor, k: int, dst: int = 0, group=None):
+    """seq.kmer.pos with the query windows split across ranks; rows gathered on `dst`."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n_windows = max(0, seq.numel() - k + 1)
+    w0, w1 = shard_ranges(n_windows, world)[rank]
+    local = engine.query_range(seq, k, w0, w1)
+    return gather_rows(local, dst, group)
+
+
+class HipQueryEngine:
+    """Adapter: a DeviceIndex (libkmhgpu) as a sharded-query engine."""
+
+    def __init__(self, index):
+        self.index = index
+
+    def query_range(self, seq: torch.Tensor, k: int, w0: int, w1: int) -> torch.Tensor:
+        q = self.index.query_range(seq, k, w0, w1)
+        try:
+            return q.rows(seq.device)
+        finally:
+            q.free()
+
+
+def broadcast_index(index, device: torch.device, src: int = 0, group=None):
+    """Replicate rank `src`'s DeviceIndex on every rank (index image over RCCL)."""
+    from .device import DeviceIndex
+    rank = dist.get_rank(group)
+    if rank == src:
+        meta, bufs = index.export_image()
+        torch.cuda.synchronize(device)
+        broadcast_buffers(meta, bufs, src, device, group)
+        return index
+    meta, bufs = broadcast_buffers(None, None, src, device, group)
+    torch.cuda.synchronize(device)
+    return DeviceIndex.import_image(meta.cpu(), bufs)

@@ -1,0 +1,62 @@
+"""Device-resident API (inputs in HBM), window-range query shards and index images on one GPU."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _seq(torch, n=300_000, seed=6):
+    from kmer_hasher_amd import synth
+    s = synth.add_lowercase(synth.add_n_runs(synth.repeat_rich(n, seed, n_gap_every=50_000),
+                                             0.002, 3), 0.05, 4)
+    return s, torch.from_numpy(s).cuda()
+
+
+def test_device_build_query_positions_match_oracle(gpu):
+    torch = gpu
+    from kmer_hasher_amd.device import DeviceIndex
+    s, t = _seq(torch)
+    for k in (17, 31):
+        idx = DeviceIndex.build(t, k)
+        oi = O.OracleIndex(s.tobytes(), k)
+        inf = idx.info()
+        assert (inf["n_kmers"], inf["n_positions"], inf["n_pairs"]) == (oi.U, oi.N, oi.P)
+        res = idx.positions(15)
+        assert np.array_equal(res["count"].cpu().numpy(), oi.counts)
+        assert np.array_equal(res["pos"].cpu().numpy().reshape(-1), oi.pos_rows())
+        assert np.array_equal(res["pair.pos"].cpu().numpy().reshape(-1), oi.pair_rows())
+        q = idx.query(t, k)
+        assert np.array_equal(q.rows().cpu().numpy().reshape(-1), oi.query(s.tobytes(), k))
+        q.free()
+        idx.free()
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_range_shards_concatenate_to_full_query(gpu, nshards):
+    torch = gpu
+    from kmer_hasher_amd import dist as kd
+    from kmer_hasher_amd.device import DeviceIndex
+    s, t = _seq(torch, 200_000, 8)
+    k = 21
+    idx = DeviceIndex.build(t, k)
+    want = O.OracleIndex(s.tobytes(), k).query(s.tobytes(), 19)
+    eng = kd.HipQueryEngine(idx)
+    parts = [eng.query_range(t, 19, a, b) for a, b in kd.shard_ranges(t.numel() - 19 + 1, nshards)]
+    got = torch.cat(parts).cpu().numpy().reshape(-1)
+    assert np.array_equal(got, want)
+
+
+def test_image_export_import_roundtrip(gpu):
+    torch = gpu
+    from kmer_hasher_amd.device import DeviceIndex
+    s, t = _seq(torch, 150_000, 10)
+    a = DeviceIndex.build(t, 25)
+    meta, bufs = a.export_image()
+    b = DeviceIndex.import_image(meta, [x.clone() for x in bufs])
+    qa, qb = a.query(t, 25), b.query(t, 25)
+    assert torch.equal(qa.rows(), qb.rows())
+    pa, pb = a.positions(15), b.positions(15)
+    for f in ("count", "pos", "pair.pos", "kmer"):
+        assert torch.equal(pa[f], pb[f])
