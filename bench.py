@@ -1,6 +1,6 @@
 """bench.py -- the headline benchmark of BASELINE.json on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
 
 metric: "Mbp/s indexed (make.kmer.hash k=31) at 1/2/4/8 GPUs; seq.kmer.pos query Mbp/s".
 A step is one make.kmer.hash build (kmhg_build_device: table init, encode/insert, compact,
@@ -36,6 +36,13 @@ CONFIGS = {
             L=10_000_000, k=31),
     3: dict(workload="configs[2]: synthetic 100 Mbp iid ACGT (splitmix64 seed 2+rank), k=21, "
                      "index build + seq.kmer.pos self-query", L=100_000_000, k=21),
+    4: dict(workload="configs[3]: synthetic 40 Mbp repeat-rich (synth.repeat_rich seed 3), k=31, "
+                     "kmer.pos(opt.flag=14: pos + pair.pos + count) readout into HBM",
+            L=40_000_000, k=31),
+    5: dict(workload="configs[4]: two synthetic 500 Mbp sequences (A iid seed 4; B = A + 1% SNV "
+                     "+ 20 inversions/translocations + N-runs), k=31, seq.kmer.pos(B vs index(A)) "
+                     "with B's windows sharded over the ranks, index broadcast once over RCCL, "
+                     "rows gathered to rank 0", L=500_000_000, k=31),
 }
 
 
@@ -118,6 +125,12 @@ def main():
 
     cfg = CONFIGS[args.config]
     L, k = cfg["L"], cfg["k"]
+    if args.config in (4, 5):
+        (bench_readout if args.config == 4 else bench_sharded_query)(args, cfg, dev, world, rank)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     seed = (1 if args.config == 2 else 2) + rank
     host_seq = synth.iid(L, seed)
     seq = torch.from_numpy(host_seq).to(dev)
@@ -225,6 +238,147 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _emit(out):
+    print(json.dumps(out), flush=True)
+
+
+def bench_readout(args, cfg, dev, world, rank):
+    """Config 4: kmer.pos pair.pos off-diagonals of a repeat-rich 40 Mbp index, per rank."""
+    import torch
+    import torch.distributed as dist
+    from kmer_hasher_amd import device as D
+    from kmer_hasher_amd import synth
+    L, k = cfg["L"], cfg["k"]
+    host = synth.repeat_rich(L, 3 + rank)
+    seq = torch.from_numpy(host).to(dev)
+    t0 = time.perf_counter()
+    idx = D.DeviceIndex.build(seq, k)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    info = idx.info()
+    opt = 14
+    for _ in range(args.warmup):
+        res = idx.positions(opt)
+        del res
+    D.timing_enable(True)
+    D.timing_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = idx.positions(opt)
+        del res
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    kt = D.timing_report()
+    D.timing_enable(False)
+    tt = torch.tensor([t], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = tt.item()
+    if rank == 0:
+        P, N, U = info["n_pairs"], info["n_positions"], info["n_kmers"]
+        per = {n: v[1] / v[0] for n, v in kt.items() if v[0]}
+        dom = max(per, key=per.get)
+        ab = {"k_read_pairs": 12 * P + 8 * P, "k_read_pos": 8 * N + 4 * N}.get(dom)
+        ach = ab / (per[dom] * 1e-3) / 1e9 if ab else None
+        _emit({"metric": "kmer.pos pair.pos rows/s (config 4)", "value": round(P * world * args.steps / t / 1e9, 4),
+               "unit": "G pair rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(t / args.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "i32", "data": "synthetic",
+               "config": {"workload": cfg["workload"], "seq_len": L, "k": k, "distinct_kmers": U,
+                          "positions": N, "pairs": P, "max_count": info["max_count"],
+                          "build_s": round(t_build, 4)},
+               "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2) if ach else None,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": None,
+                            "algorithmic_bytes": ab, "avg_ms": round(per[dom], 4)},
+               "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
+    idx.free()
+
+
+def bench_sharded_query(args, cfg, dev, world, rank):
+    """Config 5: B (500 Mbp) queried against index(A); B's windows sharded over the ranks."""
+    import torch
+    import torch.distributed as dist
+    from kmer_hasher_amd import device as D
+    from kmer_hasher_amd import dist as kd
+    from kmer_hasher_amd import synth
+    L, k = cfg["L"], cfg["k"]
+    A = synth.iid(L, 4)
+    B = synth.derived(A, 5)
+    tb = torch.from_numpy(B).to(dev)
+    if world > 1:
+        index = None
+        if rank == 0:
+            ta = torch.from_numpy(A).to(dev)
+            index = D.DeviceIndex.build(ta, k)
+            del ta
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        index = kd.broadcast_index(index, dev)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t_bcast = time.perf_counter() - t0
+    else:
+        ta = torch.from_numpy(A).to(dev)
+        index = D.DeviceIndex.build(ta, k)
+        del ta
+        t_bcast = 0.0
+    del A
+    eng = kd.HipQueryEngine(index)
+
+    def step():
+        if world > 1:
+            return kd.sharded_query(eng, tb, k, dst=0)
+        return eng.query_range(tb, k, 0, tb.numel() - k + 1)
+
+    for _ in range(args.warmup):
+        rows = step()
+        del rows
+    D.timing_enable(True)
+    D.timing_reset()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rows = step()
+        H = rows.shape[0] if rows is not None else 0
+        del rows
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    kt = D.timing_report()
+    D.timing_enable(False)
+    tt = torch.tensor([t], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = tt.item()
+    if rank == 0:
+        per = {n: v[1] / v[0] for n, v in kt.items() if v[0]}
+        dom = max(per, key=per.get)
+        Nw_rank = (L - k + 1) // world
+        ab = algorithmic_bytes(dom, L // world, Nw_rank, 0, 0, H // world)
+        ach = ab / (per[dom] * 1e-3) / 1e9 if ab else None
+        _emit({"metric": "seq.kmer.pos query Mbp/s (config 5, sharded)",
+               "value": round(L / 1e6 * args.steps / t, 2), "unit": "Mbp/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(t / args.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+               "config": {"workload": cfg["workload"], "seq_len": L, "k": k, "rows": H,
+                          "index_broadcast_s": round(t_bcast, 4), "parallelism": f"shard{world}"},
+               "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2) if ach else None,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": None,
+                            "algorithmic_bytes": ab, "avg_ms": round(per[dom], 4)},
+               "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
+    index.free()
 
 
 if __name__ == "__main__":

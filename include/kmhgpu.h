@@ -3,7 +3,7 @@
  *
  * Drop-in boundary for the hot path of lmjakt/kmer_hasheR.  Plain pointers and sizes only; no
  * torch or HIP types in the signatures (streams are passed as `void*` = hipStream_t, NULL = the
- * library's own stream).  Every function returns KMHG_OK (0) or an error code; the message is
+ * HIP null stream; host-pointer entry points run on a library-owned stream and return synced).  Every function returns KMHG_OK (0) or an error code; the message is
  * in kmhg_last_error() (thread-local).  Where the reference raises an R error() the message is
  * the reference's own text.
  *

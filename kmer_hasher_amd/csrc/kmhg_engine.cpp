@@ -512,7 +512,7 @@ int kmhg_build_device(const void* d_seq, size_t L, int k, int do_sort, void* str
   return guarded([&] {
     if (!d_seq || !out) fail(KMHG_EINVAL, "null argument");
     check_build_args(L, k);
-    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     *out = build_device((const uint8_t*)d_seq, (int64_t)L, k, s);
   });
 }
@@ -555,7 +555,7 @@ int kmhg_positions_fill_device(kmhg_index* idx, uint32_t opt, char* d_kmers, int
   return guarded([&] {
     if (!idx) fail(KMHG_EINVAL, "null index");
     DeviceGuard g(idx->device);
-    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     positions_device(idx, opt, d_kmers, d_pos, d_pairs, d_counts, s);
   });
 }
@@ -606,7 +606,7 @@ int kmhg_query_run_device(kmhg_index* idx, const void* d_seq, size_t L, int k, v
     if (!idx || !d_seq || !q) fail(KMHG_EINVAL, "null argument");
     check_query_args(L, k);
     DeviceGuard g(idx->device);
-    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     *q = query_device(idx, (const uint8_t*)d_seq, (int64_t)L, k, 0, (int64_t)L - k + 1, s);
     if (n_rows) *n_rows = (*q)->H;
   });
@@ -621,7 +621,7 @@ int kmhg_query_run_device_range(kmhg_index* idx, const void* d_seq, size_t L, in
     const int64_t Nw = (int64_t)L - k + 1;
     if (w_begin < 0 || w_end > Nw || w_begin > w_end) fail(KMHG_EINVAL, "window range out of bounds");
     DeviceGuard g(idx->device);
-    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     *q = query_device(idx, (const uint8_t*)d_seq, (int64_t)L, k, w_begin, w_end, s);
     if (n_rows) *n_rows = (*q)->H;
   });
@@ -652,7 +652,7 @@ int kmhg_query_copy_device(kmhg_query* q, void* d_dst, void* stream) {
     if (!q->H) return;
     if (!d_dst) fail(KMHG_EINVAL, "null output");
     DeviceGuard g(q->device);
-    hipStream_t s = stream ? (hipStream_t)stream : q->stream;
+    hipStream_t s = (hipStream_t)stream;
     if (s != q->stream) {   // order after the emit kernel queued on q->stream
       hipEvent_t ev;
       HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -692,7 +692,7 @@ int kmhg_image_export(const kmhg_index* idx, void* d_table, void* d_positions, v
   return guarded([&] {
     if (!idx) fail(KMHG_EINVAL, "null index");
     DeviceGuard g(idx->device);
-    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     auto cp = [&](void* dst, const void* src, size_t b) {
       if (dst && b) HIPC(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToDevice, s));
     };
@@ -701,7 +701,7 @@ int kmhg_image_export(const kmhg_index* idx, void* d_table, void* d_positions, v
     cp(d_keys, idx->ukeys.p, idx->U * 8);
     cp(d_counts, idx->counts.p, idx->U * 4);
     cp(d_offsets, idx->offsets.p, (idx->U + 1) * 4);
-    if (!stream) HIPC(hipStreamSynchronize(s));
+    HIPC(hipStreamSynchronize(s));
   });
 }
 
@@ -712,7 +712,7 @@ int kmhg_image_import(const int64_t header[8], const void* d_table, const void* 
     if (!header || !out || header[7] != 0x6B6D6867) fail(KMHG_EINVAL, "bad index image header");
     auto idx = std::make_unique<kmhg_index>();
     HIPC(hipGetDevice(&idx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : lib_stream();
+    hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     idx->k = (int)header[0]; idx->L = header[1]; idx->cap = (uint64_t)header[2];
     idx->U = (uint64_t)header[3]; idx->N = (uint64_t)header[4]; idx->P = (uint64_t)header[5];
     idx->max_n = (uint32_t)header[6];
