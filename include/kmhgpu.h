@@ -113,15 +113,14 @@ int kmhg_query_copy_device(kmhg_query *q, void *d_dst, void *stream);
 int kmhg_query_free(kmhg_query *q);
 
 /* Index replication for the multi-GPU query (the index is broadcast once over RCCL/xGMI by the
- * caller): export the device image into caller buffers, import on another device. */
+ * caller): the device image is the hash table (16-B slots {key, count, end}) + the positions;
+ * export copies it into caller device buffers, import rebuilds an index on the current device. */
 typedef struct {
-  int64_t table_bytes, positions_bytes, keys_bytes, counts_bytes, offsets_bytes;
+  int64_t table_bytes, positions_bytes;
 } kmhg_image_sizes;
 int kmhg_image_sizes_get(const kmhg_index *idx, kmhg_image_sizes *sz, int64_t header[8]);
-int kmhg_image_export(const kmhg_index *idx, void *d_table, void *d_positions, void *d_keys,
-                      void *d_counts, void *d_offsets, void *stream);
+int kmhg_image_export(const kmhg_index *idx, void *d_table, void *d_positions, void *stream);
 int kmhg_image_import(const int64_t header[8], const void *d_table, const void *d_positions,
-                      const void *d_keys, const void *d_counts, const void *d_offsets,
                       void *stream, kmhg_index **out);
 
 /* Per-kernel HIP-event timing (KMHG_TIMING=1 also enables it).  The report is JSON:

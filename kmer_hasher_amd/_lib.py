@@ -29,9 +29,7 @@ class Info(C.Structure):
 
 
 class ImageSizes(C.Structure):
-    _fields_ = [("table_bytes", C.c_int64), ("positions_bytes", C.c_int64),
-                ("keys_bytes", C.c_int64), ("counts_bytes", C.c_int64),
-                ("offsets_bytes", C.c_int64)]
+    _fields_ = [("table_bytes", C.c_int64), ("positions_bytes", C.c_int64)]
 
 
 _LIB = None
@@ -57,8 +55,8 @@ _PROTOS = {
     "kmhg_query_copy_device": (C.c_int, [vp, vp, vp]),
     "kmhg_query_free": (C.c_int, [vp]),
     "kmhg_image_sizes_get": (C.c_int, [vp, C.POINTER(ImageSizes), i64p]),
-    "kmhg_image_export": (C.c_int, [vp, vp, vp, vp, vp, vp, vp]),
-    "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, vp, vp, vp, C.POINTER(vp)]),
+    "kmhg_image_export": (C.c_int, [vp, vp, vp, vp]),
+    "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, C.POINTER(vp)]),
     "kmhg_timing_enable": (C.c_int, [C.c_int]),
     "kmhg_timing_reset": (C.c_int, []),
     "kmhg_timing_report": (C.c_int, [C.c_char_p, C.c_size_t]),

@@ -1,0 +1,499 @@
+// kmhg_build_v2.hip -- partitioned index build: no per-window global atomics.
+//
+// Replaces the same reference loops as K_insert/K_scatter/K_sort (src/kmer_pos.c:36-50, 66-98,
+// 21-33; kvec growth src/kvec.h:74-80) with an HBM-streaming design for CDNA4:
+//
+//   V_encode    LDS-staged 2-bit encode + N mask of every window (as K_insert) -> (key, pos)
+//               per window, plus a per-tile histogram of the first radix digit of its bucket
+//   V_scan      exclusive scan of the digit histograms (decoupled look-back)
+//   V_scatter   stable radix pass: every wave ranks its 512 elements by digit with ballots
+//               (no atomics), elements land at histogram offsets -- LSD over 1-3 digits sorts
+//               the windows by bucket while keeping position order inside a bucket
+//   V_hist      digit histogram for the next radix pass
+//   V_bounds    bucket start offsets in the bucket-sorted stream
+//   V_bucket    ONE WAVE PER BUCKET: the bucket's keys go into a wave-private LDS hash table
+//               (LDS CAS + LDS atomics), counts are scanned in LDS, and a second in-order pass
+//               ranks equal keys with ballots, so positions are written ascending per key by
+//               construction (no sort).  The LDS table is written out as the bucket's
+//               sub-table of the global table; CSR arrays get dense ids from a look-back over
+//               buckets.
+//
+// A bucket's windows are exactly its keys' positions, so the CSR slice of bucket b is
+// [start[b], start[b+1]) of `positions` with no global coordination.
+#include <hip/hip_runtime.h>
+#include "kmhg_common.h"
+#include "kmhg_device.h"
+#include "kmhg_kernels.h"
+
+namespace kmhg {
+
+// Diagnostic phase stamps (built only with -DKMHG_STAMPS into a separate library; the real
+// kernels execute no stamp).  Lane 0 of each bucket's wave writes s_memtime per phase.
+#ifdef KMHG_STAMPS
+__device__ uint64_t* g_stamps;
+#define STAMP(b, i)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    uint64_t _t = __builtin_amdgcn_s_memtime();                                       \
+    if (lane_id() == 0 && g_stamps) g_stamps[(uint64_t)(b) * 8 + (i)] = _t;           \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+  } while (0)
+#else
+#define STAMP(b, i) do {} while (0)
+#endif
+
+// LDS sub-table of one bucket, private to one wave (slot V2_CAPB = side slot of key ~0).
+// 16-B AoS slots: one ds_read_b128 / ds_write_b128 per slot for init and write-out.
+struct LSlot {
+  uint64_t key;
+  uint32_t cnt;   // occurrences
+  uint32_t cur;   // CSR offset, then the running cursor of pass B
+};
+struct WaveTable {
+  LSlot s[V2_CAPB + 1];
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Radix digit of a key's bucket: floor(b / div) mod R with host-computed magic multipliers,
+// floor(x / d) = mulhi64(x, ceil(2^64 / d)) exactly for x, d < 2^32 (m = 0 encodes d = 1) --
+// no integer division in the kernels.
+__device__ __forceinline__ uint32_t div_magic(uint32_t x, uint64_t m) {
+  return m ? (uint32_t)__umul64hi((uint64_t)x, m) : x;
+}
+__device__ __forceinline__ uint32_t digit_of(uint64_t key, uint32_t nb, const Digit& D) {
+  const uint32_t q = div_magic(bucket_of(mix64(key), nb), D.mdiv);
+  return q - div_magic(q, D.mR) * D.R;
+}
+
+// Lanes of the wave holding the same `v` (nbits wide) among active lanes: one ballot per bit.
+__device__ __forceinline__ uint64_t match_bits(uint32_t v, int nbits, bool act) {
+  uint64_t m = __ballot(act);
+  for (int b = 0; b < nbits; ++b) {
+    const bool bit = (v >> b) & 1u;
+    const uint64_t x = __ballot(act && bit);
+    m &= bit ? x : ~x;
+  }
+  return m;
+}
+
+// ---------------------------------------------------------------- V_encode
+__global__ void __launch_bounds__(BLOCK)
+k_v2_encode(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned, Geom g,
+            Digit D, uint64_t* __restrict__ keys, uint32_t* __restrict__ pos,
+            uint32_t* __restrict__ hist, uint32_t ntiles) {
+  __shared__ Stage st;
+  __shared__ uint32_t lh[V2_MAXR];
+  const int64_t tile0 = (int64_t)blockIdx.x * TILE;
+  const uint32_t R0 = D.R;
+  for (uint32_t d = threadIdx.x; d < R0; d += BLOCK) lh[d] = 0;
+  stage_tile(seq, L, tile0 - HALO, st, aligned != 0);
+  __syncthreads();
+#pragma unroll 2
+  for (int j = 0; j < WPT; ++j) {
+    const int w = j * BLOCK + threadIdx.x;
+    const int64_t s = tile0 + w;
+    if (s >= Nw) continue;
+    uint64_t key = 0;
+    const bool valid = window_key(st, HALO + w, s, L, k, key);
+    keys[s] = key;
+    pos[s] = valid ? (uint32_t)(s + 1) : 0u;
+    if (valid) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < R0; d += BLOCK) hist[(size_t)d * ntiles + blockIdx.x] = lh[d];
+}
+
+// ---------------------------------------------------------------- V_scan (u32, exclusive)
+// Reduce-then-scan (no tickets, no spinning): per-tile sums -> one-workgroup scan of the tile
+// sums (k_scan_tiles_u64) -> per-tile exclusive scan seeded with the tile's base.
+__global__ void __launch_bounds__(BLOCK)
+k_tile_sum_u32(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ tsum) {
+  __shared__ uint64_t sh[8];
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  uint64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    if (i < n) sum += a[i];
+  }
+  uint64_t tot;
+  block_excl_scan(sum, sh, tot);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict__ tbase) {
+  __shared__ uint64_t sh[8];
+  const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)threadIdx.x * WPT;
+  uint32_t v[WPT];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    v[j] = (base + j < n) ? a[base + j] : 0u;
+    sum += v[j];
+  }
+  uint64_t tot;
+  uint64_t run = block_excl_scan(sum, sh, tot) + tbase[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (base + j < n) a[base + j] = (uint32_t)run;
+    run += v[j];
+  }
+}
+
+__global__ void k_copy_total(const uint64_t* __restrict__ t, uint32_t* __restrict__ out) {
+  if (threadIdx.x == 0) *out = (uint32_t)*t;
+}
+
+// ---------------------------------------------------------------- V_hist (passes >= 1)
+__global__ void __launch_bounds__(BLOCK)
+k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
+          Digit D, uint32_t* __restrict__ hist, uint32_t ntiles) {
+  __shared__ uint32_t lh[V2_MAXR];
+  const uint64_t n = *n_ptr;
+  const uint32_t R = D.R;
+  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    uint64_t e = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    if (e < n) atomicAdd(&lh[digit_of(keys[e], g.nb, D)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[(size_t)d * ntiles + blockIdx.x] = lh[d];
+}
+
+// ---------------------------------------------------------------- V_scatter (stable)
+// Tile t = elements [t*TILE, (t+1)*TILE); wave w owns the contiguous 512 elements
+// [t*TILE + 512w, +512), lane l holds element 64c + l of them for c = 0..7 (coalesced loads).
+// Element order inside the tile = (wave, c, lane) = input order, so ranks assigned in that
+// order keep the pass stable.  pass 0 reads every window and drops invalid ones (pos == 0).
+__global__ void __launch_bounds__(BLOCK)
+k_v2_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
+             const uint32_t* __restrict__ n_ptr, uint64_t n_all, Geom g, Digit D,
+             const uint32_t* __restrict__ hist, uint32_t ntiles,
+             uint64_t* __restrict__ kout, uint32_t* __restrict__ pout) {
+  __shared__ uint32_t wc[4][V2_MAXR];
+  const uint32_t R = D.R;
+  const int nbits = D.nbits;
+  constexpr int PER = TILE / 4 / 64;     // 8 elements per lane
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const uint64_t n = n_ptr ? (uint64_t)*n_ptr : n_all;
+  const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)wave * (TILE / 4);
+  uint64_t key[PER];
+  uint32_t ps[PER], dg[PER];
+  bool act[PER];
+#pragma unroll
+  for (int c = 0; c < PER; ++c) {
+    const uint64_t e = base + (uint64_t)c * 64 + lane;
+    act[c] = e < n;
+    key[c] = act[c] ? kin[e] : 0;
+    ps[c] = act[c] ? pin[e] : 0;
+    act[c] = act[c] && ps[c] != 0;
+    dg[c] = act[c] ? digit_of(key[c], g.nb, D) : 0;
+  }
+  for (uint32_t d = lane; d < R; d += 64) wc[wave][d] = 0;
+  wave_sync();
+#pragma unroll
+  for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
+    if (act[c]) atomicAdd(&wc[wave][dg[c]], 1u);
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
+    uint32_t b = hist[(size_t)d * ntiles + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      uint32_t t = wc[w][d];
+      wc[w][d] = b;
+      b += t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
+    const uint64_t grp = match_bits(dg[c], nbits, act[c]);
+    const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
+    uint32_t cur = 0;
+    if (act[c] && leader == lane) {
+      cur = wc[wave][dg[c]];
+      wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
+    }
+    cur = __shfl(cur, leader);
+    wave_sync();
+    if (act[c]) {
+      const uint32_t dst = cur + (uint32_t)__popcll(grp & lanemask_lt());
+      kout[dst] = key[c];
+      pout[dst] = ps[c];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- V_bounds
+__global__ void __launch_bounds__(BLOCK)
+k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
+            uint32_t* __restrict__ start) {
+  const uint64_t n = *n_ptr;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  if (n == 0) {
+    for (uint64_t b = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; b <= g.nb; b += stride) start[b] = 0;
+    return;
+  }
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    const uint32_t b = bucket_of(mix64(keys[i]), g.nb);
+    const int64_t bp = i ? (int64_t)bucket_of(mix64(keys[i - 1]), g.nb) : -1;
+    for (int64_t x = bp + 1; x <= (int64_t)b; ++x) start[x] = (uint32_t)i;
+    if (i == n - 1)
+      for (uint64_t x = (uint64_t)b + 1; x <= g.nb; ++x) start[x] = (uint32_t)n;
+  }
+}
+
+// ---------------------------------------------------------------- V_bucket (wave per bucket)
+// One LDS round trip per probe: the CAS itself says whether the slot was free (inserted), held
+// this key (found) or another key (move on).
+__device__ __forceinline__ int lds_insert(WaveTable& W, uint64_t key) {
+  if (key == EMPTY_KEY) return (int)V2_CAPB;
+  uint32_t j = local_home(mix64(key), V2_CAPB);
+  for (uint32_t n = 0; n < V2_CAPB; ++n) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&W.s[j].key,
+                                    (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+    if (prev == EMPTY_KEY || prev == key) return (int)j;
+    if (++j == V2_CAPB) j = 0;
+  }
+  return -1;   // sub-table full: the host falls back to the global-atomic build
+}
+
+__device__ __forceinline__ int lds_find(const WaveTable& W, uint64_t key) {
+  if (key == EMPTY_KEY) return (int)V2_CAPB;
+  uint32_t j = local_home(mix64(key), V2_CAPB);
+  for (uint32_t n = 0; n < V2_CAPB; ++n) {
+    uint64_t cur = W.s[j].key;
+    if (cur == key) return (int)j;
+    if (++j == V2_CAPB) j = 0;
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
+            const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
+            int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
+            BuildMeta* __restrict__ meta) {
+  __shared__ WaveTable wt[4];
+  constexpr int PER = 2 * V2_BW / 64;             // elements per lane per batch (2x mean)
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  WaveTable& W = wt[wave];
+  // buckets are independent: no ordering, no ticket (one shared counter would serialise
+  // ~88 grabs/us chip-wide -- MI355X_MICROARCH.md "dequeue")
+  const uint32_t b = blockIdx.x * 4 + wave;
+  if (b >= g.nb) return;
+  STAMP(b, 0);
+  for (uint32_t j = lane; j <= V2_CAPB; j += 64)
+    *reinterpret_cast<uint4*>(&W.s[j]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+  const uint32_t s0 = start[b], s1 = start[b + 1];
+  const bool one_batch = s1 - s0 <= 64 * PER;     // typical bucket: everything stays in VGPRs
+  uint64_t key[PER];
+  uint32_t ps[PER];
+  int slot[PER];
+  wave_sync();
+  // pass A: distinct keys + counts (all loads of a batch issued before the first LDS probe)
+  bool ovf = false;
+  STAMP(b, 1);
+  for (uint32_t i0 = s0; i0 < s1; i0 += 64 * PER) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t i = i0 + 64 * c + lane;
+      key[c] = i < s1 ? keys[i] : 0;
+      ps[c] = i < s1 ? pos[i] : 0;
+    }
+#ifdef KMHG_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    STAMP(b, 2);
+#endif
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t i = i0 + 64 * c + lane;
+      slot[c] = -1;
+      if (i < s1) {
+        slot[c] = lds_insert(W, key[c]);
+        if (slot[c] < 0) ovf = true;
+        else atomicAdd(&W.s[slot[c]].cnt, 1u);
+      }
+    }
+  }
+  wave_sync();
+  STAMP(b, 3);
+  if (__ballot(ovf)) {
+    if (lane == 0) atomicOr(&meta->overflow, 1u);
+    return;
+  }
+  // exclusive scan of the counts over the bucket's slots; lane owns SPL contiguous slots
+  constexpr uint32_t SPL = (V2_CAPB + 1 + 63) / 64;
+  const uint32_t j0 = lane * SPL;
+  const uint32_t j1 = min(j0 + SPL, V2_CAPB + 1);
+  uint32_t cs = 0, occ = 0, mx = 0;
+  uint64_t pairs = 0;
+  for (uint32_t j = j0; j < j1; ++j) {
+    const uint32_t c = W.s[j].cnt;
+    cs += c;
+    occ += c ? 1u : 0u;
+    mx = max(mx, c);
+    pairs += (uint64_t)c * (c - (c ? 1u : 0u)) / 2;
+  }
+  const uint64_t incl = wave_incl_scan(cs);
+  uint32_t off_run = s0 + (uint32_t)(incl - cs);
+  for (uint32_t j = j0; j < j1; ++j) {
+    W.s[j].cur = off_run;
+    off_run += W.s[j].cnt;
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    pairs += __shfl_xor(pairs, d);
+    occ += __shfl_xor(occ, d);
+    mx = max(mx, (uint32_t)__shfl_xor(mx, d));
+  }
+  if (lane == 0) {
+    BucketStats st;
+    st.n_kmers = occ;
+    st.max_count = mx;
+    st.n_pairs = pairs;
+    bstats[b] = st;
+  }
+  wave_sync();
+  STAMP(b, 4);
+  // the bucket's sub-table, coalesced 16-B slots (empty ones included: no table init needed)
+  Slot* Tb = T + (uint64_t)b * V2_CAPB;
+  for (uint32_t j = lane; j < V2_CAPB; j += 64) {
+    uint4 x = *reinterpret_cast<const uint4*>(&W.s[j]);
+    x.w += x.z;                                   // end = offset + count
+    *reinterpret_cast<uint4*>(&Tb[j]) = x;
+  }
+  if (lane == 0 && b == bucket_of(mix64(EMPTY_KEY), g.nb)) {
+    uint4 x = *reinterpret_cast<const uint4*>(&W.s[V2_CAPB]);
+    *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, x.z, x.w + x.z);
+  }
+  STAMP(b, 5);
+  // pass B: positions in stream (= position) order.  Keys seen once in the bucket take their
+  // offset directly; repeated keys are ranked by ballots in lane (= position) order.
+  for (uint32_t i0 = s0; i0 < s1; i0 += 64 * PER) {
+    if (!one_batch) {
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        const uint32_t i = i0 + 64 * c + lane;
+        key[c] = i < s1 ? keys[i] : 0;
+        ps[c] = i < s1 ? pos[i] : 0;
+      }
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        const uint32_t i = i0 + 64 * c + lane;
+        slot[c] = i < s1 ? lds_find(W, key[c]) : -1;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t i = i0 + 64 * c + lane;
+      const bool act = i < s1;
+      uint2 cc = make_uint2(0u, 0u);                // {cnt, cur}
+      if (act) cc = *reinterpret_cast<const uint2*>(&W.s[slot[c]].cnt);
+      const bool multi = act && cc.x > 1;
+      if (act && !multi) positions[cc.y] = (int32_t)ps[c];
+      if (__ballot(multi)) {
+        const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS, multi);
+        const int leader = multi ? __ffsll((unsigned long long)m) - 1 : lane;
+        uint32_t cur = cc.y;
+        if (multi && leader == lane) W.s[slot[c]].cur = cur + (uint32_t)__popcll(m);
+        cur = __shfl(cur, leader);
+        wave_sync();
+        if (multi) positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
+      }
+    }
+  }
+  STAMP(b, 6);
+}
+
+// V_stats: reduce the per-bucket partials (one workgroup).
+__global__ void __launch_bounds__(1024)
+k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __restrict__ n_valid,
+           BuildMeta* __restrict__ meta) {
+  __shared__ uint64_t su[16], sp[16];
+  __shared__ uint32_t sm[16];
+  uint64_t u = 0, p = 0;
+  uint32_t m = 0;
+  for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
+    const BucketStats x = bs[b];
+    u += x.n_kmers;
+    p += x.n_pairs;
+    m = max(m, x.max_count);
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    u += __shfl_xor(u, d);
+    p += __shfl_xor(p, d);
+    m = max(m, (uint32_t)__shfl_xor(m, d));
+  }
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) { su[w] = u; sp[w] = p; sm[w] = m; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u = su[0]; p = sp[0]; m = sm[0];
+    for (int i = 1; i < 16; ++i) { u += su[i]; p += sp[i]; m = max(m, sm[i]); }
+    meta->n_kmers = u;
+    meta->n_pairs = p;
+    meta->max_count = m;
+    meta->n_positions = *n_valid;
+  }
+}
+
+#ifdef KMHG_STAMPS
+void set_stamp_buffer(uint64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
+#endif
+
+// ---------------------------------------------------------------- launchers
+static inline unsigned grid_of(uint64_t n, unsigned per) {
+  uint64_t g = (n + per - 1) / per;
+  return (unsigned)(g ? g : 1);
+}
+
+void launch_v2_encode(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
+                      Digit D, uint64_t* keys, uint32_t* pos, uint32_t* hist,
+                      uint32_t ntiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_encode, dim3(ntiles), dim3(BLOCK), 0, s, seq, L, k, Nw,
+                     aligned ? 1 : 0, g, D, keys, pos, hist, ntiles);
+}
+void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, hipStream_t s) {
+  const uint32_t nt = grid_of(n, TILE);
+  hipLaunchKernelGGL(k_tile_sum_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, tsum);
+  launch_scan_tiles_u64(tsum, nt, tsum + nt, s);
+  hipLaunchKernelGGL(k_tile_scan_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, tsum);
+  hipLaunchKernelGGL(k_copy_total, dim3(1), dim3(64), 0, s, tsum + nt, total);
+}
+void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
+                    uint32_t ntiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_hist, dim3(ntiles), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist, ntiles);
+}
+void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr,
+                       uint64_t n_all, Geom g, Digit D, const uint32_t* hist, uint32_t ntiles,
+                       uint64_t* kout, uint32_t* pout, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_scatter, dim3(ntiles), dim3(BLOCK), 0, s, kin, pin, n_ptr, n_all, g, D,
+                     hist, ntiles, kout, pout);
+}
+void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
+                      uint64_t n_max, hipStream_t s) {
+  unsigned gr = grid_of(n_max > g.nb ? n_max : g.nb, BLOCK);
+  if (gr > 16384) gr = 16384;
+  hipLaunchKernelGGL(k_v2_bounds, dim3(gr), dim3(BLOCK), 0, s, keys, n_ptr, g, start);
+}
+void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
+                      Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_bucket, dim3(grid_of(g.nb, 4)), dim3(BLOCK), 0, s, keys, pos, start, g,
+                     T, positions, bstats, meta);
+}
+void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
+                     BuildMeta* meta, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_stats, dim3(1), dim3(1024), 0, s, bstats, nb, n_valid, meta);
+}
+
+}  // namespace kmhg

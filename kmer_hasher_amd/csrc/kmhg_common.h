@@ -24,6 +24,12 @@ struct alignas(16) Slot {
   uint32_t end;    // after the build: one past the key's last position in `positions`
 };
 
+// Table geometry: nb buckets x capb slots, plus one side slot at index nb*capb (kmhg_device.h).
+struct Geom {
+  uint32_t nb;
+  uint32_t capb;
+};
+
 // Build-time tile geometry: one workgroup = 256 lanes x WPT windows, staged through LDS.
 constexpr int BLOCK = 256;
 constexpr int WPT = 8;

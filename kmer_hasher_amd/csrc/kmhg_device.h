@@ -1,0 +1,255 @@
+// kmhg_device.h -- device helpers shared by the kernel translation units (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "kmhg_common.h"
+
+namespace kmhg {
+
+// ------------------------------------------------------------------ small wave/block helpers
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Inclusive wave scan (64 lanes).
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint64_t t = __shfl_up(v, d);
+    if (lane_id() >= d) v += t;
+  }
+  return v;
+}
+
+// Exclusive scan over the 256 threads of a block (one value per thread).  `lds` needs 5 u64.
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* lds, uint64_t& total) {
+  const int wid = threadIdx.x >> 6;
+  uint64_t inc = wave_incl_scan(v);
+  if (lane_id() == 63) lds[wid] = inc;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / 64; ++w) {
+    uint64_t x = lds[w];
+    if (w < wid) off += x;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return off + inc - v;
+}
+
+// ------------------------------------------------------------------ decoupled look-back
+// status word: [63:62] = 0 not ready / 1 aggregate / 2 inclusive prefix, [61:0] payload.
+// Each word is a self-describing 8-B granule written by ONE relaxed agent-scope store and read
+// by relaxed agent-scope loads (sc1), so no separate flag, fence or payload hand-off exists.
+// Tiles come from a ticket counter so every tile a block waits on is already running.
+constexpr uint64_t LB_MASK = (1ull << 62) - 1;
+
+// Wave-parallel look-back: called by ALL 64 lanes of one wave (same tile/agg in every lane).
+// Each round the 64 lanes read the 64 nearest predecessors at once; the window is consumed up
+// to (and including) the nearest inclusive prefix once every word in front of it is ready.
+// With `prepublished`, the caller already stored the aggregate (lookback_publish) earlier, so
+// successors could start summing it while this wave did other work.
+__device__ inline void lookback_publish(uint64_t* status, uint32_t tile, uint64_t agg) {
+  if (lane_id() == 0) st_relaxed(&status[tile], ((tile == 0 ? 2ull : 1ull) << 62) | agg);
+}
+
+__device__ inline uint64_t lookback_excl(uint64_t* status, uint32_t tile, uint64_t agg,
+                                         bool prepublished = false) {
+  const int lane = lane_id();
+  if (tile == 0) {
+    if (lane == 0 && !prepublished) st_relaxed(&status[0], (2ull << 62) | agg);
+    return 0;
+  }
+  if (lane == 0 && !prepublished) st_relaxed(&status[tile], (1ull << 62) | agg);
+  uint64_t excl = 0;
+  int64_t base = (int64_t)tile - 1;
+  for (;;) {
+    int64_t j = base - lane;
+    uint64_t w = (j >= 0) ? ld_relaxed(&status[j]) : (2ull << 62);   // before tile 0: prefix 0
+    uint64_t f = w >> 62;
+    uint64_t m0 = __ballot(f == 0), m2 = __ballot(f == 2);
+    int first2 = m2 ? __ffsll((unsigned long long)m2) - 1 : 64;
+    uint64_t need = first2 == 64 ? ~0ull : ((2ull << first2) - 1ull);   // lanes 0..first2
+    if (m0 & need) { __builtin_amdgcn_s_sleep(1); continue; }
+    uint64_t v = (lane <= first2) ? (w & LB_MASK) : 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    excl += v;
+    if (first2 < 64) break;
+    base -= 64;
+  }
+  if (lane == 0) st_relaxed(&status[tile], (2ull << 62) | (excl + agg));
+  return excl;
+}
+
+// Grab a tile ticket (thread 0) and broadcast it.
+__device__ __forceinline__ uint32_t take_ticket(uint32_t* counter, uint32_t* lds) {
+  if (threadIdx.x == 0) *lds = atomicAdd(counter, 1u);
+  __syncthreads();
+  uint32_t t = *lds;
+  __syncthreads();
+  return t;
+}
+
+// ------------------------------------------------------------------ LDS staging of a tile
+// Chars [base, base + STAGE) are loaded coalesced (16 B per lane when the sequence is 16-B
+// aligned) and packed into 2-bit codes (MSB-first, 16 chars per u32) and N flags (16 chars per
+// u16 kept in a u32).  Chars outside [0, L) are flagged N: a window that touches them is never
+// valid, and position -1 acting as N gives the reference's "start of sequence" rule.
+struct Stage {
+  uint32_t code[STAGE_W16];
+  uint32_t nbit[STAGE_W16];
+};
+
+__device__ __forceinline__ void pack16(const uint8_t* c, uint32_t& code, uint32_t& nb) {
+  uint32_t cd = 0, n = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    uint32_t ch = c[i];
+    cd = (cd << 2) | ((ch >> 1) & 3u);       // UPDATE_OFFSET, src/kmer_util.h:8
+    n = (n << 1) | (((ch | 0x20u) == 'n') ? 1u : 0u);   // LC(c)=='n', src/kmer_util.h:10
+  }
+  code = cd; nb = n;
+}
+
+__device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ seq, int64_t L,
+                                           int64_t base, Stage& st, bool aligned) {
+  for (int w = threadIdx.x; w < STAGE_W16; w += BLOCK) {
+    int64_t c0 = base + 16 * (int64_t)w;
+    uint8_t buf[16];
+    if (aligned && c0 >= 0 && c0 + 16 <= L) {
+      uint4 v = *reinterpret_cast<const uint4*>(seq + c0);
+      *reinterpret_cast<uint4*>(buf) = v;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        int64_t p = c0 + i;
+        buf[i] = (p >= 0 && p < L) ? seq[p] : (uint8_t)'N';
+      }
+    }
+    uint32_t cd, nb;
+    pack16(buf, cd, nb);
+    st.code[w] = cd;
+    st.nbit[w] = nb;
+  }
+}
+
+// Window whose first char is stage offset o (global start s).  Returns validity per the
+// reference walk: no N in [s, s+k), s+k <= L, and NOT (s+k == L and the char
+// before s is N or s == 0) -- the end-drop quirk of init_kmer (src/kmer_pos.c:81-83).
+__device__ __forceinline__ bool window_key(const Stage& st, int o, int64_t s, int64_t L, int k,
+                                           uint64_t& key) {
+  if (s + k > L) return false;
+  // N flags of chars [o-1, o+k): k+1 <= 33 bits out of a 48-bit window of three u16 words
+  int p = o - 1;
+  int q = p >> 4, c = p & 15;
+  uint64_t x48 = ((uint64_t)st.nbit[q] << 32) | ((uint64_t)st.nbit[q + 1] << 16) |
+                 (uint64_t)st.nbit[q + 2];
+  uint64_t m = (x48 << (16 + c)) >> (63 - k);          // top k+1 bits
+  uint64_t winN = m & ((2ull << (k - 1)) - 1ull);      // low k bits (k <= 32)
+  if (winN) return false;
+  if (s + k == L && ((m >> k) & 1ull)) return false;
+  // 2k code bits of chars [o, o+k)
+  int qw = o >> 4, b = (o & 15) * 2;
+  uint64_t x = ((uint64_t)st.code[qw] << 32) | st.code[qw + 1];
+  uint64_t y = st.code[qw + 2];
+  uint64_t t = (x << b) | ((y << b) >> 32);
+  key = t >> (64 - 2 * k);
+  return true;
+}
+
+// ------------------------------------------------------------------ hash table primitives
+// Table geometry: nb buckets of capb slots (+ one side slot at nb*capb).  A key's bucket is
+// mulhi(h, nb) (high hash bits), its home inside the bucket mulhi32(lo32(h), capb), and linear
+// probing wraps inside the bucket -- so a bucket is a self-contained sub-table that one wave
+// can build in LDS (partitioned build) and a probe never leaves it.  nb = 1 is a plain
+// linear-probing table (the global-atomic build).
+__device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t nb) {
+  return (uint32_t)__umul64hi(h, (uint64_t)nb);
+}
+__device__ __forceinline__ uint32_t local_home(uint64_t h, uint32_t capb) {
+  return (uint32_t)(((uint64_t)(uint32_t)h * capb) >> 32);
+}
+__device__ __forceinline__ uint64_t side_slot(Geom g) { return (uint64_t)g.nb * g.capb; }
+
+// Find-or-insert (atomicCAS on the 64-bit key word).  Keys only move EMPTY -> key, so a stale
+// plain read can only show EMPTY, which the CAS then corrects.
+__device__ __forceinline__ uint32_t table_insert(Slot* __restrict__ T, Geom g, uint64_t key) {
+  if (key == EMPTY_KEY) return (uint32_t)side_slot(g);   // side slot (k = 32, all G)
+  const uint64_t h = mix64(key);
+  const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
+  uint32_t j = local_home(h, g.capb);
+  for (;;) {
+    const uint64_t i = b0 + j;
+    uint64_t cur = T[i].key;
+    if (cur == key) return (uint32_t)i;
+    if (cur == EMPTY_KEY) {
+      uint64_t prev = atomicCAS((unsigned long long*)&T[i].key, (unsigned long long)EMPTY_KEY,
+                                (unsigned long long)key);
+      if (prev == EMPTY_KEY || prev == key) return (uint32_t)i;
+    }
+    if (++j == g.capb) j = 0;
+  }
+}
+
+// Read-only probe: returns the slot or NONE; count/end from the same 16-B slot load.
+__device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom g, uint64_t key,
+                                               uint32_t& count, uint32_t& end) {
+  if (key == EMPTY_KEY) {
+    const uint64_t i = side_slot(g);
+    uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+    count = v.z; end = v.w;
+    return count ? (uint32_t)i : NONE;
+  }
+  const uint64_t h = mix64(key);
+  const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
+  uint32_t j = local_home(h, g.capb);
+  for (;;) {
+    const uint64_t i = b0 + j;
+    uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+    uint64_t cur = ((uint64_t)v.y << 32) | v.x;
+    if (cur == key) { count = v.z; end = v.w; return (uint32_t)i; }
+    if (cur == EMPTY_KEY) { count = 0; end = 0; return NONE; }
+    if (++j == g.capb) j = 0;
+  }
+}
+
+// Wave-aggregated atomicAdd on a per-slot u32 counter.  Lanes that hold the same slot are
+// grouped behind the first active lane (readfirstlane + ballot); one atomic per group.  The
+// loop stops as soon as a group of one appears (i.i.d. data: one iteration), leaving the rest
+// to plain per-lane atomics; periodic (tandem-repeat) waves collapse to one atomic per key.
+// Returns the old value + this lane's rank inside its group (ranks follow lane order).
+__device__ __forceinline__ uint32_t wave_agg_add(uint32_t* base_ptr_of_slot0, bool act,
+                                                 uint32_t slot, size_t stride_u32) {
+  uint64_t active = __ballot(act);
+  uint32_t result = 0;
+  bool done = false;
+  while (active) {
+    int leader = __ffsll((unsigned long long)active) - 1;
+    uint32_t lslot = __shfl(slot, leader);
+    uint64_t grp = __ballot(act && !done && slot == lslot) & active;
+    int gsz = __popcll(grp);
+    if (gsz == 1) break;
+    uint32_t old = 0;
+    if (lane_id() == leader)
+      old = atomicAdd(base_ptr_of_slot0 + (size_t)lslot * stride_u32, (uint32_t)gsz);
+    old = __shfl(old, leader);
+    if ((grp >> lane_id()) & 1ull) {
+      result = old + (uint32_t)__popcll(grp & lanemask_lt());
+      done = true;
+    }
+    active &= ~grp;
+  }
+  if (act && !done) result = atomicAdd(base_ptr_of_slot0 + (size_t)slot * stride_u32, 1u);
+  return result;
+}
+
+
+}  // namespace kmhg

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -292,12 +293,11 @@ struct kmhg_index {
   int k = 0;
   int device = 0;
   int64_t L = 0;
-  uint64_t cap = 0;
+  Geom geom{1, 1};             // nb buckets x capb slots (+1 side slot)
   uint64_t U = 0, N = 0, P = 0;
+  uint64_t slots() const { return (uint64_t)geom.nb * geom.capb + 1; }
   uint32_t max_n = 0;
   DBuf<Slot> table;
-  DBuf<uint64_t> ukeys;
-  DBuf<uint32_t> counts, offsets;
   DBuf<int32_t> positions;
   Canon canon;
 };
@@ -341,20 +341,20 @@ void check_query_args(size_t L, int k) {
 }
 
 // ---------------------------------------------------------------------------- build
-kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
+kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
   auto idx = std::make_unique<kmhg_index>();
   HIPC(hipGetDevice(&idx->device));
   idx->k = k;
   idx->L = L;
   const int64_t Nw = L - k + 1;
   const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
-  idx->cap = table_capacity(Nw);
-  const uint64_t nslots = idx->cap + 1;
+  idx->geom = Geom{1u, (uint32_t)table_capacity(Nw)};
+  const uint64_t nslots = idx->slots();
   idx->table.reset(nslots);
   DBuf<uint32_t> win_slot(Nw, s);
   LAUNCH("k_table_init", s, launch_table_init(idx->table.p, nslots, s));
   LAUNCH("k_build_insert", s,
-         launch_build_insert(d_seq, L, k, idx->table.p, idx->cap, win_slot.p, Nw, aligned, s));
+         launch_build_insert(d_seq, L, k, idx->table.p, idx->geom, win_slot.p, Nw, aligned, s));
   // compaction scratch: look-back status + ticket + meta in one zeroed block
   const uint32_t nt = tiles_for(nslots);
   const size_t scratch_bytes = (size_t)nt * 8 + 64 + sizeof(BuildMeta);
@@ -363,20 +363,19 @@ kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) 
   uint64_t* status = reinterpret_cast<uint64_t*>(scratch.p);
   uint32_t* ticket = reinterpret_cast<uint32_t*>(scratch.p + (size_t)nt * 8);
   BuildMeta* meta = reinterpret_cast<BuildMeta*>(scratch.p + (size_t)nt * 8 + 64);
-  idx->ukeys.reset(Nw);
-  idx->counts.reset(Nw);
-  idx->offsets.reset(Nw + 1);
+  DBuf<uint64_t> ukeys(Nw, s);            // dense CSR arrays: sort bookkeeping only
+  DBuf<uint32_t> counts(Nw, s), offsets(Nw + 1, s);
   DBuf<uint32_t> small_ids(Nw / 2 + 1, s), large_ids(Nw / LARGE_MIN + 1, s);
   LAUNCH("k_build_compact", s,
-         launch_build_compact(idx->table.p, nslots, status, ticket, idx->ukeys.p, idx->counts.p,
-                              idx->offsets.p, small_ids.p, large_ids.p, meta, s));
+         launch_build_compact(idx->table.p, nslots, status, ticket, ukeys.p, counts.p,
+                              offsets.p, small_ids.p, large_ids.p, meta, s));
   idx->positions.reset(Nw);
   LAUNCH("k_build_scatter", s, launch_build_scatter(win_slot.p, Nw, idx->table.p,
                                                     idx->positions.p, s));
-  LAUNCH("k_sort_small", s, launch_sort_small(small_ids.p, meta, idx->counts.p, idx->offsets.p,
+  LAUNCH("k_sort_small", s, launch_sort_small(small_ids.p, meta, counts.p, offsets.p,
                                               idx->positions.p, s));
   LAUNCH("k_sort_large", s,
-         launch_sort_large(large_ids.p, meta, idx->counts.p, idx->offsets.p, idx->positions.p,
+         launch_sort_large(large_ids.p, meta, counts.p, offsets.p, idx->positions.p,
                            reinterpret_cast<int32_t*>(win_slot.p), s));
   BuildMeta hm;
   HIPC(hipMemcpyAsync(&hm, meta, sizeof(hm), hipMemcpyDeviceToHost, s));
@@ -386,6 +385,109 @@ kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) 
   idx->P = hm.n_pairs;
   idx->max_n = hm.max_count;
   return idx.release();
+}
+
+// Partitioned build (kmhg_build_v2.hip): LSD radix partition of the windows by hash bucket,
+// then one wave per bucket builds its sub-table in LDS.  Falls back to v1 if a bucket's LDS
+// sub-table overflows (never observed: distinct keys per bucket ~ Binomial, mean <= V2_BW).
+kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
+  auto idx = std::make_unique<kmhg_index>();
+  HIPC(hipGetDevice(&idx->device));
+  idx->k = k;
+  idx->L = L;
+  const int64_t Nw = L - k + 1;
+  const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
+  const uint32_t nb = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW - 1) / V2_BW);
+  idx->geom = Geom{nb, V2_CAPB};
+  const Geom g = idx->geom;
+  const uint32_t ntiles = tiles_for(Nw);
+  // radix plan: fewest passes whose radix fits LDS and whose histograms stay small
+  uint32_t passes = 1, R = nb;
+  for (passes = 1; passes <= 4; ++passes) {
+    R = (uint32_t)std::ceil(std::pow((double)nb, 1.0 / passes) - 1e-9);
+    while (std::pow((double)R, (double)passes) < (double)nb) ++R;
+    if (R <= V2_MAXR && (uint64_t)R * ntiles <= (64ull << 20)) break;
+  }
+  if (passes > 4) fail(KMHG_EOVERFLOW, "sequence too long for the partitioned build");
+  const uint64_t nhist = (uint64_t)R * ntiles;
+  const uint32_t scan_tiles = tiles_for(nhist);
+  DBuf<uint64_t> kA(Nw, s), kB(Nw, s);
+  DBuf<uint32_t> pA(Nw, s), pB(Nw, s);
+  DBuf<uint32_t> hist(nhist, s);
+  DBuf<uint32_t> start((uint64_t)nb + 1, s);
+  DBuf<uint64_t> tsum((size_t)scan_tiles + 1, s);     // reduce-then-scan tile sums
+  // zeroed scratch: [n_valid][meta]
+  const size_t off_meta = 64;
+  const size_t scratch_bytes = off_meta + sizeof(BuildMeta);
+  DBuf<uint8_t> scratch(scratch_bytes, s);
+  uint8_t* sc = scratch.p;
+  uint32_t* n_valid = reinterpret_cast<uint32_t*>(sc);
+  BuildMeta* meta = reinterpret_cast<BuildMeta*>(sc + off_meta);
+  HIPC(hipMemsetAsync(sc, 0, scratch_bytes, s));
+  idx->table.reset(idx->slots());
+  idx->positions.reset(Nw);
+  DBuf<BucketStats> bstats(nb, s);
+
+  LAUNCH("k_v2_encode", s,
+         launch_v2_encode(d_seq, L, k, Nw, aligned, g, make_digit(1, R), kA.p, pA.p, hist.p,
+                          ntiles, s));
+  uint64_t *kin = kA.p, *kout = kB.p;
+  uint32_t *pin = pA.p, *pout = pB.p;
+  uint32_t div = 1;
+  for (uint32_t p = 0; p < passes; ++p) {
+    if (p > 0)
+      LAUNCH("k_v2_hist", s,
+             launch_v2_hist(kin, n_valid, g, make_digit(div, R), hist.p, ntiles, s));
+    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, tsum.p, n_valid, s));
+    LAUNCH("k_v2_scatter", s,
+           launch_v2_scatter(kin, pin, p == 0 ? nullptr : n_valid, (uint64_t)Nw, g,
+                             make_digit(div, R), hist.p, ntiles, kout, pout, s));
+    std::swap(kin, kout);
+    std::swap(pin, pout);
+    div *= R;
+  }
+  LAUNCH("k_v2_bounds", s, launch_v2_bounds(kin, n_valid, g, start.p, (uint64_t)Nw, s));
+#ifdef KMHG_STAMPS
+  static uint64_t* stamps = nullptr;
+  if (!stamps) HIPC(hipMallocManaged(&stamps, sizeof(uint64_t) * 8 * (1u << 22)));
+  HIPC(hipMemsetAsync(stamps, 0, sizeof(uint64_t) * 8 * nb, s));
+  kmhg::set_stamp_buffer(stamps);
+#endif
+  LAUNCH("k_v2_bucket", s,
+         launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
+                          meta, s));
+  LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, nb, n_valid, meta, s));
+#ifdef KMHG_STAMPS
+  if (const char* f = std::getenv("KMHG_STAMP_FILE")) {
+    HIPC(hipStreamSynchronize(s));
+    if (FILE* fp = fopen(f, "wb")) { fwrite(stamps, 8, 8 * (size_t)nb, fp); fclose(fp); }
+  }
+#endif
+  BuildMeta hm;
+  HIPC(hipMemcpyAsync(&hm, meta, sizeof(hm), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  if (hm.overflow) return nullptr;
+  idx->U = hm.n_kmers;
+  idx->N = hm.n_positions;
+  idx->P = hm.n_pairs;
+  idx->max_n = hm.max_count;
+  return idx.release();
+}
+
+int build_version() {
+  static int v = [] {
+    const char* e = std::getenv("KMHG_BUILD");
+    return (e && std::string(e) == "v1") ? 1 : 2;
+  }();
+  return v;
+}
+
+kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
+  if (build_version() == 2) {
+    kmhg_index* idx = build_device_v2(d_seq, L, k, s);
+    if (idx) return idx;
+  }
+  return build_device_v1(d_seq, L, k, s);
 }
 
 // ---------------------------------------------------------------------------- query
@@ -401,16 +503,13 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
   const uint32_t nt = tiles_for(Nw);
   DBuf<uint2> qinfo(Nw, s);
-  const size_t scratch_bytes = (size_t)nt * 16 + 64 + 16;
-  DBuf<uint8_t> scratch(scratch_bytes, s);
-  HIPC(hipMemsetAsync(scratch.p, 0, scratch_bytes, s));
-  uint64_t* status = reinterpret_cast<uint64_t*>(scratch.p);
-  uint64_t* tile_row0 = reinterpret_cast<uint64_t*>(scratch.p + (size_t)nt * 8);
-  uint32_t* ticket = reinterpret_cast<uint32_t*>(scratch.p + (size_t)nt * 16);
-  uint64_t* total = reinterpret_cast<uint64_t*>(scratch.p + (size_t)nt * 16 + 64);
+  DBuf<uint64_t> tiles((size_t)nt + 1, s);        // per-tile rows -> first row; [nt] = total
+  uint64_t* tile_row0 = tiles.p;
+  uint64_t* total = tiles.p + nt;
   LAUNCH("k_query_probe", s,
-         launch_query_probe(d_seq, L, kq, idx->table.p, idx->cap, qinfo.p, w0, w1, aligned,
-                            status, ticket, tile_row0, total, s));
+         launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
+                            tile_row0, s));
+  LAUNCH("k_scan_tiles_u64", s, launch_scan_tiles_u64(tile_row0, nt, total, s));
   uint64_t H = 0;
   HIPC(hipMemcpyAsync(&H, total, sizeof(H), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -430,7 +529,8 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
   const uint32_t U = (uint32_t)idx->U;
   DBuf<uint32_t> F(L, s);
   HIPC(hipMemsetAsync(F.p, 0xFF, (size_t)L * 4, s));
-  if (U) LAUNCH("k_read_first", s, launch_read_first(idx->offsets.p, idx->positions.p, U, F.p, s));
+  if (U) LAUNCH("k_read_first", s, launch_read_first(idx->table.p, idx->slots(), idx->positions.p,
+                                                     F.p, s));
   const uint32_t nt = tiles_for(L);
   const size_t scratch_bytes = (size_t)nt * 24 + 64 + sizeof(ReadMeta);
   DBuf<uint8_t> scratch(scratch_bytes, s);
@@ -446,7 +546,7 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
   c.pkeys.reset(idx->N / 2 + 1);
   c.pair_off.reset(idx->N / 2 + 1);
   LAUNCH("k_read_order", s,
-         launch_read_order(F.p, L, idx->counts.p, st_a, st_b, st_c, ticket, c.perm.p,
+         launch_read_order(F.p, L, idx->table.p, st_a, st_b, st_c, ticket, c.perm.p,
                            c.canon_off.p, c.pkeys.p, c.pair_off.p, rm, s));
   ReadMeta h;
   HIPC(hipMemcpyAsync(&h, rm, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -472,17 +572,17 @@ void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, 
   const uint32_t U = (uint32_t)idx->U;
   if ((opt & (KMHG_OPT_KMER | KMHG_OPT_COUNT)) && U)
     LAUNCH("k_read_keys", s,
-           launch_read_keys(c.perm.p, U, idx->ukeys.p, idx->counts.p, idx->k,
+           launch_read_keys(c.perm.p, U, idx->table.p, idx->k,
                             (opt & KMHG_OPT_COUNT) ? counts : nullptr,
                             (opt & KMHG_OPT_KMER) ? kmers : nullptr, s));
   if ((opt & KMHG_OPT_POS) && idx->N)
     LAUNCH("k_read_pos", s,
-           launch_read_pos(c.perm.p, c.canon_off.p, U, idx->N, idx->offsets.p, idx->positions.p,
+           launch_read_pos(c.perm.p, c.canon_off.p, U, idx->N, idx->table.p, idx->positions.p,
                            reinterpret_cast<int2*>(pos), s));
   if ((opt & KMHG_OPT_PAIRS) && idx->P)
     LAUNCH("k_read_pairs", s,
            launch_read_pairs(c.pkeys.p, c.pair_off.p, (uint32_t)c.n_multi, idx->P, c.perm.p,
-                             idx->counts.p, idx->offsets.p, idx->positions.p, pairs, s));
+                             idx->table.p, idx->positions.p, pairs, s));
 }
 
 }  // namespace
@@ -536,9 +636,8 @@ int kmhg_index_info(const kmhg_index* idx, kmhg_info* info) {
     info->n_positions = (int64_t)idx->N;
     info->n_pairs = (int64_t)idx->P;
     info->max_count = idx->max_n;
-    info->table_slots = (int64_t)idx->cap;
-    info->device_bytes = (int64_t)(idx->table.bytes() + idx->ukeys.bytes() + idx->counts.bytes() +
-                                   idx->offsets.bytes() + idx->positions.bytes());
+    info->table_slots = (int64_t)idx->slots();
+    info->device_bytes = (int64_t)(idx->table.bytes() + idx->positions.bytes());
   });
 }
 
@@ -676,62 +775,46 @@ int kmhg_query_free(kmhg_query* q) {
 int kmhg_image_sizes_get(const kmhg_index* idx, kmhg_image_sizes* sz, int64_t header[8]) {
   return guarded([&] {
     if (!idx || !sz || !header) fail(KMHG_EINVAL, "null argument");
-    sz->table_bytes = (int64_t)((idx->cap + 1) * sizeof(Slot));
+    sz->table_bytes = (int64_t)(idx->slots() * sizeof(Slot));
     sz->positions_bytes = (int64_t)(idx->N * 4);
-    sz->keys_bytes = (int64_t)(idx->U * 8);
-    sz->counts_bytes = (int64_t)(idx->U * 4);
-    sz->offsets_bytes = (int64_t)((idx->U + 1) * 4);
-    header[0] = idx->k; header[1] = idx->L; header[2] = (int64_t)idx->cap;
+    header[0] = idx->k; header[1] = idx->L;
+    header[2] = ((int64_t)idx->geom.nb << 32) | idx->geom.capb;
     header[3] = (int64_t)idx->U; header[4] = (int64_t)idx->N; header[5] = (int64_t)idx->P;
     header[6] = idx->max_n; header[7] = 0x6B6D6867;   // 'kmhg'
   });
 }
 
-int kmhg_image_export(const kmhg_index* idx, void* d_table, void* d_positions, void* d_keys,
-                      void* d_counts, void* d_offsets, void* stream) {
+int kmhg_image_export(const kmhg_index* idx, void* d_table, void* d_positions, void* stream) {
   return guarded([&] {
     if (!idx) fail(KMHG_EINVAL, "null index");
     DeviceGuard g(idx->device);
     hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
-    auto cp = [&](void* dst, const void* src, size_t b) {
-      if (dst && b) HIPC(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToDevice, s));
-    };
-    cp(d_table, idx->table.p, (idx->cap + 1) * sizeof(Slot));
-    cp(d_positions, idx->positions.p, idx->N * 4);
-    cp(d_keys, idx->ukeys.p, idx->U * 8);
-    cp(d_counts, idx->counts.p, idx->U * 4);
-    cp(d_offsets, idx->offsets.p, (idx->U + 1) * 4);
+    if (d_table) HIPC(hipMemcpyAsync(d_table, idx->table.p, idx->slots() * sizeof(Slot),
+                                     hipMemcpyDeviceToDevice, s));
+    if (d_positions && idx->N)
+      HIPC(hipMemcpyAsync(d_positions, idx->positions.p, idx->N * 4, hipMemcpyDeviceToDevice, s));
     HIPC(hipStreamSynchronize(s));
   });
 }
 
 int kmhg_image_import(const int64_t header[8], const void* d_table, const void* d_positions,
-                      const void* d_keys, const void* d_counts, const void* d_offsets,
                       void* stream, kmhg_index** out) {
   return guarded([&] {
     if (!header || !out || header[7] != 0x6B6D6867) fail(KMHG_EINVAL, "bad index image header");
     auto idx = std::make_unique<kmhg_index>();
     HIPC(hipGetDevice(&idx->device));
-    hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
-    idx->k = (int)header[0]; idx->L = header[1]; idx->cap = (uint64_t)header[2];
+    hipStream_t s = (hipStream_t)stream;
+    idx->k = (int)header[0]; idx->L = header[1];
+    idx->geom = Geom{(uint32_t)((uint64_t)header[2] >> 32), (uint32_t)(header[2] & 0xFFFFFFFF)};
     idx->U = (uint64_t)header[3]; idx->N = (uint64_t)header[4]; idx->P = (uint64_t)header[5];
     idx->max_n = (uint32_t)header[6];
-    idx->table.reset(idx->cap + 1);
+    idx->table.reset(idx->slots());
     idx->positions.reset(idx->N);
-    idx->ukeys.reset(idx->U);
-    idx->counts.reset(idx->U);
-    idx->offsets.reset(idx->U + 1);
-    auto cp = [&](void* dst, const void* src, size_t b) {
-      if (b) {
-        if (!src) fail(KMHG_EINVAL, "null image buffer");
-        HIPC(hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToDevice, s));
-      }
-    };
-    cp(idx->table.p, d_table, (idx->cap + 1) * sizeof(Slot));
-    cp(idx->positions.p, d_positions, idx->N * 4);
-    cp(idx->ukeys.p, d_keys, idx->U * 8);
-    cp(idx->counts.p, d_counts, idx->U * 4);
-    cp(idx->offsets.p, d_offsets, (idx->U + 1) * 4);
+    if (!d_table || (idx->N && !d_positions)) fail(KMHG_EINVAL, "null image buffer");
+    HIPC(hipMemcpyAsync(idx->table.p, d_table, idx->slots() * sizeof(Slot),
+                        hipMemcpyDeviceToDevice, s));
+    if (idx->N)
+      HIPC(hipMemcpyAsync(idx->positions.p, d_positions, idx->N * 4, hipMemcpyDeviceToDevice, s));
     HIPC(hipStreamSynchronize(s));
     *out = idx.release();
   });

@@ -6,6 +6,11 @@
 namespace kmhg {
 
 constexpr uint32_t LARGE_MIN = 64;     // keys with >= this many positions sort per workgroup
+// partitioned build (kmhg_build_v2.hip)
+constexpr uint32_t V2_BW = 256;        // mean windows per bucket
+constexpr uint32_t V2_CAPB = 384;      // slots per bucket (LDS sub-table of one wave)
+constexpr uint32_t V2_SLOT_BITS = 9;   // bits to name a slot 0..V2_CAPB
+constexpr uint32_t V2_MAXR = 1024;     // max radix of one partition pass
 constexpr uint32_t SORT_CHUNK = 4096;  // LDS bitonic chunk (16 KiB)
 
 struct BuildMeta {              // written by the build kernels, read once by the host
@@ -15,7 +20,7 @@ struct BuildMeta {              // written by the build kernels, read once by th
   uint32_t max_count;           // max n
   uint32_t n_small;             // keys with 2 <= n < LARGE_MIN
   uint32_t n_large;             // keys with n >= LARGE_MIN
-  uint32_t pad_;
+  uint32_t overflow;            // partitioned build: a bucket's LDS sub-table filled up
 };
 
 struct ReadMeta {               // canonical-order readout preparation
@@ -23,7 +28,7 @@ struct ReadMeta {               // canonical-order readout preparation
 };
 
 void launch_table_init(Slot* T, uint64_t n, hipStream_t s);
-void launch_build_insert(const uint8_t* seq, int64_t L, int k, Slot* T, uint64_t cap,
+void launch_build_insert(const uint8_t* seq, int64_t L, int k, Slot* T, Geom g,
                          uint32_t* win_slot, int64_t Nw, bool aligned, hipStream_t s);
 void launch_build_compact(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket,
                           uint64_t* ukeys, uint32_t* counts, uint32_t* offsets,
@@ -35,28 +40,70 @@ void launch_sort_small(const uint32_t* small_ids, const BuildMeta* meta, const u
                        const uint32_t* offsets, int32_t* positions, hipStream_t s);
 void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const uint32_t* counts,
                        const uint32_t* offsets, int32_t* positions, int32_t* tmp, hipStream_t s);
-void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, uint64_t cap,
-                        uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* status,
-                        uint32_t* ticket, uint64_t* tile_row0, uint64_t* total_rows,
+void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
+                        uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
                         hipStream_t s);
+void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
 void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
                        hipStream_t s);
-void launch_read_first(const uint32_t* offsets, const int32_t* positions, uint32_t U, uint32_t* F,
+void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint32_t* F,
                        hipStream_t s);
-void launch_read_order(const uint32_t* F, int64_t L, const uint32_t* counts, uint64_t* st_a,
+void launch_read_order(const uint32_t* F, int64_t L, const Slot* T, uint64_t* st_a,
                        uint64_t* st_b, uint64_t* st_c, uint32_t* ticket, uint32_t* perm,
                        uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
                        ReadMeta* rmeta, hipStream_t s);
-void launch_read_keys(const uint32_t* perm, uint32_t U, const uint64_t* ukeys,
-                      const uint32_t* counts, int k, int32_t* out_counts, char* out_kmers,
-                      hipStream_t s);
+void launch_read_keys(const uint32_t* perm, uint32_t U, const Slot* T, int k, int32_t* out_counts,
+                      char* out_kmers, hipStream_t s);
 void launch_read_pos(const uint32_t* perm, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
-                     const uint32_t* offsets, const int32_t* positions, int2* out, hipStream_t s);
+                     const Slot* T, const int32_t* positions, int2* out, hipStream_t s);
 void launch_read_pairs(const uint32_t* pkeys, const uint64_t* pair_off, uint32_t M,
-                       uint64_t nrows, const uint32_t* perm, const uint32_t* counts,
-                       const uint32_t* offsets, const int32_t* positions, int32_t* out,
-                       hipStream_t s);
+                       uint64_t nrows, const uint32_t* perm, const Slot* T,
+                       const int32_t* positions, int32_t* out, hipStream_t s);
+// radix digit of a bucket id: floor(b / div) mod R via magic multipliers (see digit_of)
+struct Digit {
+  uint64_t mdiv;   // ceil(2^64 / div), 0 for div = 1
+  uint64_t mR;     // ceil(2^64 / R), 0 for R = 1
+  uint32_t R;
+  int nbits;       // bits to name a digit 0..R-1
+};
+inline uint64_t magic64(uint32_t d) {   // ceil(2^64 / d) for d >= 2
+  return d <= 1 ? 0 : (uint64_t)(~0ull / d) + 1;
+}
+inline Digit make_digit(uint32_t div, uint32_t R) {
+  Digit d;
+  d.mdiv = magic64(div);
+  d.mR = magic64(R);
+  d.R = R;
+  d.nbits = 0;
+  while ((1u << d.nbits) < R) ++d.nbits;
+  return d;
+}
+void launch_v2_encode(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
+                      Digit D, uint64_t* keys, uint32_t* pos, uint32_t* hist,
+                      uint32_t ntiles, hipStream_t s);
+// exclusive scan of a u32 array; tsum = scratch of tiles_for(n) + 1 u64; total <- sum
+void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, hipStream_t s);
+void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
+                    uint32_t ntiles, hipStream_t s);
+void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr,
+                       uint64_t n_all, Geom g, Digit D, const uint32_t* hist, uint32_t ntiles,
+                       uint64_t* kout, uint32_t* pout, hipStream_t s);
+void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
+                      uint64_t n_max, hipStream_t s);
+struct BucketStats {           // per-bucket partials of the build statistics
+  uint32_t n_kmers, max_count;
+  uint64_t n_pairs;
+};
+void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
+                      Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
+                      hipStream_t s);
+void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
+                     BuildMeta* meta, hipStream_t s);
+
+#ifdef KMHG_STAMPS
+void set_stamp_buffer(uint64_t* p);
+#endif
 
 inline uint32_t tiles_for(uint64_t n) { return (uint32_t)((n + TILE - 1) / TILE); }
 

@@ -16,231 +16,9 @@
 #include <hip/hip_runtime.h>
 #include "kmhg_common.h"
 #include "kmhg_kernels.h"
+#include "kmhg_device.h"
 
 namespace kmhg {
-
-// ------------------------------------------------------------------ small wave/block helpers
-__device__ __forceinline__ int lane_id() { return __lane_id(); }
-__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
-
-__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Inclusive wave scan (64 lanes).
-__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint64_t t = __shfl_up(v, d);
-    if (lane_id() >= d) v += t;
-  }
-  return v;
-}
-
-// Exclusive scan over the 256 threads of a block (one value per thread).  `lds` needs 5 u64.
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* lds, uint64_t& total) {
-  const int wid = threadIdx.x >> 6;
-  uint64_t inc = wave_incl_scan(v);
-  if (lane_id() == 63) lds[wid] = inc;
-  __syncthreads();
-  uint64_t off = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < BLOCK / 64; ++w) {
-    uint64_t x = lds[w];
-    if (w < wid) off += x;
-    tot += x;
-  }
-  __syncthreads();
-  total = tot;
-  return off + inc - v;
-}
-
-// ------------------------------------------------------------------ decoupled look-back
-// status word: [63:62] = 0 not ready / 1 aggregate / 2 inclusive prefix, [61:0] payload.
-// Each word is a self-describing 8-B granule written by ONE relaxed agent-scope store and read
-// by relaxed agent-scope loads (sc1), so no separate flag, fence or payload hand-off exists.
-// Tiles come from a ticket counter so every tile a block waits on is already running.
-constexpr uint64_t LB_MASK = (1ull << 62) - 1;
-
-// Wave-parallel look-back: called by ALL 64 lanes of one wave (same tile/agg in every lane).
-// Each round the 64 lanes read the 64 nearest predecessors at once; the window is consumed up
-// to (and including) the nearest inclusive prefix once every word in front of it is ready.
-__device__ uint64_t lookback_excl(uint64_t* status, uint32_t tile, uint64_t agg) {
-  const int lane = lane_id();
-  if (tile == 0) {
-    if (lane == 0) st_relaxed(&status[0], (2ull << 62) | agg);
-    return 0;
-  }
-  if (lane == 0) st_relaxed(&status[tile], (1ull << 62) | agg);
-  uint64_t excl = 0;
-  int64_t base = (int64_t)tile - 1;
-  for (;;) {
-    int64_t j = base - lane;
-    uint64_t w = (j >= 0) ? ld_relaxed(&status[j]) : (2ull << 62);   // before tile 0: prefix 0
-    uint64_t f = w >> 62;
-    uint64_t m0 = __ballot(f == 0), m2 = __ballot(f == 2);
-    int first2 = m2 ? __ffsll((unsigned long long)m2) - 1 : 64;
-    uint64_t need = first2 == 64 ? ~0ull : ((2ull << first2) - 1ull);   // lanes 0..first2
-    if (m0 & need) { __builtin_amdgcn_s_sleep(1); continue; }
-    uint64_t v = (lane <= first2) ? (w & LB_MASK) : 0ull;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    excl += v;
-    if (first2 < 64) break;
-    base -= 64;
-  }
-  if (lane == 0) st_relaxed(&status[tile], (2ull << 62) | (excl + agg));
-  return excl;
-}
-
-// Grab a tile ticket (thread 0) and broadcast it.
-__device__ __forceinline__ uint32_t take_ticket(uint32_t* counter, uint32_t* lds) {
-  if (threadIdx.x == 0) *lds = atomicAdd(counter, 1u);
-  __syncthreads();
-  uint32_t t = *lds;
-  __syncthreads();
-  return t;
-}
-
-// ------------------------------------------------------------------ LDS staging of a tile
-// Chars [base, base + STAGE) are loaded coalesced (16 B per lane when the sequence is 16-B
-// aligned) and packed into 2-bit codes (MSB-first, 16 chars per u32) and N flags (16 chars per
-// u16 kept in a u32).  Chars outside [0, L) are flagged N: a window that touches them is never
-// valid, and position -1 acting as N gives the reference's "start of sequence" rule.
-struct Stage {
-  uint32_t code[STAGE_W16];
-  uint32_t nbit[STAGE_W16];
-};
-
-__device__ __forceinline__ void pack16(const uint8_t* c, uint32_t& code, uint32_t& nb) {
-  uint32_t cd = 0, n = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    uint32_t ch = c[i];
-    cd = (cd << 2) | ((ch >> 1) & 3u);       // UPDATE_OFFSET, src/kmer_util.h:8
-    n = (n << 1) | (((ch | 0x20u) == 'n') ? 1u : 0u);   // LC(c)=='n', src/kmer_util.h:10
-  }
-  code = cd; nb = n;
-}
-
-__device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ seq, int64_t L,
-                                           int64_t base, Stage& st, bool aligned) {
-  for (int w = threadIdx.x; w < STAGE_W16; w += BLOCK) {
-    int64_t c0 = base + 16 * (int64_t)w;
-    uint8_t buf[16];
-    if (aligned && c0 >= 0 && c0 + 16 <= L) {
-      uint4 v = *reinterpret_cast<const uint4*>(seq + c0);
-      *reinterpret_cast<uint4*>(buf) = v;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        int64_t p = c0 + i;
-        buf[i] = (p >= 0 && p < L) ? seq[p] : (uint8_t)'N';
-      }
-    }
-    uint32_t cd, nb;
-    pack16(buf, cd, nb);
-    st.code[w] = cd;
-    st.nbit[w] = nb;
-  }
-}
-
-// Window whose first char is stage offset o (global start s).  Returns validity per the
-// reference walk: no N in [s, s+k), s+k <= L, and NOT (s+k == L and the char
-// before s is N or s == 0) -- the end-drop quirk of init_kmer (src/kmer_pos.c:81-83).
-__device__ __forceinline__ bool window_key(const Stage& st, int o, int64_t s, int64_t L, int k,
-                                           uint64_t& key) {
-  if (s + k > L) return false;
-  // N flags of chars [o-1, o+k): k+1 <= 33 bits out of a 48-bit window of three u16 words
-  int p = o - 1;
-  int q = p >> 4, c = p & 15;
-  uint64_t x48 = ((uint64_t)st.nbit[q] << 32) | ((uint64_t)st.nbit[q + 1] << 16) |
-                 (uint64_t)st.nbit[q + 2];
-  uint64_t m = (x48 << (16 + c)) >> (63 - k);          // top k+1 bits
-  uint64_t winN = m & ((2ull << (k - 1)) - 1ull);      // low k bits (k <= 32)
-  if (winN) return false;
-  if (s + k == L && ((m >> k) & 1ull)) return false;
-  // 2k code bits of chars [o, o+k)
-  int qw = o >> 4, b = (o & 15) * 2;
-  uint64_t x = ((uint64_t)st.code[qw] << 32) | st.code[qw + 1];
-  uint64_t y = st.code[qw + 2];
-  uint64_t t = (x << b) | ((y << b) >> 32);
-  key = t >> (64 - 2 * k);
-  return true;
-}
-
-// ------------------------------------------------------------------ hash table primitives
-__device__ __forceinline__ uint64_t home_slot(uint64_t key, uint64_t cap) {
-  return __umul64hi(mix64(key), cap);
-}
-
-// Find-or-insert (atomicCAS on the 64-bit key word).  Keys only move EMPTY -> key, so a stale
-// plain read can only show EMPTY, which the CAS then corrects.
-__device__ __forceinline__ uint32_t table_insert(Slot* __restrict__ T, uint64_t cap, uint64_t key) {
-  if (key == EMPTY_KEY) return (uint32_t)cap;          // side slot (k = 32, all G)
-  uint64_t i = home_slot(key, cap);
-  for (;;) {
-    uint64_t cur = T[i].key;
-    if (cur == key) return (uint32_t)i;
-    if (cur == EMPTY_KEY) {
-      uint64_t prev = atomicCAS((unsigned long long*)&T[i].key, (unsigned long long)EMPTY_KEY,
-                                (unsigned long long)key);
-      if (prev == EMPTY_KEY || prev == key) return (uint32_t)i;
-    }
-    if (++i == cap) i = 0;
-  }
-}
-
-// Read-only probe: returns the slot or NONE.
-__device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, uint64_t cap,
-                                               uint64_t key, uint32_t& count, uint32_t& end) {
-  if (key == EMPTY_KEY) {
-    uint4 v = *reinterpret_cast<const uint4*>(&T[cap]);
-    count = v.z; end = v.w;
-    return count ? (uint32_t)cap : NONE;
-  }
-  uint64_t i = home_slot(key, cap);
-  for (;;) {
-    uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
-    uint64_t cur = ((uint64_t)v.y << 32) | v.x;
-    if (cur == key) { count = v.z; end = v.w; return (uint32_t)i; }
-    if (cur == EMPTY_KEY) { count = 0; end = 0; return NONE; }
-    if (++i == cap) i = 0;
-  }
-}
-
-// Wave-aggregated atomicAdd on a per-slot u32 counter.  Lanes that hold the same slot are
-// grouped behind the first active lane (readfirstlane + ballot); one atomic per group.  The
-// loop stops as soon as a group of one appears (i.i.d. data: one iteration), leaving the rest
-// to plain per-lane atomics; periodic (tandem-repeat) waves collapse to one atomic per key.
-// Returns the old value + this lane's rank inside its group (ranks follow lane order).
-__device__ __forceinline__ uint32_t wave_agg_add(uint32_t* base_ptr_of_slot0, bool act,
-                                                 uint32_t slot, size_t stride_u32) {
-  uint64_t active = __ballot(act);
-  uint32_t result = 0;
-  bool done = false;
-  while (active) {
-    int leader = __ffsll((unsigned long long)active) - 1;
-    uint32_t lslot = __shfl(slot, leader);
-    uint64_t grp = __ballot(act && !done && slot == lslot) & active;
-    int gsz = __popcll(grp);
-    if (gsz == 1) break;
-    uint32_t old = 0;
-    if (lane_id() == leader)
-      old = atomicAdd(base_ptr_of_slot0 + (size_t)lslot * stride_u32, (uint32_t)gsz);
-    old = __shfl(old, leader);
-    if ((grp >> lane_id()) & 1ull) {
-      result = old + (uint32_t)__popcll(grp & lanemask_lt());
-      done = true;
-    }
-    active &= ~grp;
-  }
-  if (act && !done) result = atomicAdd(base_ptr_of_slot0 + (size_t)slot * stride_u32, 1u);
-  return result;
-}
 
 // ================================================================== build kernels
 __global__ void __launch_bounds__(BLOCK) k_table_init(Slot* __restrict__ T, uint64_t n) {
@@ -256,7 +34,7 @@ __global__ void __launch_bounds__(BLOCK) k_table_init(Slot* __restrict__ T, uint
 // workgroup, lane-consecutive windows so the win_slot stores are coalesced.
 __global__ void __launch_bounds__(BLOCK)
 k_build_insert(const uint8_t* __restrict__ seq, int64_t L, int k, Slot* __restrict__ T,
-               uint64_t cap, uint32_t* __restrict__ win_slot, int64_t Nw, int aligned) {
+               Geom g, uint32_t* __restrict__ win_slot, int64_t Nw, int aligned) {
   __shared__ Stage st;
   const int64_t tile0 = (int64_t)blockIdx.x * TILE;
   stage_tile(seq, L, tile0 - HALO, st, aligned != 0);   // tile0 % 16 == 0: window o = HALO + w
@@ -270,7 +48,7 @@ k_build_insert(const uint8_t* __restrict__ seq, int64_t L, int k, Slot* __restri
     uint64_t key = 0;
     bool valid = (s < Nw) && window_key(st, HALO + w, s, L, k, key);
     uint32_t slot = NONE;
-    if (valid) slot = table_insert(T, cap, key);
+    if (valid) slot = table_insert(T, g, key);
     wave_agg_add(cnt0, valid, slot, stride);
     if (s < Nw) win_slot[s] = slot;
   }
@@ -487,14 +265,11 @@ k_sort_large(const uint32_t* __restrict__ ids, const BuildMeta* __restrict__ met
 // totals go through the look-back so each tile learns its first output row.
 __global__ void __launch_bounds__(BLOCK)
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
-              uint64_t cap, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
-              uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
-              uint64_t* __restrict__ tile_row0, uint64_t* __restrict__ total_rows,
-              uint32_t ntiles) {
+              Geom g, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
+              uint64_t* __restrict__ tile_rows) {
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
-  __shared__ uint32_t tk;
-  const uint32_t tile = take_ticket(ticket, &tk);
+  const uint32_t tile = blockIdx.x;
   // windows [w0, w1) of the FULL sequence: halo chars come from the real neighbours, so the
   // N / end-of-sequence rules at a shard boundary are those of the unsharded walk
   const int64_t t_start = w0 + (int64_t)tile * TILE;
@@ -510,19 +285,34 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     uint64_t key = 0;
     uint32_t count = 0, end = 0;
     if (s < w1 && window_key(st, o0 + w, s, L, kq, key))
-      table_find(T, cap, key, count, end);
+      table_find(T, g, key, count, end);
     if (s < w1) qinfo[s - w0] = make_uint2(count, end - count);
     rows += count;
   }
   uint64_t tot;
   block_excl_scan(rows, sh, tot);
-  if (threadIdx.x < 64) {
-    uint64_t ex = lookback_excl(status, tile, tot);
-    if (threadIdx.x == 0) {
-      tile_row0[tile] = ex;
-      if (tile == ntiles - 1) *total_rows = ex + tot;
-    }
+  if (threadIdx.x == 0) tile_rows[tile] = tot;
+}
+
+// Exclusive scan of n per-tile u64 totals in one workgroup (n = tiles, at most ~1M).
+__global__ void __launch_bounds__(1024)
+k_scan_tiles_u64(uint64_t* __restrict__ a, uint32_t n, uint64_t* __restrict__ total) {
+  __shared__ uint64_t part[1024];
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t i0 = threadIdx.x * per, i1 = min(n, i0 + per);
+  uint64_t s = 0;
+  for (uint32_t i = i0; i < i1; ++i) s += a[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {      // Hillis-Steele over 1024 partials
+    uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
   }
+  uint64_t run = part[threadIdx.x] - s;
+  for (uint32_t i = i0; i < i1; ++i) { uint64_t x = a[i]; a[i] = run; run += x; }
+  if (threadIdx.x == 1023) *total = part[1023];
 }
 
 // Q_emit: per tile, rows are dealt to lanes evenly (binary search over the tile's LDS prefix of
@@ -567,19 +357,26 @@ k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
 }
 
 // ================================================================== readout kernels
-// R_first: F[first position - 1] = id (first position = positions[offsets[id]] after K_sort).
+// The index is the table + positions: a key's slot carries {key, count, end} and its
+// positions are [end - count, end).  Canonical k-mer order (first occurrence) is a slot
+// permutation `perm` built once per index (R_first + R_order) and cached.
+
+// R_first: F[first position - 1] = slot, for every occupied slot (positions ascend per key).
 __global__ void __launch_bounds__(BLOCK)
-k_read_first(const uint32_t* __restrict__ offsets, const int32_t* __restrict__ positions,
-             uint32_t U, uint32_t* __restrict__ F) {
-  for (uint32_t id = blockIdx.x * BLOCK + threadIdx.x; id < U; id += gridDim.x * BLOCK)
-    F[positions[offsets[id]] - 1] = id;
+k_read_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions,
+             uint32_t* __restrict__ F) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
+       i += (uint64_t)gridDim.x * BLOCK) {
+    uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+    if (v.z) F[positions[v.w - v.z] - 1] = (uint32_t)i;
+  }
 }
 
 // R_order: compact F in position order -> perm (canonical order = first occurrence), with the
 // canonical pos-row offsets, and the list of keys that own pair rows with their pair offsets.
 // Three look-back chains: {keys, pos rows} packed 31|31, {multi keys}, {pair rows}.
 __global__ void __launch_bounds__(BLOCK)
-k_read_order(const uint32_t* __restrict__ F, int64_t L, const uint32_t* __restrict__ counts,
+k_read_order(const uint32_t* __restrict__ F, int64_t L, const Slot* __restrict__ T,
              uint64_t* __restrict__ st_a, uint64_t* __restrict__ st_b, uint64_t* __restrict__ st_c,
              uint32_t* __restrict__ ticket, uint32_t* __restrict__ perm,
              uint32_t* __restrict__ canon_off, uint32_t* __restrict__ pkeys,
@@ -597,7 +394,7 @@ k_read_order(const uint32_t* __restrict__ F, int64_t L, const uint32_t* __restri
   for (int j = 0; j < WPT; ++j) {
     int64_t p = t0 + (int64_t)threadIdx.x * WPT + j;
     id[j] = (p < L) ? F[p] : NONE;
-    uint64_t n = (id[j] != NONE) ? counts[id[j]] : 0;
+    uint64_t n = (id[j] != NONE) ? T[id[j]].count : 0;
     va[j] = (id[j] != NONE) ? ((1ull << 32) | n) : 0;
     vb[j] = (n >= 2) ? 1 : 0;
     vc[j] = n * (n - (n ? 1 : 0)) / 2;
@@ -636,15 +433,14 @@ k_read_order(const uint32_t* __restrict__ F, int64_t L, const uint32_t* __restri
 
 // R_keys: counts (opt 8) and k-mer strings (opt 1) in canonical order.
 __global__ void __launch_bounds__(BLOCK)
-k_read_keys(const uint32_t* __restrict__ perm, uint32_t U, const uint64_t* __restrict__ ukeys,
-            const uint32_t* __restrict__ counts, int k, int32_t* __restrict__ out_counts,
-            char* __restrict__ out_kmers) {
+k_read_keys(const uint32_t* __restrict__ perm, uint32_t U, const Slot* __restrict__ T, int k,
+            int32_t* __restrict__ out_counts, char* __restrict__ out_kmers) {
   const char NUC[4] = {'A', 'C', 'T', 'G'};             // src/kmer_hash.c:21
   for (uint32_t c = blockIdx.x * BLOCK + threadIdx.x; c < U; c += gridDim.x * BLOCK) {
-    uint32_t id = perm[c];
-    if (out_counts) out_counts[c] = (int32_t)counts[id];
+    const uint4 v = *reinterpret_cast<const uint4*>(&T[perm[c]]);
+    if (out_counts) out_counts[c] = (int32_t)v.z;
     if (out_kmers) {
-      uint64_t key = ukeys[id];
+      uint64_t key = ((uint64_t)v.y << 32) | v.x;
       char* o = out_kmers + (size_t)c * (k + 1);
       for (int i = k - 1; i >= 0; --i) { o[i] = NUC[key & 3]; key >>= 2; }
       o[k] = 0;
@@ -652,12 +448,12 @@ k_read_keys(const uint32_t* __restrict__ perm, uint32_t U, const uint64_t* __res
   }
 }
 
-// R_pos: rows (i, pos) in canonical order.  Each workgroup owns RROWS output rows; every key
+// R_pos: rows (i, pos) in canonical order.  Each workgroup owns TILE output rows; every key
 // owns >= 1 row so its key range fits the LDS copy of the canonical offsets.
 __global__ void __launch_bounds__(BLOCK)
 k_read_pos(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ canon_off, uint32_t U,
-           uint64_t nrows, const uint32_t* __restrict__ offsets,
-           const int32_t* __restrict__ positions, int2* __restrict__ out) {
+           uint64_t nrows, const Slot* __restrict__ T, const int32_t* __restrict__ positions,
+           int2* __restrict__ out) {
   __shared__ uint32_t off[TILE + 1];
   __shared__ uint32_t cr[2];
   const uint64_t r0 = (uint64_t)blockIdx.x * TILE;
@@ -676,9 +472,9 @@ k_read_pos(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ canon
   for (uint64_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
     uint32_t lo = 0, hi = nk - 1;
     while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (off[mid] <= r) lo = mid; else hi = mid - 1; }
-    uint32_t c = c0 + lo;
-    uint32_t id = perm[c];
-    int32_t p = positions[offsets[id] + (uint32_t)(r - off[lo])];
+    const uint32_t c = c0 + lo;
+    const uint4 v = *reinterpret_cast<const uint4*>(&T[perm[c]]);
+    const int32_t p = positions[v.w - v.z + (uint32_t)(r - off[lo])];
     out[r] = make_int2((int32_t)(c + 1), p);
   }
 }
@@ -688,8 +484,8 @@ k_read_pos(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ canon
 __global__ void __launch_bounds__(BLOCK)
 k_read_pairs(const uint32_t* __restrict__ pkeys, const uint64_t* __restrict__ pair_off,
              uint32_t M, uint64_t nrows, const uint32_t* __restrict__ perm,
-             const uint32_t* __restrict__ counts, const uint32_t* __restrict__ offsets,
-             const int32_t* __restrict__ positions, int32_t* __restrict__ out) {
+             const Slot* __restrict__ T, const int32_t* __restrict__ positions,
+             int32_t* __restrict__ out) {
   __shared__ uint64_t off[TILE + 1];
   __shared__ uint32_t cr[2];
   const uint64_t r0 = (uint64_t)blockIdx.x * TILE;
@@ -708,10 +504,10 @@ k_read_pairs(const uint32_t* __restrict__ pkeys, const uint64_t* __restrict__ pa
   for (uint64_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
     uint32_t lo = 0, hi = nk - 1;
     while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (off[mid] <= r) lo = mid; else hi = mid - 1; }
-    uint32_t c = pkeys[m0 + lo];
-    uint32_t id = perm[c];
-    uint64_t n = counts[id];
-    uint64_t t = r - off[lo];
+    const uint32_t c = pkeys[m0 + lo];
+    const uint4 v = *reinterpret_cast<const uint4*>(&T[perm[c]]);
+    const uint64_t n = v.z;
+    const uint64_t t = r - off[lo];
     // largest j with S(j) = j*(2n-j-1)/2 <= t
     double dn = (double)(2 * n - 1);
     double disc = dn * dn - 8.0 * (double)t;
@@ -721,8 +517,8 @@ k_read_pairs(const uint32_t* __restrict__ pkeys, const uint64_t* __restrict__ pa
     auto S = [n](int64_t jj) -> uint64_t { return (uint64_t)jj * (2 * n - (uint64_t)jj - 1) / 2; };
     while (j > 0 && S(j) > t) --j;
     while (j + 1 <= (int64_t)n - 2 && S(j + 1) <= t) ++j;
-    uint64_t q = (uint64_t)j + 1 + (t - S(j));
-    const int32_t* a = positions + offsets[id];
+    const uint64_t q = (uint64_t)j + 1 + (t - S(j));
+    const int32_t* a = positions + (v.w - v.z);
     int32_t* o = out + 3 * r;
     o[0] = (int32_t)(c + 1); o[1] = a[j]; o[2] = a[q];
   }
@@ -739,10 +535,10 @@ void launch_table_init(Slot* T, uint64_t n, hipStream_t s) {
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(k_table_init, dim3(g), dim3(BLOCK), 0, s, T, n);
 }
-void launch_build_insert(const uint8_t* seq, int64_t L, int k, Slot* T, uint64_t cap,
+void launch_build_insert(const uint8_t* seq, int64_t L, int k, Slot* T, Geom g,
                          uint32_t* win_slot, int64_t Nw, bool aligned, hipStream_t s) {
   hipLaunchKernelGGL(k_build_insert, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, seq, L, k, T,
-                     cap, win_slot, Nw, aligned ? 1 : 0);
+                     g, win_slot, Nw, aligned ? 1 : 0);
 }
 void launch_build_compact(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket,
                           uint64_t* ukeys, uint32_t* counts, uint32_t* offsets,
@@ -768,13 +564,15 @@ void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const u
   hipLaunchKernelGGL(k_sort_large, dim3(1024), dim3(BLOCK), 0, s, large_ids, meta, counts,
                      offsets, positions, tmp);
 }
-void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, uint64_t cap,
-                        uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* status,
-                        uint32_t* ticket, uint64_t* tile_row0, uint64_t* total_rows,
+void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
+                        uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
                         hipStream_t s) {
   uint32_t nt = grid_for(w1 - w0, TILE);
-  hipLaunchKernelGGL(k_query_probe, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, cap, qinfo, w0,
-                     w1, aligned ? 1 : 0, status, ticket, tile_row0, total_rows, nt);
+  hipLaunchKernelGGL(k_query_probe, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo, w0,
+                     w1, aligned ? 1 : 0, tile_rows);
+}
+void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
 }
 void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
@@ -782,41 +580,39 @@ void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
   hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qinfo, Nw, w0,
                      kq, positions, tile_row0, out);
 }
-void launch_read_first(const uint32_t* offsets, const int32_t* positions, uint32_t U, uint32_t* F,
+void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint32_t* F,
                        hipStream_t s) {
-  unsigned g = grid_for(U, BLOCK);
+  unsigned g = grid_for(nslots, BLOCK);
   if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(k_read_first, dim3(g), dim3(BLOCK), 0, s, offsets, positions, U, F);
+  hipLaunchKernelGGL(k_read_first, dim3(g), dim3(BLOCK), 0, s, T, nslots, positions, F);
 }
-void launch_read_order(const uint32_t* F, int64_t L, const uint32_t* counts, uint64_t* st_a,
+void launch_read_order(const uint32_t* F, int64_t L, const Slot* T, uint64_t* st_a,
                        uint64_t* st_b, uint64_t* st_c, uint32_t* ticket, uint32_t* perm,
                        uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
                        ReadMeta* rmeta, hipStream_t s) {
   uint32_t nt = grid_for(L, TILE);
-  hipLaunchKernelGGL(k_read_order, dim3(nt), dim3(BLOCK), 0, s, F, L, counts, st_a, st_b, st_c,
+  hipLaunchKernelGGL(k_read_order, dim3(nt), dim3(BLOCK), 0, s, F, L, T, st_a, st_b, st_c,
                      ticket, perm, canon_off, pkeys, pair_off, nt, rmeta);
 }
-void launch_read_keys(const uint32_t* perm, uint32_t U, const uint64_t* ukeys,
-                      const uint32_t* counts, int k, int32_t* out_counts, char* out_kmers,
-                      hipStream_t s) {
+void launch_read_keys(const uint32_t* perm, uint32_t U, const Slot* T, int k, int32_t* out_counts,
+                      char* out_kmers, hipStream_t s) {
   unsigned g = grid_for(U, BLOCK);
   if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(k_read_keys, dim3(g), dim3(BLOCK), 0, s, perm, U, ukeys, counts, k,
-                     out_counts, out_kmers);
+  hipLaunchKernelGGL(k_read_keys, dim3(g), dim3(BLOCK), 0, s, perm, U, T, k, out_counts,
+                     out_kmers);
 }
 void launch_read_pos(const uint32_t* perm, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
-                     const uint32_t* offsets, const int32_t* positions, int2* out, hipStream_t s) {
+                     const Slot* T, const int32_t* positions, int2* out, hipStream_t s) {
   if (!nrows) return;
   hipLaunchKernelGGL(k_read_pos, dim3(grid_for(nrows, TILE)), dim3(BLOCK), 0, s, perm, canon_off,
-                     U, nrows, offsets, positions, out);
+                     U, nrows, T, positions, out);
 }
 void launch_read_pairs(const uint32_t* pkeys, const uint64_t* pair_off, uint32_t M,
-                       uint64_t nrows, const uint32_t* perm, const uint32_t* counts,
-                       const uint32_t* offsets, const int32_t* positions, int32_t* out,
-                       hipStream_t s) {
+                       uint64_t nrows, const uint32_t* perm, const Slot* T,
+                       const int32_t* positions, int32_t* out, hipStream_t s) {
   if (!nrows) return;
   hipLaunchKernelGGL(k_read_pairs, dim3(grid_for(nrows, TILE)), dim3(BLOCK), 0, s, pkeys,
-                     pair_off, M, nrows, perm, counts, offsets, positions, out);
+                     pair_off, M, nrows, perm, T, positions, out);
 }
 
 }  // namespace kmhg

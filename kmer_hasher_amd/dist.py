@@ -2,7 +2,7 @@
 (backend "nccl" = RCCL over xGMI on MI355X).
 
   * the index is built once (rank 0) and its device image is broadcast to every rank
-    (five ncclBroadcast calls: table, positions, keys, counts, offsets);
+    (two ncclBroadcast calls: the hash table and the positions);
   * the query's windows are split into `world` contiguous ranges; each rank runs the HIP query
     on its range of the (replicated) query sequence -- validity at a range edge is decided on
     the full sequence, so no halo logic leaks into the result;
@@ -33,8 +33,8 @@ def shard_ranges(n: int, world: int) -> list[tuple[int, int]]:
 
 def broadcast_buffers(meta: torch.Tensor | None, bufs: list[torch.Tensor] | None, src: int,
                       device: torch.device, group=None) -> tuple[torch.Tensor, list[torch.Tensor]]:
-    """Broadcast an int64 meta vector (last 5 entries = buffer byte sizes) and the byte buffers
-    it describes from `src`.  Non-src ranks pass None and receive freshly allocated tensors."""
+    """Broadcast an int64 meta vector (after the 8-word header: one byte size per buffer) and the
+    byte buffers it describes from `src`.  Non-src ranks pass None and receive fresh tensors."""
     rank = dist.get_rank(group)
     n_meta = torch.zeros(1, dtype=torch.int64, device=device)
     if rank == src:
@@ -43,7 +43,7 @@ def broadcast_buffers(meta: torch.Tensor | None, bufs: list[torch.Tensor] | None
     m = meta.to(device) if rank == src else torch.empty(int(n_meta.item()), dtype=torch.int64,
                                                         device=device)
     dist.broadcast(m, src, group=group)
-    sizes = [int(x) for x in m[-5:].tolist()]
+    sizes = [int(x) for x in m[8:].tolist()]
     if rank != src:
         bufs = [torch.empty(max(1, s), dtype=torch.uint8, device=device) for s in sizes]
     for b in bufs:

@@ -43,11 +43,13 @@ def _worker(rank, world, port, seq_bytes, k_index, kq, out_q):
         eng = OracleEngine(seq_bytes, k_index)
         seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy())
         # image broadcast path (generic buffer broadcast) round-trips bytes exactly
-        meta = torch.tensor([7, 3, 5, 11, 13], dtype=torch.int64) if rank == 0 else None
+        meta = torch.tensor([0] * 8 + [7, 3, 5, 11, 13], dtype=torch.int64) if rank == 0 else None
         bufs = [torch.arange(s % 251, dtype=torch.uint8) for s in (7, 3, 5, 11, 13)] \
             if rank == 0 else None
         m, b = kd.broadcast_buffers(meta, bufs, 0, torch.device("cpu"))
-        ok_bcast = [x.numel() for x in b] == [7, 3, 5, 11, 13] and m.tolist() == [7, 3, 5, 11, 13]
+        ok_bcast = [x.numel() for x in b] == [7, 3, 5, 11, 13] and m.tolist()[8:] == [7, 3, 5, 11, 13]
+        ok_bcast = ok_bcast and all(torch.equal(x, torch.arange(s % 251, dtype=torch.uint8))
+                                    for x, s in zip(b, (7, 3, 5, 11, 13)))
         rows = kd.sharded_query(eng, seq, kq, dst=0)
         if rank == 0:
             out_q.put((ok_bcast, rows.numpy().reshape(-1).tolist()))
