@@ -48,6 +48,12 @@ CONFIGS = {
 
 def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) -> int | None:
     """Minimal bytes each kernel must move (DESIGN.md "Roofline accounting")."""
+    if kernel == "k_v2_scatter_seq":    # read L chars; write (key 8 B, pos 4 B) per valid window
+        return L + 12 * N
+    if kernel == "k_v2_scatter":        # one radix pass: read + write 12 B per window
+        return 24 * N
+    if kernel == "k_v2_bucket":         # read 12 B/window; write 4 B/position + key/count/end
+        return 12 * N + 4 * N + 16 * U
     if kernel == "k_build_insert":      # read L chars; key+count per distinct key; slot id/window
         return L + 12 * U + 4 * Nw
     if kernel == "k_build_compact":     # key+count read, key+count+offset written per key
@@ -194,7 +200,8 @@ def main():
         qvalue = mbp_total * args.steps / t_query
         # dominant build kernel and its roofline
         per = {n: v[1] / v[0] for n, v in ktimes.items() if v[0]}
-        dom = max(per, key=per.get)
+        tot = {n: v[1] / args.steps for n, v in ktimes.items() if v[0]}   # ms per build step
+        dom = max(tot, key=tot.get)
         ab = algorithmic_bytes(dom, L, Nw, U, N)
         achieved = ab / (per[dom] * 1e-3) / 1e9 if ab else None
         traffic = None
@@ -231,6 +238,11 @@ def main():
                       "ms_per_step": round(t_query / args.steps * 1e3, 4),
                       "kernels_ms": {n: round(v, 5) for n, v in qper.items()}},
             "kernels_ms": {n: round(v, 5) for n, v in per.items()},
+            "build_roofline": {"algorithmic_bytes": L + 12 * U + 4 * N,
+                               "kernel_ms_per_step": round(sum(tot.values()), 5),
+                               "frac_of_step": round((L + 12 * U + 4 * N) /
+                                                     (t_build / args.steps) / 1e9 / HBM_PEAK_GBS, 5),
+                               "note": "whole build, SURVEY.md §8(d): B = L + 12U + 4N"},
         }
         if not args.no_cpu and not args.profile:
             out["cpu_baseline"] = cpu_baseline(host_seq.tobytes(), k)

@@ -81,31 +81,28 @@ __device__ __forceinline__ uint64_t match_bits(uint32_t v, int nbits, bool act) 
   return m;
 }
 
-// ---------------------------------------------------------------- V_encode
+// ---------------------------------------------------------------- V_hist0 (from the sequence)
+// LDS-staged 2-bit encode + N mask of every window of the tile (as K_insert) and the tile's
+// histogram of the first radix digit of the windows' buckets.  Nothing else is written: the
+// first scatter pass re-reads the chars (1 B/window) instead of a 12 B/window key stream.
 __global__ void __launch_bounds__(BLOCK)
-k_v2_encode(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned, Geom g,
-            Digit D, uint64_t* __restrict__ keys, uint32_t* __restrict__ pos,
-            uint32_t* __restrict__ hist, uint32_t ntiles) {
+k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned, Geom g,
+           Digit D, uint32_t* __restrict__ hist, uint32_t ntiles) {
   __shared__ Stage st;
   __shared__ uint32_t lh[V2_MAXR];
   const int64_t tile0 = (int64_t)blockIdx.x * TILE;
-  const uint32_t R0 = D.R;
-  for (uint32_t d = threadIdx.x; d < R0; d += BLOCK) lh[d] = 0;
+  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) lh[d] = 0;
   stage_tile(seq, L, tile0 - HALO, st, aligned != 0);
   __syncthreads();
 #pragma unroll 2
   for (int j = 0; j < WPT; ++j) {
     const int w = j * BLOCK + threadIdx.x;
     const int64_t s = tile0 + w;
-    if (s >= Nw) continue;
     uint64_t key = 0;
-    const bool valid = window_key(st, HALO + w, s, L, k, key);
-    keys[s] = key;
-    pos[s] = valid ? (uint32_t)(s + 1) : 0u;
-    if (valid) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
+    if (s < Nw && window_key(st, HALO + w, s, L, k, key)) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < R0; d += BLOCK) hist[(size_t)d * ntiles + blockIdx.x] = lh[d];
+  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) hist[(size_t)d * ntiles + blockIdx.x] = lh[d];
 }
 
 // ---------------------------------------------------------------- V_scan (u32, exclusive)
@@ -171,65 +168,116 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
 
 // ---------------------------------------------------------------- V_scatter (stable)
 // Tile t = elements [t*TILE, (t+1)*TILE); wave w owns the contiguous 512 elements
-// [t*TILE + 512w, +512), lane l holds element 64c + l of them for c = 0..7 (coalesced loads).
-// Element order inside the tile = (wave, c, lane) = input order, so ranks assigned in that
-// order keep the pass stable.  pass 0 reads every window and drops invalid ones (pos == 0).
+// [t*TILE + 512w, +512), lane l holds element 64c + l of them for c = 0..7.  Element order
+// inside the tile = (wave, c, lane) = input order, so ranks assigned in that order keep the
+// pass stable.  FROM_SEQ (pass 0) encodes the windows from LDS-staged chars and drops invalid
+// ones; later passes read the (key, pos) stream.  The tile is re-ordered by digit in LDS first
+// and written out run by run, so each wave store covers a few contiguous runs instead of 64
+// scattered addresses.
+struct ScatterLDS {
+  uint32_t wc[4][V2_MAXR];     // per-wave digit counts -> per-wave tile-local cursors
+  uint32_t tstart[V2_MAXR];    // tile-local start of each digit
+  uint32_t gbase[V2_MAXR];     // global start of each digit for this tile (scanned histogram)
+  uint64_t skey[TILE];
+  uint32_t spos[TILE];
+  uint32_t sdst[TILE];
+  Stage st;
+};
+
+template <bool FROM_SEQ>
 __global__ void __launch_bounds__(BLOCK)
-k_v2_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
-             const uint32_t* __restrict__ n_ptr, uint64_t n_all, Geom g, Digit D,
+k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned,
+             const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
+             const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, uint32_t ntiles,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout) {
-  __shared__ uint32_t wc[4][V2_MAXR];
+  __shared__ ScatterLDS S;
   const uint32_t R = D.R;
-  const int nbits = D.nbits;
   constexpr int PER = TILE / 4 / 64;     // 8 elements per lane
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const uint64_t n = n_ptr ? (uint64_t)*n_ptr : n_all;
-  const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)wave * (TILE / 4);
+  const uint64_t tile0 = (uint64_t)blockIdx.x * TILE;
+  const uint32_t wbase = (uint32_t)wave * (TILE / 4);
   uint64_t key[PER];
   uint32_t ps[PER], dg[PER];
   bool act[PER];
+  if (FROM_SEQ) {
+    stage_tile(seq, L, (int64_t)tile0 - HALO, S.st, aligned != 0);
+    __syncthreads();
+  }
+  const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
 #pragma unroll
   for (int c = 0; c < PER; ++c) {
-    const uint64_t e = base + (uint64_t)c * 64 + lane;
-    act[c] = e < n;
-    key[c] = act[c] ? kin[e] : 0;
-    ps[c] = act[c] ? pin[e] : 0;
-    act[c] = act[c] && ps[c] != 0;
+    const uint32_t w = wbase + (uint32_t)c * 64 + lane;     // element index inside the tile
+    const uint64_t e = tile0 + w;
+    key[c] = 0;
+    if (FROM_SEQ) {
+      act[c] = e < n && window_key(S.st, HALO + (int)w, (int64_t)e, L, k, key[c]);
+      ps[c] = (uint32_t)(e + 1);
+    } else {
+      act[c] = e < n;
+      key[c] = act[c] ? kin[e] : 0;
+      ps[c] = act[c] ? pin[e] : 0;
+    }
     dg[c] = act[c] ? digit_of(key[c], g.nb, D) : 0;
   }
-  for (uint32_t d = lane; d < R; d += 64) wc[wave][d] = 0;
+  for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
   wave_sync();
 #pragma unroll
   for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
-    if (act[c]) atomicAdd(&wc[wave][dg[c]], 1u);
+    if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
-    uint32_t b = hist[(size_t)d * ntiles + blockIdx.x];
+  // tile-local digit starts: thread t owns digits [4t, 4t+4)
+  __shared__ uint64_t sh[8];
+  uint32_t dsum[4];
+  uint64_t own = 0;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      uint32_t t = wc[w][d];
-      wc[w][d] = b;
-      b += t;
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t d = threadIdx.x * 4 + q;
+    dsum[q] = d < R ? S.wc[0][d] + S.wc[1][d] + S.wc[2][d] + S.wc[3][d] : 0u;
+    own += dsum[q];
+  }
+  uint64_t tile_n;
+  uint32_t run = (uint32_t)block_excl_scan(own, sh, tile_n);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t d = threadIdx.x * 4 + q;
+    if (d < R) {
+      S.tstart[d] = run;
+      S.gbase[d] = hist[(size_t)d * ntiles + blockIdx.x];
+      uint32_t cur = run;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const uint32_t t = S.wc[w][d];
+        S.wc[w][d] = cur;
+        cur += t;
+      }
+      run += dsum[q];
     }
   }
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
-    const uint64_t grp = match_bits(dg[c], nbits, act[c]);
+    const uint64_t grp = match_bits(dg[c], D.nbits, act[c]);
     const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
     uint32_t cur = 0;
     if (act[c] && leader == lane) {
-      cur = wc[wave][dg[c]];
-      wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
+      cur = S.wc[wave][dg[c]];
+      S.wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
     }
     cur = __shfl(cur, leader);
     wave_sync();
     if (act[c]) {
-      const uint32_t dst = cur + (uint32_t)__popcll(grp & lanemask_lt());
-      kout[dst] = key[c];
-      pout[dst] = ps[c];
+      const uint32_t ld = cur + (uint32_t)__popcll(grp & lanemask_lt());
+      S.skey[ld] = key[c];
+      S.spos[ld] = ps[c];
+      S.sdst[ld] = S.gbase[dg[c]] + (ld - S.tstart[dg[c]]);
     }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < (uint32_t)tile_n; i += BLOCK) {
+    const uint32_t dst = S.sdst[i];
+    kout[dst] = S.skey[i];
+    pout[dst] = S.spos[i];
   }
 }
 
@@ -456,11 +504,10 @@ static inline unsigned grid_of(uint64_t n, unsigned per) {
   return (unsigned)(g ? g : 1);
 }
 
-void launch_v2_encode(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
-                      Digit D, uint64_t* keys, uint32_t* pos, uint32_t* hist,
-                      uint32_t ntiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_encode, dim3(ntiles), dim3(BLOCK), 0, s, seq, L, k, Nw,
-                     aligned ? 1 : 0, g, D, keys, pos, hist, ntiles);
+void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
+                     Digit D, uint32_t* hist, uint32_t ntiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_hist0, dim3(ntiles), dim3(BLOCK), 0, s, seq, L, k, Nw,
+                     aligned ? 1 : 0, g, D, hist, ntiles);
 }
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);
@@ -473,11 +520,17 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
                     uint32_t ntiles, hipStream_t s) {
   hipLaunchKernelGGL(k_v2_hist, dim3(ntiles), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist, ntiles);
 }
-void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr,
-                       uint64_t n_all, Geom g, Digit D, const uint32_t* hist, uint32_t ntiles,
-                       uint64_t* kout, uint32_t* pout, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_scatter, dim3(ntiles), dim3(BLOCK), 0, s, kin, pin, n_ptr, n_all, g, D,
-                     hist, ntiles, kout, pout);
+void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned,
+                           Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                           uint32_t* pout, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_scatter<true>, dim3(ntiles), dim3(BLOCK), 0, s, seq, L, k, Nw,
+                     aligned ? 1 : 0, nullptr, nullptr, nullptr, g, D, hist, ntiles, kout, pout);
+}
+void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
+                       Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                       uint32_t* pout, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_scatter<false>, dim3(ntiles), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
+                     (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ntiles, kout, pout);
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s) {

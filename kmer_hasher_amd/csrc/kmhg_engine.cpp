@@ -428,20 +428,21 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   idx->positions.reset(Nw);
   DBuf<BucketStats> bstats(nb, s);
 
-  LAUNCH("k_v2_encode", s,
-         launch_v2_encode(d_seq, L, k, Nw, aligned, g, make_digit(1, R), kA.p, pA.p, hist.p,
-                          ntiles, s));
+  LAUNCH("k_v2_hist0", s,
+         launch_v2_hist0(d_seq, L, k, Nw, aligned, g, make_digit(1, R), hist.p, ntiles, s));
+  LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, tsum.p, n_valid, s));
+  LAUNCH("k_v2_scatter_seq", s,
+         launch_v2_scatter_seq(d_seq, L, k, Nw, aligned, g, make_digit(1, R), hist.p, ntiles,
+                               kA.p, pA.p, s));
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
-  uint32_t div = 1;
-  for (uint32_t p = 0; p < passes; ++p) {
-    if (p > 0)
-      LAUNCH("k_v2_hist", s,
-             launch_v2_hist(kin, n_valid, g, make_digit(div, R), hist.p, ntiles, s));
+  uint32_t div = R;
+  for (uint32_t p = 1; p < passes; ++p) {
+    const Digit Dp = make_digit(div, R);
+    LAUNCH("k_v2_hist", s, launch_v2_hist(kin, n_valid, g, Dp, hist.p, ntiles, s));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, tsum.p, n_valid, s));
     LAUNCH("k_v2_scatter", s,
-           launch_v2_scatter(kin, pin, p == 0 ? nullptr : n_valid, (uint64_t)Nw, g,
-                             make_digit(div, R), hist.p, ntiles, kout, pout, s));
+           launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, s));
     std::swap(kin, kout);
     std::swap(pin, pout);
     div *= R;

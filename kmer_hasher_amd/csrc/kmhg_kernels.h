@@ -10,7 +10,7 @@ constexpr uint32_t LARGE_MIN = 64;     // keys with >= this many positions sort 
 constexpr uint32_t V2_BW = 256;        // mean windows per bucket
 constexpr uint32_t V2_CAPB = 384;      // slots per bucket (LDS sub-table of one wave)
 constexpr uint32_t V2_SLOT_BITS = 9;   // bits to name a slot 0..V2_CAPB
-constexpr uint32_t V2_MAXR = 1024;     // max radix of one partition pass
+constexpr uint32_t V2_MAXR = 512;      // max radix of one partition pass
 constexpr uint32_t SORT_CHUNK = 4096;  // LDS bitonic chunk (16 KiB)
 
 struct BuildMeta {              // written by the build kernels, read once by the host
@@ -79,16 +79,18 @@ inline Digit make_digit(uint32_t div, uint32_t R) {
   while ((1u << d.nbits) < R) ++d.nbits;
   return d;
 }
-void launch_v2_encode(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
-                      Digit D, uint64_t* keys, uint32_t* pos, uint32_t* hist,
-                      uint32_t ntiles, hipStream_t s);
+void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
+                     Digit D, uint32_t* hist, uint32_t ntiles, hipStream_t s);
 // exclusive scan of a u32 array; tsum = scratch of tiles_for(n) + 1 u64; total <- sum
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, hipStream_t s);
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     uint32_t ntiles, hipStream_t s);
-void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr,
-                       uint64_t n_all, Geom g, Digit D, const uint32_t* hist, uint32_t ntiles,
-                       uint64_t* kout, uint32_t* pout, hipStream_t s);
+void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned,
+                           Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                           uint32_t* pout, hipStream_t s);
+void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
+                       Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                       uint32_t* pout, hipStream_t s);
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s);
 struct BucketStats {           // per-bucket partials of the build statistics
