@@ -126,6 +126,7 @@ int kmhg_image_import(const int64_t header[8], const void *d_table, const void *
 /* Per-kernel HIP-event timing (KMHG_TIMING=1 also enables it).  The report is JSON:
  * {"kernel": [launches, total_ms], ...}; events are recorded on the kernels' own stream. */
 int kmhg_timing_enable(int on);
+int kmhg_timing_select(const char *kernel);   /* record only this kernel (NULL = all) */
 int kmhg_timing_reset(void);
 int kmhg_timing_report(char *buf, size_t cap);
 

@@ -58,6 +58,7 @@ _PROTOS = {
     "kmhg_image_export": (C.c_int, [vp, vp, vp, vp]),
     "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, C.POINTER(vp)]),
     "kmhg_timing_enable": (C.c_int, [C.c_int]),
+    "kmhg_timing_select": (C.c_int, [C.c_char_p]),
     "kmhg_timing_reset": (C.c_int, []),
     "kmhg_timing_report": (C.c_int, [C.c_char_p, C.c_size_t]),
     "kmhg_pool_trim": (C.c_int, []),

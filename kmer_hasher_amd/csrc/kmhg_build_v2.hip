@@ -124,7 +124,9 @@ k_tile_sum_u32(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict_
 }
 
 __global__ void __launch_bounds__(BLOCK)
-k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict__ tbase) {
+k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict__ tbase,
+                uint32_t* __restrict__ total) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *total = (uint32_t)tbase[gridDim.x];
   __shared__ uint64_t sh[8];
   const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)threadIdx.x * WPT;
   uint32_t v[WPT];
@@ -141,10 +143,6 @@ k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict
     if (base + j < n) a[base + j] = (uint32_t)run;
     run += v[j];
   }
-}
-
-__global__ void k_copy_total(const uint64_t* __restrict__ t, uint32_t* __restrict__ out) {
-  if (threadIdx.x == 0) *out = (uint32_t)*t;
 }
 
 // ---------------------------------------------------------------- V_hist (passes >= 1)
@@ -192,92 +190,114 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
              const uint32_t* __restrict__ hist, uint32_t ntiles,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout) {
   __shared__ ScatterLDS S;
+  __shared__ uint64_t sh[8];
   const uint32_t R = D.R;
   constexpr int PER = TILE / 4 / 64;     // 8 elements per lane
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const uint64_t tile0 = (uint64_t)blockIdx.x * TILE;
   const uint32_t wbase = (uint32_t)wave * (TILE / 4);
-  uint64_t key[PER];
-  uint32_t ps[PER], dg[PER];
-  bool act[PER];
-  if (FROM_SEQ) {
-    stage_tile(seq, L, (int64_t)tile0 - HALO, S.st, aligned != 0);
-    __syncthreads();
-  }
   const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
-#pragma unroll
-  for (int c = 0; c < PER; ++c) {
-    const uint32_t w = wbase + (uint32_t)c * 64 + lane;     // element index inside the tile
-    const uint64_t e = tile0 + w;
-    key[c] = 0;
+  // persistent workgroups: the next tile's inputs are in flight while this one is processed
+  uint64_t nkey[PER];
+  uint32_t npos[PER];
+  uint4 nchars = make_uint4(0u, 0u, 0u, 0u);
+  auto prefetch = [&](uint32_t t) {
+    const uint64_t t0 = (uint64_t)t * TILE;
     if (FROM_SEQ) {
-      act[c] = e < n && window_key(S.st, HALO + (int)w, (int64_t)e, L, k, key[c]);
-      ps[c] = (uint32_t)(e + 1);
+      nchars = stage_load(seq, L, (int64_t)t0 - HALO, aligned != 0);
     } else {
-      act[c] = e < n;
-      key[c] = act[c] ? kin[e] : 0;
-      ps[c] = act[c] ? pin[e] : 0;
-    }
-    dg[c] = act[c] ? digit_of(key[c], g.nb, D) : 0;
-  }
-  for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
-  wave_sync();
 #pragma unroll
-  for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
-    if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
-  __syncthreads();
-  // tile-local digit starts: thread t owns digits [4t, 4t+4)
-  __shared__ uint64_t sh[8];
-  uint32_t dsum[4];
-  uint64_t own = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t d = threadIdx.x * 4 + q;
-    dsum[q] = d < R ? S.wc[0][d] + S.wc[1][d] + S.wc[2][d] + S.wc[3][d] : 0u;
-    own += dsum[q];
-  }
-  uint64_t tile_n;
-  uint32_t run = (uint32_t)block_excl_scan(own, sh, tile_n);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t d = threadIdx.x * 4 + q;
-    if (d < R) {
-      S.tstart[d] = run;
-      S.gbase[d] = hist[(size_t)d * ntiles + blockIdx.x];
-      uint32_t cur = run;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const uint32_t t = S.wc[w][d];
-        S.wc[w][d] = cur;
-        cur += t;
+      for (int c = 0; c < PER; ++c) {
+        const uint64_t e = t0 + wbase + (uint32_t)c * 64 + lane;
+        nkey[c] = e < n ? kin[e] : 0;
+        npos[c] = e < n ? pin[e] : 0;
       }
-      run += dsum[q];
     }
-  }
-  __syncthreads();
+  };
+  uint32_t tile = blockIdx.x;
+  if (tile < ntiles) prefetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const uint64_t tile0 = (uint64_t)tile * TILE;
+    uint64_t key[PER];
+    uint32_t ps[PER], dg[PER];
+    bool act[PER];
+    if (FROM_SEQ) {
+      stage_pack(nchars, S.st);
+    } else {
 #pragma unroll
-  for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
-    const uint64_t grp = match_bits(dg[c], D.nbits, act[c]);
-    const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
-    uint32_t cur = 0;
-    if (act[c] && leader == lane) {
-      cur = S.wc[wave][dg[c]];
-      S.wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
+      for (int c = 0; c < PER; ++c) { key[c] = nkey[c]; ps[c] = npos[c]; }
     }
-    cur = __shfl(cur, leader);
-    wave_sync();
-    if (act[c]) {
-      const uint32_t ld = cur + (uint32_t)__popcll(grp & lanemask_lt());
-      S.skey[ld] = key[c];
-      S.spos[ld] = ps[c];
-      S.sdst[ld] = S.gbase[dg[c]] + (ld - S.tstart[dg[c]]);
+    if (tile + gridDim.x < ntiles) prefetch(tile + gridDim.x);
+    for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
+    __syncthreads();                       // stage packed; previous tile's write-out done
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t w = wbase + (uint32_t)c * 64 + lane;     // element index inside the tile
+      const uint64_t e = tile0 + w;
+      if (FROM_SEQ) {
+        key[c] = 0;
+        act[c] = e < n && window_key(S.st, HALO + (int)w, (int64_t)e, L, k, key[c]);
+        ps[c] = (uint32_t)(e + 1);
+      } else {
+        act[c] = e < n;
+      }
+      dg[c] = act[c] ? digit_of(key[c], g.nb, D) : 0;
     }
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < (uint32_t)tile_n; i += BLOCK) {
-    const uint32_t dst = S.sdst[i];
-    kout[dst] = S.skey[i];
-    pout[dst] = S.spos[i];
+#pragma unroll
+    for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
+      if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
+    __syncthreads();
+    // tile-local digit starts: thread t owns digits [4t, 4t+4)
+    uint32_t dsum[4];
+    uint64_t own = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t d = threadIdx.x * 4 + q;
+      dsum[q] = d < R ? S.wc[0][d] + S.wc[1][d] + S.wc[2][d] + S.wc[3][d] : 0u;
+      own += dsum[q];
+    }
+    uint64_t tile_n;
+    uint32_t run = (uint32_t)block_excl_scan(own, sh, tile_n);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t d = threadIdx.x * 4 + q;
+      if (d < R) {
+        S.tstart[d] = run;
+        S.gbase[d] = hist[(size_t)d * ntiles + tile];
+        uint32_t cur = run;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const uint32_t t = S.wc[w][d];
+          S.wc[w][d] = cur;
+          cur += t;
+        }
+        run += dsum[q];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
+      const uint64_t grp = match_bits(dg[c], D.nbits, act[c]);
+      const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
+      uint32_t cur = 0;
+      if (act[c] && leader == lane) {
+        cur = S.wc[wave][dg[c]];
+        S.wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
+      }
+      cur = __shfl(cur, leader);
+      wave_sync();
+      if (act[c]) {
+        const uint32_t ld = cur + (uint32_t)__popcll(grp & lanemask_lt());
+        S.skey[ld] = key[c];
+        S.spos[ld] = ps[c];
+        S.sdst[ld] = S.gbase[dg[c]] + (ld - S.tstart[dg[c]]);
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (uint32_t)tile_n; i += BLOCK) {
+      const uint32_t dst = S.sdst[i];
+      kout[dst] = S.skey[i];
+      pout[dst] = S.spos[i];
+    }
   }
 }
 
@@ -462,15 +482,16 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   STAMP(b, 6);
 }
 
-// V_stats: reduce the per-bucket partials (one workgroup).
-__global__ void __launch_bounds__(1024)
+// V_stats: reduce the per-bucket partials (grid-stride, one atomic per workgroup; meta is
+// zeroed before the build).
+__global__ void __launch_bounds__(BLOCK)
 k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __restrict__ n_valid,
            BuildMeta* __restrict__ meta) {
-  __shared__ uint64_t su[16], sp[16];
-  __shared__ uint32_t sm[16];
+  __shared__ uint64_t su[4], sp[4];
+  __shared__ uint32_t sm[4];
   uint64_t u = 0, p = 0;
   uint32_t m = 0;
-  for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
+  for (uint32_t b = blockIdx.x * BLOCK + threadIdx.x; b < nb; b += gridDim.x * BLOCK) {
     const BucketStats x = bs[b];
     u += x.n_kmers;
     p += x.n_pairs;
@@ -485,12 +506,13 @@ k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __re
   if (lane_id() == 0) { su[w] = u; sp[w] = p; sm[w] = m; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    u = su[0]; p = sp[0]; m = sm[0];
-    for (int i = 1; i < 16; ++i) { u += su[i]; p += sp[i]; m = max(m, sm[i]); }
-    meta->n_kmers = u;
-    meta->n_pairs = p;
-    meta->max_count = m;
-    meta->n_positions = *n_valid;
+    u = su[0] + su[1] + su[2] + su[3];
+    p = sp[0] + sp[1] + sp[2] + sp[3];
+    m = max(max(sm[0], sm[1]), max(sm[2], sm[3]));
+    if (u) atomicAdd((unsigned long long*)&meta->n_kmers, (unsigned long long)u);
+    if (p) atomicAdd((unsigned long long*)&meta->n_pairs, (unsigned long long)p);
+    if (m) atomicMax(&meta->max_count, m);
+    if (blockIdx.x == 0) meta->n_positions = *n_valid;
   }
 }
 
@@ -499,6 +521,18 @@ void set_stamp_buffer(uint64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps
 #endif
 
 // ---------------------------------------------------------------- launchers
+// Persistent grids: as many workgroups as are resident at once (CUs x the occupancy the
+// kernel's VGPR/LDS budget allows), so no workgroup waits for another to finish.
+static unsigned resident_blocks(const void* kernel) {
+  int dev = 0, cus = 256, per = 1;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, BLOCK, 0) != hipSuccess || per < 1)
+    per = 1;
+  return (unsigned)(cus > 0 ? cus : 256) * (unsigned)per;
+}
+
+
 static inline unsigned grid_of(uint64_t n, unsigned per) {
   uint64_t g = (n + per - 1) / per;
   return (unsigned)(g ? g : 1);
@@ -513,8 +547,7 @@ void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, h
   const uint32_t nt = grid_of(n, TILE);
   hipLaunchKernelGGL(k_tile_sum_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, tsum);
   launch_scan_tiles_u64(tsum, nt, tsum + nt, s);
-  hipLaunchKernelGGL(k_tile_scan_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, tsum);
-  hipLaunchKernelGGL(k_copy_total, dim3(1), dim3(64), 0, s, tsum + nt, total);
+  hipLaunchKernelGGL(k_tile_scan_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, tsum, total);
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     uint32_t ntiles, hipStream_t s) {
@@ -523,13 +556,15 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                            uint32_t* pout, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_scatter<true>, dim3(ntiles), dim3(BLOCK), 0, s, seq, L, k, Nw,
+  static unsigned cap = resident_blocks((const void*)k_v2_scatter<true>);
+  hipLaunchKernelGGL(k_v2_scatter<true>, dim3(ntiles < cap ? ntiles : cap), dim3(BLOCK), 0, s, seq, L, k, Nw,
                      aligned ? 1 : 0, nullptr, nullptr, nullptr, g, D, hist, ntiles, kout, pout);
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                        uint32_t* pout, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_scatter<false>, dim3(ntiles), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
+  static unsigned cap = resident_blocks((const void*)k_v2_scatter<false>);
+  hipLaunchKernelGGL(k_v2_scatter<false>, dim3(ntiles < cap ? ntiles : cap), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
                      (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ntiles, kout, pout);
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
@@ -546,7 +581,9 @@ void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t*
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_stats, dim3(1), dim3(1024), 0, s, bstats, nb, n_valid, meta);
+  unsigned gr = grid_of(nb, BLOCK * 8);
+  if (gr > 64) gr = 64;
+  hipLaunchKernelGGL(k_v2_stats, dim3(gr), dim3(BLOCK), 0, s, bstats, nb, n_valid, meta);
 }
 
 }  // namespace kmhg

@@ -119,6 +119,32 @@ __device__ __forceinline__ void pack16(const uint8_t* c, uint32_t& code, uint32_
   code = cd; nb = n;
 }
 
+// Split form for software pipelining: stage_load fetches this thread's 16-char chunk of the
+// stage (thread t < STAGE_W16) into registers; stage_pack encodes it into LDS later.
+__device__ __forceinline__ uint4 stage_load(const uint8_t* __restrict__ seq, int64_t L,
+                                            int64_t base, bool aligned) {
+  uint4 v = make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu);   // "NNNN..."
+  const int w = threadIdx.x;
+  if (w >= STAGE_W16) return v;
+  const int64_t c0 = base + 16 * (int64_t)w;
+  if (aligned && c0 >= 0 && c0 + 16 <= L) return *reinterpret_cast<const uint4*>(seq + c0);
+  uint8_t* b = reinterpret_cast<uint8_t*>(&v);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t p = c0 + i;
+    if (p >= 0 && p < L) b[i] = seq[p];
+  }
+  return v;
+}
+__device__ __forceinline__ void stage_pack(uint4 v, Stage& st) {
+  const int w = threadIdx.x;
+  if (w >= STAGE_W16) return;
+  uint32_t cd, nb;
+  pack16(reinterpret_cast<const uint8_t*>(&v), cd, nb);
+  st.code[w] = cd;
+  st.nbit[w] = nb;
+}
+
 __device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ seq, int64_t L,
                                            int64_t base, Stage& st, bool aligned) {
   for (int w = threadIdx.x; w < STAGE_W16; w += BLOCK) {

@@ -102,10 +102,14 @@ class DevicePool {
     if (!p) return;
     hipEvent_t ev = nullptr;
     if (ordered) {
-      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
-          hipEventRecord(ev, stream) != hipSuccess) {
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!events_.empty()) { ev = events_.back(); events_.pop_back(); }
+      }
+      if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+      if (!ev || hipEventRecord(ev, stream) != hipSuccess) {
         (void)hipStreamSynchronize(stream);
-        if (ev) (void)hipEventDestroy(ev);
+        if (ev) { std::lock_guard<std::mutex> g(mu_); events_.push_back(ev); }
         ev = nullptr;
       }
     }
@@ -124,7 +128,7 @@ class DevicePool {
     std::lock_guard<std::mutex> g(mu_);
     for (auto& pd : pending_) {
       (void)hipEventSynchronize(pd.ev);
-      (void)hipEventDestroy(pd.ev);
+      events_.push_back(pd.ev);
       free_[pd.key].push_back(pd.p);
     }
     pending_.clear();
@@ -148,7 +152,7 @@ class DevicePool {
   void poll_pending() {
     for (size_t i = 0; i < pending_.size();) {
       if (hipEventQuery(pending_[i].ev) == hipSuccess) {
-        (void)hipEventDestroy(pending_[i].ev);
+        events_.push_back(pending_[i].ev);          // recycled: no create/destroy per release
         free_[pending_[i].key].push_back(pending_[i].p);
         cached_ += pending_[i].key.second;
         pending_[i] = pending_.back();
@@ -171,6 +175,7 @@ class DevicePool {
   std::map<std::pair<int, size_t>, std::vector<void*>> free_;
   std::map<void*, std::pair<int, size_t>> live_;
   std::vector<Pending> pending_;
+  std::vector<hipEvent_t> events_;
   size_t cached_ = 0;
 };
 
@@ -208,6 +213,7 @@ struct Timing {
     return t;
   }
   bool on = false;
+  std::string only;                   // record just this kernel (empty = every kernel)
   struct Rec { std::string name; hipEvent_t a, b; };
   std::vector<Rec> recs;
   std::map<std::string, std::pair<int64_t, double>> acc;
@@ -221,12 +227,17 @@ struct Timing {
   hipEvent_t take() {
     if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
     hipEvent_t e;
-    HIPC(hipEventCreate(&e));
+    // timing-only events: no system-scope fence (a default event writes back / invalidates the
+    // caches at every record, ~10 us of dead time between the kernels it brackets)
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
+      (void)hipGetLastError();
+      HIPC(hipEventCreate(&e));
+    }
     return e;
   }
   template <class F>
   void run(const char* name, hipStream_t s, F&& launch) {
-    if (!on) { launch(); HIPC(hipGetLastError()); return; }
+    if (!on || (!only.empty() && only != name)) { launch(); HIPC(hipGetLastError()); return; }
     hipEvent_t a, b;
     {
       std::lock_guard<std::mutex> g(mu);
@@ -292,6 +303,7 @@ struct Canon {              // canonical (first-occurrence) readout order, built
 struct kmhg_index {
   int k = 0;
   int device = 0;
+  hipStream_t stream = nullptr;   // last stream the index was used on (ordered release)
   int64_t L = 0;
   Geom geom{1, 1};             // nb buckets x capb slots (+1 side slot)
   uint64_t U = 0, N = 0, P = 0;
@@ -343,6 +355,7 @@ void check_query_args(size_t L, int k) {
 // ---------------------------------------------------------------------------- build
 kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
   auto idx = std::make_unique<kmhg_index>();
+  idx->stream = s;
   HIPC(hipGetDevice(&idx->device));
   idx->k = k;
   idx->L = L;
@@ -392,6 +405,7 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 // sub-table overflows (never observed: distinct keys per bucket ~ Binomial, mean <= V2_BW).
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
   auto idx = std::make_unique<kmhg_index>();
+  idx->stream = s;
   HIPC(hipGetDevice(&idx->device));
   idx->k = k;
   idx->L = L;
@@ -499,6 +513,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   auto q = std::make_unique<kmhg_query>();
   q->device = idx->device;
   q->stream = s;
+  idx->stream = s;
   const int64_t Nw = w1 - w0;
   if (Nw <= 0) return q.release();
   const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
@@ -524,6 +539,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
 
 // ---------------------------------------------------------------------------- readout
 void prepare_canon(kmhg_index* idx, hipStream_t s) {
+  idx->stream = s;
   Canon& c = idx->canon;
   if (c.ready) return;
   const int64_t L = idx->L;
@@ -622,7 +638,14 @@ int kmhg_free(kmhg_index* idx) {
   return guarded([&] {
     if (!idx) return;
     DeviceGuard g(idx->device);
-    HIPC(hipDeviceSynchronize());            // queued readouts/queries may still read it
+    // stream-ordered release: the buffers return to the pool once work queued on the index's
+    // last stream has finished (queries on other streams are synchronised by their callers)
+    idx->table.bind(idx->stream);
+    idx->positions.bind(idx->stream);
+    idx->canon.perm.bind(idx->stream);
+    idx->canon.canon_off.bind(idx->stream);
+    idx->canon.pkeys.bind(idx->stream);
+    idx->canon.pair_off.bind(idx->stream);
     delete idx;
   });
 }
@@ -824,6 +847,10 @@ int kmhg_image_import(const int64_t header[8], const void* d_table, const void* 
 int kmhg_timing_enable(int on) {
   Timing::get().on = on != 0;
   return KMHG_OK;
+}
+
+int kmhg_timing_select(const char* kernel) {
+  return guarded([&] { Timing::get().only = kernel ? kernel : ""; });
 }
 
 int kmhg_timing_reset(void) {

@@ -171,6 +171,11 @@ def timing_enable(on: bool = True):
     _lib.check(_lib.lib().kmhg_timing_enable(1 if on else 0))
 
 
+def timing_select(kernel: str | None):
+    """Record events only around `kernel` (None = every kernel)."""
+    _lib.check(_lib.lib().kmhg_timing_select(kernel.encode() if kernel else None))
+
+
 def timing_reset():
     _lib.check(_lib.lib().kmhg_timing_reset())
 
