@@ -21,6 +21,7 @@
 // A bucket's windows are exactly its keys' positions, so the CSR slice of bucket b is
 // [start[b], start[b+1]) of `positions` with no global coordination.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include "kmhg_common.h"
 #include "kmhg_device.h"
 #include "kmhg_kernels.h"
@@ -87,22 +88,23 @@ __device__ __forceinline__ uint64_t match_bits(uint32_t v, int nbits, bool act) 
 // first scatter pass re-reads the chars (1 B/window) instead of a 12 B/window key stream.
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned, Geom g,
-           Digit D, uint32_t* __restrict__ hist, uint32_t ntiles) {
-  __shared__ Stage st;
+           Digit D, uint32_t* __restrict__ hist, uint32_t ntiles, int remap) {
+  __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
-  const int64_t tile0 = (int64_t)blockIdx.x * TILE;
+  const uint32_t tile = remap ? xcd_remap(blockIdx.x, ntiles) : blockIdx.x;
+  const int64_t tile0 = (int64_t)tile * PTILE;
   for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) lh[d] = 0;
-  stage_tile(seq, L, tile0 - HALO, st, aligned != 0);
+  stage_tile<true>(seq, L, tile0 - HALO, st, true);
   __syncthreads();
-#pragma unroll 2
-  for (int j = 0; j < WPT; ++j) {
+#pragma unroll 4
+  for (int j = 0; j < PWPT; ++j) {
     const int w = j * BLOCK + threadIdx.x;
     const int64_t s = tile0 + w;
     uint64_t key = 0;
     if (s < Nw && window_key(st, HALO + w, s, L, k, key)) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) hist[(size_t)d * ntiles + blockIdx.x] = lh[d];
+  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) hist[(size_t)d * ntiles + tile] = lh[d];
 }
 
 // ---------------------------------------------------------------- V_scan (u32, exclusive)
@@ -148,25 +150,26 @@ k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict
 // ---------------------------------------------------------------- V_hist (passes >= 1)
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
-          Digit D, uint32_t* __restrict__ hist, uint32_t ntiles) {
+          Digit D, uint32_t* __restrict__ hist, uint32_t ntiles, int remap) {
   __shared__ uint32_t lh[V2_MAXR];
   const uint64_t n = *n_ptr;
+  const uint32_t tile = remap ? xcd_remap(blockIdx.x, ntiles) : blockIdx.x;
   const uint32_t R = D.R;
   for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
   __syncthreads();
-  const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
-#pragma unroll
-  for (int j = 0; j < WPT; ++j) {
+  const uint64_t t0 = (uint64_t)tile * PTILE;
+#pragma unroll 4
+  for (int j = 0; j < PWPT; ++j) {
     uint64_t e = t0 + (uint64_t)j * BLOCK + threadIdx.x;
     if (e < n) atomicAdd(&lh[digit_of(keys[e], g.nb, D)], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[(size_t)d * ntiles + blockIdx.x] = lh[d];
+  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[(size_t)d * ntiles + tile] = lh[d];
 }
 
 // ---------------------------------------------------------------- V_scatter (stable)
-// Tile t = elements [t*TILE, (t+1)*TILE); wave w owns the contiguous 512 elements
-// [t*TILE + 512w, +512), lane l holds element 64c + l of them for c = 0..7.  Element order
+// Tile t = elements [t*PTILE, (t+1)*PTILE); wave w owns the contiguous PTILE/4 elements
+// [t*PTILE + w*PTILE/4, +PTILE/4), lane l holds element 64c + l of them.  Element order
 // inside the tile = (wave, c, lane) = input order, so ranks assigned in that order keep the
 // pass stable.  FROM_SEQ (pass 0) encodes the windows from LDS-staged chars and drops invalid
 // ones; later passes read the (key, pos) stream.  The tile is re-ordered by digit in LDS first
@@ -176,10 +179,10 @@ struct ScatterLDS {
   uint32_t wc[4][V2_MAXR];     // per-wave digit counts -> per-wave tile-local cursors
   uint32_t tstart[V2_MAXR];    // tile-local start of each digit
   uint32_t gbase[V2_MAXR];     // global start of each digit for this tile (scanned histogram)
-  uint64_t skey[TILE];
-  uint32_t spos[TILE];
-  uint32_t sdst[TILE];
-  Stage st;
+  uint64_t skey[PTILE];
+  uint32_t spos[PTILE];
+  uint32_t sdst[PTILE];
+  PStage st;
 };
 
 template <bool FROM_SEQ>
@@ -188,45 +191,65 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, uint32_t ntiles,
-             uint64_t* __restrict__ kout, uint32_t* __restrict__ pout) {
+             uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad, int remap) {
   __shared__ ScatterLDS S;
   __shared__ uint64_t sh[8];
   const uint32_t R = D.R;
-  constexpr int PER = TILE / 4 / 64;     // 8 elements per lane
+  constexpr int PER = PTILE / 4 / 64;    // elements per lane
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const uint32_t wbase = (uint32_t)wave * (TILE / 4);
+  const uint32_t wbase = (uint32_t)wave * (PTILE / 4);
   const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
   // persistent workgroups: the next tile's inputs are in flight while this one is processed
   uint64_t nkey[PER];
   uint32_t npos[PER];
-  uint4 nchars = make_uint4(0u, 0u, 0u, 0u);
-  auto prefetch = [&](uint32_t t) {
-    const uint64_t t0 = (uint64_t)t * TILE;
+  StageRegs<PSTAGE_W16> nchars;
+  uint32_t ngb[4];                         // the tile's scanned-histogram entries, digits 4t..4t+3
+  // virtual tile v = i * gridDim + blockIdx; with `remap` every XCD walks one contiguous range
+  auto tile_of = [&](uint32_t v) { return remap ? xcd_remap(v, ntiles) : v; };
+  auto prefetch = [&](uint32_t v) {
+    const uint32_t tv = tile_of(v);
+    const uint64_t t0 = (uint64_t)tv * PTILE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {             // unconditional (clamped) loads: static count
+      const uint32_t d = min(threadIdx.x * 4 + q, R - 1);
+      ngb[q] = hist[(size_t)d * ntiles + tv];
+    }
     if (FROM_SEQ) {
-      nchars = stage_load(seq, L, (int64_t)t0 - HALO, aligned != 0);
+      stage_load<PSTAGE_W16, true>(nchars, seq, L, (int64_t)t0 - HALO, true);
     } else {
 #pragma unroll
-      for (int c = 0; c < PER; ++c) {
+      for (int c = 0; c < PER; ++c) {      // e < ntiles * PTILE <= n_max + pad: in bounds
         const uint64_t e = t0 + wbase + (uint32_t)c * 64 + lane;
-        nkey[c] = e < n ? kin[e] : 0;
-        npos[c] = e < n ? pin[e] : 0;
+        nkey[c] = kin[e];
+        npos[c] = pin[e];
       }
     }
   };
-  uint32_t tile = blockIdx.x;
-  if (tile < ntiles) prefetch(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
-    const uint64_t tile0 = (uint64_t)tile * TILE;
+  // Every path into the loop top has [prefetch loads][PTILE/BLOCK x 2 stores] in flight, so the
+  // compiler waits for the prefetch with a counted vmcnt: the pad stores below stand in for the
+  // previous tile's write-out on the first iteration.
+  uint32_t vt = blockIdx.x;              // grid <= ntiles
+  prefetch(vt);
+#pragma unroll
+  for (int j = 0; j < PTILE / BLOCK; ++j) {
+    kout[pad + threadIdx.x] = 0;
+    pout[pad + threadIdx.x] = 0;
+  }
+  for (; vt < ntiles; vt += gridDim.x) {
+    const uint32_t tile = tile_of(vt);
+    const uint64_t tile0 = (uint64_t)tile * PTILE;
     uint64_t key[PER];
-    uint32_t ps[PER], dg[PER];
+    uint32_t ps[PER], dg[PER], gb[4];
     bool act[PER];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gb[q] = ngb[q];
     if (FROM_SEQ) {
       stage_pack(nchars, S.st);
     } else {
 #pragma unroll
       for (int c = 0; c < PER; ++c) { key[c] = nkey[c]; ps[c] = npos[c]; }
     }
-    if (tile + gridDim.x < ntiles) prefetch(tile + gridDim.x);
+    prefetch(min(vt + gridDim.x, ntiles - 1));   // unconditional: static vmcnt
     for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
     __syncthreads();                       // stage packed; previous tile's write-out done
 #pragma unroll
@@ -262,7 +285,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       const uint32_t d = threadIdx.x * 4 + q;
       if (d < R) {
         S.tstart[d] = run;
-        S.gbase[d] = hist[(size_t)d * ntiles + tile];
+        S.gbase[d] = gb[q];
         uint32_t cur = run;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -293,8 +316,14 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < (uint32_t)tile_n; i += BLOCK) {
-      const uint32_t dst = S.sdst[i];
+    // a static count of store instructions per lane (masked, fully unrolled), so the wait for
+    // the next tile's prefetched loads at the loop top is vmcnt(#stores), not vmcnt(0): the
+    // prefetch was issued before these stores and must not queue behind their completion
+#pragma unroll
+    for (int j = 0; j < PTILE / BLOCK; ++j) {
+      const uint32_t i = (uint32_t)(j * BLOCK) + threadIdx.x;
+      // lanes past the tile's end store into the PTILE-element pad behind the outputs
+      const uint32_t dst = i < (uint32_t)tile_n ? S.sdst[i] : pad + threadIdx.x;
       kout[dst] = S.skey[i];
       pout[dst] = S.spos[i];
     }
@@ -350,14 +379,14 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
             const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
             int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
-            BuildMeta* __restrict__ meta) {
+            BuildMeta* __restrict__ meta, int remap) {
   __shared__ WaveTable wt[4];
   constexpr int PER = 2 * V2_BW / 64;             // elements per lane per batch (2x mean)
   const int wave = threadIdx.x >> 6, lane = lane_id();
   WaveTable& W = wt[wave];
   // buckets are independent: no ordering, no ticket (one shared counter would serialise
   // ~88 grabs/us chip-wide -- MI355X_MICROARCH.md "dequeue")
-  const uint32_t b = blockIdx.x * 4 + wave;
+  const uint32_t b = (remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x) * 4 + wave;
   if (b >= g.nb) return;
   STAMP(b, 0);
   for (uint32_t j = lane; j <= V2_CAPB; j += 64)
@@ -533,6 +562,24 @@ static unsigned resident_blocks(const void* kernel) {
 }
 
 
+// XCD-contiguous tile mapping (xcd_remap), on unless KMHG_XCD=0 (A/B switch for profiling)
+static int xcd_map() {
+  static int on = [] {
+    const char* e = std::getenv("KMHG_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
+// the bucket kernel's writes are whole sub-tables: remapped only with KMHG_XCD_BUCKET=1
+static int xcd_map_bucket() {
+  static int on = [] {
+    const char* e = std::getenv("KMHG_XCD_BUCKET");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return on;
+}
+
 static inline unsigned grid_of(uint64_t n, unsigned per) {
   uint64_t g = (n + per - 1) / per;
   return (unsigned)(g ? g : 1);
@@ -541,7 +588,7 @@ static inline unsigned grid_of(uint64_t n, unsigned per) {
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
                      Digit D, uint32_t* hist, uint32_t ntiles, hipStream_t s) {
   hipLaunchKernelGGL(k_v2_hist0, dim3(ntiles), dim3(BLOCK), 0, s, seq, L, k, Nw,
-                     aligned ? 1 : 0, g, D, hist, ntiles);
+                     aligned ? 1 : 0, g, D, hist, ntiles, xcd_map());
 }
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);
@@ -551,21 +598,21 @@ void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, h
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     uint32_t ntiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_hist, dim3(ntiles), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist, ntiles);
+  hipLaunchKernelGGL(k_v2_hist, dim3(ntiles), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist, ntiles, xcd_map());
 }
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                           uint32_t* pout, hipStream_t s) {
+                           uint32_t* pout, uint32_t pad, hipStream_t s) {
   static unsigned cap = resident_blocks((const void*)k_v2_scatter<true>);
   hipLaunchKernelGGL(k_v2_scatter<true>, dim3(ntiles < cap ? ntiles : cap), dim3(BLOCK), 0, s, seq, L, k, Nw,
-                     aligned ? 1 : 0, nullptr, nullptr, nullptr, g, D, hist, ntiles, kout, pout);
+                     aligned ? 1 : 0, nullptr, nullptr, nullptr, g, D, hist, ntiles, kout, pout, pad, xcd_map());
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                       uint32_t* pout, hipStream_t s) {
+                       uint32_t* pout, uint32_t pad, hipStream_t s) {
   static unsigned cap = resident_blocks((const void*)k_v2_scatter<false>);
   hipLaunchKernelGGL(k_v2_scatter<false>, dim3(ntiles < cap ? ntiles : cap), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
-                     (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ntiles, kout, pout);
+                     (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ntiles, kout, pout, pad, xcd_map());
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s) {
@@ -577,7 +624,7 @@ void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t*
                       Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                       hipStream_t s) {
   hipLaunchKernelGGL(k_v2_bucket, dim3(grid_of(g.nb, 4)), dim3(BLOCK), 0, s, keys, pos, start, g,
-                     T, positions, bstats, meta);
+                     T, positions, bstats, meta, xcd_map_bucket());
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, hipStream_t s) {

@@ -37,6 +37,12 @@ constexpr int TILE = BLOCK * WPT;          // windows per workgroup
 constexpr int HALO = 32;                   // chars staged before/after the tile (k <= 32)
 constexpr int STAGE = TILE + 2 * HALO + 16;  // chars staged per workgroup (+16: base aligned down)
 constexpr int STAGE_W16 = STAGE / 16;      // 16-char words staged
+// Partition tile of the radix passes of the partitioned build (longer digit runs per tile ->
+// longer contiguous scatter writes)
+constexpr int PWPT = 8;
+constexpr int PTILE = BLOCK * PWPT;
+constexpr int PSTAGE = PTILE + 2 * HALO + 16;
+constexpr int PSTAGE_W16 = PSTAGE / 16;
 
 // murmur3 fmix64: keys are structured (2-bit packed DNA); khash's (key>>33)^key^(key<<11)
 // truncated to 32 bits is weak on them (SURVEY.md §7 "Random-access hash traffic").

@@ -26,6 +26,16 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
   return v;
 }
 
+// XCD-contiguous work mapping: a bijection of [0, n) that gives the blocks of one XCD (blocks
+// are dealt round-robin, b and b + 8 share an XCD -- MI355X_MICROARCH.md "Workgroup dispatch")
+// one contiguous range of work items.  Neighbouring tiles then write the partial cache lines at
+// their shared output boundaries through the SAME L2, which merges them before write-back,
+// instead of two XCDs each writing back a partial line.  Speed only: any placement is correct.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
+  const uint32_t q = n >> 3, r = n & 7u, x = b & 7u, j = b >> 3;
+  return x * q + (x < r ? x : r) + j;
+}
+
 // Exclusive scan over the 256 threads of a block (one value per thread).  `lds` needs 5 u64.
 __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* lds, uint64_t& total) {
   const int wid = threadIdx.x >> 6;
@@ -103,10 +113,14 @@ __device__ __forceinline__ uint32_t take_ticket(uint32_t* counter, uint32_t* lds
 // aligned) and packed into 2-bit codes (MSB-first, 16 chars per u32) and N flags (16 chars per
 // u16 kept in a u32).  Chars outside [0, L) are flagged N: a window that touches them is never
 // valid, and position -1 acting as N gives the reference's "start of sequence" rule.
-struct Stage {
-  uint32_t code[STAGE_W16];
-  uint32_t nbit[STAGE_W16];
+template <int W16>
+struct StageN {
+  static constexpr int kWords = W16;
+  uint32_t code[W16];
+  uint32_t nbit[W16];
 };
+using Stage = StageN<STAGE_W16>;             // one TILE of windows
+using PStage = StageN<PSTAGE_W16>;           // one partition tile (PTILE windows)
 
 __device__ __forceinline__ void pack16(const uint8_t* c, uint32_t& code, uint32_t& nb) {
   uint32_t cd = 0, n = 0;
@@ -119,58 +133,97 @@ __device__ __forceinline__ void pack16(const uint8_t* c, uint32_t& code, uint32_
   code = cd; nb = n;
 }
 
-// Split form for software pipelining: stage_load fetches this thread's 16-char chunk of the
-// stage (thread t < STAGE_W16) into registers; stage_pack encodes it into LDS later.
-__device__ __forceinline__ uint4 stage_load(const uint8_t* __restrict__ seq, int64_t L,
-                                            int64_t base, bool aligned) {
-  uint4 v = make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu);   // "NNNN..."
-  const int w = threadIdx.x;
-  if (w >= STAGE_W16) return v;
+__device__ __forceinline__ void pack16v(uint4 v, uint32_t& code, uint32_t& nb) {
+  const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+  uint32_t cd = 0, n = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t ch = (wv[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    cd = (cd << 2) | ((ch >> 1) & 3u);       // UPDATE_OFFSET, src/kmer_util.h:8
+    n = (n << 1) | (((ch | 0x20u) == 'n') ? 1u : 0u);   // LC(c)=='n', src/kmer_util.h:10
+  }
+  code = cd; nb = n;
+}
+
+// One 16-char word of the stage (word w starts at char base + 16 w), loaded coalesced when the
+// sequence is 16-B aligned; chars outside [0, L) read as 'N'.
+__device__ __forceinline__ uint4 stage_word(const uint8_t* __restrict__ seq, int64_t L,
+                                            int64_t base, int w, bool aligned) {
   const int64_t c0 = base + 16 * (int64_t)w;
-  if (aligned && c0 >= 0 && c0 + 16 <= L) return *reinterpret_cast<const uint4*>(seq + c0);
-  uint8_t* b = reinterpret_cast<uint8_t*>(&v);
+  if (aligned) {
+    // exactly ONE 16-B load on every path (a static vector-memory count lets the compiler wait
+    // for it with a counted vmcnt in pipelined loops).  c0 % 16 == 0 and the chunk never leaves
+    // the 16-B aligned block of a valid byte, so it cannot touch an unmapped page; chunks wholly
+    // outside [0, L) load chunk 0 instead and read as 'N'.
+    const bool any = c0 + 16 > 0 && c0 < L;
+    uint4 v = *reinterpret_cast<const uint4*>(seq + (any ? c0 : 0));
+    if (!any) return make_uint4(0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu);
+    if (c0 < 0 || c0 + 16 > L) {
+      uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t p = c0 + i;
+        if (p < 0 || p >= L) x[i >> 2] = (x[i >> 2] & ~(0xFFu << (8 * (i & 3)))) | (0x4Eu << (8 * (i & 3)));
+      }
+      v = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    return v;
+  }
+  uint32_t x[4] = {0u, 0u, 0u, 0u};          // register-only byte assembly (no private array)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int64_t p = c0 + i;
-    if (p >= 0 && p < L) b[i] = seq[p];
+    const uint32_t ch = (p >= 0 && p < L) ? (uint32_t)seq[p] : (uint32_t)'N';
+    x[i >> 2] |= ch << (8 * (i & 3));
   }
-  return v;
-}
-__device__ __forceinline__ void stage_pack(uint4 v, Stage& st) {
-  const int w = threadIdx.x;
-  if (w >= STAGE_W16) return;
-  uint32_t cd, nb;
-  pack16(reinterpret_cast<const uint8_t*>(&v), cd, nb);
-  st.code[w] = cd;
-  st.nbit[w] = nb;
+  return make_uint4(x[0], x[1], x[2], x[3]);
 }
 
-__device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ seq, int64_t L,
-                                           int64_t base, Stage& st, bool aligned) {
-  for (int w = threadIdx.x; w < STAGE_W16; w += BLOCK) {
-    int64_t c0 = base + 16 * (int64_t)w;
-    uint8_t buf[16];
-    if (aligned && c0 >= 0 && c0 + 16 <= L) {
-      uint4 v = *reinterpret_cast<const uint4*>(seq + c0);
-      *reinterpret_cast<uint4*>(buf) = v;
-    } else {
+// Split form for software pipelining: stage_load fetches this thread's 16-char words of the
+// stage (word threadIdx.x + j * BLOCK) into registers; stage_pack encodes them into LDS later.
+template <int W16>
+struct StageRegs {
+  static constexpr int kPer = (W16 + BLOCK - 1) / BLOCK;
+  uint4 v[kPer];
+};
+// ALWAYS_ALIGNED: the caller guarantees a 16-B aligned sequence (the partitioned build copies
+// an unaligned input first), so the byte-wise path is not even compiled in.
+template <int W16, bool ALWAYS_ALIGNED = false>
+__device__ __forceinline__ void stage_load(StageRegs<W16>& r, const uint8_t* __restrict__ seq,
+                                           int64_t L, int64_t base, bool aligned) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        int64_t p = c0 + i;
-        buf[i] = (p >= 0 && p < L) ? seq[p] : (uint8_t)'N';
-      }
-    }
-    uint32_t cd, nb;
-    pack16(buf, cd, nb);
-    st.code[w] = cd;
-    st.nbit[w] = nb;
+  for (int j = 0; j < StageRegs<W16>::kPer; ++j) {   // clamped word: one load on every path
+    const int w = min((int)threadIdx.x + j * BLOCK, W16 - 1);
+    r.v[j] = stage_word(seq, L, base, w, ALWAYS_ALIGNED || aligned);
   }
+}
+template <int W16>
+__device__ __forceinline__ void stage_pack(const StageRegs<W16>& r, StageN<W16>& st) {
+#pragma unroll
+  for (int j = 0; j < StageRegs<W16>::kPer; ++j) {
+    const int w = threadIdx.x + j * BLOCK;
+    if (w < W16) {
+      uint32_t cd, nb;
+      pack16v(r.v[j], cd, nb);
+      st.code[w] = cd;
+      st.nbit[w] = nb;
+    }
+  }
+}
+
+template <bool ALWAYS_ALIGNED = false, int W16>
+__device__ __forceinline__ void stage_tile(const uint8_t* __restrict__ seq, int64_t L,
+                                           int64_t base, StageN<W16>& st, bool aligned) {
+  StageRegs<W16> r;
+  stage_load<W16, ALWAYS_ALIGNED>(r, seq, L, base, aligned);
+  stage_pack(r, st);
 }
 
 // Window whose first char is stage offset o (global start s).  Returns validity per the
 // reference walk: no N in [s, s+k), s+k <= L, and NOT (s+k == L and the char
 // before s is N or s == 0) -- the end-drop quirk of init_kmer (src/kmer_pos.c:81-83).
-__device__ __forceinline__ bool window_key(const Stage& st, int o, int64_t s, int64_t L, int k,
+template <class ST>
+__device__ __forceinline__ bool window_key(const ST& st, int o, int64_t s, int64_t L, int k,
                                            uint64_t& key) {
   if (s + k > L) return false;
   // N flags of chars [o-1, o+k): k+1 <= 33 bits out of a 48-bit window of three u16 words

@@ -410,11 +410,19 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   idx->k = k;
   idx->L = L;
   const int64_t Nw = L - k + 1;
-  const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
+  // the partition kernels read the sequence as aligned 16-B words: copy an unaligned input
+  DBuf<uint8_t> aligned_copy;
+  if ((reinterpret_cast<uintptr_t>(d_seq) & 15) != 0) {
+    aligned_copy.reset((size_t)L);
+    aligned_copy.bind(s);
+    HIPC(hipMemcpyAsync(aligned_copy.p, d_seq, (size_t)L, hipMemcpyDeviceToDevice, s));
+    d_seq = aligned_copy.p;
+  }
+  const bool aligned = true;
   const uint32_t nb = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW - 1) / V2_BW);
   idx->geom = Geom{nb, V2_CAPB};
   const Geom g = idx->geom;
-  const uint32_t ntiles = tiles_for(Nw);
+  const uint32_t ntiles = (uint32_t)((Nw + PTILE - 1) / PTILE);   // partition tiles
   // radix plan: fewest passes whose radix fits LDS and whose histograms stay small
   uint32_t passes = 1, R = nb;
   for (passes = 1; passes <= 4; ++passes) {
@@ -425,8 +433,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   if (passes > 4) fail(KMHG_EOVERFLOW, "sequence too long for the partitioned build");
   const uint64_t nhist = (uint64_t)R * ntiles;
   const uint32_t scan_tiles = tiles_for(nhist);
-  DBuf<uint64_t> kA(Nw, s), kB(Nw, s);
-  DBuf<uint32_t> pA(Nw, s), pB(Nw, s);
+  DBuf<uint64_t> kA(Nw + PTILE, s), kB(Nw + PTILE, s);   // + pad (launch_v2_scatter)
+  DBuf<uint32_t> pA(Nw + PTILE, s), pB(Nw + PTILE, s);
+  const uint32_t pad = (uint32_t)Nw;
   DBuf<uint32_t> hist(nhist, s);
   DBuf<uint32_t> start((uint64_t)nb + 1, s);
   DBuf<uint64_t> tsum((size_t)scan_tiles + 1, s);     // reduce-then-scan tile sums
@@ -447,7 +456,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, tsum.p, n_valid, s));
   LAUNCH("k_v2_scatter_seq", s,
          launch_v2_scatter_seq(d_seq, L, k, Nw, aligned, g, make_digit(1, R), hist.p, ntiles,
-                               kA.p, pA.p, s));
+                               kA.p, pA.p, pad, s));
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = R;
@@ -456,7 +465,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     LAUNCH("k_v2_hist", s, launch_v2_hist(kin, n_valid, g, Dp, hist.p, ntiles, s));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, tsum.p, n_valid, s));
     LAUNCH("k_v2_scatter", s,
-           launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, s));
+           launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, pad, s));
     std::swap(kin, kout);
     std::swap(pin, pout);
     div *= R;

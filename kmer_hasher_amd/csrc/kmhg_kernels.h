@@ -81,16 +81,18 @@ inline Digit make_digit(uint32_t div, uint32_t R) {
 }
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
                      Digit D, uint32_t* hist, uint32_t ntiles, hipStream_t s);
+// The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
+// pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
 // exclusive scan of a u32 array; tsum = scratch of tiles_for(n) + 1 u64; total <- sum
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, hipStream_t s);
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     uint32_t ntiles, hipStream_t s);
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                           uint32_t* pout, hipStream_t s);
+                           uint32_t* pout, uint32_t pad, hipStream_t s);
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                       uint32_t* pout, hipStream_t s);
+                       uint32_t* pout, uint32_t pad, hipStream_t s);
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s);
 struct BucketStats {           // per-bucket partials of the build statistics

@@ -1,0 +1,32 @@
+#!/bin/bash
+# A/B timing of bench.py under environment variants (run through gpurun).
+#   bash tools/ab.sh "<env assignments A>" "<env assignments B>" ... -- [bench args]
+# Each variant runs twice, interleaved; the JSON lines land in gpurun_out/ab.log.
+set -uo pipefail
+REPO=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$REPO/gpurun_out
+mkdir -p "$OUT"
+VARS=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do VARS+=("$1"); shift; done
+[ $# -gt 0 ] && shift
+ARGS=("$@")
+[ ${#ARGS[@]} -eq 0 ] && ARGS=(--no-cpu)
+: > "$OUT/ab.log"
+for rep in 1 2; do
+  for v in "${VARS[@]}"; do
+    echo "### [$v] rep $rep" >> "$OUT/ab.log"
+    env $v timeout -k 10 240 python3 "$REPO/bench.py" "${ARGS[@]}" >> "$OUT/ab.log" 2>&1 || { echo "FAILED [$v]"; exit 1; }
+  done
+done
+python3 - "$OUT/ab.log" <<'PY'
+import json, sys
+cur = None
+for line in open(sys.argv[1]):
+    if line.startswith("###"):
+        cur = line.strip(); continue
+    if line.startswith("{"):
+        d = json.loads(line)
+        km = d.get("kernels_ms", {})
+        print(cur, "value", d["value"], "ms", d["ms_per_step"], "q", d.get("query", {}).get("value"),
+              " ".join(f"{k}={v:.4f}" for k, v in sorted(km.items())))
+PY
