@@ -21,6 +21,7 @@
 // A bucket's windows are exactly its keys' positions, so the CSR slice of bucket b is
 // [start[b], start[b+1]) of `positions` with no global coordination.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <cstdlib>
 #include "kmhg_common.h"
 #include "kmhg_device.h"
@@ -44,14 +45,11 @@ __device__ uint64_t* g_stamps;
 #endif
 
 // LDS sub-table of one bucket, private to one wave (slot V2_CAPB = side slot of key ~0).
-// 16-B AoS slots: one ds_read_b128 / ds_write_b128 per slot for init and write-out.
-struct LSlot {
-  uint64_t key;
-  uint32_t cnt;   // occurrences
-  uint32_t cur;   // CSR offset, then the running cursor of pass B
-};
+// SoA: 8-B keys (64-bit CAS on an 8-B stride touches 32 bank pairs, not 16) and {cnt, cur}
+// pairs (cnt = occurrences; cur = CSR offset, then the running cursor of pass B).
 struct WaveTable {
-  LSlot s[V2_CAPB + 1];
+  uint64_t key[V2_CAPB + 1];
+  uint2 cc[V2_CAPB + 1];
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -87,50 +85,48 @@ __device__ __forceinline__ uint64_t match_bits(uint32_t v, int nbits, bool act) 
 // histogram of the first radix digit of the windows' buckets.  Nothing else is written: the
 // first scatter pass re-reads the chars (1 B/window) instead of a 12 B/window key stream.
 __global__ void __launch_bounds__(BLOCK)
-k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned, Geom g,
-           Digit D, uint32_t* __restrict__ hist, uint32_t ntiles, int remap) {
+k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
+           uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
+           uint32_t n_status, BuildMeta* __restrict__ meta) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
-  const uint32_t tile = remap ? xcd_remap(blockIdx.x, ntiles) : blockIdx.x;
-  const int64_t tile0 = (int64_t)tile * PTILE;
+  // zero the next scan's look-back words + ticket and the build meta (no memset launches)
+  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
+    scan_status[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < sizeof(BuildMeta) / 4)
+    reinterpret_cast<uint32_t*>(meta)[threadIdx.x] = 0u;
+  const uint32_t c = remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x;
+  const uint32_t t_begin = c * ch.tpc, t_end = min(t_begin + ch.tpc, ch.ntiles);
   for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) lh[d] = 0;
-  stage_tile<true>(seq, L, tile0 - HALO, st, true);
-  __syncthreads();
+  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+    const int64_t tile0 = (int64_t)tile * PTILE;
+    __syncthreads();                           // previous tile's stage reads done
+    stage_tile<true>(seq, L, tile0 - HALO, st, true);
+    __syncthreads();
 #pragma unroll 4
-  for (int j = 0; j < PWPT; ++j) {
-    const int w = j * BLOCK + threadIdx.x;
-    const int64_t s = tile0 + w;
-    uint64_t key = 0;
-    if (s < Nw && window_key(st, HALO + w, s, L, k, key)) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
+    for (int j = 0; j < PWPT; ++j) {
+      const int w = j * BLOCK + threadIdx.x;
+      const int64_t s = tile0 + w;
+      uint64_t key = 0;
+      if (s < Nw && window_key(st, HALO + w, s, L, k, key)) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
+    }
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) hist[(size_t)d * ntiles + tile] = lh[d];
+  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) hist[(size_t)d * ch.C + c] = lh[d];
 }
 
 // ---------------------------------------------------------------- V_scan (u32, exclusive)
-// Reduce-then-scan (no tickets, no spinning): per-tile sums -> one-workgroup scan of the tile
-// sums (k_scan_tiles_u64) -> per-tile exclusive scan seeded with the tile's base.
+// Single pass: tiles in ticket order, decoupled look-back (kmhg_device.h) for the tile base.
+// `status` holds one look-back word per tile and the ticket at status[ntiles]; the preceding
+// histogram kernel zeroed them.  *total <- sum (the number of valid windows).
 __global__ void __launch_bounds__(BLOCK)
-k_tile_sum_u32(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ tsum) {
+k_scan_lb_u32(uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ status,
+              uint32_t ntiles, uint32_t* __restrict__ total) {
   __shared__ uint64_t sh[8];
-  const uint64_t base = (uint64_t)blockIdx.x * TILE;
-  uint64_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < WPT; ++j) {
-    const uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
-    if (i < n) sum += a[i];
-  }
-  uint64_t tot;
-  block_excl_scan(sum, sh, tot);
-  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
-}
-
-__global__ void __launch_bounds__(BLOCK)
-k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict__ tbase,
-                uint32_t* __restrict__ total) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *total = (uint32_t)tbase[gridDim.x];
-  __shared__ uint64_t sh[8];
-  const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)threadIdx.x * WPT;
+  __shared__ uint32_t tk;
+  __shared__ uint64_t base_sh;
+  const uint32_t tile = take_ticket(reinterpret_cast<uint32_t*>(status + ntiles), &tk);
+  const uint64_t base = (uint64_t)tile * TILE + (uint64_t)threadIdx.x * WPT;
   uint32_t v[WPT];
   uint64_t sum = 0;
 #pragma unroll
@@ -139,7 +135,16 @@ k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict
     sum += v[j];
   }
   uint64_t tot;
-  uint64_t run = block_excl_scan(sum, sh, tot) + tbase[blockIdx.x];
+  const uint64_t ex = block_excl_scan(sum, sh, tot);
+  if (threadIdx.x < 64) {
+    const uint64_t x = lookback_excl(status, tile, tot);
+    if (threadIdx.x == 0) {
+      base_sh = x;
+      if (tile == ntiles - 1) *total = (uint32_t)(x + tot);
+    }
+  }
+  __syncthreads();
+  uint64_t run = ex + base_sh;
 #pragma unroll
   for (int j = 0; j < WPT; ++j) {
     if (base + j < n) a[base + j] = (uint32_t)run;
@@ -150,21 +155,32 @@ k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict
 // ---------------------------------------------------------------- V_hist (passes >= 1)
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
-          Digit D, uint32_t* __restrict__ hist, uint32_t ntiles, int remap) {
+          Digit D, uint32_t* __restrict__ hist, Chunks ch, int remap,
+          uint64_t* __restrict__ scan_status, uint32_t n_status) {
   __shared__ uint32_t lh[V2_MAXR];
+  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
+    scan_status[i] = 0;
   const uint64_t n = *n_ptr;
-  const uint32_t tile = remap ? xcd_remap(blockIdx.x, ntiles) : blockIdx.x;
+  const uint32_t c = remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x;
+  const uint64_t e0 = (uint64_t)c * ch.tpc * PTILE;
+  const uint64_t e1 = min(n, e0 + (uint64_t)ch.tpc * PTILE);
   const uint32_t R = D.R;
   for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
   __syncthreads();
-  const uint64_t t0 = (uint64_t)tile * PTILE;
-#pragma unroll 4
-  for (int j = 0; j < PWPT; ++j) {
-    uint64_t e = t0 + (uint64_t)j * BLOCK + threadIdx.x;
-    if (e < n) atomicAdd(&lh[digit_of(keys[e], g.nb, D)], 1u);
+  for (uint64_t e = e0 + threadIdx.x; e < e1; e += 4 * BLOCK) {
+    uint32_t dg[4];
+    bool in[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {                // 4 loads in flight per lane
+      in[j] = e + j * BLOCK < e1;
+      dg[j] = in[j] ? digit_of(keys[e + j * BLOCK], g.nb, D) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (in[j]) atomicAdd(&lh[dg[j]], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[(size_t)d * ntiles + tile] = lh[d];
+  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[(size_t)d * ch.C + c] = lh[d];
 }
 
 // ---------------------------------------------------------------- V_scatter (stable)
@@ -190,7 +206,7 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned,
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
-             const uint32_t* __restrict__ hist, uint32_t ntiles,
+             const uint32_t* __restrict__ hist, Chunks ch,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad, int remap) {
   __shared__ ScatterLDS S;
   __shared__ uint64_t sh[8];
@@ -199,57 +215,55 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const uint32_t wbase = (uint32_t)wave * (PTILE / 4);
   const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
-  // persistent workgroups: the next tile's inputs are in flight while this one is processed
+  // one workgroup per chunk of consecutive tiles; with `remap` the chunks of one XCD are
+  // contiguous.  Thread t owns digits 4t..4t+3 and keeps their running output cursors in
+  // registers: each digit's output of the chunk is one contiguous run, written tile by tile.
+  const uint32_t chunk = remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x;
+  const uint32_t t_begin = chunk * ch.tpc, t_end = min(t_begin + ch.tpc, ch.ntiles);
+  uint32_t cursor[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t d = min(threadIdx.x * 4 + q, R - 1);
+    cursor[q] = hist[(size_t)d * ch.C + chunk];
+  }
+  // the next tile's inputs are in flight while this one is processed
   uint64_t nkey[PER];
   uint32_t npos[PER];
   StageRegs<PSTAGE_W16> nchars;
-  uint32_t ngb[4];                         // the tile's scanned-histogram entries, digits 4t..4t+3
-  // virtual tile v = i * gridDim + blockIdx; with `remap` every XCD walks one contiguous range
-  auto tile_of = [&](uint32_t v) { return remap ? xcd_remap(v, ntiles) : v; };
-  auto prefetch = [&](uint32_t v) {
-    const uint32_t tv = tile_of(v);
+  auto prefetch = [&](uint32_t tv) {
     const uint64_t t0 = (uint64_t)tv * PTILE;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {             // unconditional (clamped) loads: static count
-      const uint32_t d = min(threadIdx.x * 4 + q, R - 1);
-      ngb[q] = hist[(size_t)d * ntiles + tv];
-    }
     if (FROM_SEQ) {
       stage_load<PSTAGE_W16, true>(nchars, seq, L, (int64_t)t0 - HALO, true);
     } else {
 #pragma unroll
-      for (int c = 0; c < PER; ++c) {      // e < ntiles * PTILE <= n_max + pad: in bounds
-        const uint64_t e = t0 + wbase + (uint32_t)c * 64 + lane;
-        nkey[c] = kin[e];
-        npos[c] = pin[e];
+      for (int cc = 0; cc < PER; ++cc) {   // e < ntiles * PTILE <= n_max + pad: in bounds
+        const uint64_t e = t0 + wbase + (uint32_t)cc * 64 + lane;
+        nkey[cc] = kin[e];
+        npos[cc] = pin[e];
       }
     }
   };
   // Every path into the loop top has [prefetch loads][PTILE/BLOCK x 2 stores] in flight, so the
   // compiler waits for the prefetch with a counted vmcnt: the pad stores below stand in for the
   // previous tile's write-out on the first iteration.
-  uint32_t vt = blockIdx.x;              // grid <= ntiles
-  prefetch(vt);
+  prefetch(t_begin);
 #pragma unroll
   for (int j = 0; j < PTILE / BLOCK; ++j) {
     kout[pad + threadIdx.x] = 0;
     pout[pad + threadIdx.x] = 0;
   }
-  for (; vt < ntiles; vt += gridDim.x) {
-    const uint32_t tile = tile_of(vt);
+  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
     const uint64_t tile0 = (uint64_t)tile * PTILE;
     uint64_t key[PER];
-    uint32_t ps[PER], dg[PER], gb[4];
+    uint32_t ps[PER], dg[PER];
     bool act[PER];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) gb[q] = ngb[q];
     if (FROM_SEQ) {
       stage_pack(nchars, S.st);
     } else {
 #pragma unroll
-      for (int c = 0; c < PER; ++c) { key[c] = nkey[c]; ps[c] = npos[c]; }
+      for (int cc = 0; cc < PER; ++cc) { key[cc] = nkey[cc]; ps[cc] = npos[cc]; }
     }
-    prefetch(min(vt + gridDim.x, ntiles - 1));   // unconditional: static vmcnt
+    prefetch(min(tile + 1, t_end - 1));   // unconditional: static vmcnt
     for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
     __syncthreads();                       // stage packed; previous tile's write-out done
 #pragma unroll
@@ -285,7 +299,8 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       const uint32_t d = threadIdx.x * 4 + q;
       if (d < R) {
         S.tstart[d] = run;
-        S.gbase[d] = gb[q];
+        S.gbase[d] = cursor[q];
+        cursor[q] += dsum[q];
         uint32_t cur = run;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -356,7 +371,7 @@ __device__ __forceinline__ int lds_insert(WaveTable& W, uint64_t key) {
   if (key == EMPTY_KEY) return (int)V2_CAPB;
   uint32_t j = local_home(mix64(key), V2_CAPB);
   for (uint32_t n = 0; n < V2_CAPB; ++n) {
-    const uint64_t prev = atomicCAS((unsigned long long*)&W.s[j].key,
+    const uint64_t prev = atomicCAS((unsigned long long*)&W.key[j],
                                     (unsigned long long)EMPTY_KEY, (unsigned long long)key);
     if (prev == EMPTY_KEY || prev == key) return (int)j;
     if (++j == V2_CAPB) j = 0;
@@ -368,8 +383,7 @@ __device__ __forceinline__ int lds_find(const WaveTable& W, uint64_t key) {
   if (key == EMPTY_KEY) return (int)V2_CAPB;
   uint32_t j = local_home(mix64(key), V2_CAPB);
   for (uint32_t n = 0; n < V2_CAPB; ++n) {
-    uint64_t cur = W.s[j].key;
-    if (cur == key) return (int)j;
+    if (W.key[j] == key) return (int)j;
     if (++j == V2_CAPB) j = 0;
   }
   return -1;
@@ -389,36 +403,46 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   const uint32_t b = (remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x) * 4 + wave;
   if (b >= g.nb) return;
   STAMP(b, 0);
-  for (uint32_t j = lane; j <= V2_CAPB; j += 64)
-    *reinterpret_cast<uint4*>(&W.s[j]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
   const uint32_t s0 = start[b], s1 = start[b + 1];
   const bool one_batch = s1 - s0 <= 64 * PER;     // typical bucket: everything stays in VGPRs
   uint64_t key[PER];
   uint32_t ps[PER];
   int slot[PER];
+  bool in[PER];
+  // the first batch's loads are in flight while the sub-table is initialised
+#pragma unroll
+  for (int c = 0; c < PER; ++c) {
+    const uint32_t i = s0 + 64 * c + lane;
+    in[c] = i < s1;
+    key[c] = in[c] ? keys[i] : 0;
+    ps[c] = in[c] ? pos[i] : 0;
+  }
+  for (uint32_t j = lane; j <= V2_CAPB; j += 64) {
+    W.key[j] = EMPTY_KEY;
+    W.cc[j] = make_uint2(0u, 0u);
+  }
   wave_sync();
-  // pass A: distinct keys + counts (all loads of a batch issued before the first LDS probe)
-  bool ovf = false;
   STAMP(b, 1);
+  // pass A: distinct keys + counts
+  bool ovf = false;
   for (uint32_t i0 = s0; i0 < s1; i0 += 64 * PER) {
+    if (i0 != s0) {
 #pragma unroll
-    for (int c = 0; c < PER; ++c) {
-      const uint32_t i = i0 + 64 * c + lane;
-      key[c] = i < s1 ? keys[i] : 0;
-      ps[c] = i < s1 ? pos[i] : 0;
+      for (int c = 0; c < PER; ++c) {
+        const uint32_t i = i0 + 64 * c + lane;
+        in[c] = i < s1;
+        key[c] = in[c] ? keys[i] : 0;
+        ps[c] = in[c] ? pos[i] : 0;
+      }
     }
-#ifdef KMHG_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     STAMP(b, 2);
-#endif
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
-      const uint32_t i = i0 + 64 * c + lane;
       slot[c] = -1;
-      if (i < s1) {
+      if (in[c]) {
         slot[c] = lds_insert(W, key[c]);
         if (slot[c] < 0) ovf = true;
-        else atomicAdd(&W.s[slot[c]].cnt, 1u);
+        else atomicAdd(&W.cc[slot[c]].x, 1u);
       }
     }
   }
@@ -435,7 +459,7 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   uint32_t cs = 0, occ = 0, mx = 0;
   uint64_t pairs = 0;
   for (uint32_t j = j0; j < j1; ++j) {
-    const uint32_t c = W.s[j].cnt;
+    const uint32_t c = W.cc[j].x;
     cs += c;
     occ += c ? 1u : 0u;
     mx = max(mx, c);
@@ -444,8 +468,8 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   const uint64_t incl = wave_incl_scan(cs);
   uint32_t off_run = s0 + (uint32_t)(incl - cs);
   for (uint32_t j = j0; j < j1; ++j) {
-    W.s[j].cur = off_run;
-    off_run += W.s[j].cnt;
+    W.cc[j].y = off_run;
+    off_run += W.cc[j].x;
   }
   for (int d = 32; d >= 1; d >>= 1) {
     pairs += __shfl_xor(pairs, d);
@@ -464,13 +488,14 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   // the bucket's sub-table, coalesced 16-B slots (empty ones included: no table init needed)
   Slot* Tb = T + (uint64_t)b * V2_CAPB;
   for (uint32_t j = lane; j < V2_CAPB; j += 64) {
-    uint4 x = *reinterpret_cast<const uint4*>(&W.s[j]);
-    x.w += x.z;                                   // end = offset + count
-    *reinterpret_cast<uint4*>(&Tb[j]) = x;
+    const uint64_t kk = W.key[j];
+    const uint2 c = W.cc[j];
+    *reinterpret_cast<uint4*>(&Tb[j]) =
+        make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y + c.x);   // end = offset + count
   }
   if (lane == 0 && b == bucket_of(mix64(EMPTY_KEY), g.nb)) {
-    uint4 x = *reinterpret_cast<const uint4*>(&W.s[V2_CAPB]);
-    *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, x.z, x.w + x.z);
+    const uint2 c = W.cc[V2_CAPB];
+    *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y + c.x);
   }
   STAMP(b, 5);
   // pass B: positions in stream (= position) order.  Keys seen once in the bucket take their
@@ -494,14 +519,14 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
       const uint32_t i = i0 + 64 * c + lane;
       const bool act = i < s1;
       uint2 cc = make_uint2(0u, 0u);                // {cnt, cur}
-      if (act) cc = *reinterpret_cast<const uint2*>(&W.s[slot[c]].cnt);
+      if (act) cc = W.cc[slot[c]];
       const bool multi = act && cc.x > 1;
       if (act && !multi) positions[cc.y] = (int32_t)ps[c];
       if (__ballot(multi)) {
         const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS, multi);
         const int leader = multi ? __ffsll((unsigned long long)m) - 1 : lane;
         uint32_t cur = cc.y;
-        if (multi && leader == lane) W.s[slot[c]].cur = cur + (uint32_t)__popcll(m);
+        if (multi && leader == lane) W.cc[slot[c]].y = cur + (uint32_t)__popcll(m);
         cur = __shfl(cur, leader);
         wave_sync();
         if (multi) positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
@@ -511,11 +536,12 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   STAMP(b, 6);
 }
 
-// V_stats: reduce the per-bucket partials (grid-stride, one atomic per workgroup; meta is
-// zeroed before the build).
+// V_stats: reduce the per-bucket partials (grid-stride, one atomic per workgroup; meta was
+// zeroed by V_hist0).  The last workgroup to finish copies the totals into `host_meta`, a
+// pinned host record, so the host reads them without a copy launch.
 __global__ void __launch_bounds__(BLOCK)
 k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __restrict__ n_valid,
-           BuildMeta* __restrict__ meta) {
+           BuildMeta* __restrict__ meta, BuildMeta* __restrict__ host_meta) {
   __shared__ uint64_t su[4], sp[4];
   __shared__ uint32_t sm[4];
   uint64_t u = 0, p = 0;
@@ -541,7 +567,22 @@ k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __re
     if (u) atomicAdd((unsigned long long*)&meta->n_kmers, (unsigned long long)u);
     if (p) atomicAdd((unsigned long long*)&meta->n_pairs, (unsigned long long)p);
     if (m) atomicMax(&meta->max_count, m);
-    if (blockIdx.x == 0) meta->n_positions = *n_valid;
+    __threadfence();
+    const uint32_t done = atomicAdd(&meta->blocks_done, 1u);
+    if (done == gridDim.x - 1) {           // every other block's atomics are visible
+      __threadfence();
+      BuildMeta r;
+      r.n_kmers = __hip_atomic_load(&meta->n_kmers, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r.n_pairs = __hip_atomic_load(&meta->n_pairs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r.max_count = __hip_atomic_load(&meta->max_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r.overflow = __hip_atomic_load(&meta->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r.n_positions = *n_valid;
+      r.n_small = 0;
+      r.n_large = 0;
+      r.blocks_done = done + 1;
+      *host_meta = r;
+      __threadfence_system();
+    }
   }
 }
 
@@ -585,34 +626,42 @@ static inline unsigned grid_of(uint64_t n, unsigned per) {
   return (unsigned)(g ? g : 1);
 }
 
-void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
-                     Digit D, uint32_t* hist, uint32_t ntiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_hist0, dim3(ntiles), dim3(BLOCK), 0, s, seq, L, k, Nw,
-                     aligned ? 1 : 0, g, D, hist, ntiles, xcd_map());
+Chunks make_chunks(uint32_t ntiles) {
+  static unsigned cap = resident_blocks((const void*)k_v2_scatter<true>);
+  Chunks ch;
+  ch.ntiles = ntiles;
+  const uint32_t C0 = std::max(1u, std::min<uint32_t>(ntiles, cap));
+  ch.tpc = (ntiles + C0 - 1) / C0;
+  ch.C = (ntiles + ch.tpc - 1) / ch.tpc;   // every chunk holds >= 1 tile
+  return ch;
 }
-void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, hipStream_t s) {
+
+void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
+                     uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
+                     BuildMeta* meta, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
+                     xcd_map(), scan_status, n_status, meta);
+}
+void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);
-  hipLaunchKernelGGL(k_tile_sum_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, tsum);
-  launch_scan_tiles_u64(tsum, nt, tsum + nt, s);
-  hipLaunchKernelGGL(k_tile_scan_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, tsum, total);
+  hipLaunchKernelGGL(k_scan_lb_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, status, nt, total);
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
-                    uint32_t ntiles, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_hist, dim3(ntiles), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist, ntiles, xcd_map());
+                    Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_hist, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist, ch,
+                     xcd_map(), scan_status, n_status);
 }
-void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned,
-                           Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                           uint32_t* pout, uint32_t pad, hipStream_t s) {
-  static unsigned cap = resident_blocks((const void*)k_v2_scatter<true>);
-  hipLaunchKernelGGL(k_v2_scatter<true>, dim3(ntiles < cap ? ntiles : cap), dim3(BLOCK), 0, s, seq, L, k, Nw,
-                     aligned ? 1 : 0, nullptr, nullptr, nullptr, g, D, hist, ntiles, kout, pout, pad, xcd_map());
+void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
+                           const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                           uint32_t pad, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_scatter<true>, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, 1,
+                     nullptr, nullptr, nullptr, g, D, hist, ch, kout, pout, pad, xcd_map());
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
-                       Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                       uint32_t* pout, uint32_t pad, hipStream_t s) {
-  static unsigned cap = resident_blocks((const void*)k_v2_scatter<false>);
-  hipLaunchKernelGGL(k_v2_scatter<false>, dim3(ntiles < cap ? ntiles : cap), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
-                     (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ntiles, kout, pout, pad, xcd_map());
+                       Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                       uint32_t pad, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_scatter<false>, dim3(ch.C), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
+                     (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ch, kout, pout, pad, xcd_map());
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s) {
@@ -627,10 +676,10 @@ void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t*
                      T, positions, bstats, meta, xcd_map_bucket());
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
-                     BuildMeta* meta, hipStream_t s) {
+                     BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {
   unsigned gr = grid_of(nb, BLOCK * 8);
   if (gr > 64) gr = 64;
-  hipLaunchKernelGGL(k_v2_stats, dim3(gr), dim3(BLOCK), 0, s, bstats, nb, n_valid, meta);
+  hipLaunchKernelGGL(k_v2_stats, dim3(gr), dim3(BLOCK), 0, s, bstats, nb, n_valid, meta, host_meta);
 }
 
 }  // namespace kmhg

@@ -206,6 +206,44 @@ struct DBuf {
   size_t bytes() const { return n * sizeof(T); }
 };
 
+// Pinned, device-visible host records for the build totals (V_stats writes one directly, so the
+// host reads U / N / P after the stream sync with no copy launch).  Slots are recycled.
+class PinnedPool {
+ public:
+  static PinnedPool& get() {
+    static PinnedPool p;
+    return p;
+  }
+  BuildMeta* take() {
+    std::lock_guard<std::mutex> g(mu_);
+    if (free_.empty()) {
+      constexpr int kSlots = 64;
+      BuildMeta* blk = nullptr;
+      HIPC(hipHostMalloc(reinterpret_cast<void**>(&blk), sizeof(BuildMeta) * kSlots,
+                         hipHostMallocCoherent));
+      for (int i = 0; i < kSlots; ++i) free_.push_back(blk + i);
+    }
+    BuildMeta* m = free_.back();
+    free_.pop_back();
+    return m;
+  }
+  void give(BuildMeta* m) {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(m);
+  }
+
+ private:
+  std::mutex mu_;
+  std::vector<BuildMeta*> free_;
+};
+struct PinnedMeta {
+  BuildMeta* p;
+  PinnedMeta() : p(PinnedPool::get().take()) { std::memset(p, 0, sizeof(*p)); }
+  ~PinnedMeta() { PinnedPool::get().give(p); }
+  PinnedMeta(const PinnedMeta&) = delete;
+  PinnedMeta& operator=(const PinnedMeta&) = delete;
+};
+
 // ============================================================================ timing
 struct Timing {
   static Timing& get() {
@@ -418,54 +456,57 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     HIPC(hipMemcpyAsync(aligned_copy.p, d_seq, (size_t)L, hipMemcpyDeviceToDevice, s));
     d_seq = aligned_copy.p;
   }
-  const bool aligned = true;
   const uint32_t nb = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW - 1) / V2_BW);
   idx->geom = Geom{nb, V2_CAPB};
   const Geom g = idx->geom;
   const uint32_t ntiles = (uint32_t)((Nw + PTILE - 1) / PTILE);   // partition tiles
-  // radix plan: fewest passes whose radix fits LDS and whose histograms stay small
+  const Chunks ch = make_chunks(ntiles);
+  // radix plan: fewest passes whose radix fits LDS
   uint32_t passes = 1, R = nb;
   for (passes = 1; passes <= 4; ++passes) {
     R = (uint32_t)std::ceil(std::pow((double)nb, 1.0 / passes) - 1e-9);
     while (std::pow((double)R, (double)passes) < (double)nb) ++R;
-    if (R <= V2_MAXR && (uint64_t)R * ntiles <= (64ull << 20)) break;
+    if (R <= V2_MAXR) break;
   }
   if (passes > 4) fail(KMHG_EOVERFLOW, "sequence too long for the partitioned build");
-  const uint64_t nhist = (uint64_t)R * ntiles;
+  const uint64_t nhist = (uint64_t)R * ch.C;
   const uint32_t scan_tiles = tiles_for(nhist);
   DBuf<uint64_t> kA(Nw + PTILE, s), kB(Nw + PTILE, s);   // + pad (launch_v2_scatter)
   DBuf<uint32_t> pA(Nw + PTILE, s), pB(Nw + PTILE, s);
   const uint32_t pad = (uint32_t)Nw;
   DBuf<uint32_t> hist(nhist, s);
   DBuf<uint32_t> start((uint64_t)nb + 1, s);
-  DBuf<uint64_t> tsum((size_t)scan_tiles + 1, s);     // reduce-then-scan tile sums
-  // zeroed scratch: [n_valid][meta]
-  const size_t off_meta = 64;
-  const size_t scratch_bytes = off_meta + sizeof(BuildMeta);
+  // scratch (zeroed in-kernel by V_hist0 / V_hist, no memset): [n_valid][meta][scan status]
+  const size_t off_meta = 64, off_status = 128;
+  const uint32_t n_status = scan_tiles + 1;               // look-back words + ticket
+  const size_t scratch_bytes = off_status + (size_t)n_status * 8;
   DBuf<uint8_t> scratch(scratch_bytes, s);
   uint8_t* sc = scratch.p;
   uint32_t* n_valid = reinterpret_cast<uint32_t*>(sc);
   BuildMeta* meta = reinterpret_cast<BuildMeta*>(sc + off_meta);
-  HIPC(hipMemsetAsync(sc, 0, scratch_bytes, s));
+  uint64_t* status = reinterpret_cast<uint64_t*>(sc + off_status);
+  PinnedMeta hmeta;                                        // V_stats writes the totals here
   idx->table.reset(idx->slots());
   idx->positions.reset(Nw);
   DBuf<BucketStats> bstats(nb, s);
 
   LAUNCH("k_v2_hist0", s,
-         launch_v2_hist0(d_seq, L, k, Nw, aligned, g, make_digit(1, R), hist.p, ntiles, s));
-  LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, tsum.p, n_valid, s));
+         launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, status, n_status,
+                         meta, s));
+  LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
   LAUNCH("k_v2_scatter_seq", s,
-         launch_v2_scatter_seq(d_seq, L, k, Nw, aligned, g, make_digit(1, R), hist.p, ntiles,
-                               kA.p, pA.p, pad, s));
+         launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, kA.p, pA.p,
+                               pad, s));
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = R;
   for (uint32_t p = 1; p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
-    LAUNCH("k_v2_hist", s, launch_v2_hist(kin, n_valid, g, Dp, hist.p, ntiles, s));
-    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, tsum.p, n_valid, s));
+    LAUNCH("k_v2_hist", s,
+           launch_v2_hist(kin, n_valid, g, Dp, hist.p, ch, status, n_status, s));
+    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     LAUNCH("k_v2_scatter", s,
-           launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, pad, s));
+           launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ch, kout, pout, pad, s));
     std::swap(kin, kout);
     std::swap(pin, pout);
     div *= R;
@@ -480,16 +521,15 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   LAUNCH("k_v2_bucket", s,
          launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
                           meta, s));
-  LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, nb, n_valid, meta, s));
+  LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, nb, n_valid, meta, hmeta.p, s));
 #ifdef KMHG_STAMPS
   if (const char* f = std::getenv("KMHG_STAMP_FILE")) {
     HIPC(hipStreamSynchronize(s));
     if (FILE* fp = fopen(f, "wb")) { fwrite(stamps, 8, 8 * (size_t)nb, fp); fclose(fp); }
   }
 #endif
-  BuildMeta hm;
-  HIPC(hipMemcpyAsync(&hm, meta, sizeof(hm), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  const BuildMeta hm = *hmeta.p;
   if (hm.overflow) return nullptr;
   idx->U = hm.n_kmers;
   idx->N = hm.n_positions;

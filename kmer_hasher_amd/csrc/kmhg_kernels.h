@@ -10,7 +10,7 @@ constexpr uint32_t LARGE_MIN = 64;     // keys with >= this many positions sort 
 constexpr uint32_t V2_BW = 256;        // mean windows per bucket
 constexpr uint32_t V2_CAPB = 384;      // slots per bucket (LDS sub-table of one wave)
 constexpr uint32_t V2_SLOT_BITS = 9;   // bits to name a slot 0..V2_CAPB
-constexpr uint32_t V2_MAXR = 512;      // max radix of one partition pass
+constexpr uint32_t V2_MAXR = 640;      // max radix of one partition pass
 constexpr uint32_t SORT_CHUNK = 4096;  // LDS bitonic chunk (16 KiB)
 
 struct BuildMeta {              // written by the build kernels, read once by the host
@@ -21,6 +21,7 @@ struct BuildMeta {              // written by the build kernels, read once by th
   uint32_t n_small;             // keys with 2 <= n < LARGE_MIN
   uint32_t n_large;             // keys with n >= LARGE_MIN
   uint32_t overflow;            // partitioned build: a bucket's LDS sub-table filled up
+  uint32_t blocks_done;         // V_stats arrival counter (last block publishes to the host)
 };
 
 struct ReadMeta {               // canonical-order readout preparation
@@ -79,20 +80,33 @@ inline Digit make_digit(uint32_t div, uint32_t R) {
   while ((1u << d.nbits) < R) ++d.nbits;
   return d;
 }
-void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned, Geom g,
-                     Digit D, uint32_t* hist, uint32_t ntiles, hipStream_t s);
+// Chunked radix passes: chunk c = partition tiles [c*tpc, min((c+1)*tpc, ntiles)), one
+// workgroup per chunk (as many chunks as scatter workgroups are resident); histograms are
+// [digit][chunk] and a chunk's output for a digit is one contiguous run.
+struct Chunks {
+  uint32_t C;        // chunks (= workgroups of the histogram and scatter kernels)
+  uint32_t tpc;      // tiles per chunk
+  uint32_t ntiles;   // partition tiles (PTILE windows each)
+};
+Chunks make_chunks(uint32_t ntiles);
+// V_hist0 also zeroes the look-back words of the scan that follows (n_status u64) and `meta`
+void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
+                     uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
+                     BuildMeta* meta, hipStream_t s);
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
-// exclusive scan of a u32 array; tsum = scratch of tiles_for(n) + 1 u64; total <- sum
-void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* tsum, uint32_t* total, hipStream_t s);
+// single-pass exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the
+// histogram kernel launched before it; total <- sum
+void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s);
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
-                    uint32_t ntiles, hipStream_t s);
-void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, bool aligned,
-                           Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                           uint32_t* pout, uint32_t pad, hipStream_t s);
+                    Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s);
+// the sequence must be 16-B aligned (the engine copies an unaligned input)
+void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
+                           const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                           uint32_t pad, hipStream_t s);
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
-                       Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                       uint32_t* pout, uint32_t pad, hipStream_t s);
+                       Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                       uint32_t pad, hipStream_t s);
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s);
 struct BucketStats {           // per-bucket partials of the build statistics
@@ -103,7 +117,7 @@ void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t*
                       Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                       hipStream_t s);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
-                     BuildMeta* meta, hipStream_t s);
+                     BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);
 
 #ifdef KMHG_STAMPS
 void set_stamp_buffer(uint64_t* p);
