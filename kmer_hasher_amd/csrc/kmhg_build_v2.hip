@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include "kmhg_common.h"
 #include "kmhg_device.h"
 #include "kmhg_kernels.h"
@@ -152,6 +153,45 @@ k_scan_lb_u32(uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ statu
   }
 }
 
+// Reduce-then-scan (no tickets, no spinning) for long arrays: per-tile sums -> one-workgroup
+// scan of the tile sums (k_scan_tiles_u64) -> per-tile exclusive scan seeded with its base.
+__global__ void __launch_bounds__(BLOCK)
+k_tile_sum_u32(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ tsum) {
+  __shared__ uint64_t sh[8];
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  uint64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    if (i < n) sum += a[i];
+  }
+  uint64_t tot;
+  block_excl_scan(sum, sh, tot);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict__ tbase,
+                uint32_t* __restrict__ total) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *total = (uint32_t)tbase[gridDim.x];
+  __shared__ uint64_t sh[8];
+  const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)threadIdx.x * WPT;
+  uint32_t v[WPT];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    v[j] = (base + j < n) ? a[base + j] : 0u;
+    sum += v[j];
+  }
+  uint64_t tot;
+  uint64_t run = block_excl_scan(sum, sh, tot) + tbase[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (base + j < n) a[base + j] = (uint32_t)run;
+    run += v[j];
+  }
+}
+
 // ---------------------------------------------------------------- V_hist (passes >= 1)
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
@@ -215,23 +255,38 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const uint32_t wbase = (uint32_t)wave * (PTILE / 4);
   const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
-  // one workgroup per chunk of consecutive tiles; with `remap` the chunks of one XCD are
-  // contiguous.  Thread t owns digits 4t..4t+3 and keeps their running output cursors in
-  // registers: each digit's output of the chunk is one contiguous run, written tile by tile.
-  const uint32_t chunk = remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x;
-  const uint32_t t_begin = chunk * ch.tpc, t_end = min(t_begin + ch.tpc, ch.ntiles);
-  uint32_t cursor[4];
+  // Two tile schedules (Chunks, kmhg_kernels.h); thread t owns digits 4t..4t+3 either way.
+  //  interleaved (ch.interleaved): persistent workgroup b walks virtual tiles b, b + G, ...;
+  //    with `remap` every XCD owns one contiguous tile range, so the tiles running at the same
+  //    time on an XCD are neighbours and their partial output lines merge in that XCD's L2.
+  //    Histograms are per tile; each tile's digit bases are prefetched with its inputs.
+  //  chunked: one workgroup per chunk of consecutive tiles, histograms per chunk; the digit
+  //    cursors advance in registers from tile to tile.
+  const uint32_t G = gridDim.x;
+  const uint32_t chunk = ch.interleaved ? 0u : (remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x);
+  const uint32_t n_iter = ch.interleaved
+                              ? (ch.ntiles - blockIdx.x + G - 1) / G
+                              : min(chunk * ch.tpc + ch.tpc, ch.ntiles) - chunk * ch.tpc;
+  auto tile_at = [&](uint32_t i) -> uint32_t {
+    if (!ch.interleaved) return chunk * ch.tpc + i;
+    const uint32_t v = blockIdx.x + i * G;
+    return remap ? xcd_remap(v, ch.ntiles) : v;
+  };
+  uint32_t cursor[4], ngb[4];
+  auto load_bases = [&](uint32_t tv) {     // unconditional (clamped) loads: static count
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t d = min(threadIdx.x * 4 + q, R - 1);
-    cursor[q] = hist[(size_t)d * ch.C + chunk];
-  }
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t d = min(threadIdx.x * 4 + q, R - 1);
+      ngb[q] = hist[(size_t)d * ch.C + (ch.interleaved ? tv : chunk)];
+    }
+  };
   // the next tile's inputs are in flight while this one is processed
   uint64_t nkey[PER];
   uint32_t npos[PER];
   StageRegs<PSTAGE_W16> nchars;
   auto prefetch = [&](uint32_t tv) {
     const uint64_t t0 = (uint64_t)tv * PTILE;
+    load_bases(tv);
     if (FROM_SEQ) {
       stage_load<PSTAGE_W16, true>(nchars, seq, L, (int64_t)t0 - HALO, true);
     } else {
@@ -246,24 +301,31 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
   // Every path into the loop top has [prefetch loads][PTILE/BLOCK x 2 stores] in flight, so the
   // compiler waits for the prefetch with a counted vmcnt: the pad stores below stand in for the
   // previous tile's write-out on the first iteration.
-  prefetch(t_begin);
+  prefetch(tile_at(0));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cursor[q] = ngb[q];
 #pragma unroll
   for (int j = 0; j < PTILE / BLOCK; ++j) {
     kout[pad + threadIdx.x] = 0;
     pout[pad + threadIdx.x] = 0;
   }
-  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
+  for (uint32_t it = 0; it < n_iter; ++it) {
+    const uint32_t tile = tile_at(it);
     const uint64_t tile0 = (uint64_t)tile * PTILE;
     uint64_t key[PER];
     uint32_t ps[PER], dg[PER];
     bool act[PER];
+    if (ch.interleaved) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cursor[q] = ngb[q];
+    }
     if (FROM_SEQ) {
       stage_pack(nchars, S.st);
     } else {
 #pragma unroll
       for (int cc = 0; cc < PER; ++cc) { key[cc] = nkey[cc]; ps[cc] = npos[cc]; }
     }
-    prefetch(min(tile + 1, t_end - 1));   // unconditional: static vmcnt
+    prefetch(tile_at(min(it + 1, n_iter - 1)));   // unconditional: static vmcnt
     for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
     __syncthreads();                       // stage packed; previous tile's write-out done
 #pragma unroll
@@ -626,14 +688,34 @@ static inline unsigned grid_of(uint64_t n, unsigned per) {
   return (unsigned)(g ? g : 1);
 }
 
-Chunks make_chunks(uint32_t ntiles) {
+static unsigned scatter_cap() {
   static unsigned cap = resident_blocks((const void*)k_v2_scatter<true>);
+  return cap;
+}
+
+// Tile schedule of the radix passes: interleaved (default) or chunked (KMHG_RADIX=chunked, kept
+// for A/B: measured slower, each workgroup's R open run heads per digit overflow the L2).
+Chunks make_chunks(uint32_t ntiles) {
+  static int chunked = [] {
+    const char* e = std::getenv("KMHG_RADIX");
+    return (e && std::string(e) == "chunked") ? 1 : 0;
+  }();
   Chunks ch;
   ch.ntiles = ntiles;
-  const uint32_t C0 = std::max(1u, std::min<uint32_t>(ntiles, cap));
+  if (!chunked) {
+    ch.interleaved = 1;
+    ch.C = ntiles;
+    ch.tpc = 1;
+    return ch;
+  }
+  ch.interleaved = 0;
+  const uint32_t C0 = std::max(1u, std::min<uint32_t>(ntiles, scatter_cap()));
   ch.tpc = (ntiles + C0 - 1) / C0;
   ch.C = (ntiles + ch.tpc - 1) / ch.tpc;   // every chunk holds >= 1 tile
   return ch;
+}
+static unsigned scatter_grid(const Chunks& ch) {
+  return ch.interleaved ? std::min<unsigned>(ch.ntiles, scatter_cap()) : ch.C;
 }
 
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
@@ -644,7 +726,14 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
 }
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);
-  hipLaunchKernelGGL(k_scan_lb_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, status, nt, total);
+  if (nt <= LB_SCAN_MAX_TILES) {
+    hipLaunchKernelGGL(k_scan_lb_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, status, nt, total);
+  } else {   // long arrays: three launches beat a look-back chain of many tiles
+    hipLaunchKernelGGL(k_tile_sum_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, status);
+    launch_scan_tiles_u64(status, nt, status + nt, s);
+    hipLaunchKernelGGL(k_tile_scan_u32, dim3(nt), dim3(BLOCK), 0, s, a, n,
+                       (const uint64_t*)status, total);
+  }
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s) {
@@ -654,13 +743,13 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_scatter<true>, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, 1,
+  hipLaunchKernelGGL(k_v2_scatter<true>, dim3(scatter_grid(ch)), dim3(BLOCK), 0, s, seq, L, k, Nw, 1,
                      nullptr, nullptr, nullptr, g, D, hist, ch, kout, pout, pad, xcd_map());
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_scatter<false>, dim3(ch.C), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
+  hipLaunchKernelGGL(k_v2_scatter<false>, dim3(scatter_grid(ch)), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
                      (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ch, kout, pout, pad, xcd_map());
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,

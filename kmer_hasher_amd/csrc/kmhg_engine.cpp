@@ -466,7 +466,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   for (passes = 1; passes <= 4; ++passes) {
     R = (uint32_t)std::ceil(std::pow((double)nb, 1.0 / passes) - 1e-9);
     while (std::pow((double)R, (double)passes) < (double)nb) ++R;
-    if (R <= V2_MAXR) break;
+    // interleaved tiles of PTILE windows keep ~PTILE / R elements per digit run: beyond ~300
+    // digits the runs get too short for coalesced writes and an extra pass is cheaper
+    if (R <= (ch.interleaved ? V2_MAXR_IL : V2_MAXR)) break;
   }
   if (passes > 4) fail(KMHG_EOVERFLOW, "sequence too long for the partitioned build");
   const uint64_t nhist = (uint64_t)R * ch.C;

@@ -10,7 +10,8 @@ constexpr uint32_t LARGE_MIN = 64;     // keys with >= this many positions sort 
 constexpr uint32_t V2_BW = 256;        // mean windows per bucket
 constexpr uint32_t V2_CAPB = 384;      // slots per bucket (LDS sub-table of one wave)
 constexpr uint32_t V2_SLOT_BITS = 9;   // bits to name a slot 0..V2_CAPB
-constexpr uint32_t V2_MAXR = 640;      // max radix of one partition pass
+constexpr uint32_t V2_MAXR = 640;      // max radix of one partition pass (LDS arrays)
+constexpr uint32_t V2_MAXR_IL = 320;   // ... with the interleaved tile schedule
 constexpr uint32_t SORT_CHUNK = 4096;  // LDS bitonic chunk (16 KiB)
 
 struct BuildMeta {              // written by the build kernels, read once by the host
@@ -83,10 +84,13 @@ inline Digit make_digit(uint32_t div, uint32_t R) {
 // Chunked radix passes: chunk c = partition tiles [c*tpc, min((c+1)*tpc, ntiles)), one
 // workgroup per chunk (as many chunks as scatter workgroups are resident); histograms are
 // [digit][chunk] and a chunk's output for a digit is one contiguous run.
+// Interleaved (the default): C = ntiles chunks of one tile each, so histograms are per tile,
+// and the scatter runs a persistent grid whose XCDs each walk one contiguous tile range.
 struct Chunks {
-  uint32_t C;        // chunks (= workgroups of the histogram and scatter kernels)
-  uint32_t tpc;      // tiles per chunk
-  uint32_t ntiles;   // partition tiles (PTILE windows each)
+  uint32_t C;            // chunks = histogram columns (= histogram workgroups)
+  uint32_t tpc;          // tiles per chunk
+  uint32_t ntiles;       // partition tiles (PTILE windows each)
+  uint32_t interleaved;  // 1: per-tile schedule (see above)
 };
 Chunks make_chunks(uint32_t ntiles);
 // V_hist0 also zeroes the look-back words of the scan that follows (n_status u64) and `meta`
@@ -95,8 +99,10 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
                      BuildMeta* meta, hipStream_t s);
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
-// single-pass exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the
-// histogram kernel launched before it; total <- sum
+// exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the histogram kernel
+// launched before it; total <- sum.  Single-pass look-back up to LB_SCAN_MAX_TILES tiles,
+// reduce-then-scan (status = tile sums) beyond.
+constexpr uint32_t LB_SCAN_MAX_TILES = 256;
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s);
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s);
