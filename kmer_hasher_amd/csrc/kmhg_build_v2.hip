@@ -547,21 +547,9 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   }
   wave_sync();
   STAMP(b, 4);
-  // the bucket's sub-table, coalesced 16-B slots (empty ones included: no table init needed)
-  Slot* Tb = T + (uint64_t)b * V2_CAPB;
-  for (uint32_t j = lane; j < V2_CAPB; j += 64) {
-    const uint64_t kk = W.key[j];
-    const uint2 c = W.cc[j];
-    *reinterpret_cast<uint4*>(&Tb[j]) =
-        make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y + c.x);   // end = offset + count
-  }
-  if (lane == 0 && b == bucket_of(mix64(EMPTY_KEY), g.nb)) {
-    const uint2 c = W.cc[V2_CAPB];
-    *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y + c.x);
-  }
-  STAMP(b, 5);
-  // pass B: positions in stream (= position) order.  Keys seen once in the bucket take their
-  // offset directly; repeated keys are ranked by ballots in lane (= position) order.
+  // pass B: positions in stream (= position) order.  Repeated keys are ranked by ballots in
+  // lane (= position) order; afterwards cc.y = end for them and = the position for keys seen
+  // once, which is exactly the slot's aux word.
   for (uint32_t i0 = s0; i0 < s1; i0 += 64 * PER) {
     if (!one_batch) {
 #pragma unroll
@@ -583,7 +571,8 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
       uint2 cc = make_uint2(0u, 0u);                // {cnt, cur}
       if (act) cc = W.cc[slot[c]];
       const bool multi = act && cc.x > 1;
-      if (act && !multi) positions[cc.y] = (int32_t)ps[c];
+      // a key seen once keeps its position inline in its slot (Slot::aux); nothing is written
+      if (act && !multi) W.cc[slot[c]].y = ps[c];
       if (__ballot(multi)) {
         const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS, multi);
         const int leader = multi ? __ffsll((unsigned long long)m) - 1 : lane;
@@ -594,6 +583,19 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
         if (multi) positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
       }
     }
+  }
+  wave_sync();
+  STAMP(b, 5);
+  // the bucket's sub-table, coalesced 16-B slots (empty ones included: no table init needed)
+  Slot* Tb = T + (uint64_t)b * V2_CAPB;
+  for (uint32_t j = lane; j < V2_CAPB; j += 64) {
+    const uint64_t kk = W.key[j];
+    const uint2 c = W.cc[j];
+    *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
+  }
+  if (lane == 0 && b == bucket_of(mix64(EMPTY_KEY), g.nb)) {
+    const uint2 c = W.cc[V2_CAPB];
+    *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
   }
   STAMP(b, 6);
 }

@@ -7,9 +7,11 @@
 //                                 empty sentinel (only possible at k = 32: GGG...G = ~0)
 //   win_slot   u32[Nw]            build scratch: slot of every window start (or NONE)
 //   ukeys      u64[U]   counts u32[U]   offsets u32[U+1]     CSR, keys in table-slot order
-//   positions  i32[N]             1-based window starts, ascending inside every key
-// The table slot of a key also carries {count, end}: a query reads ONE 16-B slot and then
-// the key's positions [end - count, end) -- no second indirection.
+//   positions  i32[N]             1-based window starts of keys seen >= 2 times, ascending
+//                                 inside every key (entries of keys seen once are unused)
+// The table slot of a key also carries {count, aux}: aux = the position itself for a key seen
+// once (the common case: a query probe then needs no second read), else one past the key's
+// last position in `positions`, whose list is [aux - count, aux).
 #pragma once
 #include <stdint.h>
 
@@ -21,7 +23,7 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 struct alignas(16) Slot {
   uint64_t key;    // EMPTY_KEY when free
   uint32_t count;  // occurrences of key
-  uint32_t end;    // after the build: one past the key's last position in `positions`
+  uint32_t aux;    // count == 1: the 1-based position; count >= 2: end of its list in positions
 };
 
 // Table geometry: nb buckets x capb slots, plus one side slot at index nb*capb (kmhg_device.h).

@@ -278,13 +278,13 @@ __device__ __forceinline__ uint32_t table_insert(Slot* __restrict__ T, Geom g, u
   }
 }
 
-// Read-only probe: returns the slot or NONE; count/end from the same 16-B slot load.
+// Read-only probe: returns the slot or NONE; count/aux from the same 16-B slot load.
 __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom g, uint64_t key,
-                                               uint32_t& count, uint32_t& end) {
+                                               uint32_t& count, uint32_t& aux) {
   if (key == EMPTY_KEY) {
     const uint64_t i = side_slot(g);
     uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
-    count = v.z; end = v.w;
+    count = v.z; aux = v.w;
     return count ? (uint32_t)i : NONE;
   }
   const uint64_t h = mix64(key);
@@ -294,8 +294,8 @@ __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom 
     const uint64_t i = b0 + j;
     uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
     uint64_t cur = ((uint64_t)v.y << 32) | v.x;
-    if (cur == key) { count = v.z; end = v.w; return (uint32_t)i; }
-    if (cur == EMPTY_KEY) { count = 0; end = 0; return NONE; }
+    if (cur == key) { count = v.z; aux = v.w; return (uint32_t)i; }
+    if (cur == EMPTY_KEY) { count = 0; aux = 0; return NONE; }
     if (++j == g.capb) j = 0;
   }
 }

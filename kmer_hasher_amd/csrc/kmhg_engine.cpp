@@ -428,6 +428,7 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   LAUNCH("k_sort_large", s,
          launch_sort_large(large_ids.p, meta, counts.p, offsets.p, idx->positions.p,
                            reinterpret_cast<int32_t*>(win_slot.p), s));
+  LAUNCH("k_inline_singles", s, launch_inline_singles(idx->table.p, nslots, idx->positions.p, s));
   BuildMeta hm;
   HIPC(hipMemcpyAsync(&hm, meta, sizeof(hm), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -540,12 +541,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   return idx.release();
 }
 
-int build_version() {
-  static int v = [] {
-    const char* e = std::getenv("KMHG_BUILD");
-    return (e && std::string(e) == "v1") ? 1 : 2;
-  }();
-  return v;
+int build_version() {   // read per build so tests can exercise the fallback (KMHG_BUILD=v1)
+  const char* e = std::getenv("KMHG_BUILD");
+  return (e && std::string(e) == "v1") ? 1 : 2;
 }
 
 kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {

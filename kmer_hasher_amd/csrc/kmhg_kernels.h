@@ -42,6 +42,7 @@ void launch_sort_small(const uint32_t* small_ids, const BuildMeta* meta, const u
                        const uint32_t* offsets, int32_t* positions, hipStream_t s);
 void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const uint32_t* counts,
                        const uint32_t* offsets, int32_t* positions, int32_t* tmp, hipStream_t s);
+void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, hipStream_t s);
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
                         hipStream_t s);

@@ -122,7 +122,7 @@ k_build_compact(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ st
     ukeys[id] = keyv[j];
     counts[id] = cnt[j];
     offsets[id] = off;
-    T[i].end = off;
+    T[i].aux = off;
     uint64_t n = cnt[j];
     pairs += n * (n - 1) / 2;
     mx = max(mx, cnt[j]);
@@ -155,12 +155,12 @@ k_build_compact(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ st
   }
 }
 
-// K_scatter: positions[slot.end++] = s + 1 for every valid window (wave-aggregated, lane-order
+// K_scatter: positions[slot.aux++] = s + 1 for every valid window (wave-aggregated, lane-order
 // ranks inside a group).  Order across waves is arbitrary; K_sort restores ascending order.
 __global__ void __launch_bounds__(BLOCK)
 k_build_scatter(const uint32_t* __restrict__ win_slot, int64_t Nw, Slot* __restrict__ T,
                 int32_t* __restrict__ positions) {
-  uint32_t* end0 = &T[0].end;
+  uint32_t* end0 = &T[0].aux;
   const size_t stride = sizeof(Slot) / sizeof(uint32_t);
   const int64_t tile0 = (int64_t)blockIdx.x * TILE;
 #pragma unroll 2
@@ -260,6 +260,15 @@ k_sort_large(const uint32_t* __restrict__ ids, const BuildMeta* __restrict__ met
   }
 }
 
+// K_inline: a key seen once keeps its position inline in the slot (Slot::aux), as the
+// partitioned build writes it.
+__global__ void __launch_bounds__(BLOCK)
+k_inline_singles(Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
+       i += (uint64_t)gridDim.x * BLOCK)
+    if (T[i].count == 1) T[i].aux = (uint32_t)positions[T[i].aux - 1];
+}
+
 // ================================================================== query kernels
 // Q_probe: per query window (query k) probe the table; qinfo[s] = {count, start}; per-tile row
 // totals go through the look-back so each tile learns its first output row.
@@ -283,10 +292,11 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     const int w = j * BLOCK + threadIdx.x;
     const int64_t s = t_start + w;
     uint64_t key = 0;
-    uint32_t count = 0, end = 0;
+    uint32_t count = 0, aux = 0;
     if (s < w1 && window_key(st, o0 + w, s, L, kq, key))
-      table_find(T, g, key, count, end);
-    if (s < w1) qinfo[s - w0] = make_uint2(count, end - count);
+      table_find(T, g, key, count, aux);
+    // {count, position} for a key seen once, {count, first index} otherwise
+    if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
     rows += count;
   }
   uint64_t tot;
@@ -351,7 +361,8 @@ k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
     int lo = 0, hi = TILE - 1;
     while (lo < hi) { int mid = (lo + hi) >> 1; if (incl[mid] > r) hi = mid; else lo = mid + 1; }
     uint64_t before = lo ? incl[lo - 1] : 0;
-    int32_t j = positions[start[lo] + (uint32_t)(r - before)];
+    const uint32_t n = (uint32_t)(incl[lo] - before);
+    const int32_t j = n == 1 ? (int32_t)start[lo] : positions[start[lo] + (uint32_t)(r - before)];
     out[r0 + r] = make_int2((int32_t)(w0 + tile0 + lo + kq), j);
   }
 }
@@ -368,7 +379,7 @@ k_read_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restr
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
        i += (uint64_t)gridDim.x * BLOCK) {
     uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
-    if (v.z) F[positions[v.w - v.z] - 1] = (uint32_t)i;
+    if (v.z) F[(v.z == 1 ? (int32_t)v.w : positions[v.w - v.z]) - 1] = (uint32_t)i;
   }
 }
 
@@ -474,7 +485,7 @@ k_read_pos(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ canon
     while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (off[mid] <= r) lo = mid; else hi = mid - 1; }
     const uint32_t c = c0 + lo;
     const uint4 v = *reinterpret_cast<const uint4*>(&T[perm[c]]);
-    const int32_t p = positions[v.w - v.z + (uint32_t)(r - off[lo])];
+    const int32_t p = v.z == 1 ? (int32_t)v.w : positions[v.w - v.z + (uint32_t)(r - off[lo])];
     out[r] = make_int2((int32_t)(c + 1), p);
   }
 }
@@ -563,6 +574,11 @@ void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const u
                        const uint32_t* offsets, int32_t* positions, int32_t* tmp, hipStream_t s) {
   hipLaunchKernelGGL(k_sort_large, dim3(1024), dim3(BLOCK), 0, s, large_ids, meta, counts,
                      offsets, positions, tmp);
+}
+void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, hipStream_t s) {
+  unsigned g = grid_for(nslots, BLOCK);
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_inline_singles, dim3(g), dim3(BLOCK), 0, s, T, nslots, positions);
 }
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,

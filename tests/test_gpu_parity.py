@@ -152,3 +152,15 @@ def test_10mbp_k31_vs_oracle(gpu):
     assert sha(res["kmer"]) == sha(oi.kmer_strings())
     q = sqk(ptr, s, 31)
     assert np.array_equal(q.reshape(-1), oi.query(s, 31))
+
+
+def test_fallback_build_v1_matches_oracle(gpu, monkeypatch):
+    """The global-atomic build (used when a bucket's LDS sub-table overflows) on its own."""
+    from kmer_hasher_amd import synth
+    monkeypatch.setenv("KMHG_BUILD", "v1")
+    rng = np.random.default_rng(11)
+    for k in (5, 15, 31, 32):
+        s = "".join(rng.choice(list("ACGT"), 4000))
+        _check_against_oracle(s, k)
+    rr = synth.add_n_runs(synth.repeat_rich(60_000, 5, n_gap_every=20_000), 0.002, 3)
+    _check_against_oracle(rr.tobytes().decode("latin-1"), 21)

@@ -26,7 +26,7 @@ os.environ["KMHG_STAMP_FILE"] = f
 D.DeviceIndex.build(seq, k).free()
 a = np.fromfile(f, np.uint64).reshape(-1, 8).astype(np.int64)
 a = a[a[:, 0] > 0]
-names = ["init+start", "loads", "passA", "scan", "table", "passB"]
+names = ["init+start", "loads", "passA", "scan", "passB", "table"]
 t0 = a[:, 0].min()
 print(f"buckets {len(a)}  kernel span {a[:, 6].max() - t0} ticks")
 for i, n in enumerate(names):
