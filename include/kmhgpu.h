@@ -29,9 +29,11 @@
  *   count    N_kmers int32
  *   kmer     N_kmers strings of k chars, each followed by a NUL (stride k+1)
  *   query    2 x H int32   (i, j)        i = 1-based END of the query window, j = index pos
- * K-mer order (the `i` labels): distinct k-mers ranked by first occurrence.  The reference
- * labels them in khash bucket order; the sets, counts, position lists and pairs per k-mer are
- * identical, and seq.kmer.pos rows are identical including order (DESIGN.md "Parity").
+ * K-mer order (the `i` labels): by default distinct k-mers ranked by first occurrence; the sets,
+ * counts, position lists and pairs per k-mer equal the reference's, and seq.kmer.pos rows are
+ * identical including order (DESIGN.md "Parity").  With KMHG_ORDER_KHASH (kmhg_set_row_order, or
+ * KMHG_ROW_ORDER=khash in the environment when the index is built) kmer.pos is labelled in the
+ * reference's own khash bucket order, i.e. byte-identical to its output.
  */
 #ifndef KMHGPU_H
 #define KMHGPU_H
@@ -54,6 +56,10 @@ extern "C" {
 #define KMHG_OPT_POS 2u
 #define KMHG_OPT_PAIRS 4u
 #define KMHG_OPT_COUNT 8u
+
+/* kmer.pos k-mer (row) order */
+#define KMHG_ORDER_FIRST 0   /* ranked by first occurrence (default) */
+#define KMHG_ORDER_KHASH 1   /* the reference's khash 0.2.8 bucket order, src/kmer_hash.c:1096-1124 */
 
 typedef struct kmhg_index kmhg_index;
 typedef struct kmhg_query kmhg_query;
@@ -83,6 +89,14 @@ int kmhg_build_device(const void *d_seq, size_t L, int k, int do_sort, void *str
                       kmhg_index **out);
 int kmhg_free(kmhg_index *idx);
 int kmhg_index_info(const kmhg_index *idx, kmhg_info *info);
+
+/* Row order of later kmer.pos calls on this index (KMHG_ORDER_*).  The khash order is replayed
+ * on the host from the distinct keys (src/khash.h:230-348 semantics), once per index. */
+int kmhg_set_row_order(kmhg_index *idx, int order);
+int kmhg_get_row_order(const kmhg_index *idx, int *order);
+/* The host replay itself: order[r] = index (into keys) of the r-th live khash bucket after
+ * kh_put of the n distinct keys in the given order.  Host-only, no device work. */
+int kmhg_khash_order(const uint64_t *keys, int64_t n, uint32_t *order);
 
 /* kmer.pos, two-phase: sizes first so the caller (R's allocMatrix) can allocate, then fill.
  * Unset opt bits give 0 sizes and the corresponding pointers may be NULL. */

@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(_HERE, "libkmhgpu.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "kmhgpu.h")
 
 KMHG_OK, KMHG_EINVAL, KMHG_ENOMEM, KMHG_EDEVICE, KMHG_EOVERFLOW = 0, 1, 2, 3, 4
+KMHG_ORDER_FIRST, KMHG_ORDER_KHASH = 0, 1
 
 
 class KmhgError(RuntimeError):
@@ -43,6 +44,9 @@ _PROTOS = {
     "kmhg_build_device": (C.c_int, [vp, C.c_size_t, C.c_int, C.c_int, vp, C.POINTER(vp)]),
     "kmhg_free": (C.c_int, [vp]),
     "kmhg_index_info": (C.c_int, [vp, C.POINTER(Info)]),
+    "kmhg_set_row_order": (C.c_int, [vp, C.c_int]),
+    "kmhg_get_row_order": (C.c_int, [vp, C.POINTER(C.c_int)]),
+    "kmhg_khash_order": (C.c_int, [vp, C.c_int64, vp]),
     "kmhg_positions_size": (C.c_int, [vp, C.c_uint32, i64p, i64p, i64p, i64p]),
     "kmhg_positions_fill": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp]),
     "kmhg_positions_fill_device": (C.c_int, [vp, C.c_uint32, vp, vp, vp, vp, vp]),

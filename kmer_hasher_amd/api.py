@@ -3,6 +3,7 @@
     make_kmer_hash(seq, k, do_sort=False)  <- make.kmer.hash  (kmer_hash.R:5-8)
     kmer_pos(ex_ptr, opt_flag)             <- kmer.pos        (kmer_hash.R:10-21)
     seq_kmer_pos(ex_ptr, seq, k)           <- seq.kmer.pos    (kmer_hash.R:23-28)
+    set_row_order(ex_ptr, "khash")         kmer.pos rows in the reference's khash order (opt-in)
 
 Same argument meaning, same validation order and the reference's own error messages (raised as
 ``KmerHashError``, the analogue of R's error()).  Results follow the R wrappers after their
@@ -147,6 +148,17 @@ def kmer_pos(ex_ptr, opt_flag) -> dict:
     if cnt is not None:
         out["count"] = cnt
     return out
+
+
+def set_row_order(ex_ptr, order: str = "first") -> None:
+    """Label kmer.pos k-mers by first occurrence ("first", the default) or in the reference's own
+    khash bucket order ("khash": byte-identical kmer.pos output, src/kmer_hash.c:1096-1124).
+    KMHG_ROW_ORDER=khash in the environment makes "khash" the default for new indices."""
+    p = _extract(ex_ptr)
+    code = {"first": _lib.KMHG_ORDER_FIRST, "khash": _lib.KMHG_ORDER_KHASH}.get(order)
+    if code is None:
+        raise KmerHashError("order must be 'first' or 'khash'")
+    _lib.check(_lib.lib().kmhg_set_row_order(p.handle, code))
 
 
 def seq_kmer_pos(ex_ptr, seq, k) -> np.ndarray:

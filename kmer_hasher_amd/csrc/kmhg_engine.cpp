@@ -328,8 +328,15 @@ uint64_t table_capacity(int64_t Nw) {
   return (cap + 7) & ~7ull;
 }
 
-struct Canon {              // canonical (first-occurrence) readout order, built on first use
+// KMHG_ROW_ORDER=khash makes new indices label kmer.pos rows in the reference's khash order.
+int default_row_order() {
+  const char* e = std::getenv("KMHG_ROW_ORDER");
+  return (e && std::string(e) == "khash") ? KMHG_ORDER_KHASH : KMHG_ORDER_FIRST;
+}
+
+struct Canon {              // readout order arrays (first occurrence or khash), built on use
   bool ready = false;
+  int order = KMHG_ORDER_FIRST;   // which order the arrays below hold
   DBuf<uint32_t> perm, canon_off, pkeys;
   DBuf<uint64_t> pair_off;
   uint64_t n_multi = 0;
@@ -350,6 +357,7 @@ struct kmhg_index {
   DBuf<Slot> table;
   DBuf<int32_t> positions;
   Canon canon;
+  int row_order = default_row_order();   // kmer.pos k-mer order (KMHG_ORDER_*)
 };
 
 struct kmhg_query {
@@ -623,6 +631,127 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
   c.ready = true;
 }
 
+// khash 0.2.8 bucket-order replay (the reference's row order, src/kmer_hash.c:1096-1124).
+// The reference only ever calls kh_get (read-only) and kh_put on NEW keys, so its final table
+// depends only on the distinct keys in first-insertion order = our first-occurrence order.  This
+// replays kh_put's sizing (4 buckets minimum; when occupancy reaches (int)(0.77 nb + 0.5) the
+// table is resized to the next power of two above nb, src/khash.h:307-317), its probe sequence
+// (i + ++step) & mask from hash (u32)(key>>33 ^ key ^ key<<11) (src/khash.h:385), and kh_resize's
+// in-place rehash, which moves elements by kick-out in old-bucket order (src/khash.h:244-306).
+// Returns order[r] = first-occurrence id of the r-th live bucket.
+std::vector<uint32_t> khash_bucket_order(const std::vector<uint64_t>& keys) {
+  enum : uint8_t { LIVE = 0, MOVED = 1, EMPTY = 2 };
+  auto hash = [](uint64_t k) { return (uint32_t)((k >> 33) ^ k ^ (k << 11)); };
+  uint32_t nb = 0, size = 0, upper = 0;
+  std::vector<uint8_t> st;
+  std::vector<uint64_t> key;
+  std::vector<uint32_t> val;
+  auto resize = [&](uint32_t want) {
+    uint32_t nnb = 4;
+    while (nnb < want) nnb <<= 1;
+    if (size >= (uint32_t)(nnb * 0.77 + 0.5)) return;   // too small: unchanged
+    std::vector<uint8_t> nst(nnb, EMPTY);
+    if (nnb > nb) { key.resize(nnb); val.resize(nnb); }
+    const uint32_t nmask = nnb - 1;
+    for (uint32_t j = 0; j < nb; ++j) {
+      if (st[j] != LIVE) continue;
+      uint64_t k = key[j];
+      uint32_t v = val[j];
+      st[j] = MOVED;
+      for (;;) {                            // kick-out: displace a not-yet-moved element
+        uint32_t i = hash(k) & nmask, step = 0;
+        while (nst[i] != EMPTY) i = (i + (++step)) & nmask;
+        nst[i] = LIVE;
+        if (i < nb && st[i] == LIVE) {
+          std::swap(k, key[i]);
+          std::swap(v, val[i]);
+          st[i] = MOVED;
+        } else {
+          key[i] = k;
+          val[i] = v;
+          break;
+        }
+      }
+    }
+    st.swap(nst);
+    nb = nnb;
+    upper = (uint32_t)(nb * 0.77 + 0.5);
+  };
+  for (uint32_t u = 0; u < (uint32_t)keys.size(); ++u) {
+    if (size >= upper) resize(nb + 1);      // no deletions: n_occupied == size
+    const uint32_t mask = nb - 1;
+    uint32_t i = hash(keys[u]) & mask, step = 0;
+    while (st[i] != EMPTY) i = (i + (++step)) & mask;   // distinct keys: never a match
+    key[i] = keys[u];
+    val[i] = u;
+    st[i] = LIVE;
+    ++size;
+  }
+  std::vector<uint32_t> order;
+  order.reserve(size);
+  for (uint32_t j = 0; j < nb; ++j)
+    if (st[j] == LIVE) order.push_back(val[j]);
+  return order;
+}
+
+// Readout arrays for idx->row_order.  The first-occurrence arrays are built on the GPU
+// (prepare_canon); the khash order relabels them: the keys go to the host once, the bucket
+// order is replayed there (inherently sequential, ~0.1 us per key), and the permuted arrays
+// come back.  The readout kernels then run unchanged.
+void prepare_readout(kmhg_index* idx, hipStream_t s) {
+  Canon& c = idx->canon;
+  if (c.ready && c.order == idx->row_order) return;
+  if (c.ready && c.order != KMHG_ORDER_FIRST) c.ready = false;   // rebuild from first order
+  prepare_canon(idx, s);
+  c.order = KMHG_ORDER_FIRST;
+  if (idx->row_order == KMHG_ORDER_FIRST) return;
+  const uint32_t U = (uint32_t)idx->U;
+  std::vector<uint64_t> keys(U);
+  std::vector<uint32_t> perm(U);
+  std::vector<int32_t> cnt(U);
+  if (U) {
+    DBuf<uint64_t> dk(U, s);
+    DBuf<int32_t> dc(U, s);
+    LAUNCH("k_gather_keys", s, launch_gather_keys(c.perm.p, U, idx->table.p, dk.p, s));
+    LAUNCH("k_read_keys", s, launch_read_keys(c.perm.p, U, idx->table.p, idx->k, dc.p, nullptr, s));
+    HIPC(hipMemcpyAsync(keys.data(), dk.p, (size_t)U * 8, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(cnt.data(), dc.p, (size_t)U * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(perm.data(), c.perm.p, (size_t)U * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+  }
+  const std::vector<uint32_t> order = khash_bucket_order(keys);
+  if (order.size() != U) fail(KMHG_EDEVICE, "khash order replay lost keys (internal error)");
+  std::vector<uint32_t> perm_k(U), off_k(U + 1), pkeys;
+  std::vector<uint64_t> pair_off;
+  uint64_t rows = 0, pairs = 0;
+  for (uint32_t r = 0; r < U; ++r) {
+    const uint32_t id = order[r];
+    const uint64_t n = (uint64_t)cnt[id];
+    perm_k[r] = perm[id];
+    off_k[r] = (uint32_t)rows;
+    rows += n;
+    if (n >= 2) {
+      pkeys.push_back(r);
+      pair_off.push_back(pairs);
+      pairs += n * (n - 1) / 2;
+    }
+  }
+  off_k[U] = (uint32_t)rows;
+  if (rows != idx->N || pairs != idx->P || pkeys.size() != c.n_multi)
+    fail(KMHG_EDEVICE, "khash readout order inconsistent with the index (internal error)");
+  if (U) {
+    HIPC(hipMemcpyAsync(c.perm.p, perm_k.data(), (size_t)U * 4, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(c.canon_off.p, off_k.data(), (size_t)(U + 1) * 4, hipMemcpyHostToDevice, s));
+  }
+  if (!pkeys.empty()) {
+    HIPC(hipMemcpyAsync(c.pkeys.p, pkeys.data(), pkeys.size() * 4, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(c.pair_off.p, pair_off.data(), pair_off.size() * 8,
+                        hipMemcpyHostToDevice, s));
+  }
+  HIPC(hipStreamSynchronize(s));   // host vectors die here
+  c.order = KMHG_ORDER_KHASH;
+}
+
 void positions_sizes(kmhg_index* idx, uint32_t opt, int64_t* nk, int64_t* np, int64_t* npp,
                      int64_t* nc) {
   if (nk) *nk = (opt & KMHG_OPT_KMER) ? (int64_t)idx->U : 0;
@@ -633,7 +762,7 @@ void positions_sizes(kmhg_index* idx, uint32_t opt, int64_t* nk, int64_t* np, in
 
 void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, int32_t* pairs,
                       int32_t* counts, hipStream_t s) {
-  prepare_canon(idx, s);
+  prepare_readout(idx, s);
   Canon& c = idx->canon;
   const uint32_t U = (uint32_t)idx->U;
   if ((opt & (KMHG_OPT_KMER | KMHG_OPT_COUNT)) && U)
@@ -711,6 +840,30 @@ int kmhg_index_info(const kmhg_index* idx, kmhg_info* info) {
     info->max_count = idx->max_n;
     info->table_slots = (int64_t)idx->slots();
     info->device_bytes = (int64_t)(idx->table.bytes() + idx->positions.bytes());
+  });
+}
+
+int kmhg_set_row_order(kmhg_index* idx, int order) {
+  return guarded([&] {
+    if (!idx) fail(KMHG_EINVAL, "null index");
+    if (order != KMHG_ORDER_FIRST && order != KMHG_ORDER_KHASH) fail(KMHG_EINVAL, "unknown row order");
+    idx->row_order = order;
+  });
+}
+
+int kmhg_khash_order(const uint64_t* keys, int64_t n, uint32_t* order) {
+  return guarded([&] {
+    if (n < 0 || (n && (!keys || !order))) fail(KMHG_EINVAL, "null argument");
+    const std::vector<uint64_t> k(keys, keys + n);
+    const std::vector<uint32_t> o = khash_bucket_order(k);
+    std::copy(o.begin(), o.end(), order);
+  });
+}
+
+int kmhg_get_row_order(const kmhg_index* idx, int* order) {
+  return guarded([&] {
+    if (!idx || !order) fail(KMHG_EINVAL, "null argument");
+    *order = idx->row_order;
   });
 }
 

@@ -58,6 +58,8 @@ void launch_read_order(const uint32_t* F, int64_t L, const Slot* T, uint64_t* st
                        ReadMeta* rmeta, hipStream_t s);
 void launch_read_keys(const uint32_t* perm, uint32_t U, const Slot* T, int k, int32_t* out_counts,
                       char* out_kmers, hipStream_t s);
+void launch_gather_keys(const uint32_t* perm, uint32_t U, const Slot* T, uint64_t* out_keys,
+                        hipStream_t s);
 void launch_read_pos(const uint32_t* perm, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
                      const Slot* T, const int32_t* positions, int2* out, hipStream_t s);
 void launch_read_pairs(const uint32_t* pkeys, const uint64_t* pair_off, uint32_t M,

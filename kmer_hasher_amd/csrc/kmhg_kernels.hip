@@ -286,6 +286,8 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   const int o0 = (int)(t_start - base);
   stage_tile(seq, L, base, st, aligned != 0);
   __syncthreads();
+  // (measured: issuing all WPT home-slot loads before resolving any cost occupancy -- 94
+  // VGPRs, 5 waves/SIMD -- and ran 15 % slower than this two-deep loop)
   uint64_t rows = 0;
 #pragma unroll 2
   for (int j = 0; j < WPT; ++j) {
@@ -459,6 +461,14 @@ k_read_keys(const uint32_t* __restrict__ perm, uint32_t U, const Slot* __restric
   }
 }
 
+// Keys of the readout order (khash row-order replay input): out[c] = key of perm[c].
+__global__ void __launch_bounds__(BLOCK)
+k_gather_keys(const uint32_t* __restrict__ perm, uint32_t U, const Slot* __restrict__ T,
+              uint64_t* __restrict__ out_keys) {
+  for (uint32_t c = blockIdx.x * BLOCK + threadIdx.x; c < U; c += gridDim.x * BLOCK)
+    out_keys[c] = T[perm[c]].key;
+}
+
 // R_pos: rows (i, pos) in canonical order.  Each workgroup owns TILE output rows; every key
 // owns >= 1 row so its key range fits the LDS copy of the canonical offsets.
 __global__ void __launch_bounds__(BLOCK)
@@ -616,6 +626,12 @@ void launch_read_keys(const uint32_t* perm, uint32_t U, const Slot* T, int k, in
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(k_read_keys, dim3(g), dim3(BLOCK), 0, s, perm, U, T, k, out_counts,
                      out_kmers);
+}
+void launch_gather_keys(const uint32_t* perm, uint32_t U, const Slot* T, uint64_t* out_keys,
+                        hipStream_t s) {
+  unsigned g = grid_for(U, BLOCK);
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_gather_keys, dim3(g), dim3(BLOCK), 0, s, perm, U, T, out_keys);
 }
 void launch_read_pos(const uint32_t* perm, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
                      const Slot* T, const int32_t* positions, int2* out, hipStream_t s) {

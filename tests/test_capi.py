@@ -3,6 +3,8 @@ arguments with the reference's error messages before touching a device (CPU-safe
 import ctypes as C
 import subprocess
 
+import numpy as np
+
 import pytest
 
 from kmer_hasher_amd import _lib, api
@@ -66,3 +68,33 @@ def test_timing_report_is_json_without_device():
     buf = C.create_string_buffer(4096)
     assert _lib.lib().kmhg_timing_report(buf, len(buf)) == 0
     assert isinstance(json.loads(buf.value.decode()), dict)
+
+
+def _khash_order_product(keys: np.ndarray) -> np.ndarray:
+    keys = np.ascontiguousarray(keys, np.uint64)
+    out = np.empty(len(keys), np.uint32)
+    assert _lib.lib().kmhg_khash_order(keys.ctypes.data, len(keys), out.ctypes.data) == 0
+    return out.astype(np.int64)
+
+
+def test_khash_row_order_replay_matches_oracle(golden, testfa):
+    """The product's host replay of khash 0.2.8 (row order of kmer.pos in KMHG_ORDER_KHASH mode)
+    against the oracle's replay, which test_oracle_golden pins to the reference's raw digests --
+    and directly against those digests."""
+    from kmh_canon import sha
+    from oracle import oracle as O
+    from synth_inputs import sequence
+    for r in golden[0]["records"]:
+        if r["U"] > 300_000:
+            continue
+        oi = O.OracleIndex(sequence(r["name"], testfa), r["k"])
+        order = _khash_order_product(oi.keys)
+        assert np.array_equal(order, oi.khash_order()), (r["name"], r["k"])
+        assert sha(oi.counts[order]) == r["raw_sha"]["count"]
+    rng = np.random.default_rng(5)
+    for U in (0, 1, 3, 4, 5, 100, 5000):             # resize boundaries included
+        keys = np.unique(rng.integers(0, 2**62, U, dtype=np.uint64))
+        rng.shuffle(keys)
+        want = np.empty(len(keys), np.int64)
+        assert O._orc().orc_khash_order(np.ascontiguousarray(keys), len(keys), want) == len(keys)
+        assert np.array_equal(_khash_order_product(keys), want)

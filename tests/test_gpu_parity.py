@@ -164,3 +164,32 @@ def test_fallback_build_v1_matches_oracle(gpu, monkeypatch):
         _check_against_oracle(s, k)
     rr = synth.add_n_runs(synth.repeat_rich(60_000, 5, n_gap_every=20_000), 0.002, 3)
     _check_against_oracle(rr.tobytes().decode("latin-1"), 21)
+
+
+def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
+    """KMHG_ORDER_KHASH: kmer.pos labelled in the reference's khash bucket order reproduces the
+    reference's raw output (its digests in tests/golden) byte for byte."""
+    from kmer_hasher_amd import set_row_order
+    make, kpos, _ = _api()
+    for r in golden[0]["records"]:
+        s = sequence(r["name"], testfa)
+        ptr = make(s, r["k"])
+        set_row_order(ptr, "khash")
+        res = kpos(ptr, 15)
+        assert sha(res["count"]) == r["raw_sha"]["count"], (r["name"], r["k"])
+        assert sha(res["pos"].reshape(-1)) == r["raw_sha"]["pos"], (r["name"], r["k"])
+        assert sha(res["pair.pos"].reshape(-1)) == r["raw_sha"]["pair.pos"], (r["name"], r["k"])
+        assert sha(res["kmer"]) == r["raw_sha"]["kmer"], (r["name"], r["k"])
+        set_row_order(ptr, "first")                 # and back
+        assert sha(kpos(ptr, 8)["count"]) == r["canon_sha"]["count"]
+        ptr.free()
+    for r in golden[1]:
+        ptr = make(r["name"], r["k"])
+        set_row_order(ptr, "khash")
+        res = kpos(ptr, 15)
+        raw = r["arrays"]["raw"]
+        assert res["kmer"] == raw["kmer"], r["name"]
+        assert res["pos"].reshape(-1).tolist() == raw["pos"], r["name"]
+        assert res["pair.pos"].reshape(-1).tolist() == raw["pair.pos"], r["name"]
+        assert res["count"].tolist() == raw["count"], r["name"]
+        ptr.free()
