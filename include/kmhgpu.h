@@ -126,6 +126,17 @@ int kmhg_query_rows_device(kmhg_query *q, const int32_t **d_rows); /* owned by q
 int kmhg_query_copy_device(kmhg_query *q, void *d_dst, void *stream);
 int kmhg_query_free(kmhg_query *q);
 
+/* kmer.pairs <- .Call("kmer_pair_pos", ptr_a, ptr_b)           src/kmer_hash.c:1174-1203
+ * Rows (a, b) = (position in index a, position in index b) for every k-mer both indices hold:
+ * a's k-mers in a's kmer.pos row order (kmhg_set_row_order), a's positions outer, b's inner;
+ * the result is a query handle holding 2 x n_rows int32, read like a seq.kmer.pos result.
+ * Defined where the reference is broken: only a's live k-mers are visited (the reference reads
+ * empty buckets and calls kh_exist(b, kh_end(b)), src/kmer_hash.c:1182-1185; test.R:330 "This
+ * crashes"), and both indices must have the same k ("the two indices must have the same k"). */
+int kmhg_pairs_run(kmhg_index *a, kmhg_index *b, kmhg_query **q, int64_t *n_rows);
+int kmhg_pairs_run_device(kmhg_index *a, kmhg_index *b, void *stream, kmhg_query **q,
+                          int64_t *n_rows);
+
 /* Index replication for the multi-GPU query (the index is broadcast once over RCCL/xGMI by the
  * caller): the device image is the hash table (16-B slots {key, count, end}) + the positions;
  * export copies it into caller device buffers, import rebuilds an index on the current device. */

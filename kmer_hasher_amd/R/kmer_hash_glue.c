@@ -9,6 +9,7 @@
  *   make_kmer_h_index(seq, k, do_sort)      src/kmer_hash.c:506-540   -> EXTPTRSXP
  *   kmer_positions(ptr, opt_flag)           src/kmer_hash.c:1054-1147 -> named VECSXP[4]
  *   sequence_kmer_positions(ptr, seq, k)    src/kmer_hash.c:1151-1172 -> INTSXP 2 x H
+ *   kmer_pair_pos(ptr_a, ptr_b)             src/kmer_hash.c:1174-1203 -> INTSXP 2 x M (fixed)
  *
  * Differences, all deliberate: the finaliser frees the whole payload (the reference leaks the
  * 32-B khash_ptr, src/kmer_hash.c:56-66); a freed pointer is detected instead of dereferenced;
@@ -138,10 +139,48 @@ SEXP sequence_kmer_positions(SEXP ptr_r, SEXP seq_r, SEXP k_r) {
   return ret;
 }
 
+/* kmer_pair_pos, src/kmer_hash.c:1174-1203 (called by kmer.pairs, kmer_hash.R:30-34): rows
+ * (a, b) for the k-mers both indices hold.  The reference walks empty buckets and reads past
+ * the end of b's flags (test.R:330 "This crashes"); kmhg_pairs_run defines the intended result
+ * and refuses indices of different k. */
+SEXP kmer_pair_pos(SEXP ptr_a, SEXP ptr_b) {
+  kmhg_index *a = gpu_index_of(ptr_a);
+  kmhg_index *b = gpu_index_of(ptr_b);
+  kmhg_query *q = NULL;
+  int64_t h = 0;
+  if (kmhg_pairs_run(a, b, &q, &h) != KMHG_OK) error("%s", kmhg_last_error());
+  if (h > INT_MAX) {
+    kmhg_query_free(q);
+    error("result has more than 2^31-1 columns (R matrix limit)");
+  }
+  SEXP ret = PROTECT(allocMatrix(INTSXP, 2, (int)h));
+  int rc = h ? kmhg_query_fill(q, INTEGER(ret)) : KMHG_OK;
+  kmhg_query_free(q);
+  if (rc != KMHG_OK) error("%s", kmhg_last_error());
+  UNPROTECT(1);
+  return ret;
+}
+
+/* Not in the reference: choose the kmer.pos k-mer order of an index, "first" (first
+ * occurrence, the default) or "khash" (the reference's own bucket order, byte-identical
+ * output).  KMHG_ROW_ORDER=khash in the environment sets the default for new indices. */
+SEXP kmer_row_order(SEXP ptr_r, SEXP order_r) {
+  kmhg_index *idx = gpu_index_of(ptr_r);
+  if (TYPEOF(order_r) != STRSXP || length(order_r) != 1)
+    error("order should be \"first\" or \"khash\"");
+  const char *o = CHAR(STRING_ELT(order_r, 0));
+  int code = !strcmp(o, "khash") ? KMHG_ORDER_KHASH : (!strcmp(o, "first") ? KMHG_ORDER_FIRST : -1);
+  if (code < 0) error("order should be \"first\" or \"khash\"");
+  if (kmhg_set_row_order(idx, code) != KMHG_OK) error("%s", kmhg_last_error());
+  return R_NilValue;
+}
+
 static const R_CallMethodDef gpu_call_methods[] = {
     {"make_kmer_h_index", (DL_FUNC)&make_kmer_h_index, 3},
     {"kmer_positions", (DL_FUNC)&kmer_positions, 2},
     {"sequence_kmer_positions", (DL_FUNC)&sequence_kmer_positions, 3},
+    {"kmer_pair_pos", (DL_FUNC)&kmer_pair_pos, 2},
+    {"kmer_row_order", (DL_FUNC)&kmer_row_order, 2},
     {NULL, NULL, 0}};
 
 void R_init_kmer_hash(DllInfo *info) { R_registerRoutines(info, NULL, gpu_call_methods, NULL, NULL); }

@@ -32,3 +32,17 @@ seq.kmer.pos <- function(ex.ptr, seq, k){
     rownames(m) <- c("i", "j")
     t(m)
 }
+
+## shared k-mers of two indices: rows (a, b) = a position in ptr.a with a position in ptr.b
+## (the reference's version crashes, test.R:330; this one visits only live k-mers, same k)
+kmer.pairs <- function(ptr.a, ptr.b){
+    tmp <- t(.Call("kmer_pair_pos", ptr.a, ptr.b))
+    colnames(tmp) <- c("a", "b")
+    tmp
+}
+
+## not in the reference: kmer.pos k-mer order, "first" (default) or "khash" (the reference's
+## bucket order: byte-identical kmer.pos output)
+kmer.row.order <- function(ex.ptr, order="khash"){
+    invisible(.Call("kmer_row_order", ex.ptr, as.character(order)))
+}

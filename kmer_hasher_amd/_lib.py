@@ -54,6 +54,8 @@ _PROTOS = {
     "kmhg_query_run_device": (C.c_int, [vp, vp, C.c_size_t, C.c_int, vp, C.POINTER(vp), i64p]),
     "kmhg_query_run_device_range": (C.c_int, [vp, vp, C.c_size_t, C.c_int, C.c_int64, C.c_int64,
                                               vp, C.POINTER(vp), i64p]),
+    "kmhg_pairs_run": (C.c_int, [vp, vp, C.POINTER(vp), i64p]),
+    "kmhg_pairs_run_device": (C.c_int, [vp, vp, vp, C.POINTER(vp), i64p]),
     "kmhg_query_fill": (C.c_int, [vp, vp]),
     "kmhg_query_rows_device": (C.c_int, [vp, C.POINTER(vp)]),
     "kmhg_query_copy_device": (C.c_int, [vp, vp, vp]),

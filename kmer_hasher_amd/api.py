@@ -3,6 +3,7 @@
     make_kmer_hash(seq, k, do_sort=False)  <- make.kmer.hash  (kmer_hash.R:5-8)
     kmer_pos(ex_ptr, opt_flag)             <- kmer.pos        (kmer_hash.R:10-21)
     seq_kmer_pos(ex_ptr, seq, k)           <- seq.kmer.pos    (kmer_hash.R:23-28)
+    kmer_pairs(ptr_a, ptr_b)               <- kmer.pairs      (kmer_hash.R:30-34), fixed
     set_row_order(ex_ptr, "khash")         kmer.pos rows in the reference's khash order (opt-in)
 
 Same argument meaning, same validation order and the reference's own error messages (raised as
@@ -148,6 +149,32 @@ def kmer_pos(ex_ptr, opt_flag) -> dict:
     if cnt is not None:
         out["count"] = cnt
     return out
+
+
+def kmer_pairs(ptr_a, ptr_b) -> np.ndarray:
+    """kmer.pairs -> .Call("kmer_pair_pos", ...)  (src/kmer_hash.c:1174-1203, kmer_hash.R:30-34).
+
+    Returns an (M, 2) int32 matrix with columns (a, b): for every k-mer held by both indices,
+    each position in a paired with each position in b (a outer, b inner), k-mers in a's kmer.pos
+    row order.  Defined where the reference crashes (empty buckets of a, out-of-bounds kh_exist
+    on b); the indices must share k."""
+    a, b = _extract(ptr_a), _extract(ptr_b)
+    L = _lib.lib()
+    q = C.c_void_p()
+    h = C.c_int64()
+    rc = L.kmhg_pairs_run(a.handle, b.handle, C.byref(q), C.byref(h))
+    if rc == _lib.KMHG_EINVAL:
+        raise KmerHashError(L.kmhg_last_error().decode())
+    _lib.check(rc)
+    try:
+        if h.value > INT_MAX:
+            raise KmerHashError("result has more than 2^31-1 columns (R matrix limit)")
+        rows = np.empty(2 * h.value, np.int32)
+        if h.value:
+            _lib.check(L.kmhg_query_fill(q, rows.ctypes.data))
+    finally:
+        L.kmhg_query_free(q)
+    return rows.reshape(-1, 2)
 
 
 def set_row_order(ex_ptr, order: str = "first") -> None:

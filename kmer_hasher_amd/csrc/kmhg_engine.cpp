@@ -594,6 +594,39 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   return q.release();
 }
 
+void prepare_readout(kmhg_index* idx, hipStream_t s);
+
+// ---------------------------------------------------------------------------- kmer.pairs
+// Rows (a, b) for the k-mers both indices hold, a's k-mers in a's kmer.pos row order
+// (kmhg_join.hip).  Same two-phase shape as the query: probe + tile totals, one read-back, emit.
+kmhg_query* pairs_device(kmhg_index* a, kmhg_index* b, hipStream_t s) {
+  if (a->k != b->k) fail(KMHG_EINVAL, "the two indices must have the same k");
+  if (a->device != b->device) fail(KMHG_EINVAL, "the two indices must be on the same device");
+  prepare_readout(a, s);
+  auto q = std::make_unique<kmhg_query>();
+  q->device = a->device;
+  q->stream = s;
+  a->stream = s;
+  b->stream = s;
+  const uint32_t Ua = (uint32_t)a->U;
+  if (Ua == 0 || b->U == 0) return q.release();
+  const uint32_t nt = tiles_for(Ua);
+  DBuf<uint4> jinfo(Ua, s);
+  DBuf<uint64_t> tiles((size_t)nt + 1, s);
+  LAUNCH("k_join_probe", s, launch_join_probe(a->canon.perm.p, Ua, a->table.p, b->table.p, b->geom,
+                                              jinfo.p, tiles.p, s));
+  LAUNCH("k_scan_tiles_u64", s, launch_scan_tiles_u64(tiles.p, nt, tiles.p + nt, s));
+  uint64_t H = 0;
+  HIPC(hipMemcpyAsync(&H, tiles.p + nt, sizeof(H), hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  q->H = (int64_t)H;
+  q->rows.reset(H);
+  if (H)
+    LAUNCH("k_join_emit", s, launch_join_emit(jinfo.p, Ua, a->positions.p, b->positions.p, tiles.p,
+                                              q->rows.p, s));
+  return q.release();
+}
+
 // ---------------------------------------------------------------------------- readout
 void prepare_canon(kmhg_index* idx, hipStream_t s) {
   idx->stream = s;
@@ -906,6 +939,27 @@ int kmhg_positions_fill(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos
     if ((opt & KMHG_OPT_COUNT) && U && counts)
       HIPC(hipMemcpyAsync(counts, dc.p, dc.bytes(), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+  });
+}
+
+int kmhg_pairs_run(kmhg_index* a, kmhg_index* b, kmhg_query** q, int64_t* n_rows) {
+  return guarded([&] {
+    if (!a || !b || !q) fail(KMHG_EINVAL, "null argument");
+    DeviceGuard g(a->device);
+    hipStream_t s = lib_stream();
+    *q = pairs_device(a, b, s);
+    HIPC(hipStreamSynchronize(s));
+    if (n_rows) *n_rows = (*q)->H;
+  });
+}
+
+int kmhg_pairs_run_device(kmhg_index* a, kmhg_index* b, void* stream, kmhg_query** q,
+                          int64_t* n_rows) {
+  return guarded([&] {
+    if (!a || !b || !q) fail(KMHG_EINVAL, "null argument");
+    DeviceGuard g(a->device);
+    *q = pairs_device(a, b, (hipStream_t)stream);
+    if (n_rows) *n_rows = (*q)->H;
   });
 }
 

@@ -128,6 +128,12 @@ void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t*
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);
 
+// kmer.pairs (kmhg_join.hip)
+void launch_join_probe(const uint32_t* perm_a, uint32_t Ua, const Slot* Ta, const Slot* Tb, Geom gb,
+                       uint4* jinfo, uint64_t* tile_rows, hipStream_t s);
+void launch_join_emit(const uint4* jinfo, uint32_t Ua, const int32_t* pos_a, const int32_t* pos_b,
+                      const uint64_t* tile_row0, int2* out, hipStream_t s);
+
 #ifdef KMHG_STAMPS
 void set_stamp_buffer(uint64_t* p);
 #endif

@@ -145,6 +145,25 @@ class OracleIndex:
         assert n == self.P
         return out[:3 * self.P]
 
+    def pairs_with(self, other: "OracleIndex", order=None) -> np.ndarray:
+        """kmer_pair_pos (src/kmer_hash.c:1174-1203) as intended: for each live k-mer of self (in
+        canonical order, or `order`), if `other` holds it, all (pos_self, pos_other) with self's
+        positions outer.  2 x M interleaved int32."""
+        ids = np.arange(self.U) if order is None else np.asarray(order)
+        srt = np.argsort(other.keys, kind="stable")
+        sk = other.keys[srt]
+        at = np.searchsorted(sk, self.keys[ids]) if len(sk) else np.zeros(len(ids), np.int64)
+        out = []
+        for c, p in zip(ids, at):
+            if p < len(sk) and sk[p] == self.keys[c]:
+                o = srt[p]
+                pa = self.positions[self.offsets[c]:self.offsets[c + 1]]
+                pb = other.positions[other.offsets[o]:other.offsets[o + 1]]
+                out.append(np.stack([np.repeat(pa, len(pb)), np.tile(pb, len(pa))], 1))
+        if not out:
+            return np.empty(0, np.int32)
+        return np.concatenate(out).astype(np.int32).reshape(-1)
+
     def kmer_strings(self) -> list[str]:
         return [decode(int(x), self.k) for x in self.keys]
 
