@@ -3,9 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
 
 metric: "Mbp/s indexed (make.kmer.hash k=31) at 1/2/4/8 GPUs; seq.kmer.pos query Mbp/s".
-A step is one make.kmer.hash build (kmhg_build_device: table init, encode/insert, compact,
-scatter, sort, meta read-back) of one synthetic sequence already resident in HBM, and the index
-is freed again.  Config 2 (default, BASELINE.json configs[1]): 10 Mbp iid ACGT, k = 31.  The
+A step is one make.kmer.hash build (kmhg_build_device: radix partition of the windows by hash
+bucket, per-bucket LDS tables, totals to a pinned record) of one synthetic sequence already
+resident in HBM, and the index is freed again.  kmhg_build_device is asynchronous, so the timed
+steps pipeline host enqueue with device execution; `synchronous` reports the same steps with the
+host waiting for every build (the R API's make.kmer.hash semantics).  Config 2 (default, BASELINE.json configs[1]): 10 Mbp iid ACGT, k = 31.  The
 seq.kmer.pos self-query of the same sequence is timed the same way and reported in `query`.
 
 N > 1 (launched by torch.distributed.run, one rank per GPU): every rank indexes its own
@@ -148,9 +150,11 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    def build_step():
+    def build_step(wait=False):
+        # kmhg_build_device is asynchronous: back-to-back steps pipeline the host's enqueue of
+        # step i+1 with the device's execution of step i; every step runs the whole build
         idx = D.DeviceIndex.build(seq, k, stream)
-        info = idx.info()
+        info = idx.info() if wait else None        # info() waits for the build
         idx.free()
         return info
 
@@ -158,13 +162,20 @@ def main():
     # dominant one), then exactly K timed steps with events around the dominant kernel only, so
     # the per-kernel events add no dead time to the rest of the timed region
     for _ in range(args.warmup):
-        info = build_step()
+        info = build_step(wait=True)
+    # the same steps with a wait after each (the synchronous make.kmer.hash of the R API)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        info = build_step(wait=True)
+    barrier()
+    t_sync = time.perf_counter() - t0
     D.timing_enable(True)
     D.timing_select(None)
     D.timing_reset()
     n_id = 2
     for _ in range(n_id):
-        info = build_step()
+        info = build_step(wait=True)
     wt = D.timing_report()
     all_kernels = {n: v[1] / v[0] for n, v in wt.items() if v[0]}
     per_step = {n: v[1] / n_id for n, v in wt.items() if v[0]}
@@ -174,9 +185,10 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        info = build_step()
+        build_step()
     barrier()
     t_build = time.perf_counter() - t0
+    info = build_step(wait=True)                   # totals of one more (waited) build
     ktimes = D.timing_report()
     D.timing_enable(False)
     D.timing_select(None)
@@ -204,10 +216,10 @@ def main():
     t_query = time.perf_counter() - t0
     idx.free()
 
-    tb = torch.tensor([t_build, t_query], dtype=torch.float64, device=dev)
+    tb = torch.tensor([t_build, t_query, t_sync], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tb, op=dist.ReduceOp.MAX)
-    t_build, t_query = tb.tolist()
+    t_build, t_query, t_sync = tb.tolist()
 
     if rank == 0:
         Nw = L - k + 1
@@ -251,6 +263,9 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic, "algorithmic_bytes": ab,
                          "avg_ms": round(dom_ms, 5)},
+            "synchronous": {"value": round(mbp_total * args.steps / t_sync, 2), "unit": "Mbp/s",
+                            "ms_per_step": round(t_sync / args.steps * 1e3, 4),
+                            "note": "same steps, host waits for each build (R-API semantics)"},
             "query": {"value": round(qvalue, 2), "unit": "Mbp/s", "rows": H,
                       "ms_per_step": round(t_query / args.steps * 1e3, 4),
                       "kernels_ms": {n: round(v, 5) for n, v in qper.items()}},

@@ -84,9 +84,15 @@ int kmhg_version(void);
  * "the length of the sequence must be at least k".  do_sort is accepted for API identity; the
  * engine always stores positions ascending, which is what sort_kmer_pos would produce. */
 int kmhg_build(const char *seq, size_t L, int k, int do_sort, kmhg_index **out);
-/* Same, for a device-resident sequence (no NULs assumed) on `stream`. */
+/* Same, for a device-resident sequence (no NULs assumed) on `stream`.  Asynchronous: it returns
+ * once the build is queued, so back-to-back builds pipeline host and device work.  The first
+ * call that reads the index (info, kmer.pos, a query, export, kmhg_index_wait) waits for it;
+ * until then `d_seq` must stay valid and unmodified (the overflow fallback re-reads it).
+ * kmhg_free of an index never used does not wait. */
 int kmhg_build_device(const void *d_seq, size_t L, int k, int do_sort, void *stream,
                       kmhg_index **out);
+/* Wait for an asynchronous build to finish (no-op for a finished index). */
+int kmhg_index_wait(kmhg_index *idx);
 int kmhg_free(kmhg_index *idx);
 int kmhg_index_info(const kmhg_index *idx, kmhg_info *info);
 

@@ -43,6 +43,7 @@ _PROTOS = {
     "kmhg_build": (C.c_int, [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.POINTER(vp)]),
     "kmhg_build_device": (C.c_int, [vp, C.c_size_t, C.c_int, C.c_int, vp, C.POINTER(vp)]),
     "kmhg_free": (C.c_int, [vp]),
+    "kmhg_index_wait": (C.c_int, [vp]),
     "kmhg_index_info": (C.c_int, [vp, C.POINTER(Info)]),
     "kmhg_set_row_order": (C.c_int, [vp, C.c_int]),
     "kmhg_get_row_order": (C.c_int, [vp, C.POINTER(C.c_int)]),

@@ -73,7 +73,7 @@ class DevicePool {
     int dev = 0;
     HIPC(hipGetDevice(&dev));
     {
-      std::lock_guard<std::mutex> g(mu_);
+      std::unique_lock<std::mutex> g(mu_);
       poll_pending();
       auto& fl = free_[{dev, sz}];
       if (!fl.empty()) {
@@ -82,6 +82,19 @@ class DevicePool {
         cached_ -= sz;
         live_[p] = {dev, sz};
         return p;
+      }
+      // a block of this size still in use by queued work: wait for it rather than grow the
+      // pool -- the back-pressure that bounds how far asynchronous builds run ahead
+      for (size_t i = 0; i < pending_.size(); ++i) {
+        if (pending_[i].key != std::make_pair(dev, sz)) continue;
+        Pending pd = pending_[i];
+        pending_.erase(pending_.begin() + (long)i);
+        g.unlock();
+        (void)hipEventSynchronize(pd.ev);
+        g.lock();
+        events_.push_back(pd.ev);
+        live_[pd.p] = pd.key;
+        return pd.p;
       }
     }
     void* p = nullptr;
@@ -204,44 +217,65 @@ struct DBuf {
     p = nullptr; n = 0;
   }
   size_t bytes() const { return n * sizeof(T); }
+  void swap_with(DBuf& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(s, o.s);
+    std::swap(ordered, o.ordered);
+  }
 };
 
-// Pinned, device-visible host records for the build totals (V_stats writes one directly, so the
-// host reads U / N / P after the stream sync with no copy launch).  Slots are recycled.
+// Pinned, device-visible host records for the build totals: V_stats writes one directly, so the
+// host reads U / N / P with no copy launch.  Each record carries an event recorded after the
+// build's last kernel; a record given back while its build is still in flight (an index freed
+// before it was ever used) is reused only once that event has completed.
+struct PinnedRec {
+  BuildMeta* meta = nullptr;
+  hipEvent_t ev = nullptr;
+};
 class PinnedPool {
  public:
   static PinnedPool& get() {
     static PinnedPool p;
     return p;
   }
-  BuildMeta* take() {
+  PinnedRec take() {
     std::lock_guard<std::mutex> g(mu_);
+    for (size_t i = 0; i < pending_.size();) {
+      if (hipEventQuery(pending_[i].ev) == hipSuccess) {
+        free_.push_back(pending_[i]);
+        pending_[i] = pending_.back();
+        pending_.pop_back();
+      } else {
+        ++i;
+      }
+    }
     if (free_.empty()) {
       constexpr int kSlots = 64;
       BuildMeta* blk = nullptr;
       HIPC(hipHostMalloc(reinterpret_cast<void**>(&blk), sizeof(BuildMeta) * kSlots,
                          hipHostMallocCoherent));
-      for (int i = 0; i < kSlots; ++i) free_.push_back(blk + i);
+      for (int i = 0; i < kSlots; ++i) {
+        PinnedRec r;
+        r.meta = blk + i;
+        HIPC(hipEventCreateWithFlags(&r.ev, hipEventDisableTiming));
+        free_.push_back(r);
+      }
     }
-    BuildMeta* m = free_.back();
+    PinnedRec r = free_.back();
     free_.pop_back();
-    return m;
+    std::memset(r.meta, 0, sizeof(*r.meta));
+    return r;
   }
-  void give(BuildMeta* m) {
+  void give(PinnedRec r, bool in_flight) {
+    if (!r.meta) return;
     std::lock_guard<std::mutex> g(mu_);
-    free_.push_back(m);
+    (in_flight ? pending_ : free_).push_back(r);
   }
 
  private:
   std::mutex mu_;
-  std::vector<BuildMeta*> free_;
-};
-struct PinnedMeta {
-  BuildMeta* p;
-  PinnedMeta() : p(PinnedPool::get().take()) { std::memset(p, 0, sizeof(*p)); }
-  ~PinnedMeta() { PinnedPool::get().give(p); }
-  PinnedMeta(const PinnedMeta&) = delete;
-  PinnedMeta& operator=(const PinnedMeta&) = delete;
+  std::vector<PinnedRec> free_, pending_;
 };
 
 // ============================================================================ timing
@@ -358,6 +392,11 @@ struct kmhg_index {
   DBuf<int32_t> positions;
   Canon canon;
   int row_order = default_row_order();   // kmer.pos k-mer order (KMHG_ORDER_*)
+  // asynchronous build (kmhg_build_device returns before the kernels finish): the totals land
+  // in `rec`; `src` is kept for the overflow fallback until finish_build()
+  bool pending = false;
+  PinnedRec rec;
+  const uint8_t* src = nullptr;
 };
 
 struct kmhg_query {
@@ -451,6 +490,7 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 // then one wave per bucket builds its sub-table in LDS.  Falls back to v1 if a bucket's LDS
 // sub-table overflows (never observed: distinct keys per bucket ~ Binomial, mean <= V2_BW).
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
+  const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
   idx->stream = s;
   HIPC(hipGetDevice(&idx->device));
@@ -496,7 +536,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint32_t* n_valid = reinterpret_cast<uint32_t*>(sc);
   BuildMeta* meta = reinterpret_cast<BuildMeta*>(sc + off_meta);
   uint64_t* status = reinterpret_cast<uint64_t*>(sc + off_status);
-  PinnedMeta hmeta;                                        // V_stats writes the totals here
+  idx->rec = PinnedPool::get().take();                     // V_stats writes the totals here
   idx->table.reset(idx->slots());
   idx->positions.reset(Nw);
   DBuf<BucketStats> bstats(nb, s);
@@ -532,20 +572,17 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   LAUNCH("k_v2_bucket", s,
          launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
                           meta, s));
-  LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, nb, n_valid, meta, hmeta.p, s));
+  LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, nb, n_valid, meta, idx->rec.meta, s));
+  HIPC(hipEventRecord(idx->rec.ev, s));
 #ifdef KMHG_STAMPS
   if (const char* f = std::getenv("KMHG_STAMP_FILE")) {
     HIPC(hipStreamSynchronize(s));
     if (FILE* fp = fopen(f, "wb")) { fwrite(stamps, 8, 8 * (size_t)nb, fp); fclose(fp); }
   }
 #endif
-  HIPC(hipStreamSynchronize(s));
-  const BuildMeta hm = *hmeta.p;
-  if (hm.overflow) return nullptr;
-  idx->U = hm.n_kmers;
-  idx->N = hm.n_positions;
-  idx->P = hm.n_pairs;
-  idx->max_n = hm.max_count;
+  // no wait here: the build completes in stream order and finish_build() collects the totals
+  idx->pending = true;
+  idx->src = d_src;
   return idx.release();
 }
 
@@ -554,12 +591,38 @@ int build_version() {   // read per build so tests can exercise the fallback (KM
   return (e && std::string(e) == "v1") ? 1 : 2;
 }
 
+// Returns a possibly pending index (partitioned build); finish_build() completes it.
 kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
-  if (build_version() == 2) {
-    kmhg_index* idx = build_device_v2(d_seq, L, k, s);
-    if (idx) return idx;
-  }
+  if (build_version() == 2) return build_device_v2(d_seq, L, k, s);
   return build_device_v1(d_seq, L, k, s);
+}
+
+// Wait for a pending build and collect its totals.  If a bucket's LDS sub-table overflowed
+// (never observed: distinct keys per bucket ~ Binomial with mean <= V2_BW), the index is rebuilt
+// with the global-atomic build from the retained input.
+void finish_build(kmhg_index* idx) {
+  if (!idx->pending) return;
+  HIPC(hipEventSynchronize(idx->rec.ev));
+  const BuildMeta hm = *idx->rec.meta;
+  PinnedPool::get().give(idx->rec, false);
+  idx->rec = PinnedRec{};
+  idx->pending = false;
+  const uint8_t* src = idx->src;
+  idx->src = nullptr;
+  if (hm.overflow) {
+    std::unique_ptr<kmhg_index> v1(build_device_v1(src, idx->L, idx->k, idx->stream));
+    idx->geom = v1->geom;
+    idx->table.swap_with(v1->table);
+    idx->positions.swap_with(v1->positions);
+    idx->U = v1->U; idx->N = v1->N; idx->P = v1->P; idx->max_n = v1->max_n;
+    v1->table.bind(idx->stream);
+    v1->positions.bind(idx->stream);
+    return;
+  }
+  idx->U = hm.n_kmers;
+  idx->N = hm.n_positions;
+  idx->P = hm.n_pairs;
+  idx->max_n = hm.max_count;
 }
 
 // ---------------------------------------------------------------------------- query
@@ -567,6 +630,7 @@ kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) 
 // end, so shards of consecutive window ranges concatenate to the unsharded result.
 kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int kq, int64_t w0,
                          int64_t w1, hipStream_t s) {
+  finish_build(idx);
   auto q = std::make_unique<kmhg_query>();
   q->device = idx->device;
   q->stream = s;
@@ -576,13 +640,14 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
   const uint32_t nt = tiles_for(Nw);
   DBuf<uint2> qinfo(Nw, s);
-  DBuf<uint64_t> tiles((size_t)nt + 1, s);        // per-tile rows -> first row; [nt] = total
+  // per-tile rows -> first row; [nt] = total; then the long-scan scratch
+  DBuf<uint64_t> tiles((size_t)nt + 1 + scan_u64_scratch(nt), s);
   uint64_t* tile_row0 = tiles.p;
   uint64_t* total = tiles.p + nt;
   LAUNCH("k_query_probe", s,
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
                             tile_row0, s));
-  LAUNCH("k_scan_tiles_u64", s, launch_scan_tiles_u64(tile_row0, nt, total, s));
+  LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, total + 1, s));
   uint64_t H = 0;
   HIPC(hipMemcpyAsync(&H, total, sizeof(H), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -600,6 +665,8 @@ void prepare_readout(kmhg_index* idx, hipStream_t s);
 // Rows (a, b) for the k-mers both indices hold, a's k-mers in a's kmer.pos row order
 // (kmhg_join.hip).  Same two-phase shape as the query: probe + tile totals, one read-back, emit.
 kmhg_query* pairs_device(kmhg_index* a, kmhg_index* b, hipStream_t s) {
+  finish_build(a);
+  finish_build(b);
   if (a->k != b->k) fail(KMHG_EINVAL, "the two indices must have the same k");
   if (a->device != b->device) fail(KMHG_EINVAL, "the two indices must be on the same device");
   prepare_readout(a, s);
@@ -612,10 +679,10 @@ kmhg_query* pairs_device(kmhg_index* a, kmhg_index* b, hipStream_t s) {
   if (Ua == 0 || b->U == 0) return q.release();
   const uint32_t nt = tiles_for(Ua);
   DBuf<uint4> jinfo(Ua, s);
-  DBuf<uint64_t> tiles((size_t)nt + 1, s);
+  DBuf<uint64_t> tiles((size_t)nt + 1 + scan_u64_scratch(nt), s);
   LAUNCH("k_join_probe", s, launch_join_probe(a->canon.perm.p, Ua, a->table.p, b->table.p, b->geom,
                                               jinfo.p, tiles.p, s));
-  LAUNCH("k_scan_tiles_u64", s, launch_scan_tiles_u64(tiles.p, nt, tiles.p + nt, s));
+  LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tiles.p, nt, tiles.p + nt, tiles.p + nt + 1, s));
   uint64_t H = 0;
   HIPC(hipMemcpyAsync(&H, tiles.p + nt, sizeof(H), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -732,6 +799,7 @@ std::vector<uint32_t> khash_bucket_order(const std::vector<uint64_t>& keys) {
 // order is replayed there (inherently sequential, ~0.1 us per key), and the permuted arrays
 // come back.  The readout kernels then run unchanged.
 void prepare_readout(kmhg_index* idx, hipStream_t s) {
+  finish_build(idx);
   Canon& c = idx->canon;
   if (c.ready && c.order == idx->row_order) return;
   if (c.ready && c.order != KMHG_ORDER_FIRST) c.ready = false;   // rebuild from first order
@@ -830,7 +898,9 @@ int kmhg_build(const char* seq, size_t L, int k, int do_sort, kmhg_index** out) 
     hipStream_t s = lib_stream();
     DBuf<uint8_t> d(L + 16, s);
     HIPC(hipMemcpyAsync(d.p, seq, L, hipMemcpyHostToDevice, s));
-    *out = build_device(d.p, (int64_t)L, k, s);
+    std::unique_ptr<kmhg_index> idx(build_device(d.p, (int64_t)L, k, s));
+    finish_build(idx.get());   // synchronous, like make_kmer_h_index (and d dies here)
+    *out = idx.release();
   });
 }
 
@@ -849,6 +919,10 @@ int kmhg_free(kmhg_index* idx) {
   return guarded([&] {
     if (!idx) return;
     DeviceGuard g(idx->device);
+    if (idx->pending) {                  // never used: no need to wait, the record is recycled
+      PinnedPool::get().give(idx->rec, true);   // once the build's event has completed
+      idx->pending = false;
+    }
     // stream-ordered release: the buffers return to the pool once work queued on the index's
     // last stream has finished (queries on other streams are synchronised by their callers)
     idx->table.bind(idx->stream);
@@ -861,9 +935,20 @@ int kmhg_free(kmhg_index* idx) {
   });
 }
 
-int kmhg_index_info(const kmhg_index* idx, kmhg_info* info) {
+int kmhg_index_wait(kmhg_index* idx) {
   return guarded([&] {
-    if (!idx || !info) fail(KMHG_EINVAL, "null argument");
+    if (!idx) fail(KMHG_EINVAL, "null index");
+    DeviceGuard g(idx->device);
+    finish_build(idx);
+  });
+}
+
+int kmhg_index_info(const kmhg_index* cidx, kmhg_info* info) {
+  return guarded([&] {
+    if (!cidx || !info) fail(KMHG_EINVAL, "null argument");
+    kmhg_index* idx = const_cast<kmhg_index*>(cidx);   // completes a pending build
+    DeviceGuard g(idx->device);
+    finish_build(idx);
     info->k = idx->k;
     info->device = idx->device;
     info->seq_len = idx->L;
@@ -904,6 +989,8 @@ int kmhg_positions_size(kmhg_index* idx, uint32_t opt, int64_t* n_kmers, int64_t
                         int64_t* n_pair_rows, int64_t* n_counts) {
   return guarded([&] {
     if (!idx) fail(KMHG_EINVAL, "null index");
+    DeviceGuard g(idx->device);
+    finish_build(idx);
     positions_sizes(idx, opt, n_kmers, n_pos_rows, n_pair_rows, n_counts);
   });
 }
@@ -1052,9 +1139,12 @@ int kmhg_query_free(kmhg_query* q) {
   });
 }
 
-int kmhg_image_sizes_get(const kmhg_index* idx, kmhg_image_sizes* sz, int64_t header[8]) {
+int kmhg_image_sizes_get(const kmhg_index* cidx, kmhg_image_sizes* sz, int64_t header[8]) {
   return guarded([&] {
-    if (!idx || !sz || !header) fail(KMHG_EINVAL, "null argument");
+    if (!cidx || !sz || !header) fail(KMHG_EINVAL, "null argument");
+    kmhg_index* idx = const_cast<kmhg_index*>(cidx);   // completes a pending build
+    DeviceGuard g(idx->device);
+    finish_build(idx);
     sz->table_bytes = (int64_t)(idx->slots() * sizeof(Slot));
     sz->positions_bytes = (int64_t)(idx->N * 4);
     header[0] = idx->k; header[1] = idx->L;
@@ -1064,10 +1154,12 @@ int kmhg_image_sizes_get(const kmhg_index* idx, kmhg_image_sizes* sz, int64_t he
   });
 }
 
-int kmhg_image_export(const kmhg_index* idx, void* d_table, void* d_positions, void* stream) {
+int kmhg_image_export(const kmhg_index* cidx, void* d_table, void* d_positions, void* stream) {
   return guarded([&] {
-    if (!idx) fail(KMHG_EINVAL, "null index");
+    if (!cidx) fail(KMHG_EINVAL, "null index");
+    kmhg_index* idx = const_cast<kmhg_index*>(cidx);
     DeviceGuard g(idx->device);
+    finish_build(idx);
     hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     if (d_table) HIPC(hipMemcpyAsync(d_table, idx->table.p, idx->slots() * sizeof(Slot),
                                      hipMemcpyDeviceToDevice, s));

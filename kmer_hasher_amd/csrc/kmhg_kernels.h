@@ -47,6 +47,11 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
                         hipStream_t s);
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
+// exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
+// reduce-then-scan with `scratch` = scan_u64_scratch(n) u64
+constexpr uint64_t SCAN1_MAX = 16384;
+inline uint64_t scan_u64_scratch(uint64_t n) { return (n + TILE - 1) / TILE + 1; }
+void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch, hipStream_t s);
 void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
                        hipStream_t s);

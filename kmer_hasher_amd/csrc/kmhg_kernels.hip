@@ -327,6 +327,43 @@ k_scan_tiles_u64(uint64_t* __restrict__ a, uint32_t n, uint64_t* __restrict__ to
   if (threadIdx.x == 1023) *total = part[1023];
 }
 
+// Long u64 scans (many query tiles, e.g. 244K for a 500 Mbp query): reduce-then-scan over
+// 2048-entry blocks instead of one workgroup walking the whole array.
+__global__ void __launch_bounds__(BLOCK)
+k_block_sum_u64(const uint64_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ bsum) {
+  __shared__ uint64_t sh[8];
+  const uint64_t base = (uint64_t)blockIdx.x * TILE;
+  uint64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
+    if (i < n) sum += a[i];
+  }
+  uint64_t tot;
+  block_excl_scan(sum, sh, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_block_scan_u64(uint64_t* __restrict__ a, uint64_t n, const uint64_t* __restrict__ bbase) {
+  __shared__ uint64_t sh[8];
+  const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)threadIdx.x * WPT;
+  uint64_t v[WPT];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    v[j] = (base + j < n) ? a[base + j] : 0ull;
+    sum += v[j];
+  }
+  uint64_t tot;
+  uint64_t run = block_excl_scan(sum, sh, tot) + bbase[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (base + j < n) a[base + j] = run;
+    run += v[j];
+  }
+}
+
 // Q_emit: per tile, rows are dealt to lanes evenly (binary search over the tile's LDS prefix of
 // hit counts), so a window with thousands of hits does not serialise one lane.  Output rows are
 // (i = 1-based window end, j = 1-based index position), ordered by i then j as in the reference.
@@ -599,6 +636,17 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
+}
+void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch, hipStream_t s) {
+  if (n <= SCAN1_MAX) {
+    launch_scan_tiles_u64(a, (uint32_t)n, total, s);
+    return;
+  }
+  const uint32_t nb = grid_for(n, TILE);
+  hipLaunchKernelGGL(k_block_sum_u64, dim3(nb), dim3(BLOCK), 0, s, a, n, scratch);
+  launch_scan_tiles_u64(scratch, nb, total, s);
+  hipLaunchKernelGGL(k_block_scan_u64, dim3(nb), dim3(BLOCK), 0, s, a, n,
+                     (const uint64_t*)scratch);
 }
 void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,

@@ -42,6 +42,11 @@ class DeviceIndex:
     def handle(self):
         return self._h
 
+    def wait(self) -> "DeviceIndex":
+        """Block until the (asynchronous) build has finished; info/queries/readout also wait."""
+        _lib.check(_lib.lib().kmhg_index_wait(self._h))
+        return self
+
     def info(self) -> dict:
         inf = _lib.Info()
         _lib.check(_lib.lib().kmhg_index_info(self._h, C.byref(inf)))

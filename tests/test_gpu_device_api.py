@@ -60,3 +60,33 @@ def test_image_export_import_roundtrip(gpu):
     pa, pb = a.positions(15), b.positions(15)
     for f in ("count", "pos", "pair.pos", "kmer"):
         assert torch.equal(pa[f], pb[f])
+
+
+def test_full_size_self_query_properties(gpu):
+    """Size-independent properties at BASELINE sizes (the oracle is too slow here): every window
+    of a self-query matches at least itself, rows are ordered by (i, j), and an i.i.d. 40 Mbp
+    sequence (every 31-mer distinct) gives exactly the identity dot plot.  40 M windows take the
+    query's multi-block tile scan; the 100 Mbp k = 21 index (config 3) builds with three radix
+    passes."""
+    torch = gpu
+    from kmer_hasher_amd import synth
+    from kmer_hasher_amd.device import DeviceIndex
+    for L, k in ((40_000_000, 31), (100_000_000, 21)):
+        seq = torch.from_numpy(synth.iid(L, 7)).cuda()
+        idx = DeviceIndex.build(seq, k)
+        inf = idx.info()
+        assert inf["n_positions"] == L - k + 1
+        q = idx.query(seq, k)
+        rows = q.rows().cpu().numpy().astype(np.int64)
+        assert rows.shape[0] == q.n_rows >= L - k + 1
+        i, j = rows[:, 0], rows[:, 1]
+        d = np.diff(i)
+        assert np.all(d >= 0) and np.all(np.diff(j)[d == 0] > 0)    # sorted by (i, j)
+        assert np.count_nonzero(i - k + 1 == j) == L - k + 1         # each window finds itself
+        if inf["n_kmers"] == L - k + 1:
+            assert q.n_rows == L - k + 1
+            assert np.array_equal(i, np.arange(k, L + 1))
+        q.free()
+        idx.free()
+        del seq
+        torch.cuda.empty_cache()
