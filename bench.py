@@ -54,19 +54,35 @@ def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) 
         return L + 12 * N
     if kernel == "k_v2_scatter":        # one radix pass: read + write 12 B per window
         return 24 * N
-    if kernel == "k_v2_bucket":         # read 12 B/window; write 4 B/position + key/count/end
-        return 12 * N + 4 * N + 16 * U
+    if kernel == "k_v2_bucket":         # read 12 B/window; one 16-B slot per distinct key; 4 B per
+        return 12 * N + 16 * U + 4 * (N - U)   # position of a repeated key (>= N - U of them)
     if kernel == "k_build_insert":      # read L chars; key+count per distinct key; slot id/window
         return L + 12 * U + 4 * Nw
     if kernel == "k_build_compact":     # key+count read, key+count+offset written per key
         return 12 * U + 16 * U
     if kernel == "k_build_scatter":     # slot id read + position write per window
         return 8 * N
-    if kernel == "k_query_probe":       # read L chars; 8-B slot probe + 8-B window record
-        return L + 16 * Nw
-    if kernel == "k_query_emit":        # window record read + 8-B row write + 4-B position read
-        return 8 * Nw + 12 * H
+    if kernel == "k_query_probe":       # read L chars; one 16-B slot probe + 8-B record per window
+        return L + 24 * Nw
+    if kernel == "k_query_emit":        # window record read + 8-B row write (positions of keys
+        return 8 * Nw + 8 * H             # seen once are inline in the record)
     return None
+
+
+def query_roofline(qper: dict, L: int, Nw: int, H: int, pmc: dict) -> dict | None:
+    """Roofline of the dominant query kernel from its HIP-event average duration."""
+    if not qper:
+        return None
+    dom = max(qper, key=qper.get)
+    ab = algorithmic_bytes(dom, L, Nw, 0, 0, H)
+    if not ab:
+        return None
+    ach = ab / (qper[dom] * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": pmc.get(dom, {}).get("hbm_bytes_per_launch"), "algorithmic_bytes": ab,
+            "avg_ms": round(qper[dom], 5),
+            "note": "random 16-B slot probes move >= 64 B each (one DRAM burst)"}
 
 
 def cpu_baseline(seq_bytes: bytes, k: int, budget_s: float = 20.0) -> dict | None:
@@ -234,13 +250,14 @@ def main():
         dom_ms = ktimes[dom][1] / ktimes[dom][0] if ktimes.get(dom, [0])[0] else per[dom]
         ab = algorithmic_bytes(dom, L, Nw, U, N)
         achieved = ab / (dom_ms * 1e-3) / 1e9 if ab else None
-        traffic = None
+        pmc = {}
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_config{args.config}.json")
         if os.path.exists(pmc_path):
             try:
-                traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
+                pmc = json.load(open(pmc_path))
             except Exception:
-                traffic = None
+                pmc = {}
+        traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
         out = {
             "metric": "Mbp/s indexed (make.kmer.hash k=31) at 1/2/4/8 GPUs; "
                       "seq.kmer.pos query Mbp/s",
@@ -268,7 +285,8 @@ def main():
                             "note": "same steps, host waits for each build (R-API semantics)"},
             "query": {"value": round(qvalue, 2), "unit": "Mbp/s", "rows": H,
                       "ms_per_step": round(t_query / args.steps * 1e3, 4),
-                      "kernels_ms": {n: round(v, 5) for n, v in qper.items()}},
+                      "kernels_ms": {n: round(v, 5) for n, v in qper.items()},
+                      "roofline": query_roofline(qper, L, Nw, H, pmc)},
             "kernels_ms": {n: round(v, 5) for n, v in per.items()},
             "build_roofline": {"algorithmic_bytes": L + 12 * U + 4 * N,
                                "kernel_ms_per_step": round(sum(tot.values()), 5),

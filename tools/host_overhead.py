@@ -1,4 +1,5 @@
-"""Host-side cost of one build step (ctypes + engine enqueue + sync + free), on the GPU box."""
+"""Host-side cost of one build step on the GPU box: the asynchronous enqueue (ctypes + engine +
+launches), the wait, and the free -- to see whether the host or the device paces the steps."""
 import os
 import sys
 import time
@@ -19,24 +20,27 @@ for _ in range(5):
     D.DeviceIndex.build(seq, 31).free()
 torch.cuda.synchronize()
 N = 50
-acc = {"py_build": 0.0, "raw_build": 0.0, "info": 0.0, "free": 0.0, "loop": 0.0}
-t_loop = time.perf_counter()
+acc = {"enqueue": 0.0, "wait": 0.0, "free": 0.0}
 for _ in range(N):
     t0 = time.perf_counter()
     idx = D.DeviceIndex.build(seq, 31, stream)
     t1 = time.perf_counter()
-    idx.info()
+    idx.wait()
     t2 = time.perf_counter()
     idx.free()
     t3 = time.perf_counter()
-    acc["py_build"] += t1 - t0
-    acc["info"] += t2 - t1
+    acc["enqueue"] += t1 - t0
+    acc["wait"] += t2 - t1
     acc["free"] += t3 - t2
-acc["loop"] = time.perf_counter() - t_loop
 out = C.c_void_p()
+torch.cuda.synchronize()
 t0 = time.perf_counter()
 for _ in range(N):
     L.kmhg_build_device(C.c_void_p(seq.data_ptr()), seq.numel(), 31, 0, sp, C.byref(out))
     L.kmhg_free(out)
-acc["raw_build"] = time.perf_counter() - t0
+t1 = time.perf_counter()
+torch.cuda.synchronize()
+t2 = time.perf_counter()
+acc["raw_enqueue_loop"] = t1 - t0
+acc["raw_total_loop"] = t2 - t0
 print({k: round(v / N * 1e6, 1) for k, v in acc.items()}, "us per step")
