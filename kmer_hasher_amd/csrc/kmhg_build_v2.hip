@@ -600,6 +600,176 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   STAMP(b, 6);
 }
 
+// ---------------------------------------------------------------- V_bucket_wg (group per bucket)
+// Large buckets (V2_BW_WG windows on average): ONE WORKGROUP per bucket with one shared LDS
+// sub-table of V2_CAPW slots.  Four times fewer buckets means one radix pass less from ~16 Mbp
+// (65K wave buckets) up to ~100 Mbp (102K group buckets at radix 320).  Keys seen once need no
+// ranking; buckets holding repeated keys rank them c by c, the waves taking turns.
+struct GroupTable {
+  uint64_t key[V2_CAPW + 1];
+  uint2 cc[V2_CAPW + 1];
+};
+
+__device__ __forceinline__ int lds_insert_g(GroupTable& W, uint64_t key) {
+  if (key == EMPTY_KEY) return (int)V2_CAPW;
+  uint32_t j = local_home(mix64(key), V2_CAPW);
+  for (uint32_t n = 0; n < V2_CAPW; ++n) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&W.key[j],
+                                    (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+    if (prev == EMPTY_KEY || prev == key) return (int)j;
+    if (++j == V2_CAPW) j = 0;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int lds_find_g(const GroupTable& W, uint64_t key) {
+  if (key == EMPTY_KEY) return (int)V2_CAPW;
+  uint32_t j = local_home(mix64(key), V2_CAPW);
+  for (uint32_t n = 0; n < V2_CAPW; ++n) {
+    if (W.key[j] == key) return (int)j;
+    if (++j == V2_CAPW) j = 0;
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
+               const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
+               int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
+               BuildMeta* __restrict__ meta) {
+  __shared__ GroupTable W;
+  __shared__ uint64_t sh[8];
+  __shared__ uint32_t red[3][4];
+  constexpr int PER = 2 * V2_BW_WG / BLOCK;           // elements per thread per batch (2x mean)
+  constexpr uint32_t BATCH = BLOCK * PER;
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const uint32_t b = blockIdx.x;
+  const uint32_t s0 = start[b], s1 = start[b + 1];
+  const bool one_batch = s1 - s0 <= BATCH;
+  uint64_t key[PER];
+  uint32_t ps[PER];
+  int slot[PER];
+  // element c of thread t in a batch: i0 + c * BLOCK + t, so position order = (c, wave, lane)
+  auto elem = [&](uint32_t i0, int c) { return i0 + (uint32_t)c * BLOCK + threadIdx.x; };
+  auto load = [&](uint32_t i0) {
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t i = elem(i0, c);
+      key[c] = i < s1 ? keys[i] : 0;
+      ps[c] = i < s1 ? pos[i] : 0;
+    }
+  };
+  load(s0);                                           // in flight while the table is cleared
+  for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += BLOCK) {
+    W.key[j] = EMPTY_KEY;
+    W.cc[j] = make_uint2(0u, 0u);
+  }
+  __syncthreads();
+  // pass A: distinct keys + counts (CAS on a table shared by the four waves)
+  bool ovf = false;
+  for (uint32_t i0 = s0; i0 < s1; i0 += BATCH) {
+    if (i0 != s0) load(i0);
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      slot[c] = -1;
+      if (elem(i0, c) < s1) {
+        slot[c] = lds_insert_g(W, key[c]);
+        if (slot[c] < 0) ovf = true;
+        else atomicAdd(&W.cc[slot[c]].x, 1u);
+      }
+    }
+  }
+  if (__syncthreads_or(ovf)) {
+    if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
+    return;
+  }
+  // exclusive scan of the counts; thread t owns SPT contiguous slots
+  constexpr uint32_t SPT = (V2_CAPW + 1 + BLOCK - 1) / BLOCK;
+  const uint32_t j0 = threadIdx.x * SPT;
+  const uint32_t j1 = min(j0 + SPT, V2_CAPW + 1);
+  uint32_t cs = 0, occ = 0, mx = 0;
+  uint64_t pairs = 0;
+  for (uint32_t j = j0; j < j1; ++j) {
+    const uint32_t c = W.cc[j].x;
+    cs += c;
+    occ += c ? 1u : 0u;
+    mx = max(mx, c);
+    pairs += (uint64_t)c * (c - (c ? 1u : 0u)) / 2;
+  }
+  uint64_t tot;
+  uint32_t off_run = s0 + (uint32_t)block_excl_scan(cs, sh, tot);
+  for (uint32_t j = j0; j < j1; ++j) {
+    W.cc[j].y = off_run;
+    off_run += W.cc[j].x;
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    pairs += __shfl_xor(pairs, d);
+    occ += __shfl_xor(occ, d);
+    mx = max(mx, (uint32_t)__shfl_xor(mx, d));
+  }
+  if (lane == 0) {
+    red[0][wave] = occ;
+    red[1][wave] = mx;
+    sh[4 + wave] = pairs;                  // sh[4..7]: the block scan above uses sh[0..3]
+  }
+  const bool has_multi = __syncthreads_or(mx > 1);
+  if (threadIdx.x == 0) {
+    BucketStats st;
+    st.n_kmers = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    st.max_count = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+    st.n_pairs = sh[4] + sh[5] + sh[6] + sh[7];
+    bstats[b] = st;
+  }
+  // pass B: keys seen once keep their position inline (cc.y); repeated keys are ranked in
+  // position order, the waves taking turns so that wave w follows waves < w
+  for (uint32_t i0 = s0; i0 < s1; i0 += BATCH) {
+    if (!one_batch) {
+      load(i0);
+#pragma unroll
+      for (int c = 0; c < PER; ++c) slot[c] = elem(i0, c) < s1 ? lds_find_g(W, key[c]) : -1;
+    }
+    if (!has_multi) {                    // every key seen once: positions go inline
+#pragma unroll
+      for (int c = 0; c < PER; ++c)
+        if (elem(i0, c) < s1) W.cc[slot[c]].y = ps[c];
+      continue;
+    }
+    for (int c = 0; c < PER; ++c) {
+      const bool act = elem(i0, c) < s1;
+      // waves take turns on this c: wave w ranks after waves < w have advanced the cursors
+      for (int turn = 0; turn < 4; ++turn) {
+        if (wave == turn) {
+          uint2 cc = make_uint2(0u, 0u);
+          if (act) cc = W.cc[slot[c]];
+          const bool multi = act && cc.x > 1;
+          if (act && !multi) W.cc[slot[c]].y = ps[c];
+          if (__ballot(multi)) {
+            const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS_WG, multi);
+            const int leader = multi ? __ffsll((unsigned long long)m) - 1 : lane;
+            uint32_t cur = cc.y;
+            if (multi && leader == lane) W.cc[slot[c]].y = cur + (uint32_t)__popcll(m);
+            cur = __shfl(cur, leader);
+            if (multi) positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  __syncthreads();
+  // the bucket's sub-table, coalesced 16-B slots
+  Slot* Tb = T + (uint64_t)b * V2_CAPW;
+  for (uint32_t j = threadIdx.x; j < V2_CAPW; j += BLOCK) {
+    const uint64_t kk = W.key[j];
+    const uint2 c = W.cc[j];
+    *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
+  }
+  if (threadIdx.x == 0 && b == bucket_of(mix64(EMPTY_KEY), g.nb)) {
+    const uint2 c = W.cc[V2_CAPW];
+    *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
+  }
+}
+
 // V_stats: reduce the per-bucket partials (grid-stride, one atomic per workgroup; meta was
 // zeroed by V_hist0).  The last workgroup to finish copies the totals into `host_meta`, a
 // pinned host record, so the host reads them without a copy launch.
@@ -765,6 +935,12 @@ void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t*
                       hipStream_t s) {
   hipLaunchKernelGGL(k_v2_bucket, dim3(grid_of(g.nb, 4)), dim3(BLOCK), 0, s, keys, pos, start, g,
                      T, positions, bstats, meta, xcd_map_bucket());
+}
+void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
+                         Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_bucket_wg, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
+                     positions, bstats, meta);
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {

@@ -505,21 +505,39 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     HIPC(hipMemcpyAsync(aligned_copy.p, d_seq, (size_t)L, hipMemcpyDeviceToDevice, s));
     d_seq = aligned_copy.p;
   }
-  const uint32_t nb = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW - 1) / V2_BW);
-  idx->geom = Geom{nb, V2_CAPB};
-  const Geom g = idx->geom;
   const uint32_t ntiles = (uint32_t)((Nw + PTILE - 1) / PTILE);   // partition tiles
   const Chunks ch = make_chunks(ntiles);
-  // radix plan: fewest passes whose radix fits LDS
-  uint32_t passes = 1, R = nb;
-  for (passes = 1; passes <= 4; ++passes) {
-    R = (uint32_t)std::ceil(std::pow((double)nb, 1.0 / passes) - 1e-9);
-    while (std::pow((double)R, (double)passes) < (double)nb) ++R;
-    // interleaved tiles of PTILE windows keep ~PTILE / R elements per digit run: beyond ~300
-    // digits the runs get too short for coalesced writes and an extra pass is cheaper
-    if (R <= (ch.interleaved ? V2_MAXR_IL : V2_MAXR)) break;
+  // radix plan: fewest passes whose radix fits LDS.  Interleaved tiles of PTILE windows keep
+  // ~PTILE / R elements per digit run: beyond ~300 digits the runs get too short for coalesced
+  // writes and an extra pass is cheaper.
+  const uint32_t maxr = ch.interleaved ? V2_MAXR_IL : V2_MAXR;
+  auto plan = [&](uint32_t nbk, uint32_t& R) {
+    for (uint32_t passes = 1; passes <= 4; ++passes) {
+      R = (uint32_t)std::ceil(std::pow((double)nbk, 1.0 / passes) - 1e-9);
+      while (std::pow((double)R, (double)passes) < (double)nbk) ++R;
+      if (R <= maxr) return passes;
+    }
+    return 5u;
+  };
+  // bucket size: group buckets (1024 windows, one workgroup each) unless wave buckets (256
+  // windows, one wave each) need fewer radix passes (only for tiny inputs).  Measured: group
+  // buckets halve the radix (longer digit runs) -- config 2 26.1 vs 24.8 Gbp/s -- and save a pass
+  // from ~26 M windows -- config 3 26.3 vs 24.5.  KMHG_BUCKET=wave|group forces one.
+  const uint32_t nb_w = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW - 1) / V2_BW);
+  const uint32_t nb_g = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW_WG - 1) / V2_BW_WG);
+  uint32_t R_w = 0, R_g = 0;
+  const uint32_t passes_w = plan(nb_w, R_w), passes_g = plan(nb_g, R_g);
+  bool group = passes_g <= passes_w;
+  if (const char* e = std::getenv("KMHG_BUCKET")) {
+    if (std::string(e) == "group") group = true;
+    if (std::string(e) == "wave") group = false;
   }
+  const uint32_t nb = group ? nb_g : nb_w;
+  const uint32_t passes = group ? passes_g : passes_w;
+  const uint32_t R = group ? R_g : R_w;
   if (passes > 4) fail(KMHG_EOVERFLOW, "sequence too long for the partitioned build");
+  idx->geom = Geom{nb, group ? V2_CAPW : V2_CAPB};
+  const Geom g = idx->geom;
   const uint64_t nhist = (uint64_t)R * ch.C;
   const uint32_t scan_tiles = tiles_for(nhist);
   DBuf<uint64_t> kA(Nw + PTILE, s), kB(Nw + PTILE, s);   // + pad (launch_v2_scatter)
@@ -569,9 +587,14 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   HIPC(hipMemsetAsync(stamps, 0, sizeof(uint64_t) * 8 * nb, s));
   kmhg::set_stamp_buffer(stamps);
 #endif
-  LAUNCH("k_v2_bucket", s,
-         launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
-                          meta, s));
+  if (group)
+    LAUNCH("k_v2_bucket", s,
+           launch_v2_bucket_wg(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
+                               meta, s));
+  else
+    LAUNCH("k_v2_bucket", s,
+           launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
+                            meta, s));
   LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, nb, n_valid, meta, idx->rec.meta, s));
   HIPC(hipEventRecord(idx->rec.ev, s));
 #ifdef KMHG_STAMPS

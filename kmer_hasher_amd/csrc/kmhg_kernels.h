@@ -10,6 +10,9 @@ constexpr uint32_t LARGE_MIN = 64;     // keys with >= this many positions sort 
 constexpr uint32_t V2_BW = 256;        // mean windows per bucket
 constexpr uint32_t V2_CAPB = 384;      // slots per bucket (LDS sub-table of one wave)
 constexpr uint32_t V2_SLOT_BITS = 9;   // bits to name a slot 0..V2_CAPB
+constexpr uint32_t V2_BW_WG = 1024;    // ... group buckets: mean windows per bucket
+constexpr uint32_t V2_CAPW = 1536;     // slots per group bucket (LDS sub-table of one workgroup)
+constexpr uint32_t V2_SLOT_BITS_WG = 11;
 constexpr uint32_t V2_MAXR = 640;      // max radix of one partition pass (LDS arrays)
 constexpr uint32_t V2_MAXR_IL = 320;   // ... with the interleaved tile schedule
 constexpr uint32_t SORT_CHUNK = 4096;  // LDS bitonic chunk (16 KiB)
@@ -130,6 +133,9 @@ struct BucketStats {           // per-bucket partials of the build statistics
 void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                       Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                       hipStream_t s);
+void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
+                         Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
+                         hipStream_t s);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);
 

@@ -193,3 +193,22 @@ def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
         assert res["pair.pos"].reshape(-1).tolist() == raw["pair.pos"], r["name"]
         assert res["count"].tolist() == raw["count"], r["name"]
         ptr.free()
+
+
+@pytest.mark.parametrize("bucket", ["wave", "group"])
+def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
+    """Both bucket kernels on every size class: one wave per 256-window bucket, and one
+    workgroup per 1024-window bucket (chosen automatically when it saves a radix pass, e.g. at
+    100 Mbp): repeated keys spanning waves, buckets beyond one batch (tandem repeats), N-runs."""
+    from kmer_hasher_amd import synth
+    monkeypatch.setenv("KMHG_BUCKET", bucket)
+    rng = np.random.default_rng(21)
+    for k in (3, 12, 31, 32):
+        _check_against_oracle("".join(rng.choice(list("ACGT"), 5000)), k)
+    s = "A" * 20000 + "ACGT" * 100 + "AC" * 9000 + "N" * 7 + "ACG" * 7000 + "T"
+    for k in (5, 31):
+        _check_against_oracle(s, k, qks=[k], pairs=(k != 5))
+    rr = synth.add_n_runs(synth.repeat_rich(400_000, 13, n_gap_every=100_000), 0.001, 5)
+    _check_against_oracle(rr.tobytes().decode("latin-1"), 21, qks=[21], pairs=True)
+    _check_against_oracle(synth.iid(3_000_000, 17).tobytes().decode(), 31, pairs=False)
+    _check_against_oracle("G" * 40, 32, qks=[31])
