@@ -48,13 +48,17 @@ CONFIGS = {
 }
 
 
+# HIP-event labels (kmhg_timing_*) -> kernel names as rocprofv3 reports them
+PMC_NAME = {"k_v2_scatter_seq": "k_v2_scatter<true>", "k_v2_scatter": "k_v2_scatter<false>"}
+
+
 def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) -> int | None:
     """Minimal bytes each kernel must move (DESIGN.md "Roofline accounting")."""
     if kernel == "k_v2_scatter_seq":    # read L chars; write (key 8 B, pos 4 B) per valid window
         return L + 12 * N
     if kernel == "k_v2_scatter":        # one radix pass: read + write 12 B per window
         return 24 * N
-    if kernel == "k_v2_bucket":         # read 12 B/window; one 16-B slot per distinct key; 4 B per
+    if kernel in ("k_v2_bucket", "k_v2_bucket_wg"):   # read 12 B/window; one 16-B slot per distinct key; 4 B per
         return 12 * N + 16 * U + 4 * (N - U)   # position of a repeated key (>= N - U of them)
     if kernel == "k_build_insert":      # read L chars; key+count per distinct key; slot id/window
         return L + 12 * U + 4 * Nw
@@ -257,7 +261,7 @@ def main():
                 pmc = json.load(open(pmc_path))
             except Exception:
                 pmc = {}
-        traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
+        traffic = pmc.get(PMC_NAME.get(dom, dom), {}).get("hbm_bytes_per_launch")
         out = {
             "metric": "Mbp/s indexed (make.kmer.hash k=31) at 1/2/4/8 GPUs; "
                       "seq.kmer.pos query Mbp/s",

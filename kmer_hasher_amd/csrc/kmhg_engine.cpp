@@ -588,7 +588,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   kmhg::set_stamp_buffer(stamps);
 #endif
   if (group)
-    LAUNCH("k_v2_bucket", s,
+    LAUNCH("k_v2_bucket_wg", s,
            launch_v2_bucket_wg(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
                                meta, s));
   else
