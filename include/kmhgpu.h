@@ -20,6 +20,8 @@
  *   kmhg_query_run / kmhg_query_run_device / kmhg_query_fill / kmhg_query_rows_device
  *        <- .Call("sequence_kmer_positions", ptr, seq, k)    src/kmer_hash.c:1151-1172
  *           (+ seq_kmer_positions, src/kmer_pos.c:110-136)
+ *   kmhg_count / kmhg_count_device
+ *        <- .Call("count_kmers", hash.ptr, params, seq)       src/kmer_hash.c:548-591
  *   registration of the three symbols with arities 3/2/3    src/kmer_hash.c:1205-1224
  *           is done by the R glue (kmer_hasher_amd/R/kmer_hash_glue.c) over this ABI.
  *
@@ -74,6 +76,9 @@ typedef struct {
   int64_t max_count;     /* largest position list */
   int64_t table_slots;   /* hash-table capacity */
   int64_t device_bytes;  /* device memory held by the index */
+  int32_t sources;       /* counts index (count.kmers): source_n; 0 for a position index */
+  int32_t reserved;
+  int64_t kmer_count;    /* khash_ptr.kmer_count: distinct k-mers added (both kinds) */
 } kmhg_info;
 
 const char *kmhg_last_error(void);
@@ -142,6 +147,28 @@ int kmhg_query_free(kmhg_query *q);
 int kmhg_pairs_run(kmhg_index *a, kmhg_index *b, kmhg_query **q, int64_t *n_rows);
 int kmhg_pairs_run_device(kmhg_index *a, kmhg_index *b, void *stream, kmhg_query **q,
                           int64_t *n_rows);
+
+/* count.kmers <- .Call("count_kmers", hash.ptr, c(k, source, source_n), seq)
+ *                                                            src/kmer_hash.c:548-591
+ *        (+ seq_to_counts :220-251, kmer_count_insert :185-208)
+ * Per-source k-mer counts: every valid window (the window walk of make.kmer.hash) of every
+ * sequence adds one to entry `source` of its k-mer's vector of source_n ints.  *idx == NULL
+ * makes a new counts index, else the counts are added to *idx (same k and source_n).  Sequences
+ * of length <= k are skipped; windows never span two sequences.  A negative source counts
+ * nothing (the reference warns for every window).  Errors, in the reference's order and words:
+ * "seq_r should be a character vector of length at least one", "k must be a positive integer
+ * less than 1+MAX_K", "source_n must be larger than 1 and larger than source", "mismatch between
+ * specified k and that given in the external pointer"; and, where the reference would write
+ * out of bounds, a position index or a different source_n is refused.
+ * A counts index reads like a position index whose "positions" are the count vectors, as the
+ * reference's kmer_positions / sequence_kmer_positions read them: kmer.pos gives count = source_n
+ * per k-mer and pos rows (i, count_s) for s = 0..source_n-1, seq.kmer.pos rows (i, count_s);
+ * k-mers are ranked by first insertion, or in khash order (kmhg_set_row_order). */
+int kmhg_count(kmhg_index **idx, const char *const *seqs, const size_t *lens, int64_t n_seqs,
+               int k, int source, int source_n);
+/* One device-resident sequence on `stream` (synchronous). */
+int kmhg_count_device(kmhg_index **idx, const void *d_seq, size_t L, int k, int source,
+                      int source_n, void *stream);
 
 /* Index replication for the multi-GPU query (the index is broadcast once over RCCL/xGMI by the
  * caller): the device image is the hash table (16-B slots {key, count, end}) + the positions;

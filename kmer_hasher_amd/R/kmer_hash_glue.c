@@ -10,6 +10,7 @@
  *   kmer_positions(ptr, opt_flag)           src/kmer_hash.c:1054-1147 -> named VECSXP[4]
  *   sequence_kmer_positions(ptr, seq, k)    src/kmer_hash.c:1151-1172 -> INTSXP 2 x H
  *   kmer_pair_pos(ptr_a, ptr_b)             src/kmer_hash.c:1174-1203 -> INTSXP 2 x M (fixed)
+ *   count_kmers(hash_ptr, params, seq)      src/kmer_hash.c:548-591   -> EXTPTRSXP (counts)
  *
  * Differences, all deliberate: the finaliser frees the whole payload (the reference leaks the
  * 32-B khash_ptr, src/kmer_hash.c:56-66); a freed pointer is detected instead of dereferenced;
@@ -161,6 +162,52 @@ SEXP kmer_pair_pos(SEXP ptr_a, SEXP ptr_b) {
   return ret;
 }
 
+/* count_kmers, src/kmer_hash.c:548-591 (count.kmers, kmer_hash.R:43-46): per-source counts of
+ * every k-mer of a character vector, added to hash_ptr_r or to a new counts pointer (same tag,
+ * so kmer.pos / seq.kmer.pos read it, test.R:340-343).  Validation order and texts as the
+ * reference; kmhg_count also refuses a position index and a different source_n, where the
+ * reference would write past the end of a k-mer's vector. */
+SEXP count_kmers(SEXP hash_ptr_r, SEXP params_r, SEXP seq_r) {
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) < 1)
+    error("seq_r should be a character vector of length at least one");
+  if (TYPEOF(params_r) != INTSXP || length(params_r) != 3)
+    error("k_r must be an integer vector of length 3");
+  const int *params = INTEGER(params_r);
+  const int k = params[0], source = params[1], source_n = params[2];
+  if (k < 1 || k > 32) error("k must be a positive integer less than 1+MAX_K");
+  if (source_n < 1 || source >= source_n)
+    error("source_n must be larger than 1 and larger than source");
+  kmhg_index *idx = NULL;
+  if (hash_ptr_r != R_NilValue) {
+    if (TYPEOF(hash_ptr_r) != EXTPTRSXP) error("failed to extract kmer_hash from external pointer");
+    SEXP tag = R_ExternalPtrTag(hash_ptr_r);
+    if (TYPEOF(tag) != STRSXP || length(tag) != 1 ||
+        strcmp(CHAR(STRING_ELT(tag, 0)), kmer_hash_tag))
+      error("failed to extract kmer_hash from external pointer");
+    idx = (kmhg_index *)R_ExternalPtrAddr(hash_ptr_r);
+    if (!idx) error("failed to extract kmer_hash from external pointer");
+  }
+  const R_xlen_t n = XLENGTH(seq_r);
+  const char **seqs = (const char **)R_alloc((size_t)n, sizeof(char *));
+  size_t *lens = (size_t *)R_alloc((size_t)n, sizeof(size_t));
+  for (R_xlen_t i = 0; i < n; ++i) {
+    SEXP e = STRING_ELT(seq_r, i);
+    seqs[i] = CHAR(e);
+    lens[i] = (size_t)length(e);
+  }
+  kmhg_index *out = idx;
+  if (kmhg_count(&out, seqs, lens, (int64_t)n, k, source, source_n) != KMHG_OK)
+    error("%s", kmhg_last_error());
+  if (source < 0) warning("source (%d) equal to or larger than source_n (%d)", source, source_n);
+  if (idx) return hash_ptr_r;
+  SEXP tag = PROTECT(allocVector(STRSXP, 1));
+  SET_STRING_ELT(tag, 0, mkChar(kmer_hash_tag));
+  SEXP ptr = PROTECT(R_MakeExternalPtr(out, tag, R_NilValue));
+  R_RegisterCFinalizerEx(ptr, finalise_gpu_index, TRUE);
+  UNPROTECT(2);
+  return ptr;
+}
+
 /* Not in the reference: choose the kmer.pos k-mer order of an index, "first" (first
  * occurrence, the default) or "khash" (the reference's own bucket order, byte-identical
  * output).  KMHG_ROW_ORDER=khash in the environment sets the default for new indices. */
@@ -180,6 +227,7 @@ static const R_CallMethodDef gpu_call_methods[] = {
     {"kmer_positions", (DL_FUNC)&kmer_positions, 2},
     {"sequence_kmer_positions", (DL_FUNC)&sequence_kmer_positions, 3},
     {"kmer_pair_pos", (DL_FUNC)&kmer_pair_pos, 2},
+    {"count_kmers", (DL_FUNC)&count_kmers, 3},
     {"kmer_row_order", (DL_FUNC)&kmer_row_order, 2},
     {NULL, NULL, 0}};
 

@@ -41,6 +41,13 @@ kmer.pairs <- function(ptr.a, ptr.b){
     tmp
 }
 
+## per-source k-mer counts; params = c(k, source, source_n); kmer.pos / seq.kmer.pos read the
+## count vectors of the returned pointer as positions (reference kmer_hash.R:43-46)
+count.kmers <- function(seq, params, hash.ptr=NULL){
+    params <- as.integer(params)
+    .Call("count_kmers", hash.ptr, params, seq)
+}
+
 ## not in the reference: kmer.pos k-mer order, "first" (default) or "khash" (the reference's
 ## bucket order: byte-identical kmer.pos output)
 kmer.row.order <- function(ex.ptr, order="khash"){

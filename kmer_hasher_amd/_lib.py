@@ -26,7 +26,8 @@ class KmhgError(RuntimeError):
 class Info(C.Structure):
     _fields_ = [("k", C.c_int32), ("device", C.c_int32), ("seq_len", C.c_int64),
                 ("n_kmers", C.c_int64), ("n_positions", C.c_int64), ("n_pairs", C.c_int64),
-                ("max_count", C.c_int64), ("table_slots", C.c_int64), ("device_bytes", C.c_int64)]
+                ("max_count", C.c_int64), ("table_slots", C.c_int64), ("device_bytes", C.c_int64),
+                ("sources", C.c_int32), ("reserved", C.c_int32), ("kmer_count", C.c_int64)]
 
 
 class ImageSizes(C.Structure):
@@ -61,6 +62,10 @@ _PROTOS = {
     "kmhg_query_rows_device": (C.c_int, [vp, C.POINTER(vp)]),
     "kmhg_query_copy_device": (C.c_int, [vp, vp, vp]),
     "kmhg_query_free": (C.c_int, [vp]),
+    "kmhg_count": (C.c_int, [C.POINTER(vp), C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
+                             C.c_int64, C.c_int, C.c_int, C.c_int]),
+    "kmhg_count_device": (C.c_int, [C.POINTER(vp), vp, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                    vp]),
     "kmhg_image_sizes_get": (C.c_int, [vp, C.POINTER(ImageSizes), i64p]),
     "kmhg_image_export": (C.c_int, [vp, vp, vp, vp]),
     "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, C.POINTER(vp)]),

@@ -4,6 +4,7 @@
     kmer_pos(ex_ptr, opt_flag)             <- kmer.pos        (kmer_hash.R:10-21)
     seq_kmer_pos(ex_ptr, seq, k)           <- seq.kmer.pos    (kmer_hash.R:23-28)
     kmer_pairs(ptr_a, ptr_b)               <- kmer.pairs      (kmer_hash.R:30-34), fixed
+    count_kmers(seq, params, hash_ptr)     <- count.kmers     (kmer_hash.R:43-46)
     set_row_order(ex_ptr, "khash")         kmer.pos rows in the reference's khash order (opt-in)
 
 Same argument meaning, same validation order and the reference's own error messages (raised as
@@ -19,6 +20,7 @@ src/kmer_hash.c:56-66).
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 import weakref
 
 import numpy as np
@@ -216,3 +218,47 @@ def seq_kmer_pos(ex_ptr, seq, k) -> np.ndarray:
     finally:
         L.kmhg_query_free(q)
     return rows.reshape(-1, 2)
+
+
+def count_kmers(seq, params, hash_ptr=None) -> ExtPtr:
+    """count.kmers -> .Call("count_kmers", hash.ptr, params, seq)  (src/kmer_hash.c:548-591).
+
+    seq: a character vector (str or list of str); params = (k, source, source_n).  Every valid
+    window of every sequence adds one to entry `source` of its k-mer's vector of source_n
+    counts.  hash_ptr None makes a new counts pointer; otherwise the counts are added to it and
+    the same pointer is returned.  kmer.pos / seq.kmer.pos read the count vectors as positions,
+    as the reference does (test.R:340-343)."""
+    if isinstance(seq, (str, bytes, bytearray)):
+        seq = [seq]
+    if not isinstance(seq, (list, tuple)) or len(seq) < 1 or \
+            not all(isinstance(x, (str, bytes, bytearray)) for x in seq):
+        raise KmerHashError("seq_r should be a character vector of length at least one")
+    try:
+        prm = [int(x) for x in params]
+    except (TypeError, ValueError):
+        raise KmerHashError("k_r must be an integer vector of length 3") from None
+    if len(prm) != 3:
+        raise KmerHashError("k_r must be an integer vector of length 3")
+    k, source, source_n = prm
+    if k < 1 or k > 32:
+        raise KmerHashError("k must be a positive integer less than 1+MAX_K")
+    if source_n < 1 or source >= source_n:
+        raise KmerHashError("source_n must be larger than 1 and larger than source")
+    if hash_ptr is not None and (not isinstance(hash_ptr, ExtPtr) or
+                                 hash_ptr.tag != KMER_HASH_TAG or not hash_ptr._h):
+        # extract_ext_ptr returns NULL (src/kmer_hash.c:574-577)
+        raise KmerHashError("failed to extract kmer_hash from external pointer")
+    bs = [x.encode("latin-1") if isinstance(x, str) else bytes(x) for x in seq]
+    arr = (C.c_char_p * len(bs))(*bs)
+    lens = (C.c_size_t * len(bs))(*[len(b) for b in bs])
+    h = C.c_void_p(hash_ptr._h.value if hash_ptr is not None and hash_ptr._h else None)
+    L = _lib.lib()
+    rc = L.kmhg_count(C.byref(h), arr, lens, len(bs), k, source, source_n)
+    if rc == _lib.KMHG_EINVAL:
+        raise KmerHashError(L.kmhg_last_error().decode())
+    _lib.check(rc)
+    if source < 0:   # kmer_count_insert: one warning() per window, nothing counted
+        warnings.warn(f"source ({source % 2**64}) equal to or larger than source_n ({source_n})")
+    if hash_ptr is not None:
+        return hash_ptr
+    return ExtPtr(h.value)

@@ -397,6 +397,18 @@ struct kmhg_index {
   bool pending = false;
   PinnedRec rec;
   const uint8_t* src = nullptr;
+  // counts index (count.kmers, kmhg_count.hip): sources > 0.  `positions` then holds the
+  // U x sources count matrix (row-major, rows in first-insertion order, rows_cap allocated),
+  // `ckeys` the keys of the rows, slot_row / row_slot the table <-> row maps.
+  uint32_t sources = 0;
+  uint64_t rows_cap = 0, kmer_count = 0;
+  DBuf<uint64_t> ckeys;
+  DBuf<uint32_t> slot_row, row_slot;
+  // stream-ordered release of everything the index holds (work queued on `s` may still read it)
+  void bind_all(hipStream_t s) {
+    table.bind(s); positions.bind(s); ckeys.bind(s); slot_row.bind(s); row_slot.bind(s);
+    canon.perm.bind(s); canon.canon_off.bind(s); canon.pkeys.bind(s); canon.pair_off.bind(s);
+  }
 };
 
 struct kmhg_query {
@@ -416,6 +428,8 @@ struct DeviceGuard {
   }
   ~DeviceGuard() { (void)hipSetDevice(prev); }
 };
+
+inline bool LCN(char c) { return (c | 0x20) == 'n'; }   // LC(c) == 'n', src/kmer_util.h:10
 
 size_t effective_len(const char* seq, size_t L) {   // a C string ends at its first NUL
   const void* z = memchr(seq, 0, L);
@@ -717,11 +731,101 @@ kmhg_query* pairs_device(kmhg_index* a, kmhg_index* b, hipStream_t s) {
   return q.release();
 }
 
+// ---------------------------------------------------------------------------- count.kmers
+void prepare_canon(kmhg_index* idx, hipStream_t s);
+
+// One count.kmers batch (a device-resident sequence) merged into the counts index `idx`
+// (kmhg_count.hip): partitioned build of the batch -> its distinct keys in first-occurrence
+// order -> probe / append into the count matrix -> table rebuilt for the grown key list.
+void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t source,
+                  hipStream_t s) {
+  idx->stream = s;
+  const int k = idx->k;
+  const uint32_t S = idx->sources;
+  if (L <= k) return;
+  std::unique_ptr<kmhg_index> B(build_device(d_seq, L, k, s));
+  struct Release {                 // the batch index dies in stream order
+    kmhg_index* b; hipStream_t s;
+    ~Release() { b->bind_all(s); }
+  } rel{B.get(), s};
+  finish_build(B.get());
+  B->stream = s;
+  const uint64_t Ub = B->U;
+  if (!Ub) return;
+  prepare_canon(B.get(), s);       // batch keys in first-occurrence order
+  const uint64_t U0 = idx->U;
+  const uint64_t need = U0 + Ub;
+  if (need * S > (uint64_t)INT32_MAX)
+    fail(KMHG_EOVERFLOW, "counts index larger than 2^31-1 counts (R vector limit)");
+  if (need > idx->rows_cap) {      // grow geometrically: repeated calls amortise the copy
+    const uint64_t cap = std::max<uint64_t>(need, idx->rows_cap * 2);
+    DBuf<uint64_t> nk(cap);
+    DBuf<int32_t> nm(cap * S);
+    if (U0) {
+      HIPC(hipMemcpyAsync(nk.p, idx->ckeys.p, U0 * 8, hipMemcpyDeviceToDevice, s));
+      HIPC(hipMemcpyAsync(nm.p, idx->positions.p, U0 * S * 4, hipMemcpyDeviceToDevice, s));
+    }
+    idx->ckeys.bind(s);
+    idx->positions.bind(s);
+    idx->ckeys.swap_with(nk);
+    idx->positions.swap_with(nm);
+    idx->rows_cap = cap;
+  }
+  const uint32_t nt = tiles_for(Ub);
+  DBuf<uint32_t> rank(Ub + 1, s);                 // flags -> ranks of the new keys; [Ub] = total
+  DBuf<uint64_t> status((size_t)nt + 1, s);
+  HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
+  const uint32_t* perm_b = B->canon.perm.p;
+  LAUNCH("k_count_probe", s,
+         launch_count_probe(perm_b, (uint32_t)Ub, B->table.p, U0 ? idx->table.p : nullptr,
+                            idx->geom, idx->slot_row.p, S, source, idx->positions.p, rank.p, s));
+  LAUNCH("k_scan_u32", s, launch_scan_u32(rank.p, Ub, status.p, rank.p + Ub, s));
+  LAUNCH("k_count_append", s,
+         launch_count_append(perm_b, (uint32_t)Ub, B->table.p, rank.p, rank.p + Ub,
+                             (uint32_t)U0, S, source, idx->ckeys.p, idx->positions.p, s));
+  uint32_t n_new = 0;
+  HIPC(hipMemcpyAsync(&n_new, rank.p + Ub, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  const uint64_t U1 = U0 + n_new;
+  // rebuild the table for U1 keys (aux of a source_n = 1 index carries the count itself, so
+  // even a batch of known keys changes the slots)
+  idx->table.bind(s);
+  idx->slot_row.bind(s);
+  idx->geom = Geom{1u, (uint32_t)table_capacity((int64_t)U1)};
+  idx->table.reset(idx->slots());
+  idx->slot_row.reset(idx->slots());
+  idx->row_slot.bind(s);
+  idx->row_slot.reset(U1);
+  LAUNCH("k_table_init", s, launch_table_init(idx->table.p, idx->slots(), s));
+  LAUNCH("k_count_insert", s,
+         launch_count_insert(idx->ckeys.p, (uint32_t)U1, idx->table.p, idx->geom, S,
+                             idx->positions.p, idx->slot_row.p, idx->row_slot.p, s));
+  idx->U = U1;
+  idx->N = U1 * S;
+  idx->P = U1 * ((uint64_t)S * (S - 1) / 2);
+  idx->max_n = U1 ? S : 0;
+  idx->L += L;
+  idx->kmer_count += n_new;
+  idx->canon.ready = false;
+}
+
 // ---------------------------------------------------------------------------- readout
 void prepare_canon(kmhg_index* idx, hipStream_t s) {
   idx->stream = s;
   Canon& c = idx->canon;
   if (c.ready) return;
+  if (idx->sources) {            // counts index: rows are already in first-insertion order
+    const uint32_t U = (uint32_t)idx->U, S = idx->sources;
+    c.perm.reset(U);
+    c.canon_off.reset(U + 1);
+    c.pkeys.reset(S >= 2 ? U : 1);
+    c.pair_off.reset(S >= 2 ? U : 1);
+    LAUNCH("k_count_canon", s, launch_count_canon(idx->row_slot.p, U, S, c.perm.p, c.canon_off.p,
+                                                  c.pkeys.p, c.pair_off.p, s));
+    c.n_multi = S >= 2 ? U : 0;
+    c.ready = true;
+    return;
+  }
   const int64_t L = idx->L;
   const uint32_t U = (uint32_t)idx->U;
   DBuf<uint32_t> F(L, s);
@@ -948,13 +1052,100 @@ int kmhg_free(kmhg_index* idx) {
     }
     // stream-ordered release: the buffers return to the pool once work queued on the index's
     // last stream has finished (queries on other streams are synchronised by their callers)
-    idx->table.bind(idx->stream);
-    idx->positions.bind(idx->stream);
-    idx->canon.perm.bind(idx->stream);
-    idx->canon.canon_off.bind(idx->stream);
-    idx->canon.pkeys.bind(idx->stream);
-    idx->canon.pair_off.bind(idx->stream);
+    idx->bind_all(idx->stream);
     delete idx;
+  });
+}
+
+// count.kmers: windows never span two sequences of the character vector, so a batch is the
+// sequences joined by 'N'.  Alone, a sequence's final N-free run of exactly k chars yields no
+// window (init_kmer reaches the string's end, src/kmer_hash.c:235-237); followed by the 'N' it
+// would, so such a run is left out of the batch.
+constexpr size_t COUNT_BATCH = (size_t)1 << 30;   // chars per build
+
+kmhg_index* new_counts_index(int k, int source_n) {
+  auto idx = std::make_unique<kmhg_index>();
+  HIPC(hipGetDevice(&idx->device));
+  idx->k = k;
+  idx->sources = (uint32_t)source_n;
+  idx->stream = lib_stream();
+  return idx.release();
+}
+
+void check_count_args(int64_t n_seqs, int k, int source, int source_n, kmhg_index* c) {
+  // count_kmers, src/kmer_hash.c:549-563 and 579-581 (same order, same texts)
+  if (n_seqs < 1) fail(KMHG_EINVAL, "seq_r should be a character vector of length at least one");
+  if (k < 1 || k > 32) fail(KMHG_EINVAL, "k must be a positive integer less than 1+MAX_K");
+  if (source_n < 1 || source >= source_n)
+    fail(KMHG_EINVAL, "source_n must be larger than 1 and larger than source");
+  if (!c) return;
+  if (!c->sources)
+    fail(KMHG_EINVAL, "count.kmers needs a counts pointer (one made by count.kmers)");
+  if (c->k != k)
+    fail(KMHG_EINVAL, "mismatch between specified k and that given in the external pointer");
+  if ((uint32_t)source_n != c->sources)
+    fail(KMHG_EINVAL, "source_n differs from the source_n the counts pointer was made with");
+}
+
+int kmhg_count(kmhg_index** idx, const char* const* seqs, const size_t* lens, int64_t n_seqs,
+               int k, int source, int source_n) {
+  return guarded([&] {
+    if (!idx || (n_seqs > 0 && (!seqs || !lens))) fail(KMHG_EINVAL, "null argument");
+    check_count_args(n_seqs, k, source, source_n, *idx);
+    std::unique_ptr<kmhg_index> fresh;
+    kmhg_index* c = *idx;
+    if (!c) {
+      fresh.reset(new_counts_index(k, source_n));
+      c = fresh.get();
+    }
+    DeviceGuard g(c->device);
+    if (source >= 0) {   // negative: every insert fails its source check, nothing is counted
+      hipStream_t s = lib_stream();
+      std::vector<char> buf;
+      auto flush = [&] {
+        if (buf.empty()) return;
+        if (buf.size() >= (size_t)INT32_MAX)
+          fail(KMHG_EOVERFLOW, "sequence longer than 2^31-1 (int positions)");
+        DBuf<uint8_t> d(buf.size() + 16, s);
+        HIPC(hipMemcpyAsync(d.p, buf.data(), buf.size(), hipMemcpyHostToDevice, s));
+        count_device(c, d.p, (int64_t)buf.size(), (uint32_t)source, s);
+        HIPC(hipStreamSynchronize(s));   // buf is reused
+        buf.clear();
+      };
+      for (int64_t i = 0; i < n_seqs; ++i) {
+        const char* q = seqs[i];
+        if (!q) continue;
+        size_t n = effective_len(q, lens[i]);
+        if ((int64_t)n <= k) continue;                  // src/kmer_hash.c:583-584
+        bool tail_k = LCN(q[n - k - 1]);                // final run of exactly k chars?
+        for (size_t j = n - k; tail_k && j < n; ++j) tail_k = !LCN(q[j]);
+        if (tail_k) n -= (size_t)k;
+        if (!buf.empty() && buf.size() + n + 1 > COUNT_BATCH) flush();
+        buf.insert(buf.end(), q, q + n);
+        buf.push_back('N');
+      }
+      flush();
+    }
+    if (fresh) *idx = fresh.release();
+  });
+}
+
+int kmhg_count_device(kmhg_index** idx, const void* d_seq, size_t L, int k, int source,
+                      int source_n, void* stream) {
+  return guarded([&] {
+    if (!idx || (L && !d_seq)) fail(KMHG_EINVAL, "null argument");
+    check_count_args(1, k, source, source_n, *idx);
+    if (L >= (size_t)INT32_MAX) fail(KMHG_EOVERFLOW, "sequence longer than 2^31-1 (int positions)");
+    std::unique_ptr<kmhg_index> fresh;
+    kmhg_index* c = *idx;
+    if (!c) {
+      fresh.reset(new_counts_index(k, source_n));
+      c = fresh.get();
+    }
+    DeviceGuard g(c->device);
+    if (source >= 0) count_device(c, (const uint8_t*)d_seq, (int64_t)L, (uint32_t)source,
+                                  (hipStream_t)stream);
+    if (fresh) *idx = fresh.release();
   });
 }
 
@@ -980,7 +1171,12 @@ int kmhg_index_info(const kmhg_index* cidx, kmhg_info* info) {
     info->n_pairs = (int64_t)idx->P;
     info->max_count = idx->max_n;
     info->table_slots = (int64_t)idx->slots();
-    info->device_bytes = (int64_t)(idx->table.bytes() + idx->positions.bytes());
+    info->device_bytes = (int64_t)(idx->table.bytes() + idx->positions.bytes() +
+                                   idx->ckeys.bytes() + idx->slot_row.bytes() +
+                                   idx->row_slot.bytes());
+    info->sources = (int32_t)idx->sources;
+    info->reserved = 0;
+    info->kmer_count = (int64_t)(idx->sources ? idx->kmer_count : idx->U);
   });
 }
 
@@ -1166,6 +1362,7 @@ int kmhg_image_sizes_get(const kmhg_index* cidx, kmhg_image_sizes* sz, int64_t h
   return guarded([&] {
     if (!cidx || !sz || !header) fail(KMHG_EINVAL, "null argument");
     kmhg_index* idx = const_cast<kmhg_index*>(cidx);   // completes a pending build
+    if (idx->sources) fail(KMHG_EINVAL, "index images hold position indices only");
     DeviceGuard g(idx->device);
     finish_build(idx);
     sz->table_bytes = (int64_t)(idx->slots() * sizeof(Slot));
@@ -1181,6 +1378,7 @@ int kmhg_image_export(const kmhg_index* cidx, void* d_table, void* d_positions, 
   return guarded([&] {
     if (!cidx) fail(KMHG_EINVAL, "null index");
     kmhg_index* idx = const_cast<kmhg_index*>(cidx);
+    if (idx->sources) fail(KMHG_EINVAL, "index images hold position indices only");
     DeviceGuard g(idx->device);
     finish_build(idx);
     hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream

@@ -145,6 +145,20 @@ void launch_join_probe(const uint32_t* perm_a, uint32_t Ua, const Slot* Ta, cons
 void launch_join_emit(const uint4* jinfo, uint32_t Ua, const int32_t* pos_a, const int32_t* pos_b,
                       const uint64_t* tile_row0, int2* out, hipStream_t s);
 
+// count.kmers (kmhg_count.hip)
+void launch_count_probe(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb, const Slot* Tc,
+                        Geom gc, const uint32_t* slot_row, uint32_t S, uint32_t source,
+                        int32_t* M, uint32_t* newf, hipStream_t s);
+void launch_count_append(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb,
+                         const uint32_t* rank, const uint32_t* n_new, uint32_t U0, uint32_t S,
+                         uint32_t source, uint64_t* ckeys, int32_t* M, hipStream_t s);
+void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uint32_t S,
+                         const int32_t* M, uint32_t* slot_row, uint32_t* row_slot,
+                         hipStream_t s);
+void launch_count_canon(const uint32_t* row_slot, uint32_t U, uint32_t S, uint32_t* perm,
+                        uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
+                        hipStream_t s);
+
 #ifdef KMHG_STAMPS
 void set_stamp_buffer(uint64_t* p);
 #endif

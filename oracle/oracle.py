@@ -80,6 +80,11 @@ def _ref():
         lib.ref_positions.argtypes = [C.c_void_p, C.c_uint, C.POINTER(_RefPos)]
         lib.ref_query.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(C.c_long),
                                   C.POINTER(C.POINTER(C.c_int))]
+        lib.ref_count.restype = C.c_void_p
+        lib.ref_count.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.POINTER(C.c_int)]
+        lib.ref_kmer_count.restype = C.c_long
+        lib.ref_kmer_count.argtypes = [C.c_void_p]
         _REF = lib
     return _REF
 
@@ -186,6 +191,54 @@ class OracleIndex:
         return rows[:2 * h]
 
 
+class OracleCounts:
+    """count.kmers restated (reference src/kmer_hash.c:548-591, seq_to_counts :220-251,
+    kmer_count_insert :185-208): distinct keys in first-insertion order, each with a vector of
+    `source_n` per-source window counts.  add() is one count.kmers call."""
+
+    def __init__(self, k: int, source_n: int):
+        self.k, self.S = k, source_n
+        self.keys: list[int] = []
+        self.row: dict[int, int] = {}
+        self.M: list[np.ndarray] = []
+        self.kmer_count = 0
+
+    def add(self, seqs, source: int) -> None:
+        if source < 0 or source >= self.S:      # every insert warns and fails: nothing counted
+            return
+        for seq in seqs:
+            b = _as_bytes(seq)
+            if len(b) <= self.k:
+                continue
+            keys, _, _ = windows(b, self.k)
+            uk, first, cnt = np.unique(keys, return_index=True, return_counts=True)
+            for j in np.argsort(first, kind="stable"):
+                key = int(uk[j])
+                r = self.row.get(key)
+                if r is None:
+                    r = self.row[key] = len(self.keys)
+                    self.keys.append(key)
+                    self.M.append(np.zeros(self.S, np.int32))
+                    self.kmer_count += 1
+                self.M[r][source] += int(cnt[j])
+
+    @property
+    def U(self) -> int:
+        return len(self.keys)
+
+    def index(self) -> "OracleIndex":
+        """The counts as an OracleIndex-shaped CSR (positions = per-source counts)."""
+        ix = OracleIndex.__new__(OracleIndex)
+        U, S = self.U, self.S
+        ix.k, ix.U, ix.N, ix.P, ix.max_n = self.k, U, U * S, U * S * (S - 1) // 2, S if U else 0
+        ix.keys = np.array(self.keys, np.uint64)
+        ix.counts = np.full(U, S, np.int32)
+        ix.offsets = np.arange(U + 1, dtype=np.int64) * S
+        ix.positions = (np.stack(self.M).reshape(-1) if U else np.empty(0, np.int32)).astype(
+            np.int32)
+        return ix
+
+
 _NUC = "ACTG"
 
 
@@ -239,6 +292,26 @@ class RefIndex:
         if opt & 8:
             out["count"] = take(r.counts, r.n_counts, np.int32)
         return out
+
+    @classmethod
+    def counts(cls, seqs, k: int, source: int, source_n: int, into: "RefIndex | None" = None):
+        """count.kmers(seqs, c(k, source, source_n), into) on the compiled reference core."""
+        lib = _ref()
+        self = into if into is not None else cls.__new__(cls)
+        if into is None:
+            self.k, self.h = k, None
+        bs = [_as_bytes(x) for x in seqs]
+        arr = (C.c_char_p * len(bs))(*bs)
+        err = C.c_int(0)
+        h = lib.ref_count(self.h, arr, len(bs), k, source, source_n, C.byref(err))
+        msgs = {1: "k must be a positive integer less than 1+MAX_K",
+                4: "source_n must be larger than 1 and larger than source",
+                5: "mismatch between specified k and that given in the external pointer"}
+        if err.value:
+            raise ValueError(msgs[err.value])
+        self.h = h
+        self.kmer_count = int(lib.ref_kmer_count(h))
+        return self
 
     def query(self, seq, kq: int) -> np.ndarray:
         lib = _ref()

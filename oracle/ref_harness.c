@@ -11,6 +11,9 @@
  *   ref_query      <- sequence_kmer_positions(reference src/kmer_hash.c:1151-1172)
  *   ref_free_index <- finalise_khash_ptr     (reference src/kmer_hash.c:56-66)
  *   decode_kmer    <- kmer_seq               (reference src/kmer_hash.c:123-133)
+ *   ref_count      <- count_kmers            (reference src/kmer_hash.c:548-591)
+ *                     + seq_to_counts :220-251, kmer_count_insert :185-208 (also in
+ *                     kmer_hash.c, so restated here over the compiled khash/kvec/init_kmer)
  *
  * The heavy lifting (seq_to_hash, seq_kmer_positions, sort_kmer_pos, clear_kmer_h and the
  * khash/kvec containers) is the reference's compiled code, linked in unchanged.
@@ -113,3 +116,71 @@ int ref_query(void *h, const char *seq, int k, long *n_rows, int **rows) {
   *rows = pp.a;  /* caller frees with ref_free */
   return 0;
 }
+
+/* ---------------------------------------------------------------- count.kmers
+ * Per-source counts: a key's kvec holds source_n ints, one per source, and a window adds one
+ * to slot `source`.  Returns 1 for a new key, 0 for a known one, -1 when source >= source_n
+ * (the reference warning()s and the caller gives up on that sequence). */
+static int count_one(khash_t(kmer_h) *hash, uint64_t key, size_t source, size_t source_n) {
+  if (source >= source_n) return -1;
+  int is_new = 0, ret = 0;
+  khiter_t it = kh_get(kmer_h, hash, key);
+  if (it == kh_end(hash)) {
+    it = kh_put(kmer_h, hash, key, &ret);
+    if (it == kh_end(hash)) return -1;
+    kmer_pos_t *e = &kh_val(hash, it);
+    e->kmer = key;
+    e->v.a = calloc(source_n, sizeof(int));
+    e->v.n = e->v.m = source_n;
+    is_new = 1;
+  }
+  kh_val(hash, it).v.a[source] += 1;
+  return is_new;
+}
+
+/* the window walk of seq_to_counts: the same visit order as seq_to_hash (init_kmer restarts
+ * after N runs; a restart that reaches the end of the string counts nothing) */
+static int count_seq(const char *seq, int k, khash_t(kmer_h) *hash, size_t source,
+                     size_t source_n) {
+  const uint64_t mask = k < 32 ? (((uint64_t)1) << (2 * k)) - 1 : ~(uint64_t)0;
+  uint64_t off = 0;
+  size_t i = 0;
+  int added = 0, r;
+  while (seq[i]) {
+    i = init_kmer(seq, i, &off, k);
+    if (!seq[i]) break;
+    if ((r = count_one(hash, off & mask, source, source_n)) < 0) return r;
+    added += r;
+    for (; seq[i] && LC(seq[i]) != 'n'; ++i) {
+      off = UPDATE_OFFSET(off, seq[i]);
+      if ((r = count_one(hash, off & mask, source, source_n)) < 0) return r;
+      added += r;
+    }
+  }
+  return added;
+}
+
+#define REF_ESRC 4  /* source_n must be larger than 1 and larger than source */
+#define REF_EKMM 5  /* mismatch between specified k and that given in the external pointer */
+
+/* h == NULL: a new counts pointer.  Sequences of length <= k are skipped. */
+void *ref_count(void *h, const char **seqs, int n, int k, int source, int source_n, int *err) {
+  *err = 0;
+  if (k < 1 || k > MAX_K) { *err = REF_EK; return 0; }
+  if (source_n < 1 || source >= source_n) { *err = REF_ESRC; return 0; }
+  khash_ptr *p = (khash_ptr *)h;
+  if (!p) {
+    p = calloc(1, sizeof(khash_ptr));
+    p->k = k;
+    p->hash = kh_init(kmer_h);
+  }
+  if (p->k != k) { *err = REF_EKMM; return h; }
+  for (int s = 0; s < n; ++s) {
+    if ((long)strlen(seqs[s]) <= k) continue;
+    int added = count_seq(seqs[s], k, p->hash, (size_t)source, (size_t)source_n);
+    if (added > 0) p->kmer_count += (size_t)added;
+  }
+  return p;
+}
+
+long ref_kmer_count(void *h) { return (long)((khash_ptr *)h)->kmer_count; }
