@@ -11,6 +11,8 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkmhgpu.so")
+if os.environ.get("KMHG_LIB_VARIANT"):      # A/B experiments only (tools/ab.sh): a variant build
+    LIB_PATH = os.path.join(_HERE, f"libkmhgpu_{os.environ['KMHG_LIB_VARIANT']}.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "kmhgpu.h")
 
 KMHG_OK, KMHG_EINVAL, KMHG_ENOMEM, KMHG_EDEVICE, KMHG_EOVERFLOW = 0, 1, 2, 3, 4

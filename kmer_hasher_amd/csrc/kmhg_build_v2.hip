@@ -41,8 +41,10 @@ __device__ uint64_t* g_stamps;
     if (lane_id() == 0 && g_stamps) g_stamps[(uint64_t)(b) * 8 + (i)] = _t;           \
     __builtin_amdgcn_sched_barrier(0);                                                \
   } while (0)
+#define STAMP_WG(b, i) do { if (threadIdx.x < 64) STAMP(b, i); } while (0)
 #else
 #define STAMP(b, i) do {} while (0)
+#define STAMP_WG(b, i) do {} while (0)
 #endif
 
 // LDS sub-table of one bucket, private to one wave (slot V2_CAPB = side slot of key ~0).
@@ -659,13 +661,16 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
       ps[c] = i < s1 ? pos[i] : 0;
     }
   };
+  STAMP_WG(b, 0);
   load(s0);                                           // in flight while the table is cleared
   for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += BLOCK) {
     W.key[j] = EMPTY_KEY;
     W.cc[j] = make_uint2(0u, 0u);
   }
   __syncthreads();
-  // pass A: distinct keys + counts (CAS on a table shared by the four waves)
+  STAMP_WG(b, 1);
+  // pass A: distinct keys + counts (CAS on a table shared by the four waves).  (Measured:
+  // skipping the count atomic for a key's claiming occurrence ran 35 % slower, 141 vs 105 us.)
   bool ovf = false;
   for (uint32_t i0 = s0; i0 < s1; i0 += BATCH) {
     if (i0 != s0) load(i0);
@@ -683,6 +688,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
     return;
   }
+  STAMP_WG(b, 2);
   // exclusive scan of the counts; thread t owns SPT contiguous slots
   constexpr uint32_t SPT = (V2_CAPW + 1 + BLOCK - 1) / BLOCK;
   const uint32_t j0 = threadIdx.x * SPT;
@@ -713,6 +719,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     sh[4 + wave] = pairs;                  // sh[4..7]: the block scan above uses sh[0..3]
   }
   const bool has_multi = __syncthreads_or(mx > 1);
+  STAMP_WG(b, 3);
   if (threadIdx.x == 0) {
     BucketStats st;
     st.n_kmers = red[0][0] + red[0][1] + red[0][2] + red[0][3];
@@ -757,6 +764,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     }
   }
   __syncthreads();
+  STAMP_WG(b, 4);
   // the bucket's sub-table, coalesced 16-B slots
   Slot* Tb = T + (uint64_t)b * V2_CAPW;
   for (uint32_t j = threadIdx.x; j < V2_CAPW; j += BLOCK) {
@@ -768,6 +776,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     const uint2 c = W.cc[V2_CAPW];
     *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
   }
+  STAMP_WG(b, 5);
 }
 
 // V_stats: reduce the per-bucket partials (grid-stride, one atomic per workgroup; meta was

@@ -685,14 +685,22 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
                             tile_row0, s));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, total + 1, s));
+  // emit into a guessed capacity before the total is known (no host round trip between the
+  // kernels); a query with more rows than the guess -- heavy repeats -- is emitted again
+  const uint64_t cap = (uint64_t)Nw + ((uint64_t)Nw >> 3) + 64;
+  q->rows.reset(cap);
+  LAUNCH("k_query_emit", s,
+         launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap, s));
   uint64_t H = 0;
   HIPC(hipMemcpyAsync(&H, total, sizeof(H), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   q->H = (int64_t)H;
-  q->rows.reset(H);
-  if (H)
+  if (H > cap) {
+    q->rows.bind(s);
+    q->rows.reset(H);
     LAUNCH("k_query_emit", s,
-           launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, s));
+           launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, H, s));
+  }
   return q.release();
 }
 

@@ -11,7 +11,10 @@ constexpr uint32_t V2_BW = 256;        // mean windows per bucket
 constexpr uint32_t V2_CAPB = 384;      // slots per bucket (LDS sub-table of one wave)
 constexpr uint32_t V2_SLOT_BITS = 9;   // bits to name a slot 0..V2_CAPB
 constexpr uint32_t V2_BW_WG = 1024;    // ... group buckets: mean windows per bucket
-constexpr uint32_t V2_CAPW = 1536;     // slots per group bucket (LDS sub-table of one workgroup)
+#ifndef KMHG_CAPW
+#define KMHG_CAPW 1536
+#endif
+constexpr uint32_t V2_CAPW = KMHG_CAPW;  // slots per group bucket (LDS sub-table of one workgroup)
 constexpr uint32_t V2_SLOT_BITS_WG = 11;
 constexpr uint32_t V2_MAXR = 640;      // max radix of one partition pass (LDS arrays)
 constexpr uint32_t V2_MAXR_IL = 320;   // ... with the interleaved tile schedule
@@ -55,9 +58,10 @@ void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t
 constexpr uint64_t SCAN1_MAX = 16384;
 inline uint64_t scan_u64_scratch(uint64_t n) { return (n + TILE - 1) / TILE + 1; }
 void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch, hipStream_t s);
+// rows >= cap are dropped (the caller re-runs the emit into an exact buffer if the total exceeds cap)
 void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
-                       hipStream_t s);
+                       uint64_t cap, hipStream_t s);
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint32_t* F,
                        hipStream_t s);
 void launch_read_order(const uint32_t* F, int64_t L, const Slot* T, uint64_t* st_a,

@@ -364,17 +364,25 @@ k_block_scan_u64(uint64_t* __restrict__ a, uint64_t n, const uint64_t* __restric
   }
 }
 
-// Q_emit: per tile, rows are dealt to lanes evenly (binary search over the tile's LDS prefix of
-// hit counts), so a window with thousands of hits does not serialise one lane.  Output rows are
-// (i = 1-based window end, j = 1-based index position), ordered by i then j as in the reference.
+// Q_emit: output rows (i = 1-based window end, j = 1-based index position), ordered by i then j
+// as in the reference.  Per tile: LDS prefix of the windows' hit counts; windows with at most
+// EMIT_DIRECT hits write their rows themselves, lane-consecutive windows so that the common
+// one-hit rows are consecutive (coalesced) stores; windows with more hits are then dealt to the
+// whole workgroup one at a time, so a window with thousands of hits does not serialise a lane.
+// Rows at or beyond `cap` are dropped: the host launches the emit before it knows the total and
+// re-runs it into an exact-size buffer in the rare case the guess was short.
+constexpr uint32_t EMIT_DIRECT = 4;
 __global__ void __launch_bounds__(BLOCK)
 k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
              const int32_t* __restrict__ positions, const uint64_t* __restrict__ tile_row0,
-             int2* __restrict__ out) {
+             int2* __restrict__ out, uint64_t cap) {
   __shared__ uint64_t incl[TILE];
   __shared__ uint32_t start[TILE];
+  __shared__ uint32_t heavy[TILE];
+  __shared__ uint32_t n_heavy;
   __shared__ uint64_t sh[8];
   const int64_t tile0 = (int64_t)blockIdx.x * TILE;
+  if (threadIdx.x == 0) n_heavy = 0;
   // load counts / starts (coalesced), then thread-contiguous prefix over WPT entries
   for (int j = 0; j < WPT; ++j) {
     int w = j * BLOCK + threadIdx.x;
@@ -395,14 +403,36 @@ k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
   __syncthreads();
   if (tot == 0) return;
   const uint64_t r0 = tile_row0[blockIdx.x];
-  for (uint64_t r = threadIdx.x; r < tot; r += BLOCK) {
-    // first w with incl[w] > r
-    int lo = 0, hi = TILE - 1;
-    while (lo < hi) { int mid = (lo + hi) >> 1; if (incl[mid] > r) hi = mid; else lo = mid + 1; }
-    uint64_t before = lo ? incl[lo - 1] : 0;
-    const uint32_t n = (uint32_t)(incl[lo] - before);
-    const int32_t j = n == 1 ? (int32_t)start[lo] : positions[start[lo] + (uint32_t)(r - before)];
-    out[r0 + r] = make_int2((int32_t)(w0 + tile0 + lo + kq), j);
+  const int32_t i0 = (int32_t)(w0 + tile0 + kq);
+#pragma unroll 2
+  for (int j = 0; j < WPT; ++j) {
+    const int w = j * BLOCK + threadIdx.x;
+    const uint64_t before = w ? incl[w - 1] : 0;
+    const uint64_t n = incl[w] - before;
+    if (n == 0) continue;
+    if (n > EMIT_DIRECT) {
+      heavy[atomicAdd(&n_heavy, 1u)] = (uint32_t)w;
+      continue;
+    }
+    const uint64_t r = r0 + before;
+    const uint32_t st0 = start[w];
+    if (n == 1) {
+      if (r < cap) out[r] = make_int2(i0 + w, (int32_t)st0);
+    } else {
+      for (uint32_t q = 0; q < (uint32_t)n; ++q)
+        if (r + q < cap) out[r + q] = make_int2(i0 + w, positions[st0 + q]);
+    }
+  }
+  __syncthreads();
+  const uint32_t nh = n_heavy;
+  for (uint32_t h = 0; h < nh; ++h) {
+    const uint32_t w = heavy[h];
+    const uint64_t before = w ? incl[w - 1] : 0;
+    const uint64_t n = incl[w] - before;
+    const uint64_t r = r0 + before;
+    const uint32_t st0 = start[w];
+    for (uint64_t q = threadIdx.x; q < n; q += BLOCK)
+      if (r + q < cap) out[r + q] = make_int2(i0 + (int32_t)w, positions[st0 + (uint32_t)q]);
   }
 }
 
@@ -650,9 +680,9 @@ void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch
 }
 void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
-                       hipStream_t s) {
+                       uint64_t cap, hipStream_t s) {
   hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qinfo, Nw, w0,
-                     kq, positions, tile_row0, out);
+                     kq, positions, tile_row0, out, cap);
 }
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint32_t* F,
                        hipStream_t s) {

@@ -14,3 +14,7 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT
 timeout -k 10 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
   --output-format csv -d "$OUT/p2" -o run -- python3 "$REPO/bench.py" "${ARGS[@]}" > "$OUT/p2.log" 2>&1
 echo "pmc $TAG done"
+# L2 request sizes / hit rate (random slot probes: 32/64/128-B fills?)
+timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum \
+  --output-format csv -d "$OUT/p3" -o run -- python3 "$REPO/bench.py" "${ARGS[@]}" > "$OUT/p3.log" 2>&1
+echo "pmc $TAG tcc done"

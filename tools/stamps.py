@@ -26,13 +26,16 @@ os.environ["KMHG_STAMP_FILE"] = f
 D.DeviceIndex.build(seq, k).free()
 a = np.fromfile(f, np.uint64).reshape(-1, 8).astype(np.int64)
 a = a[a[:, 0] > 0]
-names = ["init+start", "loads", "passA", "scan", "passB", "table"]
+wg = os.environ.get("KMHG_BUCKET", "group") != "wave"
+names = (["clear", "passA(+load)", "scan", "passB", "table"] if wg else
+         ["init+start", "loads", "passA", "scan", "passB", "table"])
+last = len(names)
 t0 = a[:, 0].min()
-print(f"buckets {len(a)}  kernel span {a[:, 6].max() - t0} ticks")
+print(f"buckets {len(a)}  kernel span {a[:, last].max() - t0} ticks")
 for i, n in enumerate(names):
     d = a[:, i + 1] - a[:, i]
     print(f"{n:12s} mean {d.mean():9.0f}  median {np.median(d):9.0f}  p99 {np.percentile(d, 99):9.0f}")
-life = a[:, 6] - a[:, 0]
+life = a[:, last] - a[:, 0]
 print(f"{'lifetime':12s} mean {life.mean():9.0f}  median {np.median(life):9.0f}")
 st = np.sort(a[:, 0] - t0)
 print("start ticks quantiles", [int(x) for x in np.percentile(st, [0, 10, 50, 90, 100])])
