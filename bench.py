@@ -123,6 +123,25 @@ def cpu_baseline(seq_bytes: bytes, k: int, budget_s: float = 20.0) -> dict | Non
                 "sample": f"unavailable: {e}"}
 
 
+def cpu_counts_baseline(seq_bytes: bytes, k: int, sample_bp: int = 3_000_000) -> dict:
+    """count_kmers (src/kmer_hash.c:548-591: seq_to_counts over the reference's khash core,
+    oracle/_ref) on a bounded prefix of the same sequence, 1 thread."""
+    try:
+        from oracle import oracle as O
+        sample = seq_bytes[:sample_bp]
+        t0 = time.perf_counter()
+        r = O.RefIndex.counts([sample], k, 0, 2)
+        t = time.perf_counter() - t0
+        r.close()
+        return {"value": round(len(sample) / 1e6 / t, 3), "unit": "Mbp/s", "cores": 1,
+                "kind": "reference",
+                "sample": f"{len(sample) / 1e6:.1f} Mbp prefix, k={k}, count_kmers(source 0 of 2) "
+                          "restated over the compiled khash core (oracle/_ref, gcc -O2)"}
+    except Exception as e:  # reported, never required
+        return {"value": None, "unit": "Mbp/s", "cores": 1, "kind": "reference",
+                "sample": f"unavailable: {e}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -236,10 +255,32 @@ def main():
     t_query = time.perf_counter() - t0
     idx.free()
 
-    tb = torch.tensor([t_build, t_query, t_sync], dtype=torch.float64, device=dev)
+    # ---------------- count.kmers (SURVEY.md §8 f next-4) of the same sequence: one call per step
+    # into a new counts pointer (k, source 0 of 2)
+    cper, t_count, cU = {}, 0.0, 0
+    if not args.profile:
+        for _ in range(max(1, args.warmup)):
+            D.DeviceIndex.count(seq, k, 0, 2, stream=stream).free()
+        D.timing_enable(True)
+        D.timing_reset()
+        for _ in range(2):
+            c = D.DeviceIndex.count(seq, k, 0, 2, stream=stream)
+            cU = c.info()["n_kmers"]
+            c.free()
+        ct = D.timing_report()
+        cper = {n: v[1] / 2 for n, v in ct.items() if v[0]}
+        D.timing_enable(False)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            D.DeviceIndex.count(seq, k, 0, 2, stream=stream).free()
+        barrier()
+        t_count = time.perf_counter() - t0
+
+    tb = torch.tensor([t_build, t_query, t_sync, t_count], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tb, op=dist.ReduceOp.MAX)
-    t_build, t_query, t_sync = tb.tolist()
+    t_build, t_query, t_sync, t_count = tb.tolist()
 
     if rank == 0:
         Nw = L - k + 1
@@ -298,8 +339,17 @@ def main():
                                                      (t_build / args.steps) / 1e9 / HBM_PEAK_GBS, 5),
                                "note": "whole build, SURVEY.md §8(d): B = L + 12U + 4N"},
         }
+        if t_count:
+            out["counts"] = {
+                "value": round(mbp_total * args.steps / t_count, 2), "unit": "Mbp/s",
+                "ms_per_step": round(t_count / args.steps * 1e3, 4), "distinct_kmers": cU,
+                "kernels_ms_per_step": {n: round(v, 5) for n, v in cper.items()},
+                "note": "count.kmers(seq, c(k, 0, 2)) into a new pointer per step: partitioned "
+                        "build of the batch + merge into the count matrix + table rebuild"}
         if not args.no_cpu and not args.profile:
             out["cpu_baseline"] = cpu_baseline(host_seq.tobytes(), k)
+            if t_count:
+                out["counts"]["cpu_baseline"] = cpu_counts_baseline(host_seq.tobytes(), k)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

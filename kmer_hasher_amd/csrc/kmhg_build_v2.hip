@@ -410,6 +410,9 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
 }
 
 // ---------------------------------------------------------------- V_bounds
+// start[b] = first element of bucket b in the partitioned keys (start[nb] = n).  Each wave walks
+// chunks of 4 x 64 consecutive elements; an element's left neighbour's bucket comes from the lane
+// below by a shuffle (one extra load per chunk), so every key is read and hashed once.
 __global__ void __launch_bounds__(BLOCK)
 k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
             uint32_t* __restrict__ start) {
@@ -419,12 +422,30 @@ k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_pt
     for (uint64_t b = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; b <= g.nb; b += stride) start[b] = 0;
     return;
   }
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
-    const uint32_t b = bucket_of(mix64(keys[i]), g.nb);
-    const int64_t bp = i ? (int64_t)bucket_of(mix64(keys[i - 1]), g.nb) : -1;
-    for (int64_t x = bp + 1; x <= (int64_t)b; ++x) start[x] = (uint32_t)i;
-    if (i == n - 1)
-      for (uint64_t x = (uint64_t)b + 1; x <= g.nb; ++x) start[x] = (uint32_t)n;
+  const int lane = lane_id();
+  const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
+  const uint64_t wid = (uint64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
+  for (uint64_t c0 = wid * 256; c0 < n; c0 += nwaves * 256) {
+    uint32_t bk[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = c0 + (uint64_t)j * 64 + lane;
+      bk[j] = i < n ? bucket_of(mix64(keys[i]), g.nb) : g.nb;
+    }
+    int64_t before = -1;                       // bucket of element c0 - 1
+    if (c0) before = (int64_t)bucket_of(mix64(keys[c0 - 1]), g.nb);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t i = c0 + (uint64_t)j * 64 + lane;
+      const uint32_t up = __shfl_up(bk[j], 1);
+      const uint32_t last_prev = __shfl(j ? bk[j - 1] : 0u, 63);
+      const int64_t bp = lane ? (int64_t)up : (j ? (int64_t)last_prev : before);
+      if (i < n) {
+        for (int64_t x = bp + 1; x <= (int64_t)bk[j]; ++x) start[x] = (uint32_t)i;
+        if (i == n - 1)
+          for (uint64_t x = (uint64_t)bk[j] + 1; x <= g.nb; ++x) start[x] = (uint32_t)n;
+      }
+    }
   }
 }
 

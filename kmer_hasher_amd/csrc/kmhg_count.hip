@@ -12,9 +12,11 @@
 //             raises its flag
 //   (k_scan_u32 of the flags: new rows keep first-occurrence order)
 //   C_append  new key r -> row U0 + rank: key + a count vector with only `source` set
-//   C_insert  the table is rebuilt for the grown key list (global linear probing, nb = 1):
-//             slot {key, count = source_n, aux}, aux = the count itself for source_n = 1 (the
-//             inline convention of the position index), else the end of the row's vector
+//   (table)   the table is rebuilt for the grown key list by the partitioned build run over the
+//             key stream (values = row + 1), then C_fix gives each slot {key, count = source_n,
+//             aux}, aux = the count itself for source_n = 1 (the inline convention of the
+//             position index), else the end of the row's vector.  C_insert (global linear
+//             probing, nb = 1) is the fallback should a bucket overflow.
 //   C_canon   readout arrays in row order (perm, row offsets, keys owning pairs)
 // The count matrix (U x source_n int32, row-major) takes the place of `positions`, so
 // kmer.pos and seq.kmer.pos read a counts index with the position index's kernels -- the
@@ -90,7 +92,36 @@ k_count_canon(const uint32_t* __restrict__ row_slot, uint32_t U, uint32_t S,
   }
 }
 
+// values base, base + 1, ... of the key stream of a table rebuild
+__global__ void __launch_bounds__(BLOCK) k_iota_u32(uint32_t* __restrict__ a, uint64_t n,
+                                                    uint32_t base) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * BLOCK)
+    a[i] = base + (uint32_t)i;
+}
+
+// C_fix: a table rebuilt by the partitioned build from the key list holds {key, 1, row + 1};
+// give every occupied slot its counts-index fields and record the slot <-> row maps.
+__global__ void __launch_bounds__(BLOCK)
+k_count_fix(Slot* __restrict__ T, uint64_t nslots, uint32_t S, const int32_t* __restrict__ M,
+            uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
+       i += (uint64_t)gridDim.x * BLOCK) {
+    const uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+    if (!v.z) continue;
+    const uint32_t r = v.w - 1;
+    T[i].count = S;
+    T[i].aux = S == 1 ? (uint32_t)M[r] : (r + 1) * S;
+    slot_row[i] = r;
+    row_slot[r] = (uint32_t)i;
+  }
+}
+
 static inline unsigned grid_of(uint64_t n) { return (unsigned)((n + BLOCK - 1) / BLOCK); }
+static inline unsigned grid_cap(uint64_t n) {
+  const unsigned g = grid_of(n);
+  return g > 16384 ? 16384 : (g ? g : 1);
+}
 
 void launch_count_probe(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb, const Slot* Tc,
                         Geom gc, const uint32_t* slot_row, uint32_t S, uint32_t source,
@@ -108,6 +139,14 @@ void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uin
                          const int32_t* M, uint32_t* slot_row, uint32_t* row_slot,
                          hipStream_t s) {
   hipLaunchKernelGGL(k_count_insert, dim3(grid_of(U)), dim3(BLOCK), 0, s, ckeys, U, T, g, S, M,
+                     slot_row, row_slot);
+}
+void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s) {
+  hipLaunchKernelGGL(k_iota_u32, dim3(grid_cap(n)), dim3(BLOCK), 0, s, a, n, base);
+}
+void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
+                      uint32_t* row_slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_count_fix, dim3(grid_cap(nslots)), dim3(BLOCK), 0, s, T, nslots, S, M,
                      slot_row, row_slot);
 }
 void launch_count_canon(const uint32_t* row_slot, uint32_t U, uint32_t S, uint32_t* perm,

@@ -503,17 +503,22 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 // Partitioned build (kmhg_build_v2.hip): LSD radix partition of the windows by hash bucket,
 // then one wave per bucket builds its sub-table in LDS.  Falls back to v1 if a bucket's LDS
 // sub-table overflows (never observed: distinct keys per bucket ~ Binomial, mean <= V2_BW).
-kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
+// Partitioned build over the windows of a sequence (d_seq), or over a stream of n_keys
+// distinct keys (d_keys, d_seq == nullptr; the counts index's table rebuild): key r is stored
+// with count 1 and aux = r + 1.
+kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
+                            const uint64_t* d_keys = nullptr, int64_t n_keys = 0) {
   const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
   idx->stream = s;
   HIPC(hipGetDevice(&idx->device));
   idx->k = k;
   idx->L = L;
-  const int64_t Nw = L - k + 1;
+  const bool from_keys = d_seq == nullptr;
+  const int64_t Nw = from_keys ? n_keys : L - k + 1;
   // the partition kernels read the sequence as aligned 16-B words: copy an unaligned input
   DBuf<uint8_t> aligned_copy;
-  if ((reinterpret_cast<uintptr_t>(d_seq) & 15) != 0) {
+  if (!from_keys && (reinterpret_cast<uintptr_t>(d_seq) & 15) != 0) {
     aligned_copy.reset((size_t)L);
     aligned_copy.bind(s);
     HIPC(hipMemcpyAsync(aligned_copy.p, d_seq, (size_t)L, hipMemcpyDeviceToDevice, s));
@@ -524,7 +529,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // radix plan: fewest passes whose radix fits LDS.  Interleaved tiles of PTILE windows keep
   // ~PTILE / R elements per digit run: beyond ~300 digits the runs get too short for coalesced
   // writes and an extra pass is cheaper.
-  const uint32_t maxr = ch.interleaved ? V2_MAXR_IL : V2_MAXR;
+  uint32_t maxr = ch.interleaved ? V2_MAXR_IL : V2_MAXR;
+  if (const char* e = std::getenv("KMHG_MAXR"))   // testing knob: force more radix passes
+    maxr = std::max<uint32_t>(2u, std::min<uint32_t>(maxr, (uint32_t)std::atoi(e)));
   auto plan = [&](uint32_t nbk, uint32_t& R) {
     for (uint32_t passes = 1; passes <= 4; ++passes) {
       R = (uint32_t)std::ceil(std::pow((double)nbk, 1.0 / passes) - 1e-9);
@@ -573,17 +580,25 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   idx->positions.reset(Nw);
   DBuf<BucketStats> bstats(nb, s);
 
-  LAUNCH("k_v2_hist0", s,
-         launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, status, n_status,
-                         meta, s));
-  LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
-  LAUNCH("k_v2_scatter_seq", s,
-         launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, kA.p, pA.p,
-                               pad, s));
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
-  uint32_t div = R;
-  for (uint32_t p = 1; p < passes; ++p) {
+  uint32_t div = 1;
+  if (from_keys) {   // pass 0 reads the key stream like every later pass
+    HIPC(hipMemcpyAsync(kA.p, d_keys, (size_t)Nw * 8, hipMemcpyDeviceToDevice, s));
+    LAUNCH("k_iota_u32", s, launch_iota_u32(pA.p, (uint64_t)Nw, 1u, s));
+    HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(n_valid), (int)Nw, 1, s));
+    HIPC(hipMemsetAsync(meta, 0, sizeof(BuildMeta), s));
+  } else {
+    LAUNCH("k_v2_hist0", s,
+           launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, status, n_status,
+                           meta, s));
+    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
+    LAUNCH("k_v2_scatter_seq", s,
+           launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, kA.p, pA.p,
+                                 pad, s));
+    div = R;
+  }
+  for (uint32_t p = from_keys ? 0 : 1; p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
     LAUNCH("k_v2_hist", s,
            launch_v2_hist(kin, n_valid, g, Dp, hist.p, ch, status, n_status, s));
@@ -796,18 +811,40 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
   HIPC(hipStreamSynchronize(s));
   const uint64_t U1 = U0 + n_new;
   // rebuild the table for U1 keys (aux of a source_n = 1 index carries the count itself, so
-  // even a batch of known keys changes the slots)
+  // even a batch of known keys changes the slots): the partitioned build over the key list,
+  // or global linear probing should a bucket overflow (never observed: distinct keys)
   idx->table.bind(s);
   idx->slot_row.bind(s);
-  idx->geom = Geom{1u, (uint32_t)table_capacity((int64_t)U1)};
-  idx->table.reset(idx->slots());
-  idx->slot_row.reset(idx->slots());
   idx->row_slot.bind(s);
+  const char* ct = std::getenv("KMHG_COUNT_TABLE");   // "probe": the fallback (tests)
+  const bool probe_only = ct && std::string(ct) == "probe";
+  std::unique_ptr<kmhg_index> K;
+  bool ovf = true;
+  if (!probe_only) {
+    K.reset(build_device_v2(nullptr, 0, k, s, idx->ckeys.p, (int64_t)U1));
+    HIPC(hipEventSynchronize(K->rec.ev));
+    ovf = K->rec.meta->overflow != 0;
+    PinnedPool::get().give(K->rec, false);
+    K->rec = PinnedRec{};
+    K->pending = false;
+  }
+  Release relk{K ? K.get() : B.get(), s};
   idx->row_slot.reset(U1);
-  LAUNCH("k_table_init", s, launch_table_init(idx->table.p, idx->slots(), s));
-  LAUNCH("k_count_insert", s,
-         launch_count_insert(idx->ckeys.p, (uint32_t)U1, idx->table.p, idx->geom, S,
-                             idx->positions.p, idx->slot_row.p, idx->row_slot.p, s));
+  if (!ovf) {
+    idx->geom = K->geom;
+    idx->table.swap_with(K->table);
+    idx->slot_row.reset(idx->slots());
+    LAUNCH("k_count_fix", s, launch_count_fix(idx->table.p, idx->slots(), S, idx->positions.p,
+                                              idx->slot_row.p, idx->row_slot.p, s));
+  } else {
+    idx->geom = Geom{1u, (uint32_t)table_capacity((int64_t)U1)};
+    idx->table.reset(idx->slots());
+    idx->slot_row.reset(idx->slots());
+    LAUNCH("k_table_init", s, launch_table_init(idx->table.p, idx->slots(), s));
+    LAUNCH("k_count_insert", s,
+           launch_count_insert(idx->ckeys.p, (uint32_t)U1, idx->table.p, idx->geom, S,
+                               idx->positions.p, idx->slot_row.p, idx->row_slot.p, s));
+  }
   idx->U = U1;
   idx->N = U1 * S;
   idx->P = U1 * ((uint64_t)S * (S - 1) / 2);

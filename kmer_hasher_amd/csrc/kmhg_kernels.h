@@ -159,6 +159,9 @@ void launch_count_append(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb,
 void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uint32_t S,
                          const int32_t* M, uint32_t* slot_row, uint32_t* row_slot,
                          hipStream_t s);
+void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s);
+void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
+                      uint32_t* row_slot, hipStream_t s);
 void launch_count_canon(const uint32_t* row_slot, uint32_t U, uint32_t S, uint32_t* perm,
                         uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
                         hipStream_t s);

@@ -38,6 +38,19 @@ class DeviceIndex:
                                                     _stream_ptr(stream), C.byref(out)))
         return cls(out.value)
 
+    @classmethod
+    def count(cls, seq: torch.Tensor, k: int, source: int, source_n: int,
+              into: "DeviceIndex | None" = None, stream=None) -> "DeviceIndex":
+        """count.kmers of one HBM-resident sequence (kmhg_count_device): adds to `into`, or
+        makes a new counts index.  Synchronous (the merge reads the number of new k-mers)."""
+        _check_seq(seq)
+        h = C.c_void_p(into._h.value if into is not None else None)
+        with torch.cuda.device(seq.device):
+            _lib.check(_lib.lib().kmhg_count_device(C.byref(h), C.c_void_p(seq.data_ptr()),
+                                                    seq.numel(), k, source, source_n,
+                                                    _stream_ptr(stream)))
+        return into if into is not None else cls(h.value)
+
     @property
     def handle(self):
         return self._h

@@ -148,8 +148,13 @@ def test_gpu_counts_golden_khash_order(gpu, cgold):
 
 
 @pytest.mark.gpu
-def test_gpu_counts_first_order_vs_oracle(gpu, cgold):
+@pytest.mark.parametrize("table", ["partitioned", "probe"])
+def test_gpu_counts_first_order_vs_oracle(gpu, cgold, monkeypatch, table):
+    """Both ways of rebuilding the counts table: the partitioned build over the key list (the
+    default) and global linear probing (its overflow fallback, KMHG_COUNT_TABLE=probe)."""
     from kmer_hasher_amd import kmer_pos
+    if table == "probe":
+        monkeypatch.setenv("KMHG_COUNT_TABLE", "probe")
     for case, _ in cgold:
         oc = _oracle(case)
         ix = oc.index()

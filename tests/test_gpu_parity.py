@@ -212,3 +212,16 @@ def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     _check_against_oracle(rr.tobytes().decode("latin-1"), 21, qks=[21], pairs=True)
     _check_against_oracle(synth.iid(3_000_000, 17).tobytes().decode(), 31, pairs=False)
     _check_against_oracle("G" * 40, 32, qks=[31])
+
+
+@pytest.mark.parametrize("maxr", ["6", "12", "40"])
+def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr):
+    """More radix passes than the input needs (KMHG_MAXR caps the radix): 2-4 passes, so the
+    last pass's bucket counts (which replace a bounds search) are exercised with 1, 2 and 3
+    low digits below the last one, chunks spanning many low values, and N-runs."""
+    from kmer_hasher_amd import synth
+    monkeypatch.setenv("KMHG_MAXR", maxr)
+    s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
+    _check_against_oracle(s, 31, pairs=False)
+    rr = synth.repeat_rich(300_000, 42, n_gap_every=100_000).tobytes().decode("latin-1")
+    _check_against_oracle(rr, 17, qks=[17], pairs=True)
