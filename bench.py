@@ -58,7 +58,7 @@ def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) 
         return L + 12 * N
     if kernel == "k_v2_scatter":        # one radix pass: read + write 12 B per window
         return 24 * N
-    if kernel in ("k_v2_bucket", "k_v2_bucket_wg"):   # read 12 B/window; one 16-B slot per distinct key; 4 B per
+    if kernel in ("k_v2_bucket", "k_v2_bucket_wg", "k_v2_bucket_sort"):   # read 12 B/window; one 16-B slot per distinct key; 4 B per
         return 12 * N + 16 * U + 4 * (N - U)   # position of a repeated key (>= N - U of them)
     if kernel == "k_build_insert":      # read L chars; key+count per distinct key; slot id/window
         return L + 12 * U + 4 * Nw

@@ -42,9 +42,13 @@ __device__ uint64_t* g_stamps;
     __builtin_amdgcn_sched_barrier(0);                                                \
   } while (0)
 #define STAMP_WG(b, i) do { if (threadIdx.x < 64) STAMP(b, i); } while (0)
+// ... after this wave's outstanding loads have landed (splits load latency from the work after)
+#define STAMP_WG_DRAIN(b, i) \
+  do { __builtin_amdgcn_s_waitcnt(0); if (threadIdx.x < 64) STAMP(b, i); } while (0)
 #else
 #define STAMP(b, i) do {} while (0)
 #define STAMP_WG(b, i) do {} while (0)
+#define STAMP_WG_DRAIN(b, i) do {} while (0)
 #endif
 
 // LDS sub-table of one bucket, private to one wave (slot V2_CAPB = side slot of key ~0).
@@ -655,18 +659,19 @@ __device__ __forceinline__ int lds_find_g(const GroupTable& W, uint64_t key) {
   return -1;
 }
 
-__global__ void __launch_bounds__(BLOCK)
-k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
-               const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
-               int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
-               BuildMeta* __restrict__ meta) {
-  __shared__ GroupTable W;
-  __shared__ uint64_t sh[8];
-  __shared__ uint32_t red[3][4];
+// The CAS build of one group bucket (the body of V_bucket_wg; also the fallback of V_bucket_sort
+// for buckets it does not take).  W, sh, red are the caller's LDS.
+__device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint32_t (*red)[4],
+                                              const uint64_t* __restrict__ keys,
+                                              const uint32_t* __restrict__ pos,
+                                              const uint32_t* __restrict__ start, Geom g,
+                                              Slot* __restrict__ T,
+                                              int32_t* __restrict__ positions,
+                                              BucketStats* __restrict__ bstats,
+                                              BuildMeta* __restrict__ meta, const uint32_t b) {
   constexpr int PER = 2 * V2_BW_WG / BLOCK;           // elements per thread per batch (2x mean)
   constexpr uint32_t BATCH = BLOCK * PER;
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const uint32_t b = blockIdx.x;
   const uint32_t s0 = start[b], s1 = start[b + 1];
   const bool one_batch = s1 - s0 <= BATCH;
   uint64_t key[PER];
@@ -690,6 +695,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   }
   __syncthreads();
   STAMP_WG(b, 1);
+  STAMP_WG_DRAIN(b, 6);
   // pass A: distinct keys + counts (CAS on a table shared by the four waves).  (Measured:
   // skipping the count atomic for a key's claiming occurrence ran 35 % slower, 141 vs 105 us.)
   bool ovf = false;
@@ -798,6 +804,278 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
   }
   STAMP_WG(b, 5);
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
+               const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
+               int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
+               BuildMeta* __restrict__ meta) {
+  __shared__ GroupTable W;
+  __shared__ uint64_t sh[8];
+  __shared__ uint32_t red[3][4];
+  bucket_wg_cas(W, sh, red, keys, pos, start, g, T, positions, bstats, meta, blockIdx.x);
+}
+
+// ---------------------------------------------------------------- V_bucket_sort (group per bucket)
+// The same group bucket built without LDS atomics (the CAS build is bound by the LDS atomic
+// unit: one 64-bit CAS + one add per window).  The bucket's windows (<= V2_CAPW of them, in
+// position order) are stably sorted by sk = the top 16 bits of lo32(mix64(key)) with two 8-bit
+// passes of ballot ranks (the scatter passes' multi-split, per-wave digit counters), so:
+//   * equal keys become contiguous runs (a run = one distinct k-mer, its length = its count, its
+//     windows already in position order -> positions[s0 + sorted index] directly),
+//   * runs come in home order (home = (sk * capb) >> 16, non-decreasing in sk), and the linear-
+//     probing table is laid out directly: run q goes to p_q = max(home_q, p_{q-1} + 1), i.e.
+//     p_q = q + max(over, max_{q' <= q}(home_q' - q')) -- one block max-scan -- where `over`
+//     (the runs pushed past the end, which wrap into slots [0, over)) is max(0, D - capb + M).
+// Different keys with equal sk that interleave (needs an sk collision AND a repeated key, both
+// rare), the k = 32 key ~0, and buckets larger than V2_CAPW take the CAS build instead.
+constexpr uint32_t NS = V2_CAPW;            // windows a sorted bucket may hold
+constexpr int PS = NS / BLOCK;              // ... per thread
+struct SortLDS {
+  uint64_t ekey[NS];                        // windows in position order
+  uint32_t epos[NS];
+  uint16_t esk[NS];
+  uint16_t sidx[2][NS];                     // sort passes: window indices in sorted order
+  uint32_t cntw[4][256];                    // per-wave digit counters -> bases
+  uint16_t rs[NS + 1];                      // run starts (sorted index), rs[D] = n
+  uint8_t occ[V2_CAPW];                     // table slots taken by a run
+};
+union BucketLDS {
+  GroupTable W;
+  SortLDS S;
+};
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d));
+  return v;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_v2_bucket_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
+                 const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
+                 int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
+                 BuildMeta* __restrict__ meta) {
+  __shared__ BucketLDS U;
+  __shared__ uint64_t sh[8];
+  __shared__ uint32_t red[3][4];
+  __shared__ int wmax[4];
+  const uint32_t b = blockIdx.x;
+  const uint32_t s0 = start[b], s1 = start[b + 1];
+  const uint32_t n = s1 - s0;
+  if (n > NS) {
+    bucket_wg_cas(U.W, sh, red, keys, pos, start, g, T, positions, bstats, meta, b);
+    return;
+  }
+  SortLDS& S = U.S;
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  STAMP_WG(b, 0);
+  constexpr uint32_t WSPAN = NS / 4;        // windows per wave, contiguous: e = wave*WSPAN + c*64 + lane
+  // ---- load (coalesced per wave), sort keys in registers and LDS
+  uint32_t skr[PS];
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < PS; ++c) {
+    const uint32_t e = wave * WSPAN + (uint32_t)c * 64 + lane;
+    skr[c] = 0;
+    if (e < n) {
+      const uint64_t k = keys[s0 + e];
+      S.ekey[e] = k;
+      S.epos[e] = pos[s0 + e];
+      skr[c] = (uint32_t)mix64(k) >> 16;
+      S.esk[e] = (uint16_t)skr[c];
+      bad |= k == EMPTY_KEY;
+    }
+  }
+  for (uint32_t j = threadIdx.x; j < V2_CAPW / 4; j += BLOCK)
+    reinterpret_cast<uint32_t*>(S.occ)[j] = 0u;
+  if (__syncthreads_or(bad)) {
+    bucket_wg_cas(U.W, sh, red, keys, pos, start, g, T, positions, bstats, meta, b);
+    return;
+  }
+  STAMP_WG(b, 1);
+  // ---- two stable 8-bit passes; element order inside a pass = (wave, c, lane)
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    for (uint32_t d = lane; d < 256; d += 64) S.cntw[wave][d] = 0u;
+    wave_sync();
+    uint32_t dg[PS], rk[PS], el[PS];
+    bool act[PS];
+#pragma unroll
+    for (int c = 0; c < PS; ++c) {
+      const uint32_t q = wave * WSPAN + (uint32_t)c * 64 + lane;
+      act[c] = q < n;
+      el[c] = pass == 0 ? q : (act[c] ? S.sidx[0][q] : 0u);
+      const uint32_t sk = pass == 0 ? skr[c] : (act[c] ? (uint32_t)S.esk[el[c]] : 0u);
+      dg[c] = pass == 0 ? (sk & 255u) : (sk >> 8);
+      const uint64_t grp = match_bits(dg[c], 8, act[c]);
+      const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
+      uint32_t cur = 0;
+      if (act[c] && leader == lane) {
+        cur = S.cntw[wave][dg[c]];
+        S.cntw[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
+      }
+      cur = __shfl(cur, leader);
+      wave_sync();
+      rk[c] = cur + (uint32_t)__popcll(grp & lanemask_lt());
+    }
+    __syncthreads();
+    {   // digit bases: thread t owns digit t over the 4 waves
+      const uint32_t t = threadIdx.x;
+      const uint32_t c0 = S.cntw[0][t], c1 = S.cntw[1][t], c2 = S.cntw[2][t], c3 = S.cntw[3][t];
+      uint64_t tot;
+      const uint32_t base = (uint32_t)block_excl_scan(c0 + c1 + c2 + c3, sh, tot);
+      S.cntw[0][t] = base;
+      S.cntw[1][t] = base + c0;
+      S.cntw[2][t] = base + c0 + c1;
+      S.cntw[3][t] = base + c0 + c1 + c2;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < PS; ++c)
+      if (act[c]) S.sidx[pass][S.cntw[wave][dg[c]] + rk[c]] = (uint16_t)el[c];
+    __syncthreads();
+    STAMP_WG(b, 2 + pass);
+  }
+  // ---- runs: thread t takes sorted indices [t*PS, t*PS + PS)
+  const uint16_t* srt = S.sidx[1];
+  const uint32_t i0 = threadIdx.x * PS;
+  uint64_t kk[PS];
+  uint32_t pp[PS], sk[PS];
+  bool rst[PS];
+  uint64_t prevk = 0;
+  uint32_t prevsk = 0x10000u;
+  if (i0 > 0 && i0 < n) {
+    const uint32_t e = srt[i0 - 1];
+    prevk = S.ekey[e];
+    prevsk = S.esk[e];
+  }
+  bool il = false;                          // interleaved keys of equal sk
+  uint32_t nrun = 0;
+#pragma unroll
+  for (int j = 0; j < PS; ++j) {
+    const uint32_t i = i0 + j;
+    rst[j] = false;
+    if (i >= n) continue;
+    const uint32_t e = srt[i];
+    kk[j] = S.ekey[e];
+    pp[j] = S.epos[e];
+    sk[j] = S.esk[e];
+    rst[j] = i == 0 || kk[j] != prevk;
+    if (rst[j] && i > 0 && sk[j] == prevsk) {  // sk collision: is this key already a run?
+      for (int m = (int)i - 2; m >= 0; --m) {
+        const uint32_t em = srt[m];
+        if (S.esk[em] != sk[j]) break;
+        if (S.ekey[em] == kk[j]) { il = true; break; }
+      }
+    }
+    nrun += rst[j] ? 1u : 0u;
+    prevk = kk[j];
+    prevsk = sk[j];
+  }
+  if (__syncthreads_or(il)) {
+    bucket_wg_cas(U.W, sh, red, keys, pos, start, g, T, positions, bstats, meta, b);
+    return;
+  }
+  STAMP_WG(b, 4);
+  uint64_t D64;
+  uint32_t q = (uint32_t)block_excl_scan(nrun, sh, D64);   // run index of this thread's first run
+  const uint32_t D = (uint32_t)D64;
+  {
+    uint32_t qq = q;
+#pragma unroll
+    for (int j = 0; j < PS; ++j)
+      if (rst[j]) S.rs[qq++] = (uint16_t)(i0 + j);
+    if (threadIdx.x == 0) S.rs[D] = (uint16_t)n;
+  }
+  // prefix max of (home - q) over runs: thread-local running max, then across threads
+  int lmax = INT_MIN;
+  {
+    uint32_t qq = q;
+#pragma unroll
+    for (int j = 0; j < PS; ++j)
+      if (rst[j]) {
+        const int home = (int)((sk[j] * V2_CAPW) >> 16);
+        lmax = max(lmax, home - (int)qq);
+        ++qq;
+      }
+  }
+  // exclusive max over threads < t: wave inclusive max-scan + per-wave maxima in LDS
+  int incl = lmax;
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(incl, d);
+    if (lane >= d) incl = max(incl, y);
+  }
+  if (lane == 63) wmax[wave] = incl;
+  int excl = __shfl_up(incl, 1);
+  if (lane == 0) excl = INT_MIN;
+  __syncthreads();                          // also publishes S.rs
+  for (int w = 0; w < wave; ++w) excl = max(excl, wmax[w]);
+  const int M = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+  const int over = max(0, (int)D - (int)V2_CAPW + M);
+  const bool full = D >= V2_CAPW;           // no empty slot left: the host rebuilds with v1
+  // ---- table slots of this thread's runs, positions of repeated k-mers
+  Slot* Tb = T + (uint64_t)b * V2_CAPW;
+  uint32_t mx = 0;
+  uint64_t pairs = 0;
+  {
+    uint32_t qq = q;
+    int run_max = excl;
+    uint32_t cur_q = q - 1;                 // run of the element before this thread's first run start
+#pragma unroll
+    for (int j = 0; j < PS; ++j) {
+      const uint32_t i = i0 + j;
+      if (i >= n) continue;
+      if (rst[j]) {
+        cur_q = qq++;
+        const int home = (int)((sk[j] * V2_CAPW) >> 16);
+        run_max = max(run_max, home - (int)cur_q);
+        const uint32_t cnt = (uint32_t)S.rs[cur_q + 1] - i;
+        mx = max(mx, cnt);
+        pairs += (uint64_t)cnt * (cnt - 1) / 2;
+        if (!full) {
+          const int p = (int)cur_q + max(over, run_max);
+          const uint32_t slot = p < (int)V2_CAPW ? (uint32_t)p : (uint32_t)p - V2_CAPW;
+          S.occ[slot] = 1;
+          *reinterpret_cast<uint4*>(&Tb[slot]) =
+              make_uint4((uint32_t)kk[j], (uint32_t)(kk[j] >> 32), cnt,
+                         cnt == 1 ? pp[j] : s0 + i + cnt);
+        }
+      }
+      // repeated k-mer: every window writes its position at its sorted index
+      const uint32_t rq = rst[j] ? cur_q : (cur_q == 0xFFFFFFFFu ? 0u : cur_q);
+      const uint32_t cnt_here = (uint32_t)S.rs[rq + 1] - (uint32_t)S.rs[rq];
+      if (cnt_here > 1 && !full) positions[s0 + i] = (int32_t)pp[j];
+    }
+  }
+  // stats
+  for (int d = 32; d >= 1; d >>= 1) {
+    pairs += __shfl_xor(pairs, d);
+    mx = max(mx, (uint32_t)__shfl_xor(mx, d));
+  }
+  if (lane == 0) {
+    red[1][wave] = mx;
+    sh[4 + wave] = pairs;
+  }
+  __syncthreads();                          // S.occ complete
+  STAMP_WG(b, 5);
+  if (full) {
+    if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
+    return;
+  }
+  for (uint32_t j = threadIdx.x; j < V2_CAPW; j += BLOCK)
+    if (!S.occ[j])
+      *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+  if (threadIdx.x == 0) {
+    BucketStats st;
+    st.n_kmers = D;
+    st.max_count = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+    st.n_pairs = sh[4] + sh[5] + sh[6] + sh[7];
+    bstats[b] = st;
+    if (b == bucket_of(mix64(EMPTY_KEY), g.nb))   // no window of this bucket is key ~0
+      *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+  }
+  STAMP_WG(b, 6);
 }
 
 // V_stats: reduce the per-bucket partials (grid-stride, one atomic per workgroup; meta was
@@ -965,6 +1243,12 @@ void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t*
                       hipStream_t s) {
   hipLaunchKernelGGL(k_v2_bucket, dim3(grid_of(g.nb, 4)), dim3(BLOCK), 0, s, keys, pos, start, g,
                      T, positions, bstats, meta, xcd_map_bucket());
+}
+void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint32_t* start,
+                           Geom g, Slot* T, int32_t* positions, BucketStats* bstats,
+                           BuildMeta* meta, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_bucket_sort, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
+                     positions, bstats, meta);
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,

@@ -253,8 +253,10 @@ __device__ __forceinline__ bool window_key(const ST& st, int o, int64_t s, int64
 __device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t nb) {
   return (uint32_t)__umul64hi(h, (uint64_t)nb);
 }
+// home slot from the top 16 bits of lo32(h): a non-decreasing function of the 16-bit sort key
+// the sorted bucket build orders windows by (V_bucket_sort)
 __device__ __forceinline__ uint32_t local_home(uint64_t h, uint32_t capb) {
-  return (uint32_t)(((uint64_t)(uint32_t)h * capb) >> 32);
+  return (uint32_t)((((uint64_t)((uint32_t)h >> 16)) * capb) >> 16);
 }
 __device__ __forceinline__ uint64_t side_slot(Geom g) { return (uint64_t)g.nb * g.capb; }
 

@@ -549,8 +549,10 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint32_t R_w = 0, R_g = 0;
   const uint32_t passes_w = plan(nb_w, R_w), passes_g = plan(nb_g, R_g);
   bool group = passes_g <= passes_w;
+  bool sorted = false;   // group buckets built by V_bucket_sort instead of the CAS build
   if (const char* e = std::getenv("KMHG_BUCKET")) {
     if (std::string(e) == "group") group = true;
+    if (std::string(e) == "sort") group = sorted = true;
     if (std::string(e) == "wave") group = false;
   }
   const uint32_t nb = group ? nb_g : nb_w;
@@ -616,7 +618,11 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   HIPC(hipMemsetAsync(stamps, 0, sizeof(uint64_t) * 8 * nb, s));
   kmhg::set_stamp_buffer(stamps);
 #endif
-  if (group)
+  if (sorted)
+    LAUNCH("k_v2_bucket_sort", s,
+           launch_v2_bucket_sort(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
+                                 meta, s));
+  else if (group)
     LAUNCH("k_v2_bucket_wg", s,
            launch_v2_bucket_wg(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
                                meta, s));

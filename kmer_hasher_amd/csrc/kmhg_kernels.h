@@ -137,6 +137,9 @@ struct BucketStats {           // per-bucket partials of the build statistics
 void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                       Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                       hipStream_t s);
+void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint32_t* start,
+                           Geom g, Slot* T, int32_t* positions, BucketStats* bstats,
+                           BuildMeta* meta, hipStream_t s);
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          hipStream_t s);

@@ -286,10 +286,15 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   const int o0 = (int)(t_start - base);
   stage_tile(seq, L, base, st, aligned != 0);
   __syncthreads();
-  // (measured: issuing all WPT home-slot loads before resolving any cost occupancy -- 94
-  // VGPRs, 5 waves/SIMD -- and ran 15 % slower than this two-deep loop)
   uint64_t rows = 0;
-#pragma unroll 2
+  // (measured: issuing all WPT home-slot loads before resolving any cost occupancy -- 94
+  // VGPRs, 5 waves/SIMD -- and ran 15 % slower than this two-deep loop; a per-lane state
+  // machine walking two probe streams one slot per step ran 30 % slower, and compacting the
+  // windows not resolved at their home slot into LDS queue rounds 40 % slower)
+#ifndef KMHG_PROBE_UNROLL
+#define KMHG_PROBE_UNROLL 2
+#endif
+#pragma unroll KMHG_PROBE_UNROLL
   for (int j = 0; j < WPT; ++j) {
     const int w = j * BLOCK + threadIdx.x;
     const int64_t s = t_start + w;

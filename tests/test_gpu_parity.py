@@ -195,7 +195,7 @@ def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
         ptr.free()
 
 
-@pytest.mark.parametrize("bucket", ["wave", "group"])
+@pytest.mark.parametrize("bucket", ["wave", "group", "sort"])
 def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     """Both bucket kernels on every size class: one wave per 256-window bucket, and one
     workgroup per 1024-window bucket (chosen automatically when it saves a radix pass, e.g. at

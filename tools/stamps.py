@@ -26,9 +26,11 @@ os.environ["KMHG_STAMP_FILE"] = f
 D.DeviceIndex.build(seq, k).free()
 a = np.fromfile(f, np.uint64).reshape(-1, 8).astype(np.int64)
 a = a[a[:, 0] > 0]
-wg = os.environ.get("KMHG_BUCKET", "group") != "wave"
-names = (["clear", "passA(+load)", "scan", "passB", "table"] if wg else
-         ["init+start", "loads", "passA", "scan", "passB", "table"])
+mode = os.environ.get("KMHG_BUCKET", "group")
+wg = mode == "group"
+names = {"group": ["clear", "passA(+load)", "scan", "passB", "table"],
+         "sort": ["load", "sort pass 0", "sort pass 1", "runs", "place", "empties+stats"],
+         "wave": ["init+start", "loads", "passA", "scan", "passB", "table"]}[mode]
 last = len(names)
 t0 = a[:, 0].min()
 print(f"buckets {len(a)}  kernel span {a[:, last].max() - t0} ticks")
@@ -37,5 +39,8 @@ for i, n in enumerate(names):
     print(f"{n:12s} mean {d.mean():9.0f}  median {np.median(d):9.0f}  p99 {np.percentile(d, 99):9.0f}")
 life = a[:, last] - a[:, 0]
 print(f"{'lifetime':12s} mean {life.mean():9.0f}  median {np.median(life):9.0f}")
+if wg:   # stamp 6: after wave 0's loads landed (drained right after stamp 1)
+    d = a[:, 6] - a[:, 1]
+    print(f"{'load wait':12s} mean {d.mean():9.0f}  median {np.median(d):9.0f}  (inside passA)")
 st = np.sort(a[:, 0] - t0)
 print("start ticks quantiles", [int(x) for x in np.percentile(st, [0, 10, 50, 90, 100])])
