@@ -77,7 +77,7 @@ typedef struct {
   int64_t table_slots;   /* hash-table capacity */
   int64_t device_bytes;  /* device memory held by the index */
   int32_t sources;       /* counts index (count.kmers): source_n; 0 for a position index */
-  int32_t reserved;
+  int32_t kind;          /* 0 position index, 1 counts index, 2 suffix hash (canonical counts) */
   int64_t kmer_count;    /* khash_ptr.kmer_count: distinct k-mers added (both kinds) */
 } kmhg_info;
 
@@ -169,6 +169,66 @@ int kmhg_count(kmhg_index **idx, const char *const *seqs, const size_t *lens, in
 /* One device-resident sequence on `stream` (synchronous). */
 int kmhg_count_device(kmhg_index **idx, const void *d_seq, size_t L, int k, int source,
                       int source_n, void *stream);
+
+/* ---- read counting: the suffix_hash_n path (SURVEY.md §8 f next-4, depth half) -------------
+ * A suffix hash is a counts index of CANONICAL k-mers (min of forward and reverse complement,
+ * info.kind = 2, info.sources = counts_n), the reference's suffix_hash_n (src/suffix_hash.c).
+ *
+ * count.kmers.fq.sh.rp <- .Call("count_kmers_fastq_sh_rp", hash.ptr, params, fq.file)
+ *                                                       src/kmer_hash.c:810-857
+ *        (+ init_kmer_reader_pool(_sh) / kmer_reader_read src/kmer_reader.c:41-147, the k-mer
+ *         iterator src/kmer_util.c:64-162, sh_n_add_kmer src/suffix_hash.c:179-285)
+ * params = (k, prefix_bits, min_q, thread_n, max_reads, max_mem, source_n, source).  Reads the
+ * FASTA/FASTQ file (plain or gzip) as the reference's kseq does, the first max_reads records
+ * (negative: all), skips records of length <= k, and adds one to entry `source` of every
+ * canonical k-mer the quality iterator accepts (threshold q_to_ll['!' + min_q]; FASTA records
+ * only break at N).  *sh == NULL makes a new suffix hash of source_n counts; into an existing one
+ * a different k or a source >= its counts_n prints the reference's message and counts nothing.
+ * prefix_bits, thread_n and max_mem do not change the counts.  Errors (reference order and
+ * words): "k must be a positive integer less than 1+MAX_K", "Source_n must be in the range
+ * 1 - 4", "source_i must be less than source_n"; deviations on the reference's undefined paths:
+ * k = 32 and (k < 16, prefix_bits > 2k) are refused. */
+int kmhg_sh_count_fastq(kmhg_index **sh, const char *path, const int32_t params[8]);
+
+/* The host reader alone (kseq semantics): records up to max_reads, those longer than k kept,
+ * packed as bases / qualities (0 for FASTA records) / offsets[n+1] / has_qual[n]. */
+typedef struct kmhg_reads kmhg_reads;
+int kmhg_fastx_read(const char *path, int64_t max_reads, int k, kmhg_reads **out);
+int kmhg_reads_info(const kmhg_reads *r, int64_t *n_records, int64_t *n_reads, int64_t *n_bases);
+int kmhg_reads_copy(const kmhg_reads *r, uint8_t *seq, uint8_t *qual, int64_t *offsets,
+                    uint8_t *has_qual);
+int kmhg_reads_free(kmhg_reads *r);
+/* Count reads already read (same params as kmhg_sh_count_fastq; max_reads is not applied). */
+int kmhg_sh_count_reads(kmhg_index **sh, const kmhg_reads *r, const int32_t params[8]);
+/* Device-resident packed reads on `stream`: d_seq / d_qual 8-byte aligned with >= 8 readable
+ * bytes past the last read, d_offsets[n_reads + 1] (int64), d_has_qual[n_reads]. */
+int kmhg_sh_count_reads_device(kmhg_index **sh, const void *d_seq, const void *d_qual,
+                               const int64_t *d_offsets, const uint8_t *d_has_qual,
+                               int64_t n_reads, const int32_t params[8], void *stream);
+
+/* seq.kmer.depth.sh <- .Call("seq_kmer_depth_sh", hash.ptr, seq, k)  src/kmer_hash.c:859-879
+ *        (+ seq_kmer_counts src/kmer_reader.c:155-193)
+ * counts = counts_n x L int32 (R column-major): the counts of the canonical k-mer the reference's
+ * walk writes at each position (its write lands at window start - 1 in normal flow, at the start
+ * for an init window; see kmhg_sh.hip), zeros for k-mers absent from the hash, INT_MIN (NA)
+ * where nothing is written.  Errors: "unable to obtain suffix_hash_n from external pointer",
+ * "Receieved error from seq_kmer_counts" (k differs from the hash's); L < k writes nothing at
+ * L - k (the reference writes before its buffer). */
+int kmhg_sh_depth(kmhg_index *sh, const char *seq, size_t L, int k, int32_t *counts);
+int kmhg_sh_depth_device(kmhg_index *sh, const void *d_seq, size_t L, int k, int32_t *d_counts,
+                         void *stream);
+
+/* kmer.spec.sh.n <- .Call("kmer_spectrum_suffix_hash_n", ptr, max.count, comb, comb.inner,
+ *                          source.min)          src/kmer_hash.c:1010-1039
+ *        (+ sh_count_spectrum_nc src/suffix_hash.c:338-421)
+ * counts = (comb_n * counts_n) x (max_count + 1) doubles (R column-major).  *status = 1, or the
+ * reference's code -3 (comb_inner not 0/1) / -4 (comb >= 2^counts_n) with all counts zero. */
+int kmhg_sh_spectrum(kmhg_index *sh, int max_count, const int32_t *comb,
+                     const int32_t *comb_inner, int comb_n, const int32_t *source_min,
+                     int n_source_min, double *counts, int *status);
+
+/* Rows of a counts index or suffix hash: keys[U] and counts[U * sources] in row order. */
+int kmhg_counts_export(kmhg_index *idx, uint64_t *keys, int32_t *counts);
 
 /* Index replication for the multi-GPU query (the index is broadcast once over RCCL/xGMI by the
  * caller): the device image is the hash table (16-B slots {key, count, end}) + the positions;

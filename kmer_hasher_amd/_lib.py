@@ -29,7 +29,7 @@ class Info(C.Structure):
     _fields_ = [("k", C.c_int32), ("device", C.c_int32), ("seq_len", C.c_int64),
                 ("n_kmers", C.c_int64), ("n_positions", C.c_int64), ("n_pairs", C.c_int64),
                 ("max_count", C.c_int64), ("table_slots", C.c_int64), ("device_bytes", C.c_int64),
-                ("sources", C.c_int32), ("reserved", C.c_int32), ("kmer_count", C.c_int64)]
+                ("sources", C.c_int32), ("kind", C.c_int32), ("kmer_count", C.c_int64)]
 
 
 class ImageSizes(C.Structure):
@@ -68,6 +68,18 @@ _PROTOS = {
                              C.c_int64, C.c_int, C.c_int, C.c_int]),
     "kmhg_count_device": (C.c_int, [C.POINTER(vp), vp, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                     vp]),
+    "kmhg_sh_count_fastq": (C.c_int, [C.POINTER(vp), C.c_char_p, vp]),
+    "kmhg_fastx_read": (C.c_int, [C.c_char_p, C.c_int64, C.c_int, C.POINTER(vp)]),
+    "kmhg_reads_info": (C.c_int, [vp, i64p, i64p, i64p]),
+    "kmhg_reads_copy": (C.c_int, [vp, vp, vp, vp, vp]),
+    "kmhg_reads_free": (C.c_int, [vp]),
+    "kmhg_sh_count_reads": (C.c_int, [C.POINTER(vp), vp, vp]),
+    "kmhg_sh_count_reads_device": (C.c_int, [C.POINTER(vp), vp, vp, vp, vp, C.c_int64, vp, vp]),
+    "kmhg_sh_depth": (C.c_int, [vp, C.c_char_p, C.c_size_t, C.c_int, vp]),
+    "kmhg_sh_depth_device": (C.c_int, [vp, vp, C.c_size_t, C.c_int, vp, vp]),
+    "kmhg_sh_spectrum": (C.c_int, [vp, C.c_int, vp, vp, C.c_int, vp, C.c_int, vp,
+                                   C.POINTER(C.c_int)]),
+    "kmhg_counts_export": (C.c_int, [vp, vp, vp]),
     "kmhg_image_sizes_get": (C.c_int, [vp, C.POINTER(ImageSizes), i64p]),
     "kmhg_image_export": (C.c_int, [vp, vp, vp, vp]),
     "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, C.POINTER(vp)]),

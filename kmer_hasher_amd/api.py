@@ -5,6 +5,10 @@
     seq_kmer_pos(ex_ptr, seq, k)           <- seq.kmer.pos    (kmer_hash.R:23-28)
     kmer_pairs(ptr_a, ptr_b)               <- kmer.pairs      (kmer_hash.R:30-34), fixed
     count_kmers(seq, params, hash_ptr)     <- count.kmers     (kmer_hash.R:43-46)
+    count_kmers_fq_sh_rp(fq, params, ptr)  <- count.kmers.fq.sh.rp (kmer_hash.R:75-78)
+    seq_kmer_depth_sh(ptr, seq, k)         <- seq.kmer.depth.sh    (kmer_hash.R:80-83)
+    kmer_spec_sh_n(ptr, max_count, comb, comb_inner, source_min)
+                                           <- kmer.spec.sh.n       (kmer_hash.R:93-96)
     set_row_order(ex_ptr, "khash")         kmer.pos rows in the reference's khash order (opt-in)
 
 Same argument meaning, same validation order and the reference's own error messages (raised as
@@ -28,6 +32,7 @@ import numpy as np
 from . import _lib
 
 KMER_HASH_TAG = "kmer_hash_250930"
+SUFFIX_HASH_N_TAG = "suffix_hash_n_250930"          # src/kmer_hash.c:25
 OPT_KMER, OPT_POS, OPT_PAIRS, OPT_COUNT = 1, 2, 4, 8
 FIELDS = ("kmer", "pos", "pair.pos", "count")          # src/kmer_hash.c:18
 INT_MAX = 2**31 - 1
@@ -262,3 +267,127 @@ def count_kmers(seq, params, hash_ptr=None) -> ExtPtr:
     if hash_ptr is not None:
         return hash_ptr
     return ExtPtr(h.value)
+
+
+# ------------------------------------------------------------------ read counting (suffix hash)
+def _int_vec(x, n: int | None, what: str) -> list[int]:
+    if isinstance(x, (int, np.integer)):
+        x = [x]
+    try:
+        v = [int(a) for a in x]
+    except (TypeError, ValueError):
+        raise KmerHashError(what) from None
+    if n is not None and len(v) != n:
+        raise KmerHashError(what)
+    return v
+
+
+def _extract_sh(ptr):
+    # extract_ext_ptr(hash_ptr_r, suffix_hash_n_tag): NULL for anything else (src/kmer_hash.c:41-52)
+    if isinstance(ptr, ExtPtr) and ptr.tag == SUFFIX_HASH_N_TAG and ptr._h:
+        return ptr
+    return None
+
+
+def count_kmers_fq_sh_rp(fq_file, params, hash_ptr=None) -> ExtPtr:
+    """count.kmers.fq.sh.rp -> .Call("count_kmers_fastq_sh_rp", hash.ptr, params, fq.file)
+    (src/kmer_hash.c:810-857; reader src/kmer_reader.c:41-147).
+
+    params = (k, prefix_bits, min_q, thread_n, max_reads, max_mem, source_n, source).  Counts the
+    canonical k-mers of the FASTA/FASTQ file (plain or gzip) the reference's quality iterator
+    accepts into entry `source` of a suffix hash of source_n counts.  A hash_ptr that is not a
+    suffix hash is ignored and a new one returned, as extract_ext_ptr yields NULL for it."""
+    if isinstance(fq_file, (list, tuple)):
+        if len(fq_file) != 1:
+            raise KmerHashError("fq_file should be a character vector of length at least one")
+        fq_file = fq_file[0]
+    if not isinstance(fq_file, (str, bytes)):
+        raise KmerHashError("fq_file should be a character vector of length at least one")
+    prm = _int_vec(params, 8, "k_r must be an integer vector of length 6 (k, prefix_bits, min_q, "
+                              "thread_n, max_reads, max_mem, source_n, source")
+    sh = _extract_sh(hash_ptr)
+    h = C.c_void_p(sh._h.value if sh is not None else None)
+    arr = (C.c_int32 * 8)(*[((x + 2**31) % 2**32) - 2**31 for x in prm])
+    path = fq_file.encode() if isinstance(fq_file, str) else fq_file
+    L = _lib.lib()
+    rc = L.kmhg_sh_count_fastq(C.byref(h), path, arr)
+    if rc == _lib.KMHG_EINVAL:
+        raise KmerHashError(L.kmhg_last_error().decode())
+    _lib.check(rc)
+    if sh is not None:
+        return sh
+    return ExtPtr(h.value, tag=SUFFIX_HASH_N_TAG)
+
+
+def seq_kmer_depth_sh(hash_ptr, seq, k) -> np.ndarray:
+    """seq.kmer.depth.sh -> .Call("seq_kmer_depth_sh", hash.ptr, seq, k)
+    (src/kmer_hash.c:859-879, seq_kmer_counts src/kmer_reader.c:155-193).
+
+    Returns the (counts_n, L) int32 matrix R gets (no t() in the wrapper); NA is INT_MIN."""
+    sh = _extract_sh(hash_ptr)
+    if sh is None:
+        raise KmerHashError("unable to obtain suffix_hash_n from external pointer")
+    if isinstance(k, (list, tuple, np.ndarray)) and len(k) != 1:
+        raise KmerHashError("k_r should be a single integer")
+    kk = _as_int(k, "k_r should be a single integer")
+    if isinstance(seq, (list, tuple)) and len(seq) != 1:
+        raise KmerHashError("seq_r should be a character vector of length 1")
+    b = _as_seq_bytes(seq, "seq_r should be a character vector of length 1")
+    S = sh.info().sources
+    out = np.empty(max(len(b) * S, 1), np.int32)
+    L = _lib.lib()
+    rc = L.kmhg_sh_depth(sh.handle, b, len(b), kk, out.ctypes.data)
+    if rc == _lib.KMHG_EINVAL:
+        raise KmerHashError(L.kmhg_last_error().decode())
+    _lib.check(rc)
+    return out[:len(b) * S].reshape(len(b), S).T
+
+
+def kmer_spec_sh_n(hash_ptr, max_count, comb, comb_inner, source_min) -> np.ndarray:
+    """kmer.spec.sh.n -> .Call("kmer_spectrum_suffix_hash_n", ...)  (src/kmer_hash.c:1010-1039,
+    sh_count_spectrum_nc src/suffix_hash.c:338-421).
+
+    Returns the (comb_n * counts_n, max_count + 1) float64 matrix; an invalid comb / comb_inner
+    gives zeros and the reference's message, as its Rprintf branch does."""
+    sh = _extract_sh(hash_ptr)
+    if sh is None:
+        raise KmerHashError("unable to obtain suffix_hash_n from external pointer")
+    mc = _int_vec(max_count, 1, "max_count_r should be a single integer")[0]
+    cb = _int_vec(comb, None, "comb_r should be an integer vector of length > 0")
+    if len(cb) < 1:
+        raise KmerHashError("comb_r should be an integer vector of length > 0")
+    ci = _int_vec(comb_inner, None,
+                  "comb_inner_r should be an integer vector of the same length as comb_r")
+    if len(ci) != len(cb):
+        raise KmerHashError("comb_inner_r should be an integer vector of the same length as comb_r")
+    S = sh.info().sources
+    sm = _int_vec(source_min, None,
+                  "source_min_r should be an integer vector of length sh->counts_n")
+    if len(sm) != S:
+        raise KmerHashError("source_min_r should be an integer vector of length sh->counts_n")
+    a32 = lambda v: np.array([((x + 2**31) % 2**32) - 2**31 for x in v], np.int32)  # noqa: E731
+    cb_a, ci_a, sm_a = a32(cb), a32(ci), a32(sm)
+    if mc < 0:
+        raise KmerHashError("max_count must be >= 0")
+    out = np.zeros(max((mc + 1) * len(cb) * S, 1), np.float64)
+    st = C.c_int(0)
+    L = _lib.lib()
+    rc = L.kmhg_sh_spectrum(sh.handle, mc, cb_a.ctypes.data, ci_a.ctypes.data, len(cb),
+                            sm_a.ctypes.data, len(sm), out.ctypes.data, C.byref(st))
+    if rc == _lib.KMHG_EINVAL:
+        raise KmerHashError(L.kmhg_last_error().decode())
+    _lib.check(rc)
+    if st.value != 1:
+        warnings.warn(f"sh_count_spectrum_nc returned an error: {st.value}")
+    return out[:(mc + 1) * len(cb) * S].reshape(mc + 1, len(cb) * S).T
+
+
+def counts_table(ptr):
+    """(keys, counts) rows of a counts pointer or suffix hash (tests and inspection)."""
+    if not isinstance(ptr, ExtPtr):
+        raise KmerHashError("ptr_r should be an external pointer")
+    inf = ptr.info()
+    keys = np.zeros(max(inf.n_kmers, 1), np.uint64)
+    M = np.zeros(max(inf.n_kmers * inf.sources, 1), np.int32)
+    _lib.check(_lib.lib().kmhg_counts_export(ptr.handle, keys.ctypes.data, M.ctypes.data))
+    return keys[:inf.n_kmers], M[:inf.n_kmers * inf.sources].reshape(inf.n_kmers, inf.sources)

@@ -7,6 +7,8 @@
 // A count.kmers call is one partitioned build of the batch (the distinct keys with their
 // occurrence counts, in first-occurrence order = the readout permutation) merged into the
 // counts index:
+// perm_b = nullptr walks the batch table's slots instead (order-free merges: the read counts of
+// kmhg_sh.hip), empty slots contributing nothing.
 //   C_probe   batch key r -> one probe of the counts table; a known key adds its count to its
 //             row (distinct keys own distinct rows: a plain read-modify-write), a new key
 //             raises its flag
@@ -34,7 +36,8 @@ k_count_probe(const uint32_t* __restrict__ perm_b, uint32_t Ub, const Slot* __re
               uint32_t S, uint32_t source, int32_t* __restrict__ M, uint32_t* __restrict__ newf) {
   const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
   if (r >= Ub) return;
-  const uint4 v = *reinterpret_cast<const uint4*>(&Tb[perm_b[r]]);
+  const uint4 v = *reinterpret_cast<const uint4*>(&Tb[perm_b ? perm_b[r] : r]);
+  if (!perm_b && !v.z) { newf[r] = 0; return; }        // slot walk: an empty slot adds nothing
   const uint64_t key = ((uint64_t)v.y << 32) | v.x;
   uint32_t f = 1;
   if (Tc) {
@@ -57,8 +60,8 @@ k_count_append(const uint32_t* __restrict__ perm_b, uint32_t Ub, const Slot* __r
   if (r >= Ub) return;
   const uint32_t o = rank[r];
   const uint32_t nx = r + 1 < Ub ? rank[r + 1] : *n_new;
-  if (nx == o) return;                                  // known key
-  const uint4 v = *reinterpret_cast<const uint4*>(&Tb[perm_b[r]]);
+  if (nx == o) return;                                  // known key (or an empty slot)
+  const uint4 v = *reinterpret_cast<const uint4*>(&Tb[perm_b ? perm_b[r] : r]);
   const uint64_t row = (uint64_t)U0 + o;
   ckeys[row] = ((uint64_t)v.y << 32) | v.x;
   for (uint32_t j = 0; j < S; ++j) M[row * S + j] = j == source ? (int32_t)v.z : 0;

@@ -8,10 +8,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -20,6 +22,8 @@
 
 #include "kmhg_common.h"
 #include "kmhg_kernels.h"
+#include "kmhg_fastx.h"
+#include "kmhg_sh.h"
 #include "../../include/kmhgpu.h"
 
 using namespace kmhg;
@@ -401,6 +405,7 @@ struct kmhg_index {
   // U x sources count matrix (row-major, rows in first-insertion order, rows_cap allocated),
   // `ckeys` the keys of the rows, slot_row / row_slot the table <-> row maps.
   uint32_t sources = 0;
+  bool canonical = false;         // suffix hash (count.kmers.fq.sh.rp): canonical k-mer counts
   uint64_t rows_cap = 0, kmer_count = 0;
   DBuf<uint64_t> ckeys;
   DBuf<uint32_t> slot_row, row_slot;
@@ -688,6 +693,7 @@ void finish_build(kmhg_index* idx) {
 // end, so shards of consecutive window ranges concatenate to the unsharded result.
 kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int kq, int64_t w0,
                          int64_t w1, hipStream_t s) {
+  if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
   finish_build(idx);
   auto q = std::make_unique<kmhg_query>();
   q->device = idx->device;
@@ -731,6 +737,7 @@ void prepare_readout(kmhg_index* idx, hipStream_t s);
 // Rows (a, b) for the k-mers both indices hold, a's k-mers in a's kmer.pos row order
 // (kmhg_join.hip).  Same two-phase shape as the query: probe + tile totals, one read-back, emit.
 kmhg_query* pairs_device(kmhg_index* a, kmhg_index* b, hipStream_t s) {
+  if (a->canonical || b->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
   finish_build(a);
   finish_build(b);
   if (a->k != b->k) fail(KMHG_EINVAL, "the two indices must have the same k");
@@ -766,22 +773,37 @@ void prepare_canon(kmhg_index* idx, hipStream_t s);
 // One count.kmers batch (a device-resident sequence) merged into the counts index `idx`
 // (kmhg_count.hip): partitioned build of the batch -> its distinct keys in first-occurrence
 // order -> probe / append into the count matrix -> table rebuilt for the grown key list.
+struct Release {                   // a batch index dies in stream order
+  kmhg_index* b; hipStream_t s;
+  ~Release() { b->bind_all(s); }
+};
+
+void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_t n_items,
+                 uint32_t source, hipStream_t s);
+
 void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t source,
                   hipStream_t s) {
   idx->stream = s;
   const int k = idx->k;
-  const uint32_t S = idx->sources;
   if (L <= k) return;
   std::unique_ptr<kmhg_index> B(build_device(d_seq, L, k, s));
-  struct Release {                 // the batch index dies in stream order
-    kmhg_index* b; hipStream_t s;
-    ~Release() { b->bind_all(s); }
-  } rel{B.get(), s};
+  Release rel{B.get(), s};
   finish_build(B.get());
   B->stream = s;
-  const uint64_t Ub = B->U;
-  if (!Ub) return;
+  if (!B->U) return;
   prepare_canon(B.get(), s);       // batch keys in first-occurrence order
+  merge_batch(idx, B.get(), B->canon.perm.p, B->U, source, s);
+  idx->L += L;
+}
+
+// Merge a batch index B (distinct keys with their counts in the slots) into the counts index:
+// items r < n_items are B's slots perm_b[r] (or slot r itself when perm_b is null: order-free,
+// empty slots skipped).  New keys get rows in item order.
+void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_t n_items,
+                 uint32_t source, hipStream_t s) {
+  const int k = idx->k;
+  const uint32_t S = idx->sources;
+  const uint64_t Ub = B->U;
   const uint64_t U0 = idx->U;
   const uint64_t need = U0 + Ub;
   if (need * S > (uint64_t)INT32_MAX)
@@ -800,20 +822,20 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
     idx->positions.swap_with(nm);
     idx->rows_cap = cap;
   }
-  const uint32_t nt = tiles_for(Ub);
-  DBuf<uint32_t> rank(Ub + 1, s);                 // flags -> ranks of the new keys; [Ub] = total
+  const uint64_t ni = n_items;
+  const uint32_t nt = tiles_for(ni);
+  DBuf<uint32_t> rank(ni + 1, s);                 // flags -> ranks of the new keys; [ni] = total
   DBuf<uint64_t> status((size_t)nt + 1, s);
   HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
-  const uint32_t* perm_b = B->canon.perm.p;
   LAUNCH("k_count_probe", s,
-         launch_count_probe(perm_b, (uint32_t)Ub, B->table.p, U0 ? idx->table.p : nullptr,
+         launch_count_probe(perm_b, (uint32_t)ni, B->table.p, U0 ? idx->table.p : nullptr,
                             idx->geom, idx->slot_row.p, S, source, idx->positions.p, rank.p, s));
-  LAUNCH("k_scan_u32", s, launch_scan_u32(rank.p, Ub, status.p, rank.p + Ub, s));
+  LAUNCH("k_scan_u32", s, launch_scan_u32(rank.p, ni, status.p, rank.p + ni, s));
   LAUNCH("k_count_append", s,
-         launch_count_append(perm_b, (uint32_t)Ub, B->table.p, rank.p, rank.p + Ub,
+         launch_count_append(perm_b, (uint32_t)ni, B->table.p, rank.p, rank.p + ni,
                              (uint32_t)U0, S, source, idx->ckeys.p, idx->positions.p, s));
   uint32_t n_new = 0;
-  HIPC(hipMemcpyAsync(&n_new, rank.p + Ub, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipMemcpyAsync(&n_new, rank.p + ni, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   const uint64_t U1 = U0 + n_new;
   // rebuild the table for U1 keys (aux of a source_n = 1 index carries the count itself, so
@@ -834,7 +856,7 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
     K->rec = PinnedRec{};
     K->pending = false;
   }
-  Release relk{K ? K.get() : B.get(), s};
+  Release relk{K ? K.get() : B, s};
   idx->row_slot.reset(U1);
   if (!ovf) {
     idx->geom = K->geom;
@@ -855,9 +877,198 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
   idx->N = U1 * S;
   idx->P = U1 * ((uint64_t)S * (S - 1) / 2);
   idx->max_n = U1 ? S : 0;
-  idx->L += L;
   idx->kmer_count += n_new;
   idx->canon.ready = false;
+}
+
+// ---------------------------------------------------------------------------- read counting
+// count.kmers.fq.sh.rp / seq.kmer.depth.sh / kmer.spec.sh.n (kmhg_sh.hip).  The suffix_hash_n
+// of the reference is a counts index of canonical k-mers (canonical = true, sources = counts_n).
+
+// q_to_ll (src/Q_to_log_likelihood.h): -708 below '"', else log(1 - 10^(-(q-33)/10)) printed
+// to 15 significant digits -- exactly the doubles the reference's table holds (checked against
+// it by tests/golden/make_sh_golden.py), uploaded once per device.
+const double* qll_device(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<int, double*> tables;
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(mu);
+  auto it = tables.find(dev);
+  if (it != tables.end()) return it->second;
+  double h[256];
+  for (int q = 0; q < 256; ++q) {
+    if (q < 34) { h[q] = -708.0; continue; }
+    char buf[64];
+    snprintf(buf, sizeof buf, "%.15g", std::log(1.0 - std::pow(10.0, -(double)(q - 33) / 10.0)));
+    h[q] = std::strtod(buf, nullptr);
+  }
+  double* d = static_cast<double*>(DevicePool::get().alloc(sizeof h));
+  HIPC(hipMemcpyAsync(d, h, sizeof h, hipMemcpyHostToDevice, s));
+  HIPC(hipStreamSynchronize(s));
+  tables[dev] = d;
+  return d;
+}
+
+double qll_host(int q) {   // the same table on the host (the iterator's threshold)
+  if (q < 34) return -708.0;
+  char buf[64];
+  snprintf(buf, sizeof buf, "%.15g", std::log(1.0 - std::pow(10.0, -(double)(q - 33) / 10.0)));
+  return std::strtod(buf, nullptr);
+}
+
+kmhg_index* new_sh_index(int k, int counts_n, hipStream_t s) {
+  auto idx = std::make_unique<kmhg_index>();
+  HIPC(hipGetDevice(&idx->device));
+  idx->k = k;
+  idx->sources = (uint32_t)counts_n;
+  idx->canonical = true;
+  idx->stream = s;
+  idx->geom = Geom{1u, 8u};                      // an empty table: lookups before any count
+  idx->table.reset(idx->slots());
+  LAUNCH("k_table_init", s, launch_table_init(idx->table.p, idx->slots(), s));
+  return idx.release();
+}
+
+// One batch of packed reads (device-resident) merged into the suffix hash: R_kmers count ->
+// scan -> R_kmers emit -> partitioned build of the key stream (occurrence counts per distinct
+// key) -> merge over the batch table's slots.
+void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t* d_qual,
+                           const int64_t* d_off, const uint8_t* d_hasq, uint32_t n_reads,
+                           double min_ll, uint32_t source, hipStream_t s) {
+  idx->stream = s;
+  if (!n_reads) return;
+  const int k = idx->k;
+  const double* qll = qll_device(s);
+  DBuf<uint32_t> cnt((size_t)n_reads + 1, s);
+  const uint32_t nt = tiles_for(n_reads);
+  DBuf<uint64_t> status((size_t)nt + 1, s);
+  HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
+  LAUNCH("k_read_kmers_count", s,
+         launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cnt.p, nullptr,
+                           false, s));
+  LAUNCH("k_scan_u32", s, launch_scan_u32(cnt.p, n_reads, status.p, cnt.p + n_reads, s));
+  uint32_t total = 0;
+  HIPC(hipMemcpyAsync(&total, cnt.p + n_reads, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  if (!total) return;
+  DBuf<uint64_t> keys(total, s);
+  LAUNCH("k_read_kmers_emit", s,
+         launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cnt.p, keys.p,
+                           true, s));
+  std::unique_ptr<kmhg_index> B(build_device_v2(nullptr, 0, k, s, keys.p, (int64_t)total));
+  Release rel{B.get(), s};
+  HIPC(hipEventSynchronize(B->rec.ev));
+  const BuildMeta hm = *B->rec.meta;
+  PinnedPool::get().give(B->rec, false);
+  B->rec = PinnedRec{};
+  B->pending = false;
+  B->stream = s;
+  if (hm.overflow) {                             // never observed: global find-or-insert
+    B->geom = Geom{1u, (uint32_t)table_capacity((int64_t)total)};
+    B->table.reset(B->slots());
+    LAUNCH("k_table_init", s, launch_table_init(B->table.p, B->slots(), s));
+    LAUNCH("k_key_count_insert", s,
+           launch_key_count_insert(keys.p, total, B->table.p, B->geom, s));
+    B->U = total;                                // an upper bound (row capacity only)
+  } else {
+    B->U = hm.n_kmers;
+  }
+  merge_batch(idx, B.get(), nullptr, B->slots(), source, s);
+}
+
+// Host reads packed for the GPU: bases and qualities concatenated, read r = [off[r], off[r+1]).
+struct ReadsHost {
+  std::vector<uint8_t> seq, qual, hasq;
+  std::vector<int64_t> off{0};
+  int64_t records = 0;                           // records consumed, short ones included
+  void clear() { seq.clear(); qual.clear(); hasq.clear(); off.assign(1, 0); }
+  void add(const std::string& sq, const std::string& ql, bool hq) {
+    seq.insert(seq.end(), sq.begin(), sq.end());
+    if (hq) qual.insert(qual.end(), ql.begin(), ql.end());
+    else qual.resize(seq.size(), 0);
+    hasq.push_back(hq ? 1 : 0);
+    off.push_back((int64_t)seq.size());
+  }
+  size_t n() const { return hasq.size(); }
+};
+
+void sh_count_reads_host(kmhg_index* idx, const ReadsHost& r, double min_ll, uint32_t source,
+                         hipStream_t s) {
+  const size_t n = r.n();
+  if (!n) return;
+  if (n >= (size_t)UINT32_MAX) fail(KMHG_EOVERFLOW, "more than 2^32-1 reads in one batch");
+  const size_t nb = r.seq.size();
+  DBuf<uint8_t> dseq(nb + 16, s), dqual(nb + 16, s), dhq(n, s);
+  DBuf<int64_t> doff(n + 1, s);
+  HIPC(hipMemcpyAsync(dseq.p, r.seq.data(), nb, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(dqual.p, r.qual.data(), nb, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(dhq.p, r.hasq.data(), n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(doff.p, r.off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+  sh_count_reads_device(idx, dseq.p, dqual.p, doff.p, dhq.p, (uint32_t)n, min_ll, source, s);
+  HIPC(hipStreamSynchronize(s));                 // the host arrays are reused
+}
+
+// kmer_reader_read's loop (src/kmer_reader.c:51-73): records up to max_reads, those longer
+// than k kept, qualities used when the record has them.  Batches of SH_BATCH bases.
+constexpr size_t SH_BATCH = (size_t)256 << 20;
+
+int64_t read_fastx(const char* path, uint64_t max_reads, int k, ReadsHost& r,
+                   const std::function<void(ReadsHost&)>& flush) {
+  FastxReader rd(path);
+  if (!rd.ok()) {   // gzopen failed: the reference's reader then reads nothing
+    fprintf(stderr, "kmhg: unable to open %s: nothing counted\n", path);
+    return 0;
+  }
+  std::string sq, ql;
+  bool hq = false;
+  uint64_t read_n = 0;
+  int l;
+  while ((l = rd.read(sq, ql, hq)) >= 0 && read_n < max_reads) {
+    ++read_n;
+    ++r.records;
+    if (l <= k) continue;
+    r.add(sq, ql, hq);
+    if (r.seq.size() >= SH_BATCH && flush) { flush(r); r.clear(); }
+  }
+  return (int64_t)read_n;
+}
+
+void sh_depth_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k, int32_t* d_out,
+                     hipStream_t s) {
+  idx->stream = s;
+  const uint32_t S = idx->sources;
+  if (L > 0)
+    HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_out), (int)INT_MIN,
+                           (size_t)L * S, s));
+  if (L <= 0) return;
+  const uint32_t nt = depth_tiles(L);
+  DBuf<uint32_t> tcnt((size_t)nt + 1, s);
+  const uint32_t ntt = tiles_for(nt);
+  DBuf<uint64_t> status((size_t)ntt + 1, s);
+  HIPC(hipMemsetAsync(status.p, 0, ((size_t)ntt + 1) * 8, s));
+  LAUNCH("k_depth_seg_count", s, launch_depth_seg_count(d_seq, L, tcnt.p, s));
+  LAUNCH("k_scan_u32", s, launch_scan_u32(tcnt.p, nt, status.p, tcnt.p + nt, s));
+  uint32_t M = 0;
+  HIPC(hipMemcpyAsync(&M, tcnt.p + nt, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  DBuf<uint32_t> seg((size_t)2 * M + 2, s);
+  DBuf<uint8_t> stale((size_t)M + 1, s);
+  uint32_t* sstart = seg.p;
+  uint32_t* send = seg.p + M + 1;
+  if (M) LAUNCH("k_depth_seg_emit", s, launch_depth_seg_emit(d_seq, L, tcnt.p, sstart, send, s));
+  LAUNCH("k_depth_modes", s,
+         launch_depth_modes(d_seq, L, k, sstart, send, tcnt.p + nt, stale.p, idx->table.p,
+                            idx->geom, S, idx->positions.p, d_out, s));
+  if (M)
+    LAUNCH("k_depth_probe", s,
+           launch_depth_probe(d_seq, L, k, sstart, send, tcnt.p + nt, stale.p, idx->table.p,
+                              idx->geom, S, idx->positions.p, d_out, s));
+}
+
+void check_sh(const kmhg_index* idx) {
+  if (!idx || !idx->canonical)
+    fail(KMHG_EINVAL, "unable to obtain suffix_hash_n from external pointer");
 }
 
 // ---------------------------------------------------------------------------- readout
@@ -1033,6 +1244,7 @@ void prepare_readout(kmhg_index* idx, hipStream_t s) {
 
 void positions_sizes(kmhg_index* idx, uint32_t opt, int64_t* nk, int64_t* np, int64_t* npp,
                      int64_t* nc) {
+  if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
   if (nk) *nk = (opt & KMHG_OPT_KMER) ? (int64_t)idx->U : 0;
   if (np) *np = (opt & KMHG_OPT_POS) ? (int64_t)idx->N : 0;
   if (npp) *npp = (opt & KMHG_OPT_PAIRS) ? (int64_t)idx->P : 0;
@@ -1041,6 +1253,7 @@ void positions_sizes(kmhg_index* idx, uint32_t opt, int64_t* nk, int64_t* np, in
 
 void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, int32_t* pairs,
                       int32_t* counts, hipStream_t s) {
+  if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
   prepare_readout(idx, s);
   Canon& c = idx->canon;
   const uint32_t U = (uint32_t)idx->U;
@@ -1130,7 +1343,7 @@ void check_count_args(int64_t n_seqs, int k, int source, int source_n, kmhg_inde
   if (source_n < 1 || source >= source_n)
     fail(KMHG_EINVAL, "source_n must be larger than 1 and larger than source");
   if (!c) return;
-  if (!c->sources)
+  if (!c->sources || c->canonical)
     fail(KMHG_EINVAL, "count.kmers needs a counts pointer (one made by count.kmers)");
   if (c->k != k)
     fail(KMHG_EINVAL, "mismatch between specified k and that given in the external pointer");
@@ -1200,6 +1413,281 @@ int kmhg_count_device(kmhg_index** idx, const void* d_seq, size_t L, int k, int 
   });
 }
 
+// ---------------------------------------------------------------- suffix hash (read counting)
+// count_kmers_fastq_sh_rp (src/kmer_hash.c:810-857): argument checks in the reference's order
+// and with its texts; the remaining deviations are undefined-behaviour paths of the reference.
+static void check_sh_params(const int32_t* p) {
+  const int k = p[0];
+  const uint32_t source_n = (uint32_t)p[6], source_i = (uint32_t)p[7];
+  if (k < 1 || k > 32) fail(KMHG_EINVAL, "k must be a positive integer less than 1+MAX_K");
+  if (source_n > 4 || source_n < 1) fail(KMHG_EINVAL, "Source_n must be in the range 1 - 4");
+  if (source_i >= source_n) fail(KMHG_EINVAL, "source_i must be less than source_n");
+  // k = 32: the reference's (1 << 2k) - 1 masks shift by 64 (undefined); prefix_bits > 2k with
+  // k < 16 makes its suffix/prefix split underflow (src/kmer_reader.c:84-92)
+  if (k == 32) fail(KMHG_EINVAL, "k must be at most 31 for the suffix hash");
+  uint32_t pb = (uint32_t)p[1];
+  if (pb > 36) pb = 36;
+  if (2 * (uint32_t)k < 32 && pb > 2 * (uint32_t)k)
+    fail(KMHG_EINVAL, "prefix_bits must not exceed 2k");
+}
+
+struct kmhg_reads {
+  ReadsHost r;
+};
+
+// Into an existing suffix hash the reference checks k and source (src/kmer_reader.c:118-126):
+// a mismatch prints a message and counts nothing.
+static bool sh_accepts(const kmhg_index* sh, int k, uint32_t source) {
+  if ((int)sh->k != k) {
+    fprintf(stderr, "Incompatible arguments: k and total bit numbers do not add up\n");
+    return false;
+  }
+  if (source >= sh->sources) {
+    fprintf(stderr, "Value of source is too large\n");
+    return false;
+  }
+  return true;
+}
+
+int kmhg_sh_count_fastq(kmhg_index** sh, const char* path, const int32_t params[8]) {
+  return guarded([&] {
+    if (!sh || !path || !params) fail(KMHG_EINVAL, "null argument");
+    if (*sh) check_sh(*sh);
+    check_sh_params(params);
+    const int k = params[0];
+    const double min_ll = qll_host((unsigned char)('!' + (unsigned char)params[2]));
+    const uint64_t max_reads = (uint64_t)(int64_t)params[4];   // (size_t) of an int
+    const uint32_t source = (uint32_t)params[7];
+    hipStream_t s = lib_stream();
+    std::unique_ptr<kmhg_index> fresh;
+    kmhg_index* c = *sh;
+    if (!c) {
+      fresh.reset(new_sh_index(k, params[6], s));
+      c = fresh.get();
+    } else if (!sh_accepts(c, k, source)) {
+      return;
+    }
+    DeviceGuard g(c->device);
+    ReadsHost r;
+    read_fastx(path, max_reads, k, r, [&](ReadsHost& b) {
+      sh_count_reads_host(c, b, min_ll, source, s);
+      c->L += (int64_t)b.seq.size();
+    });
+    sh_count_reads_host(c, r, min_ll, source, s);
+    c->L += (int64_t)r.seq.size();
+    if (fresh) *sh = fresh.release();
+  });
+}
+
+int kmhg_fastx_read(const char* path, int64_t max_reads, int k, kmhg_reads** out) {
+  return guarded([&] {
+    if (!path || !out) fail(KMHG_EINVAL, "null argument");
+    auto r = std::make_unique<kmhg_reads>();
+    read_fastx(path, (uint64_t)max_reads, k, r->r, nullptr);
+    *out = r.release();
+  });
+}
+
+int kmhg_reads_info(const kmhg_reads* r, int64_t* n_records, int64_t* n_reads,
+                    int64_t* n_bases) {
+  return guarded([&] {
+    if (!r) fail(KMHG_EINVAL, "null argument");
+    if (n_records) *n_records = r->r.records;
+    if (n_reads) *n_reads = (int64_t)r->r.n();
+    if (n_bases) *n_bases = (int64_t)r->r.seq.size();
+  });
+}
+
+int kmhg_reads_copy(const kmhg_reads* r, uint8_t* seq, uint8_t* qual, int64_t* offsets,
+                    uint8_t* has_qual) {
+  return guarded([&] {
+    if (!r) fail(KMHG_EINVAL, "null argument");
+    const ReadsHost& h = r->r;
+    if (seq) memcpy(seq, h.seq.data(), h.seq.size());
+    if (qual) memcpy(qual, h.qual.data(), h.qual.size());
+    if (offsets) memcpy(offsets, h.off.data(), h.off.size() * 8);
+    if (has_qual) memcpy(has_qual, h.hasq.data(), h.hasq.size());
+  });
+}
+
+int kmhg_reads_free(kmhg_reads* r) {
+  delete r;
+  return KMHG_OK;
+}
+
+int kmhg_sh_count_reads(kmhg_index** sh, const kmhg_reads* r, const int32_t params[8]) {
+  return guarded([&] {
+    if (!sh || !r || !params) fail(KMHG_EINVAL, "null argument");
+    if (*sh) check_sh(*sh);
+    check_sh_params(params);
+    const int k = params[0];
+    const double min_ll = qll_host((unsigned char)('!' + (unsigned char)params[2]));
+    const uint32_t source = (uint32_t)params[7];
+    hipStream_t s = lib_stream();
+    std::unique_ptr<kmhg_index> fresh;
+    kmhg_index* c = *sh;
+    if (!c) {
+      fresh.reset(new_sh_index(k, params[6], s));
+      c = fresh.get();
+    } else if (!sh_accepts(c, k, source)) {
+      return;
+    }
+    DeviceGuard g(c->device);
+    // reads no longer than k were dropped when r was read with a smaller k
+    ReadsHost keep;
+    const ReadsHost* use = &r->r;
+    bool all_long = true;
+    for (size_t i = 0; i < r->r.n() && all_long; ++i)
+      all_long = r->r.off[i + 1] - r->r.off[i] > k;
+    if (!all_long) {
+      for (size_t i = 0; i < r->r.n(); ++i) {
+        const int64_t a = r->r.off[i], b = r->r.off[i + 1];
+        if (b - a <= k) continue;
+        keep.add(std::string((const char*)r->r.seq.data() + a, (size_t)(b - a)),
+                 std::string((const char*)r->r.qual.data() + a, (size_t)(b - a)),
+                 r->r.hasq[i] != 0);
+      }
+      use = &keep;
+    }
+    sh_count_reads_host(c, *use, min_ll, source, s);
+    c->L += (int64_t)use->seq.size();
+    if (fresh) *sh = fresh.release();
+  });
+}
+
+int kmhg_sh_count_reads_device(kmhg_index** sh, const void* d_seq, const void* d_qual,
+                               const int64_t* d_offsets, const uint8_t* d_has_qual,
+                               int64_t n_reads, const int32_t params[8], void* stream) {
+  return guarded([&] {
+    if (!sh || !params || (n_reads > 0 && (!d_seq || !d_qual || !d_offsets || !d_has_qual)))
+      fail(KMHG_EINVAL, "null argument");
+    if (*sh) check_sh(*sh);
+    check_sh_params(params);
+    if (n_reads < 0 || n_reads >= (int64_t)UINT32_MAX) fail(KMHG_EINVAL, "bad read count");
+    if ((reinterpret_cast<uintptr_t>(d_seq) | reinterpret_cast<uintptr_t>(d_qual)) & 7)
+      fail(KMHG_EINVAL, "read bases and qualities must be 8-byte aligned");
+    const int k = params[0];
+    const double min_ll = qll_host((unsigned char)('!' + (unsigned char)params[2]));
+    const uint32_t source = (uint32_t)params[7];
+    hipStream_t s = (hipStream_t)stream;
+    std::unique_ptr<kmhg_index> fresh;
+    kmhg_index* c = *sh;
+    if (!c) {
+      fresh.reset(new_sh_index(k, params[6], s));
+      c = fresh.get();
+    } else if (!sh_accepts(c, k, source)) {
+      return;
+    }
+    DeviceGuard g(c->device);
+    sh_count_reads_device(c, (const uint8_t*)d_seq, (const uint8_t*)d_qual, d_offsets,
+                          d_has_qual, (uint32_t)n_reads, min_ll, source, s);
+    if (fresh) *sh = fresh.release();
+  });
+}
+
+// seq_kmer_depth_sh (src/kmer_hash.c:859-879) + seq_kmer_counts (src/kmer_reader.c:155-193)
+static void check_depth(const kmhg_index* sh, int k) {
+  check_sh(sh);
+  if (k != sh->k) fail(KMHG_EINVAL, "Receieved error from seq_kmer_counts");
+}
+
+int kmhg_sh_depth(kmhg_index* sh, const char* seq, size_t L, int k, int32_t* counts) {
+  return guarded([&] {
+    check_depth(sh, k);
+    if (L && (!seq || !counts)) fail(KMHG_EINVAL, "null argument");
+    if (L >= (size_t)INT32_MAX) fail(KMHG_EOVERFLOW, "sequence longer than 2^31-1");
+    DeviceGuard g(sh->device);
+    hipStream_t s = lib_stream();
+    const size_t n = effective_len(seq, L);     // the walk ends at a NUL
+    const size_t S = sh->sources;
+    DBuf<uint8_t> d(n + 16, s);
+    DBuf<int32_t> out(std::max<size_t>(L * S, 1), s);
+    if (n) HIPC(hipMemcpyAsync(d.p, seq, n, hipMemcpyHostToDevice, s));
+    sh_depth_device(sh, d.p, (int64_t)n, k, out.p, s);
+    if (L > n)   // past a NUL: never written (NA)
+      HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(out.p + n * S), (int)INT_MIN,
+                             (L - n) * S, s));
+    if (L) HIPC(hipMemcpyAsync(counts, out.p, L * S * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+  });
+}
+
+int kmhg_sh_depth_device(kmhg_index* sh, const void* d_seq, size_t L, int k, int32_t* d_counts,
+                         void* stream) {
+  return guarded([&] {
+    check_depth(sh, k);
+    if (L && (!d_seq || !d_counts)) fail(KMHG_EINVAL, "null argument");
+    if (L >= (size_t)INT32_MAX) fail(KMHG_EOVERFLOW, "sequence longer than 2^31-1");
+    DeviceGuard g(sh->device);
+    sh_depth_device(sh, (const uint8_t*)d_seq, (int64_t)L, k, d_counts, (hipStream_t)stream);
+  });
+}
+
+// kmer_spectrum_suffix_hash_n (src/kmer_hash.c:1010-1039) + sh_count_spectrum_nc
+// (src/suffix_hash.c:338-421).  *status = 1, or the reference's negative code (counts zero).
+int kmhg_sh_spectrum(kmhg_index* sh, int max_count, const int32_t* comb,
+                     const int32_t* comb_inner, int comb_n, const int32_t* source_min,
+                     int n_source_min, double* counts, int* status) {
+  return guarded([&] {
+    check_sh(sh);
+    if (comb_n < 1) fail(KMHG_EINVAL, "comb_r should be an integer vector of length > 0");
+    if (!comb || !comb_inner)
+      fail(KMHG_EINVAL, "comb_inner_r should be an integer vector of the same length as comb_r");
+    if (n_source_min != (int)sh->sources || !source_min)
+      fail(KMHG_EINVAL, "source_min_r should be an integer vector of length sh->counts_n");
+    if (max_count < 0) fail(KMHG_EINVAL, "max_count must be >= 0");   // reference: R alloc error
+    if (!counts) fail(KMHG_EINVAL, "null argument");
+    const uint32_t S = sh->sources;
+    const size_t nbins = (size_t)(max_count + 1) * (size_t)comb_n * S;
+    std::fill(counts, counts + nbins, 0.0);
+    int st = 1;
+    for (int i = 0; i < comb_n && st == 1; ++i) {
+      if ((uint32_t)comb_inner[i] > 1) st = -3;
+      else if ((uint32_t)comb[i] >= (1u << S)) st = -4;
+    }
+    if (status) *status = st;
+    if (st != 1) {
+      fprintf(stderr, "sh_count_spectrum_nc returned an error: %d\n", st);
+      return;
+    }
+    DeviceGuard g(sh->device);
+    hipStream_t s = lib_stream();
+    finish_build(sh);
+    if (!sh->U) return;
+    std::vector<uint32_t> args((size_t)2 * comb_n + S);
+    for (int i = 0; i < comb_n; ++i) {
+      args[i] = (uint32_t)comb[i];
+      args[comb_n + i] = (uint32_t)comb_inner[i];
+    }
+    for (uint32_t j = 0; j < S; ++j) args[2 * comb_n + j] = (uint32_t)source_min[j];
+    DBuf<uint32_t> dargs(args.size(), s), bins(nbins, s);
+    HIPC(hipMemcpyAsync(dargs.p, args.data(), args.size() * 4, hipMemcpyHostToDevice, s));
+    HIPC(hipMemsetAsync(bins.p, 0, nbins * 4, s));
+    LAUNCH("k_spectrum", s,
+           launch_spectrum(sh->positions.p, sh->U, S, (uint32_t)max_count, dargs.p,
+                           dargs.p + comb_n, (uint32_t)comb_n, dargs.p + 2 * comb_n, bins.p, s));
+    std::vector<uint32_t> h(nbins);
+    HIPC(hipMemcpyAsync(h.data(), bins.p, nbins * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    for (size_t i = 0; i < nbins; ++i) counts[i] = (double)h[i];
+  });
+}
+
+// (key, counts) rows of a counts index in row order (tests, export)
+int kmhg_counts_export(kmhg_index* idx, uint64_t* keys, int32_t* counts) {
+  return guarded([&] {
+    if (!idx || !idx->sources) fail(KMHG_EINVAL, "not a counts index");
+    DeviceGuard g(idx->device);
+    hipStream_t s = lib_stream();
+    if (idx->U && keys)
+      HIPC(hipMemcpyAsync(keys, idx->ckeys.p, idx->U * 8, hipMemcpyDeviceToHost, s));
+    if (idx->U && counts)
+      HIPC(hipMemcpyAsync(counts, idx->positions.p, idx->U * idx->sources * 4,
+                          hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+  });
+}
+
 int kmhg_index_wait(kmhg_index* idx) {
   return guarded([&] {
     if (!idx) fail(KMHG_EINVAL, "null index");
@@ -1226,7 +1714,7 @@ int kmhg_index_info(const kmhg_index* cidx, kmhg_info* info) {
                                    idx->ckeys.bytes() + idx->slot_row.bytes() +
                                    idx->row_slot.bytes());
     info->sources = (int32_t)idx->sources;
-    info->reserved = 0;
+    info->kind = idx->canonical ? 2 : (idx->sources ? 1 : 0);
     info->kmer_count = (int64_t)(idx->sources ? idx->kmer_count : idx->U);
   });
 }

@@ -1,0 +1,41 @@
+// kmhg_sh.h -- launch wrappers of kmhg_sh.hip (read counting, depth, spectrum).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "kmhg_common.h"
+
+namespace kmhg {
+
+constexpr int DP_CPT = 16;                   // depth: chars per lane
+constexpr int DP_TILE = BLOCK * DP_CPT;      // depth: chars per workgroup
+inline uint32_t depth_tiles(int64_t L) { return (uint32_t)((L + DP_TILE - 1) / DP_TILE); }
+
+// one lane per read of a packed batch: seq / qual bytes (8-B aligned, >= 8 B of padding),
+// read r = [off[r], off[r+1]), hasq[r] = 0 for a FASTA record.  emit = false: cnt[r] = k-mers
+// accepted; emit = true: cnt = exclusive offsets, keys[cnt[r] + t] = canonical k-mer t.
+void launch_read_kmers(const uint8_t* seq, const uint8_t* qual, const int64_t* off,
+                       const uint8_t* hasq, uint32_t n_reads, int k, double min_ll,
+                       const double* qll, uint32_t* cnt, uint64_t* keys, bool emit,
+                       hipStream_t s);
+
+// depth: tcnt = depth_tiles(L) u32 (segment starts per tile, scanned in place by the caller),
+// sstart / send = segment bounds, n_seg = number of segments, stale = per-segment flag
+void launch_depth_seg_count(const uint8_t* seq, int64_t L, uint32_t* tcnt, hipStream_t s);
+void launch_depth_seg_emit(const uint8_t* seq, int64_t L, const uint32_t* tbase, uint32_t* sstart,
+                           uint32_t* send, hipStream_t s);
+void launch_depth_modes(const uint8_t* seq, int64_t L, int k, const uint32_t* sstart,
+                        const uint32_t* send, const uint32_t* n_seg, uint8_t* stale, const Slot* T,
+                        Geom g, uint32_t S, const int32_t* M, int32_t* out, hipStream_t s);
+void launch_depth_probe(const uint8_t* seq, int64_t L, int k, const uint32_t* sstart,
+                        const uint32_t* send, const uint32_t* n_seg, const uint8_t* stale,
+                        const Slot* T, Geom g, uint32_t S, const int32_t* M, int32_t* out,
+                        hipStream_t s);
+
+// batch-table fallback (a bucket of the partitioned build overflowed): T initialised empty
+void launch_key_count_insert(const uint64_t* keys, uint64_t n, Slot* T, Geom g, hipStream_t s);
+
+// spectrum bins: (max_count + 1) x comb_n x S u32, zeroed by the caller
+void launch_spectrum(const int32_t* M, uint64_t U, uint32_t S, uint32_t max_count,
+                     const uint32_t* comb, const uint32_t* inner, uint32_t comb_n,
+                     const uint32_t* smin, uint32_t* bins, hipStream_t s);
+
+}  // namespace kmhg

@@ -143,3 +143,46 @@ def derived(A: np.ndarray, seed: int = 5, snv: float = 0.01, n_rearr: int = 20,
     if n_frac > 0:
         B = add_n_runs(B, n_frac, seed + 1)
     return B
+
+
+def reads(genome: np.ndarray, n_reads: int, read_len: int = 150, seed: int = 31,
+          err: float = 0.005, n_frac: float = 0.0005, rc_frac: float = 0.5):
+    """Short reads sampled from ``genome`` for count.kmers.fq.sh.rp (SURVEY.md §8 f next-4).
+
+    Returns (seq, qual), each (n_reads, read_len) uint8: random start, reverse-complemented with
+    probability rc_frac, substitutions at rate err (their qualities drawn low), N calls at rate
+    n_frac (quality '#'), and Illumina-like phred+33 qualities ('#'..'J') that decay along the
+    read, so the reference's quality filter accepts, rejects and restarts windows."""
+    rng = _rng(seed, 17)
+    L = len(genome)
+    start = rng.integers(0, L - read_len, n_reads)
+    idx = start[:, None] + np.arange(read_len)[None, :]
+    s = genome[idx].copy()
+    flip = rng.random(n_reads) < rc_frac
+    comp = np.zeros(256, np.uint8)
+    comp[list(b"ACGTNacgtn")] = list(b"TGCANtgcan")
+    s[flip] = comp[s[flip][:, ::-1]]
+    # qualities: mean decays from Q38 to Q25 along the read, noise +-8, clipped to [2, 41]
+    mean = np.linspace(38, 25, read_len)[None, :]
+    q = np.clip(np.rint(mean + rng.normal(0, 5, (n_reads, read_len))), 2, 41).astype(np.uint8)
+    e = rng.random((n_reads, read_len)) < err
+    s[e] = _BASES[rng.integers(0, 4, int(e.sum()))]
+    q[e] = rng.integers(2, 15, int(e.sum())).astype(np.uint8)
+    nm = rng.random((n_reads, read_len)) < n_frac
+    s[nm] = ord("N")
+    q[nm] = 2
+    return s, (q + 33).astype(np.uint8)
+
+
+def fastq_bytes(seq: np.ndarray, qual: np.ndarray, prefix: str = "r") -> bytes:
+    """4-line FASTQ text of equal-length reads (seq, qual as returned by reads())."""
+    n, rl = seq.shape
+    names = [f"@{prefix}{i}\n".encode() for i in range(n)]
+    body = np.empty((n, 2 * rl + 4), np.uint8)
+    body[:, :rl] = seq
+    body[:, rl] = 10
+    body[:, rl + 1] = ord("+")
+    body[:, rl + 2] = 10
+    body[:, rl + 3:2 * rl + 3] = qual
+    body[:, 2 * rl + 3] = 10
+    return b"".join(h + r.tobytes() for h, r in zip(names, body))

@@ -336,3 +336,249 @@ class RefIndex:
             self.close()
         except Exception:
             pass
+
+
+# --------------------------------------------------------------------------- read counting
+# count.kmers.fq.sh.rp / seq.kmer.depth.sh / kmer.spec.sh.n (SURVEY.md §8 f next-4, depth half)
+def _orc_sh():
+    lib = _orc()
+    if not hasattr(lib, "_sh_ready"):
+        d256 = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        lib.orc_qll.argtypes = [d256]
+        lib.orc_read_kmers.restype = C.c_long
+        lib.orc_read_kmers.argtypes = [C.c_char_p, C.c_char_p, C.c_long, C.c_int, C.c_int, u64p]
+        lib.orc_depth.restype = C.c_int
+        lib.orc_depth.argtypes = [u64p, i32p, C.c_long, C.c_int, C.c_char_p, C.c_long, C.c_int,
+                                  i32p]
+        lib._sh_ready = True
+    return lib
+
+
+def qll_table() -> np.ndarray:
+    """q_to_ll (src/Q_to_log_likelihood.h) regenerated from its formula (sh_oracle.c)."""
+    out = np.zeros(256, np.float64)
+    _orc_sh().orc_qll(out)
+    return out
+
+
+def fastx_records(data: bytes):
+    """kseq_read (klib kseq.h bundled as src/kseq.h, __KSEQ_READ) restated over a decompressed
+    byte string: yields (seq, qual) where qual is None for a FASTA record, and stops at the end
+    of the file (-1) or at the first record whose quality length differs from its sequence (-2),
+    as kmer_reader_read's loop does (src/kmer_reader.c:55)."""
+    n = len(data)
+    pos = 0
+    last_char = 0
+
+    def line_from(p):                      # rest of the line, the '\n' consumed
+        e = data.find(b"\n", p)
+        return (data[p:], n) if e < 0 else (data[p:e], e + 1)
+
+    while True:
+        if last_char == 0:                 # jump to the next header
+            while pos < n and data[pos] not in b">@":
+                pos += 1
+            if pos >= n:
+                return
+            pos += 1
+        if pos >= n:                       # name: EOF with nothing read
+            return
+        e = pos
+        while e < n and data[e] not in b" \t\n\v\f\r":
+            e += 1
+        delim = data[e] if e < n else 0
+        pos = min(e + 1, n)
+        if delim != 0x0A and pos < n:      # comment: rest of the header line
+            _, pos = line_from(pos)
+        seq = bytearray()
+        c = -1
+        while pos < n:
+            c = data[pos]
+            pos += 1
+            if c in b">+@":
+                break
+            if c == 0x0A:
+                c = -1
+                continue
+            seq.append(c)
+            if pos < n:                    # ks_getuntil2 strips '\r' only when it read bytes
+                rest, pos = line_from(pos)
+                seq += rest
+                if len(seq) > 1 and seq[-1] == 0x0D:
+                    seq.pop()
+            c = -1
+        last_char = c if c in (0x3E, 0x40) else 0
+        if c != 0x2B:                      # FASTA
+            yield bytes(seq), None
+            continue
+        while pos < n and data[pos] != 0x0A:   # rest of the '+' line
+            pos += 1
+        if pos >= n:
+            return                         # -2: no quality string
+        pos += 1
+        qual = bytearray()
+        while pos < n:                     # at least one line, then while shorter than seq
+            rest, pos = line_from(pos)
+            qual += rest
+            if len(qual) > 1 and qual[-1] == 0x0D:
+                qual.pop()
+            if len(qual) >= len(seq):
+                break
+        last_char = 0
+        if len(qual) != len(seq):
+            return                         # -2
+        yield bytes(seq), bytes(qual)
+
+
+def read_fastx(path: str) -> bytes:
+    raw = open(path, "rb").read()
+    if raw[:2] == b"\x1f\x8b":
+        import gzip
+        raw = gzip.decompress(raw)
+    return raw
+
+
+def read_kmers(seq: bytes, qual, k: int, min_q: int) -> np.ndarray:
+    """Canonical k-mers of one read in iteration order (orc_read_kmers)."""
+    out = np.zeros(max(len(seq) - k + 1, 1), np.uint64)
+    n = _orc_sh().orc_read_kmers(seq, qual, len(seq), k, min_q, out)
+    return out[:n]
+
+
+class OracleSH:
+    """suffix_hash_n restated as {canonical key: counts[counts_n]} (src/suffix_hash.c:179-285),
+    filled by count.kmers.fq.sh.rp's reader (src/kmer_reader.c:41-76)."""
+
+    def __init__(self, k: int, counts_n: int):
+        self.k, self.S = k, counts_n
+        self.table: dict[int, np.ndarray] = {}
+
+    def add_fastq(self, path_or_bytes, min_q: int, max_reads: int, source: int) -> "OracleSH":
+        data = path_or_bytes if isinstance(path_or_bytes, (bytes, bytearray)) else \
+            read_fastx(path_or_bytes)
+        chunks = []
+        for i, (s, q) in enumerate(fastx_records(bytes(data))):
+            if i >= max_reads:
+                break
+            if len(s) <= self.k:
+                continue
+            chunks.append(read_kmers(s, q, self.k, min_q))
+        if chunks:
+            allk = np.concatenate(chunks)
+            uk, cnt = np.unique(allk, return_counts=True)
+            for key, c in zip(uk.tolist(), cnt.tolist()):
+                v = self.table.get(key)
+                if v is None:
+                    v = self.table[key] = np.zeros(self.S, np.int64)
+                v[source] += c
+        return self
+
+    def arrays(self):
+        """(keys ascending, counts U x S int32)"""
+        keys = np.array(sorted(self.table), np.uint64)
+        M = np.array([self.table[int(x)] for x in keys], np.int64).reshape(-1, self.S)
+        return keys, M.astype(np.int32)
+
+    def depth(self, seq, k: int) -> np.ndarray:
+        """seq.kmer.depth.sh: (L, counts_n) int32; NA = INT_MIN"""
+        b = _as_bytes(seq)
+        keys, M = self.arrays()
+        out = np.zeros(len(b) * self.S, np.int32)
+        _orc_sh().orc_depth(keys, np.ascontiguousarray(M.reshape(-1)), len(keys), self.S, b,
+                            len(b), k, out)
+        return out.reshape(len(b), self.S)
+
+    def spectrum(self, max_count: int, comb, comb_inner, source_min) -> np.ndarray:
+        """sh_count_spectrum_nc (src/suffix_hash.c:338-421): (comb_n * S, max_count + 1)."""
+        comb = [int(c) & 0xFFFFFFFF for c in comb]
+        inner = [int(c) & 0xFFFFFFFF for c in comb_inner]
+        smin = np.array([int(c) & 0xFFFFFFFF for c in source_min], np.int64)
+        cn, S = len(comb), self.S
+        out = np.zeros((max_count + 1, cn * S), np.float64)
+        if any(x > 1 for x in inner) or any(c >= (1 << S) for c in comb):
+            return out.T.copy()
+        _, M = self.arrays()
+        M = M.astype(np.int64) & 0xFFFFFFFF
+        flag = np.zeros(len(M), np.int64)
+        for j in range(S):
+            flag |= (M[:, j] >= smin[j]).astype(np.int64) << j
+        capped = np.minimum(M, max_count)
+        for jj in range(cn):
+            sel = (flag == comb[jj]) if inner[jj] else ((flag & comb[jj]) > 0)
+            for kk in range(S):
+                np.add.at(out[:, jj * S + kk], capped[sel, kk], 1.0)
+        return out.T.copy()
+
+
+def _ref_sh():
+    lib = C.CDLL(os.path.join(_HERE, "_ref", "libkmh_ref_sh.so"))
+    lib.ref_sh_count_fastq.restype = C.c_void_p
+    lib.ref_sh_count_fastq.argtypes = [C.c_void_p, C.c_char_p, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_long, C.c_int, C.c_int]
+    lib.ref_sh_size.restype = C.c_long
+    lib.ref_sh_size.argtypes = [C.c_void_p]
+    lib.ref_sh_counts_n.argtypes = [C.c_void_p]
+    lib.ref_sh_dump.restype = C.c_long
+    lib.ref_sh_dump.argtypes = [C.c_void_p, u64p, i32p]
+    lib.ref_sh_depth.argtypes = [C.c_void_p, C.c_char_p, C.c_long, C.c_int, i32p]
+    lib.ref_sh_spectrum.argtypes = [C.c_void_p, C.c_int, i32p, i32p, C.c_int, i32p,
+                                    np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")]
+    lib.ref_sh_free.argtypes = [C.c_void_p]
+    return lib
+
+
+def ref_sh_available() -> bool:
+    return os.path.exists(os.path.join(_HERE, "_ref", "libkmh_ref_sh.so"))
+
+
+class RefSH:
+    """The compiled reference suffix_hash_n (count_kmers_fastq_sh_rp & co., ref_sh_harness.c)."""
+
+    def __init__(self):
+        self.lib = _ref_sh()
+        self.h = None
+
+    def add_fastq(self, path: str, k: int, prefix_bits: int, min_q: int, max_reads: int,
+                  source_n: int, source: int, thread_n: int = 1) -> "RefSH":
+        self.h = self.lib.ref_sh_count_fastq(self.h, path.encode(), k, prefix_bits, min_q,
+                                             thread_n, max_reads, source_n, source)
+        return self
+
+    def arrays(self):
+        n = self.lib.ref_sh_size(self.h)
+        S = self.lib.ref_sh_counts_n(self.h)
+        keys = np.zeros(max(n, 1), np.uint64)
+        M = np.zeros(max(n, 1) * S, np.int32)
+        n2 = self.lib.ref_sh_dump(self.h, keys, M)
+        assert n2 == n
+        o = np.argsort(keys[:n], kind="stable")
+        return keys[:n][o], M[:n * S].reshape(n, S)[o]
+
+    def depth(self, seq, k: int) -> np.ndarray:
+        b = _as_bytes(seq)
+        S = self.lib.ref_sh_counts_n(self.h)
+        out = np.zeros(max(len(b), 1) * S, np.int32)
+        rc = self.lib.ref_sh_depth(self.h, b, len(b), k, out)
+        if rc != 1:
+            raise ValueError("Receieved error from seq_kmer_counts")
+        return out[:len(b) * S].reshape(len(b), S)
+
+    def spectrum(self, max_count, comb, comb_inner, source_min) -> np.ndarray:
+        S = self.lib.ref_sh_counts_n(self.h)
+        cn = len(comb)
+        out = np.zeros(cn * S * (max_count + 1), np.float64)
+        self.lib.ref_sh_spectrum(self.h, max_count, np.array(comb, np.int32),
+                                 np.array(comb_inner, np.int32), cn,
+                                 np.array(source_min, np.int32), out)
+        return out.reshape(max_count + 1, cn * S).T.copy()
+
+    def close(self):
+        if self.h:
+            self.lib.ref_sh_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,159 @@
+"""Read counting on the GPU (count.kmers.fq.sh.rp -> seq.kmer.depth.sh / kmer.spec.sh.n,
+SURVEY.md §8 f next-4): the HIP path through the C-ABI against the reference's golden vectors
+(tests/golden/sh_golden.json, made from the compiled reference core) and against the oracle at
+larger sizes.  Keys and counts are compared as the key-sorted table (the suffix hash has no
+row order the reference exposes: depth and spectrum are order-free)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import sh_inputs as I
+from kmh_canon import sha
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = I.load_golden()
+
+
+@pytest.fixture(scope="module")
+def inputs(tmp_path_factory):
+    return I.materialise(str(tmp_path_factory.mktemp("shg")))
+
+
+def _params(k, pb, mq, mr, S, src):
+    return [k, pb, mq, 1, mr, 1, S, src]
+
+
+def _sorted_table(ptr):
+    from kmer_hasher_amd import api
+    keys, M = api.counts_table(ptr)
+    o = np.argsort(keys, kind="stable")
+    return keys[o], M[o]
+
+
+@pytest.mark.parametrize("case", GOLD["cases"], ids=lambda c: c["name"])
+def test_sh_golden(gpu, case, inputs):
+    from kmer_hasher_amd import api
+    files, genome = inputs
+    ptr = None
+    for f, pb, mq, mr, src in case["calls"]:
+        ptr = api.count_kmers_fq_sh_rp(files[f], _params(case["k"], pb, mq, mr, case["source_n"],
+                                                         src), ptr)
+    inf = ptr.info()
+    assert inf.kind == 2 and inf.sources == case["source_n"] and inf.k == case["k"]
+    keys, M = _sorted_table(ptr)
+    assert len(keys) == case["U"]
+    assert sha(keys) == case["keys_sha"]
+    assert sha(M.astype(np.int32)) == case["counts_sha"]
+    strings = I.depth_strings(genome, case["k"])
+    for d in case["depth"]:
+        got = api.seq_kmer_depth_sh(ptr, strings[d["string"]], case["k"])   # (S, L)
+        assert sha(np.ascontiguousarray(got.T)) == d["sha"], d
+    for sp in case["spectra"]:
+        got = api.kmer_spec_sh_n(ptr, sp["max_count"], sp["comb"], sp["comb_inner"],
+                                 sp["source_min"])
+        assert sha(np.ascontiguousarray(got)) == sp["sha"]
+
+
+def test_sh_depth_short_and_edge_strings(gpu, inputs):
+    """Strings the golden set leaves out (L < k: the reference writes before its buffer) and
+    NUL-terminated input: all NA where nothing is written, as the oracle defines it."""
+    from kmer_hasher_amd import api
+    files, genome = inputs
+    k = 15
+    ptr = api.count_kmers_fq_sh_rp(files["sim.fq"], _params(k, 10, 0, -1, 1, 0))
+    o = O.OracleSH(k, 1).add_fastq(files["sim.fq"], 0, 2**62, 0)
+    for s in I.depth_strings(genome, k) + [genome[:40] + b"\0" + genome[50:90]]:
+        want = o.depth(s.split(b"\0")[0], k)
+        got = api.seq_kmer_depth_sh(ptr, s, k).T
+        assert np.array_equal(got[:len(want)], want)
+        assert (got[len(want):] == np.iinfo(np.int32).min).all()
+
+
+def test_sh_errors_and_noops(gpu, inputs, tmp_path):
+    from kmer_hasher_amd import api
+    files, genome = inputs
+    E = api.KmerHashError
+    with pytest.raises(E, match="k must be a positive integer"):
+        api.count_kmers_fq_sh_rp(files["sim.fq"], _params(0, 10, 0, -1, 1, 0))
+    with pytest.raises(E, match="Source_n must be in the range 1 - 4"):
+        api.count_kmers_fq_sh_rp(files["sim.fq"], _params(15, 10, 0, -1, 5, 0))
+    with pytest.raises(E, match="source_i must be less than source_n"):
+        api.count_kmers_fq_sh_rp(files["sim.fq"], _params(15, 10, 0, -1, 2, 2))
+    with pytest.raises(E, match="k_r must be an integer vector of length 6"):
+        api.count_kmers_fq_sh_rp(files["sim.fq"], [15, 10, 0])
+    ptr = api.count_kmers_fq_sh_rp(files["sim.fq"], _params(15, 10, 0, 200, 2, 0))
+    keys0, M0 = _sorted_table(ptr)
+    # into an existing hash: a different k or a source >= its counts_n counts nothing
+    api.count_kmers_fq_sh_rp(files["sim.fq"], _params(17, 10, 0, -1, 2, 1), ptr)
+    api.count_kmers_fq_sh_rp(files["sim.fq"], _params(15, 10, 0, -1, 4, 3), ptr)
+    keys1, M1 = _sorted_table(ptr)
+    assert np.array_equal(keys0, keys1) and np.array_equal(M0, M1)
+    # a missing file: the reference's reader reads nothing; a new, empty hash
+    empty = api.count_kmers_fq_sh_rp(str(tmp_path / "nope.fq"), _params(15, 10, 0, -1, 1, 0))
+    assert empty.info().n_kmers == 0
+    d = api.seq_kmer_depth_sh(empty, genome[:100], 15)
+    assert (d[:, :85] == 0).sum() > 0 and d.shape == (1, 100)
+    with pytest.raises(E, match="Receieved error from seq_kmer_counts"):
+        api.seq_kmer_depth_sh(ptr, genome[:100], 16)
+    with pytest.raises(E, match="unable to obtain suffix_hash_n"):
+        api.seq_kmer_depth_sh(api.make_kmer_hash(genome[:100], 15), genome[:100], 15)
+    with pytest.raises(E, match="incorrect tag"):
+        api.kmer_pos(ptr, 15)
+    with pytest.warns(UserWarning, match="returned an error: -3"):
+        z = api.kmer_spec_sh_n(ptr, 5, [1], [2], [1, 1])
+    assert not z.any()
+    with pytest.warns(UserWarning, match="returned an error: -4"):
+        api.kmer_spec_sh_n(ptr, 5, [4], [0], [1, 1])
+
+
+def _pack(torch, seq, qual, hasq=None):
+    n, rl = seq.shape
+    flat = np.zeros(n * rl + 16, np.uint8)
+    flat[:n * rl] = seq.reshape(-1)
+    qf = np.zeros(n * rl + 16, np.uint8)
+    qf[:n * rl] = qual.reshape(-1)
+    off = (np.arange(n + 1, dtype=np.int64) * rl)
+    hq = np.ones(n, np.uint8) if hasq is None else hasq
+    t = lambda a: torch.from_numpy(a).to("cuda")  # noqa: E731
+    return t(flat), t(qf), t(off), t(hq)
+
+
+def _oracle_counts(seq, qual, hasq, k, mq):
+    ks = [O.read_kmers(s.tobytes(), q.tobytes() if h else None, k, mq)
+          for s, q, h in zip(seq, qual, hasq)]
+    allk = np.concatenate(ks) if ks else np.empty(0, np.uint64)
+    return np.unique(allk, return_counts=True)
+
+
+@pytest.mark.parametrize("k,mq", [(31, 20), (21, 0), (11, 30)])
+def test_sh_device_reads_match_oracle(gpu, k, mq):
+    """Device-resident packed reads (kmhg_sh_count_reads_device): 60 K reads x 150 bp of an
+    iid genome with N calls, one third of them as FASTA records (N-only iterator)."""
+    torch = gpu
+    from kmer_hasher_amd import _lib, api, synth
+    g = synth.add_n_runs(synth.iid(400_000, 41), 0.001, 42, max_run=30)
+    seq, qual = synth.reads(g, 60_000, 150, 43 + k)
+    hasq = (np.arange(len(seq)) % 3 != 0).astype(np.uint8)
+    ds, dq, do, dh = _pack(torch, seq, qual, hasq)
+    h = C.c_void_p()
+    prm = (C.c_int32 * 8)(k, 10, mq, 1, -1, 1, 1, 0)
+    L = _lib.lib()
+    _lib.check(L.kmhg_sh_count_reads_device(C.byref(h), ds.data_ptr(), dq.data_ptr(),
+                                            do.data_ptr(), dh.data_ptr(), len(seq), prm, None))
+    torch.cuda.synchronize()
+    ptr = api.ExtPtr(h.value, tag=api.SUFFIX_HASH_N_TAG)
+    keys, M = _sorted_table(ptr)
+    uk, cnt = _oracle_counts(seq, qual, hasq, k, mq)
+    assert np.array_equal(keys, uk)
+    assert np.array_equal(M[:, 0], cnt)
+    # depth of the genome, device entry point
+    dseq = torch.from_numpy(g.copy()).to("cuda")
+    out = torch.empty(len(g), dtype=torch.int32, device="cuda")
+    _lib.check(L.kmhg_sh_depth_device(ptr.handle, dseq.data_ptr(), len(g), k, out.data_ptr(),
+                                      None))
+    torch.cuda.synchronize()
+    o = O.OracleSH(k, 1)
+    o.table = {int(a): np.array([c]) for a, c in zip(uk, cnt)}
+    assert np.array_equal(out.cpu().numpy(), o.depth(g.tobytes(), k)[:, 0])
