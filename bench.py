@@ -8,7 +8,10 @@ bucket, per-bucket LDS tables, totals to a pinned record) of one synthetic seque
 resident in HBM, and the index is freed again.  kmhg_build_device is asynchronous, so the timed
 steps pipeline host enqueue with device execution; `synchronous` reports the same steps with the
 host waiting for every build (the R API's make.kmer.hash semantics).  Config 2 (default, BASELINE.json configs[1]): 10 Mbp iid ACGT, k = 31.  The
-seq.kmer.pos self-query of the same sequence is timed the same way and reported in `query`.
+seq.kmer.pos self-query of the same sequence is timed the same way and reported in `query`;
+`counts` times count.kmers of it, `reads` count.kmers.fq.sh.rp of 400 K simulated 150-bp reads
+sampled from it (packed in HBM) and `depth` seq.kmer.depth.sh of it against that suffix hash
+(SURVEY.md §8 f next-4), each with the reference's own core timed beside it.
 
 N > 1 (launched by torch.distributed.run, one rank per GPU): every rank indexes its own
 sequence (seed = 1 + rank), no data-path collective -> weak scaling; value = all ranks' Mbp
@@ -142,6 +145,57 @@ def cpu_counts_baseline(seq_bytes: bytes, k: int, sample_bp: int = 3_000_000) ->
                 "sample": f"unavailable: {e}"}
 
 
+# the reference's own usage (test.R:146): count.kmers.fq.sh.rp(fq, c(31, 28, 10, 47, -1, 200, 2, 0))
+READS_N, READS_LEN, READS_MINQ, READS_CPU = 400_000, 150, 10, 40_000
+
+
+def reads_algorithmic_bytes(kernel: str, n_bases: int, n_reads: int, words: int) -> int | None:
+    """Minimum bytes of the read-counting kernels: the iterator reads every base and quality
+    once (2 B/base) and its read's offset (8 B) and count/offset (4 B); the emit pass also writes
+    8 B per accepted k-mer (`words`, the k-mer occurrences counted)."""
+    if kernel == "k_read_kmers_count":
+        return 2 * n_bases + 12 * n_reads
+    if kernel == "k_read_kmers_emit":
+        return 2 * n_bases + 12 * n_reads + 8 * words
+    return None
+
+
+def cpu_reads_baseline(fq: bytes, seq_bytes: bytes, k: int, depth_bp: int = 2_000_000):
+    """count_kmers_fastq_sh_rp (src/kmer_hash.c:810-857, 1 reader thread) and seq_kmer_counts
+    (src/kmer_reader.c:155-193) of the reference's own counting core (oracle/_ref) on a bounded
+    sample: the first READS_CPU reads written as FASTQ, and a depth_bp prefix."""
+    try:
+        import tempfile
+        from oracle import oracle as O
+        with tempfile.NamedTemporaryFile(suffix=".fq") as f:
+            f.write(fq)
+            f.flush()
+            r = O.RefSH()
+            t0 = time.perf_counter()
+            r.add_fastq(f.name, k, 28, READS_MINQ, 2**62, 2, 0)
+            t = time.perf_counter() - t0
+        bases = READS_CPU * READS_LEN
+        rb = {"value": round(bases / 1e6 / t, 3), "unit": "Mbp/s", "cores": 1,
+              "kind": "reference",
+              "sample": f"{READS_CPU} reads x {READS_LEN} bp ({bases / 1e6:.1f} Mbp) from a FASTQ "
+                        "file, count_kmers_fastq_sh_rp core (kmer_reader_read, 1 thread, "
+                        "oracle/_ref gcc -O2)"}
+        s = seq_bytes[:depth_bp]
+        t0 = time.perf_counter()
+        r.depth(s, k)
+        t = time.perf_counter() - t0
+        r.close()
+        db = {"value": round(len(s) / 1e6 / t, 3), "unit": "Mbp/s", "cores": 1,
+              "kind": "reference",
+              "sample": f"{len(s) / 1e6:.1f} Mbp prefix, seq_kmer_counts against the suffix hash "
+                        "of the sample reads (oracle/_ref)"}
+        return rb, db
+    except Exception as e:  # reported, never required
+        na = {"value": None, "unit": "Mbp/s", "cores": 1, "kind": "reference",
+              "sample": f"unavailable: {e}"}
+        return na, dict(na)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,6 +203,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-reads", action="store_true",
+                    help="skip the read-counting / depth legs (count.kmers.fq.sh.rp)")
     ap.add_argument("--profile", action="store_true",
                     help="short run for rocprofv3 (no CPU leg, no JSON extras)")
     args = ap.parse_args()
@@ -277,10 +333,66 @@ def main():
         barrier()
         t_count = time.perf_counter() - t0
 
-    tb = torch.tensor([t_build, t_query, t_sync, t_count], dtype=torch.float64, device=dev)
+    # ---------------- count.kmers.fq.sh.rp over reads sampled from the same sequence (packed reads
+    # resident in HBM, one new suffix hash per step), then seq.kmer.depth.sh of the sequence
+    # against it (SURVEY.md §8 f next-4)
+    rper, dper, t_reads, t_depth, rU, n_bases, sample_fq = {}, {}, 0.0, 0.0, 0, 0, None
+    r_words = 0
+    if not args.profile and not args.no_reads:
+        rs, rq = synth.reads(host_seq, READS_N, READS_LEN, 51 + rank)
+        reads = D.DeviceReads.from_arrays(rs, rq, dev)
+        n_bases = READS_N * READS_LEN
+        if rank == 0 and not args.no_cpu:
+            sample_fq = synth.fastq_bytes(rs[:READS_CPU], rq[:READS_CPU])
+        del rs, rq
+        prm = (k, 28, READS_MINQ, 47, -1, 200, 2, 0)
+        for _ in range(max(1, args.warmup)):
+            D.DeviceIndex.count_reads(reads, prm, stream=stream).free()
+        D.timing_enable(True)
+        D.timing_reset()
+        for _ in range(2):
+            c = D.DeviceIndex.count_reads(reads, prm, stream=stream)
+            rU = c.info()["n_kmers"]
+            c.free()
+        rper = {n: v[1] / 2 for n, v in D.timing_report().items() if v[0]}
+        D.timing_enable(False)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            D.DeviceIndex.count_reads(reads, prm, stream=stream).free()
+        barrier()
+        t_reads = time.perf_counter() - t0
+        sh = D.DeviceIndex.count_reads(reads, prm, stream=stream)
+        dout = torch.empty((L, 2), dtype=torch.int32, device=dev)
+        for _ in range(max(1, args.warmup)):
+            sh.depth(seq, k, dout, stream=stream)
+        D.timing_enable(True)
+        D.timing_reset()
+        for _ in range(2):
+            sh.depth(seq, k, dout, stream=stream)
+        dper = {n: v[1] / 2 for n, v in D.timing_report().items() if v[0]}
+        D.timing_enable(False)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            sh.depth(seq, k, dout, stream=stream)
+        barrier()
+        t_depth = time.perf_counter() - t0
+        import ctypes as _C
+        import numpy as np
+        from kmer_hasher_amd import _lib
+        _inf = sh.info()
+        _M = np.zeros(_inf["n_kmers"] * _inf["sources"], np.int32)
+        _lib.check(_lib.lib().kmhg_counts_export(sh.handle, None, _C.c_void_p(_M.ctypes.data)))
+        r_words = int(_M.astype(np.int64).sum())      # k-mer occurrences counted per step
+        sh.free()
+        del reads, dout
+
+    tb = torch.tensor([t_build, t_query, t_sync, t_count, t_reads, t_depth], dtype=torch.float64,
+                      device=dev)
     if world > 1:
         dist.all_reduce(tb, op=dist.ReduceOp.MAX)
-    t_build, t_query, t_sync, t_count = tb.tolist()
+    t_build, t_query, t_sync, t_count, t_reads, t_depth = tb.tolist()
 
     if rank == 0:
         Nw = L - k + 1
@@ -346,10 +458,37 @@ def main():
                 "kernels_ms_per_step": {n: round(v, 5) for n, v in cper.items()},
                 "note": "count.kmers(seq, c(k, 0, 2)) into a new pointer per step: partitioned "
                         "build of the batch + merge into the count matrix + table rebuild"}
+        if t_reads:
+            dom_r = "k_read_kmers_emit"      # the row's own kernel (the batch build is the index's)
+            ab_r = reads_algorithmic_bytes(dom_r, n_bases, READS_N, r_words)
+            out["reads"] = {
+                "value": round(n_bases * world / 1e6 * args.steps / t_reads, 2), "unit": "Mbp/s",
+                "ms_per_step": round(t_reads / args.steps * 1e3, 4), "reads": READS_N,
+                "read_len": READS_LEN, "k": k, "min_q": READS_MINQ, "distinct_kmers": rU,
+                "kmer_words": r_words,
+                "kernels_ms_per_step": {n: round(v, 5) for n, v in rper.items()},
+                "roofline": {"bound": "hbm", "kernel": dom_r,
+                             "achieved": round(ab_r / (rper[dom_r] * 1e-3) / 1e9, 2)
+                             if ab_r else None,
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ab_r / (rper[dom_r] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                             if ab_r else None, "algorithmic_bytes": ab_r},
+                "note": "count.kmers.fq.sh.rp(c(k, 28, min_q, 47, -1, 200, 2, 0)) of reads sampled "
+                        "from the bench sequence (synth.reads: 150 bp, decaying phred, 0.5% "
+                        "substitutions), packed in HBM, a new suffix hash per step"}
+            out["depth"] = {
+                "value": round(L * world / 1e6 * args.steps / t_depth, 2), "unit": "Mbp/s",
+                "ms_per_step": round(t_depth / args.steps * 1e3, 4),
+                "kernels_ms_per_step": {n: round(v, 5) for n, v in dper.items()},
+                "note": "seq.kmer.depth.sh of the bench sequence against that suffix hash"}
         if not args.no_cpu and not args.profile:
             out["cpu_baseline"] = cpu_baseline(host_seq.tobytes(), k)
             if t_count:
                 out["counts"]["cpu_baseline"] = cpu_counts_baseline(host_seq.tobytes(), k)
+            if t_reads and sample_fq is not None:
+                rb, db = cpu_reads_baseline(sample_fq, host_seq.tobytes(), k)
+                out["reads"]["cpu_baseline"] = rb
+                out["depth"]["cpu_baseline"] = db
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -200,7 +200,7 @@ int kmhg_reads_copy(const kmhg_reads *r, uint8_t *seq, uint8_t *qual, int64_t *o
 int kmhg_reads_free(kmhg_reads *r);
 /* Count reads already read (same params as kmhg_sh_count_fastq; max_reads is not applied). */
 int kmhg_sh_count_reads(kmhg_index **sh, const kmhg_reads *r, const int32_t params[8]);
-/* Device-resident packed reads on `stream`: d_seq / d_qual 8-byte aligned with >= 8 readable
+/* Device-resident packed reads on `stream`: d_seq / d_qual 16-byte aligned with >= 16 readable
  * bytes past the last read, d_offsets[n_reads + 1] (int64), d_has_qual[n_reads]. */
 int kmhg_sh_count_reads_device(kmhg_index **sh, const void *d_seq, const void *d_qual,
                                const int64_t *d_offsets, const uint8_t *d_has_qual,

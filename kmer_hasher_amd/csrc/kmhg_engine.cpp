@@ -935,7 +935,7 @@ kmhg_index* new_sh_index(int k, int counts_n, hipStream_t s) {
 // key) -> merge over the batch table's slots.
 void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t* d_qual,
                            const int64_t* d_off, const uint8_t* d_hasq, uint32_t n_reads,
-                           double min_ll, uint32_t source, hipStream_t s) {
+                           double mean_len, double min_ll, uint32_t source, hipStream_t s) {
   idx->stream = s;
   if (!n_reads) return;
   const int k = idx->k;
@@ -944,9 +944,10 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   const uint32_t nt = tiles_for(n_reads);
   DBuf<uint64_t> status((size_t)nt + 1, s);
   HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
+  const uint32_t cap = read_kmers_cap(mean_len);
   LAUNCH("k_read_kmers_count", s,
-         launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cnt.p, nullptr,
-                           false, s));
+         launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
+                           nullptr, false, s));
   LAUNCH("k_scan_u32", s, launch_scan_u32(cnt.p, n_reads, status.p, cnt.p + n_reads, s));
   uint32_t total = 0;
   HIPC(hipMemcpyAsync(&total, cnt.p + n_reads, 4, hipMemcpyDeviceToHost, s));
@@ -954,8 +955,8 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   if (!total) return;
   DBuf<uint64_t> keys(total, s);
   LAUNCH("k_read_kmers_emit", s,
-         launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cnt.p, keys.p,
-                           true, s));
+         launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
+                           keys.p, true, s));
   std::unique_ptr<kmhg_index> B(build_device_v2(nullptr, 0, k, s, keys.p, (int64_t)total));
   Release rel{B.get(), s};
   HIPC(hipEventSynchronize(B->rec.ev));
@@ -1005,7 +1006,8 @@ void sh_count_reads_host(kmhg_index* idx, const ReadsHost& r, double min_ll, uin
   HIPC(hipMemcpyAsync(dqual.p, r.qual.data(), nb, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(dhq.p, r.hasq.data(), n, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(doff.p, r.off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
-  sh_count_reads_device(idx, dseq.p, dqual.p, doff.p, dhq.p, (uint32_t)n, min_ll, source, s);
+  sh_count_reads_device(idx, dseq.p, dqual.p, doff.p, dhq.p, (uint32_t)n, (double)nb / (double)n,
+                        min_ll, source, s);
   HIPC(hipStreamSynchronize(s));                 // the host arrays are reused
 }
 
@@ -1564,8 +1566,8 @@ int kmhg_sh_count_reads_device(kmhg_index** sh, const void* d_seq, const void* d
     if (*sh) check_sh(*sh);
     check_sh_params(params);
     if (n_reads < 0 || n_reads >= (int64_t)UINT32_MAX) fail(KMHG_EINVAL, "bad read count");
-    if ((reinterpret_cast<uintptr_t>(d_seq) | reinterpret_cast<uintptr_t>(d_qual)) & 7)
-      fail(KMHG_EINVAL, "read bases and qualities must be 8-byte aligned");
+    if ((reinterpret_cast<uintptr_t>(d_seq) | reinterpret_cast<uintptr_t>(d_qual)) & 15)
+      fail(KMHG_EINVAL, "read bases and qualities must be 16-byte aligned");
     const int k = params[0];
     const double min_ll = qll_host((unsigned char)('!' + (unsigned char)params[2]));
     const uint32_t source = (uint32_t)params[7];
@@ -1579,8 +1581,17 @@ int kmhg_sh_count_reads_device(kmhg_index** sh, const void* d_seq, const void* d
       return;
     }
     DeviceGuard g(c->device);
+    // mean read length for the LDS staging size: the span of the whole batch (two int64 reads)
+    double mean_len = 150;
+    if (n_reads > 0) {
+      int64_t ends[2] = {0, 0};
+      HIPC(hipMemcpyAsync(&ends[0], d_offsets, 8, hipMemcpyDeviceToHost, s));
+      HIPC(hipMemcpyAsync(&ends[1], d_offsets + n_reads, 8, hipMemcpyDeviceToHost, s));
+      HIPC(hipStreamSynchronize(s));
+      mean_len = (double)(ends[1] - ends[0]) / (double)n_reads;
+    }
     sh_count_reads_device(c, (const uint8_t*)d_seq, (const uint8_t*)d_qual, d_offsets,
-                          d_has_qual, (uint32_t)n_reads, min_ll, source, s);
+                          d_has_qual, (uint32_t)n_reads, mean_len, min_ll, source, s);
     if (fresh) *sh = fresh.release();
   });
 }

@@ -21,8 +21,8 @@
 namespace kmhg {
 
 // ------------------------------------------------------------------ k-mer iterator per read
-// Forward byte reader over an 8-B aligned buffer (padded by >= 8 bytes): one dword pair load
-// per 8 chars; the iterator only ever moves forward.
+// Forward byte reader over an 8-B aligned buffer (padded by >= 8 bytes): one 8-B load per
+// 8 chars; the iterator only ever moves forward.  (The global-memory walk of long reads.)
 struct ByteCursor {
   const uint64_t* base;
   int64_t w;
@@ -43,108 +43,129 @@ __device__ __forceinline__ uint64_t rev_push(uint64_t r, uint32_t c) {
   return (r >> 2) | (((code2(c) + 2) & 3u) << 62);   // UPDATE_OFFSET_RC, src/kmer_util.h:9
 }
 
-// The reference's kmer_iterator (src/kmer_util.c:64-162) for one read [b, e) of the packed
-// batch, its tail recursion unrolled.  With qualities the window's running log-likelihood is
-// kept exactly as the reference accumulates it (double adds in the same order: bit-identical).
-struct ReadIter {
-  ByteCursor s, q;
-  int64_t p, e;
-  int k;
-  bool hasq;
-  uint64_t f, r;
-  double kll, prev, min_ll;
-  const double* qll;
-
-  __device__ bool end(int64_t x) { return x >= e || s.at(x) == 0; }
-
-  __device__ bool begin_nq(int64_t x) {           // kmer_iterator_nq_begin
-    for (;;) {
-      uint64_t ff = 0, rr = 0;
-      int i = 0;
-      while (!end(x) && !is_n(s.at(x)) && i < k) {
-        const uint32_t c = s.at(x);
-        ff = fwd_push(ff, c); rr = rev_push(rr, c); ++x; ++i;
-      }
-      if (i == k) { f = ff; r = rr; p = x; return true; }
-      while (!end(x) && is_n(s.at(x))) ++x;
-      if (end(x)) return false;
-    }
-  }
-  __device__ bool begin_q(int64_t x) {            // kmer_iterator_begin
-    for (;;) {
-      uint64_t ff = 0, rr = 0;
-      double kl = 0, pv = 0;
-      int i = 0;
-      // the next base's term is added before i < k is tested (a k + 1-th term mid-read)
-      while (!end(x) && ((kl = kl + qll[q.at(x)]) > min_ll) && i < k) {
-        const uint32_t c = s.at(x);
-        ff = fwd_push(ff, c); rr = rev_push(rr, c);
-        pv = qll[q.at(x)];
-        ++x; ++i;
-      }
-      if (i == k) { f = ff; r = rr; p = x; prev = pv; kll = kl; return true; }
-      while (!end(x) && qll[q.at(x)] <= min_ll) ++x;
-      if (end(x)) return false;
-    }
-  }
-  __device__ bool begin() { return hasq ? begin_q(p) : begin_nq(p); }
-  __device__ bool next() {                        // kmer_iterator_next / _nq_next
-    if (end(p)) return false;
-    const uint32_t c = s.at(p);
-    if (!hasq) {
-      if (is_n(c)) return begin_nq(p + 1);
-    } else {
-      const double t = qll[q.at(p)];
-      kll += (t - prev);
-      if (kll < min_ll) return begin_q(p + 1);
-      prev = t;
-    }
-    f = fwd_push(f, c); r = rev_push(r, c);
-    ++p;
-    return true;
-  }
+// LDS-staged bytes of a workgroup's reads (absolute index p, staged from `base`)
+struct LdsBytes {
+  const uint8_t* b;
+  int64_t base;
+  __device__ __forceinline__ uint32_t at(int64_t p) const { return b[p - base]; }
 };
 
-template <bool EMIT>
-__global__ void __launch_bounds__(BLOCK)
-k_read_kmers(const uint8_t* __restrict__ seq, const uint8_t* __restrict__ qual,
-             const int64_t* __restrict__ off, const uint8_t* __restrict__ hasq, uint32_t n_reads,
-             int k, double min_ll, const double* __restrict__ qll_g, uint32_t* __restrict__ cnt,
-             uint64_t* __restrict__ keys) {
-  __shared__ double qll[256];
-  qll[threadIdx.x] = qll_g[threadIdx.x];
-  __syncthreads();
-  const uint32_t rd = blockIdx.x * BLOCK + threadIdx.x;
-  if (rd >= n_reads) return;
-  ReadIter it{ByteCursor(seq), ByteCursor(qual), off[rd], off[rd + 1], k, hasq[rd] != 0,
-              0, 0, 0, 0, min_ll, qll};
+// The reference's kmer_iterator (src/kmer_util.c:64-162) for one read [x, e) of the packed batch,
+// as a per-base automaton: every loop trip looks at
+// exactly one position, so the lanes of a wave stay in step -- the nested restart loops of
+// ReadIter serialise a wave whenever any one lane restarts (measured: 4.6x slower).  States:
+// SEEK (= kmer_iterator_begin accumulating i < k bases), SKIP (its skip loop), RUN (_next).
+template <bool EMIT, class Acc>
+__device__ __forceinline__ void walk_read(Acc s, Acc q, int64_t x, int64_t e, bool hasq, int k,
+                                          double min_ll, const double* qll, uint32_t* cnt,
+                                          uint32_t rd, uint64_t* keys) {
+  enum : int { SEEK = 0, SKIP = 1, RUN = 2 };
   const uint64_t mask = (1ull << (2 * k)) - 1;
   const int shift = 64 - 2 * k;
-  uint32_t n = 0;
   uint64_t* out = EMIT ? keys + cnt[rd] : nullptr;
-  bool ok = it.begin();
-  while (ok) {
+  uint32_t n = 0;
+  int st = SEEK, i = 0;
+  uint64_t f = 0, r = 0;
+  double kl = 0, pv = 0;                     // SEEK: running sum, last base's term
+  double kll = 0, prev = 0;                  // RUN
+  while (x < e) {
+    const uint32_t c = s.at(x);
+    if (c == 0) break;                       // the C string ends
+    const double t = hasq ? qll[q.at(x)] : 0.0;
+    if (st == SKIP) {
+      if (hasq ? (t <= min_ll) : is_n(c)) { ++x; continue; }
+      st = SEEK; i = 0; f = 0; r = 0; kl = 0; pv = 0;      // the attempt restarts here
+    }
+    if (st == SEEK) {
+      bool ok;
+      if (hasq) { kl = kl + t; ok = kl > min_ll; }
+      else ok = !is_n(c);
+      if (!ok) { st = SKIP; continue; }      // the skip loop starts at this same base
+      f = fwd_push(f, c); r = rev_push(r, c); pv = t; ++x; ++i;
+      if (i < k) continue;
+      // success: the loop test adds the following base's term before it sees i == k
+      kll = kl; prev = pv;
+      if (hasq && x < e && s.at(x) != 0) kll = kll + qll[q.at(x)];
+      st = RUN;
+    } else {                                 // RUN: kmer_iterator_next / _nq_next
+      bool restart;
+      if (hasq) {
+        kll += (t - prev);
+        restart = kll < min_ll;
+        prev = t;
+      } else {
+        restart = is_n(c);
+      }
+      ++x;
+      if (restart) { st = SEEK; i = 0; f = 0; r = 0; kl = 0; pv = 0; continue; }
+      f = fwd_push(f, c); r = rev_push(r, c);
+    }
     if (EMIT) {
-      const uint64_t a = it.f & mask, b = it.r >> shift;
-      out[n] = a < b ? a : b;
+      const uint64_t a = f & mask, bb = r >> shift;
+      out[n] = a < bb ? a : bb;
     }
     ++n;
-    ok = it.next();
   }
   if (!EMIT) cnt[rd] = n;
 }
 
+// One wave per RK_READS consecutive reads, one lane per read.  The wave's bases and qualities
+// are staged in LDS with 16-B loads (the iterator's byte-serial walk then waits on LDS, not on
+// HBM); a wave whose reads span more than `cap` bytes walks them from global memory instead.
+constexpr int RK_READS = 64;
+
+template <bool EMIT>
+__global__ void __launch_bounds__(RK_READS)
+k_read_kmers(const uint8_t* __restrict__ seq, const uint8_t* __restrict__ qual,
+             const int64_t* __restrict__ off, const uint8_t* __restrict__ hasq, uint32_t n_reads,
+             int k, double min_ll, const double* __restrict__ qll_g, uint32_t cap,
+             uint32_t* __restrict__ cnt, uint64_t* __restrict__ keys) {
+  extern __shared__ uint4 rk_smem[];
+  double* qll = reinterpret_cast<double*>(rk_smem);
+  uint8_t* ls = reinterpret_cast<uint8_t*>(rk_smem) + 256 * sizeof(double);
+  uint8_t* lq = ls + cap;
+  for (int i = threadIdx.x; i < 256; i += RK_READS) qll[i] = qll_g[i];
+  const uint32_t r0 = blockIdx.x * RK_READS;
+  const uint32_t r1 = min(n_reads, r0 + RK_READS);
+  const int64_t base = off[r0] & ~(int64_t)15;
+  const int64_t span = off[r1] - base;
+  const bool fits = span <= (int64_t)cap;
+  if (fits) {
+    const uint32_t nw = (uint32_t)((span + 15) >> 4);
+    const uint4* gs = reinterpret_cast<const uint4*>(seq + base);
+    const uint4* gq = reinterpret_cast<const uint4*>(qual + base);
+    uint4* ws = reinterpret_cast<uint4*>(ls);
+    uint4* wq = reinterpret_cast<uint4*>(lq);
+    for (uint32_t i = threadIdx.x; i < nw; i += RK_READS) {
+      const uint4 a = gs[i], b = gq[i];
+      ws[i] = a;
+      wq[i] = b;
+    }
+  }
+  __syncthreads();
+  const uint32_t rd = r0 + threadIdx.x;
+  if (rd >= r1) return;
+  const int64_t b = off[rd], e = off[rd + 1];
+  const bool hq = hasq[rd] != 0;
+  if (fits)
+    walk_read<EMIT>(LdsBytes{ls, base}, LdsBytes{lq, base}, b, e, hq, k, min_ll, qll, cnt, rd,
+                    keys);
+  else
+    walk_read<EMIT>(ByteCursor(seq), ByteCursor(qual), b, e, hq, k, min_ll, qll, cnt, rd, keys);
+}
+
 void launch_read_kmers(const uint8_t* seq, const uint8_t* qual, const int64_t* off,
                        const uint8_t* hasq, uint32_t n_reads, int k, double min_ll,
-                       const double* qll, uint32_t* cnt, uint64_t* keys, bool emit,
-                       hipStream_t s) {
-  const dim3 grid((n_reads + BLOCK - 1) / BLOCK);
+                       const double* qll, uint32_t cap, uint32_t* cnt, uint64_t* keys,
+                       bool emit, hipStream_t s) {
+  const dim3 grid((n_reads + RK_READS - 1) / RK_READS);
+  const size_t smem = 256 * sizeof(double) + 2 * (size_t)cap;
   if (emit)
-    hipLaunchKernelGGL(k_read_kmers<true>, grid, dim3(BLOCK), 0, s, seq, qual, off, hasq, n_reads,
-                       k, min_ll, qll, cnt, keys);
+    hipLaunchKernelGGL(k_read_kmers<true>, grid, dim3(RK_READS), smem, s, seq, qual, off, hasq,
+                       n_reads, k, min_ll, qll, cap, cnt, keys);
   else
-    hipLaunchKernelGGL(k_read_kmers<false>, grid, dim3(BLOCK), 0, s, seq, qual, off, hasq,
-                       n_reads, k, min_ll, qll, cnt, keys);
+    hipLaunchKernelGGL(k_read_kmers<false>, grid, dim3(RK_READS), smem, s, seq, qual, off, hasq,
+                       n_reads, k, min_ll, qll, cap, cnt, keys);
 }
 
 // ------------------------------------------------------------------ depth: N-free segments
@@ -306,61 +327,75 @@ k_depth_modes(const uint8_t* __restrict__ s, int64_t L, int k, const uint32_t* _
   depth_write(T, g, S, M, fa < rb ? fa : rb, out, L - k);
 }
 
-// One lane per DP_CPT consecutive bases: the base's segment (binary search once, then walk), its
-// write rule, the rolling canonical key, the probe, the write.
+// reverse complement of a forward key of k bases: complement = code ^ 2 (A0 C1 T2 G3), then
+// the 2-bit groups in reverse order -- equals the reference's rolling UPDATE_OFFSET_RC register
+// shifted down by 64 - 2k (src/kmer_util.h:9, src/kmer_reader.c:168-169)
+__device__ __forceinline__ uint64_t revcomp(uint64_t f, int k) {
+  const uint64_t x = __builtin_bitreverse64(f ^ 0xAAAAAAAAAAAAAAAAull);
+  const uint64_t y = ((x >> 1) & 0x5555555555555555ull) | ((x & 0x5555555555555555ull) << 1);
+  return y >> (64 - 2 * k);
+}
+
+constexpr int DP_STAGE_W16 = 22;             // chars [tile - 63.., +352): every window ending in the tile
+
+// One lane per base i of a 256-base tile (the base that ENDS a window).  The tile's chars are
+// staged as 2-bit codes in LDS; the window's forward key comes from the stage and its reverse
+// complement by bit reversal (no per-lane k-char loop).  The write rule (kmhg_sh.hip header):
+// seek segments longer than k write window [i-k+1, i] at i - k from offset k on; a segment of
+// exactly k writes its window at its start; stale segments write every base, the first k - 1
+// of them (their windows span the N gap) by a short loop over global memory.
 __global__ void __launch_bounds__(BLOCK)
-k_depth_probe(const uint8_t* __restrict__ s, int64_t L, int k,
+k_depth_probe(const uint8_t* __restrict__ s, int64_t L, int k, bool aligned,
               const uint32_t* __restrict__ sstart, const uint32_t* __restrict__ send,
               const uint32_t* __restrict__ n_seg, const uint8_t* __restrict__ stale,
               const Slot* __restrict__ T, Geom g, uint32_t S, const int32_t* __restrict__ M,
               int32_t* __restrict__ out) {
-  const int64_t i0 = (int64_t)blockIdx.x * DP_TILE + (int64_t)threadIdx.x * DP_CPT;
-  if (i0 >= L) return;
+  __shared__ StageN<DP_STAGE_W16> st;
+  __shared__ int32_t mrange[2];
+  const int64_t t0 = (int64_t)blockIdx.x * BLOCK;
+  const int64_t base = (t0 - 48) & ~(int64_t)15;
+  stage_tile<false, DP_STAGE_W16>(s, L, base, st, aligned);
   const uint32_t ms = *n_seg;
-  if (!ms) return;
-  // last segment starting at or before i0
-  uint32_t lo = 0, hi = ms;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if ((int64_t)sstart[mid] <= i0) lo = mid + 1; else hi = mid;
-  }
-  int64_t m = (int64_t)lo - 1;
-  const uint64_t mask = (1ull << (2 * k)) - 1;
-  const int shift = 64 - 2 * k;
-  uint64_t f = 0, r = 0;
-  int64_t have_at = -2;                        // the register holds the window ending here
-  for (int t = 0; t < DP_CPT; ++t) {
-    const int64_t i = i0 + t;
-    if (i >= L) break;
-    while (m + 1 < (int64_t)ms && (int64_t)sstart[m + 1] <= i) ++m;
-    if (m < 0) continue;
-    const int64_t a = sstart[m], b = send[m];
-    if (i >= b) continue;                      // an N
-    const int64_t off = i - a, len = b - a;
-    const bool st = stale[m] != 0;
-    int64_t w;
-    if (st) w = i - k;
-    else if (len > k && off >= k) w = i - k;
-    else if (len == k && off == k - 1) w = a;
-    else continue;
-    if (have_at == i - 1) {
-      const uint32_t c = s[i];
-      f = fwd_push(f, c); r = rev_push(r, c);
-    } else {                                   // (re)load the k stream bases ending at i
-      f = 0; r = 0;
-      const int64_t from_prev = st ? (int64_t)k - 1 - off : 0;   // > 0 only across the gap
-      if (from_prev > 0) {
-        const int64_t pb = send[m - 1];
-        for (int64_t j = pb - from_prev; j < pb; ++j) { f = fwd_push(f, s[j]); r = rev_push(r, s[j]); }
-        for (int64_t j = a; j <= i; ++j) { f = fwd_push(f, s[j]); r = rev_push(r, s[j]); }
-      } else {
-        for (int64_t j = i - k + 1; j <= i; ++j) { f = fwd_push(f, s[j]); r = rev_push(r, s[j]); }
-      }
+  if (threadIdx.x < 2 && ms) {                 // segments holding the tile's first / last base
+    const int64_t at = threadIdx.x == 0 ? t0 : min(t0 + BLOCK, L) - 1;
+    uint32_t lo = 0, hi = ms;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if ((int64_t)sstart[mid] <= at) lo = mid + 1; else hi = mid;
     }
-    have_at = i;
-    const uint64_t fa = f & mask, rb = r >> shift;
-    depth_write(T, g, S, M, fa < rb ? fa : rb, out, w);
+    mrange[threadIdx.x] = (int32_t)lo - 1;
   }
+  __syncthreads();
+  const int64_t i = t0 + threadIdx.x;
+  if (i >= L || !ms) return;
+  int32_t m = mrange[0];
+  while (m < mrange[1] && (int64_t)sstart[m + 1] <= i) ++m;
+  if (m < 0) return;
+  const int64_t a = sstart[m], b = send[m];
+  if (i >= b) return;                          // an N
+  const int64_t off = i - a, len = b - a;
+  const bool stl = stale[m] != 0;
+  int64_t w;
+  if (stl) w = i - k;
+  else if (len > k && off >= k) w = i - k;
+  else if (len == k && off == k - 1) w = a;
+  else return;
+  uint64_t f;
+  const int64_t from_prev = stl ? (int64_t)k - 1 - off : 0;
+  if (from_prev > 0) {                         // window across the gap: previous segment's tail
+    f = 0;
+    const int64_t pb = send[m - 1];
+    for (int64_t j = pb - from_prev; j < pb; ++j) f = fwd_push(f, s[j]);
+    for (int64_t j = a; j <= i; ++j) f = fwd_push(f, s[j]);
+  } else {
+    const int o = (int)(i - k + 1 - base);
+    const int qw = o >> 4, bsh = (o & 15) * 2;
+    const uint64_t x = ((uint64_t)st.code[qw] << 32) | st.code[qw + 1];
+    const uint64_t y = st.code[qw + 2];
+    f = ((x << bsh) | ((y << bsh) >> 32)) >> (64 - 2 * k);
+  }
+  const uint64_t rc = revcomp(f, k);
+  depth_write(T, g, S, M, f < rc ? f : rc, out, w);
 }
 
 void launch_depth_seg_count(const uint8_t* seq, int64_t L, uint32_t* tcnt, hipStream_t s) {
@@ -381,8 +416,9 @@ void launch_depth_probe(const uint8_t* seq, int64_t L, int k, const uint32_t* ss
                         const uint32_t* send, const uint32_t* n_seg, const uint8_t* stale,
                         const Slot* T, Geom g, uint32_t S, const int32_t* M, int32_t* out,
                         hipStream_t s) {
-  hipLaunchKernelGGL(k_depth_probe, dim3(depth_tiles(L)), dim3(BLOCK), 0, s, seq, L, k, sstart,
-                     send, n_seg, stale, T, g, S, M, out);
+  const bool aligned = (reinterpret_cast<uintptr_t>(seq) & 15) == 0;
+  hipLaunchKernelGGL(k_depth_probe, dim3((unsigned)((L + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                     seq, L, k, aligned, sstart, send, n_seg, stale, T, g, S, M, out);
 }
 
 // ------------------------------------------------------------------ spectrum

@@ -51,6 +51,36 @@ class DeviceIndex:
                                                     _stream_ptr(stream)))
         return into if into is not None else cls(h.value)
 
+    @classmethod
+    def count_reads(cls, reads: "DeviceReads", params, into: "DeviceIndex | None" = None,
+                    stream=None) -> "DeviceIndex":
+        """count.kmers.fq.sh.rp over HBM-resident packed reads (kmhg_sh_count_reads_device):
+        params = (k, prefix_bits, min_q, thread_n, max_reads, max_mem, source_n, source)."""
+        h = C.c_void_p(into._h.value if into is not None else None)
+        prm = (C.c_int32 * 8)(*[int(x) for x in params])
+        with torch.cuda.device(reads.seq.device):
+            _lib.check(_lib.lib().kmhg_sh_count_reads_device(
+                C.byref(h), C.c_void_p(reads.seq.data_ptr()), C.c_void_p(reads.qual.data_ptr()),
+                C.c_void_p(reads.off.data_ptr()), C.c_void_p(reads.hasq.data_ptr()), reads.n,
+                prm, _stream_ptr(stream)))
+        return into if into is not None else cls(h.value)
+
+    def depth(self, seq: torch.Tensor, k: int, out: torch.Tensor | None = None,
+              stream=None) -> torch.Tensor:
+        """seq.kmer.depth.sh of an HBM-resident sequence: (L, counts_n) int32 (INT_MIN = NA)."""
+        _check_seq(seq)
+        S = self.info()["sources"]
+        if out is None:
+            out = torch.empty((seq.numel(), S), dtype=torch.int32, device=seq.device)
+        if out.dtype != torch.int32 or not out.is_contiguous() or out.numel() < seq.numel() * S:
+            raise ValueError(f"out must be a contiguous int32 tensor of >= {seq.numel() * S} "
+                             "elements (L x counts_n)")
+        with torch.cuda.device(seq.device):
+            _lib.check(_lib.lib().kmhg_sh_depth_device(self._h, C.c_void_p(seq.data_ptr()),
+                                                       seq.numel(), k, C.c_void_p(out.data_ptr()),
+                                                       _stream_ptr(stream)))
+        return out
+
     @property
     def handle(self):
         return self._h
@@ -202,3 +232,30 @@ def timing_report() -> dict:
     buf = C.create_string_buffer(1 << 16)
     _lib.check(_lib.lib().kmhg_timing_report(buf, len(buf)))
     return json.loads(buf.value.decode())
+
+
+class DeviceReads:
+    """Packed reads in HBM for kmhg_sh_count_reads_device: bases and qualities (8-B aligned,
+    16 B of padding), int64 offsets[n + 1], has_qual[n] (0 = FASTA record)."""
+
+    def __init__(self, seq, qual, off, hasq):
+        self.seq, self.qual, self.off, self.hasq = seq, qual, off, hasq
+        self.n = int(hasq.numel())
+
+    @classmethod
+    def from_arrays(cls, seq, qual, device, has_qual=None) -> "DeviceReads":
+        """seq / qual: (n_reads, read_len) uint8 numpy arrays (synth.reads)."""
+        import numpy as np
+        n, rl = seq.shape
+        flat = np.zeros(n * rl + 16, np.uint8)
+        flat[:n * rl] = seq.reshape(-1)
+        qf = np.zeros(n * rl + 16, np.uint8)
+        qf[:n * rl] = qual.reshape(-1)
+        off = np.arange(n + 1, dtype=np.int64) * rl
+        hq = np.ones(n, np.uint8) if has_qual is None else has_qual.astype(np.uint8)
+        t = lambda a: torch.from_numpy(a).to(device)  # noqa: E731
+        return cls(t(flat), t(qf), t(off), t(hq))
+
+    @property
+    def n_bases(self) -> int:
+        return int(self.off[-1].item())

@@ -157,3 +157,40 @@ def test_sh_device_reads_match_oracle(gpu, k, mq):
     o = O.OracleSH(k, 1)
     o.table = {int(a): np.array([c]) for a, c in zip(uk, cnt)}
     assert np.array_equal(out.cpu().numpy(), o.depth(g.tobytes(), k)[:, 0])
+
+
+def test_sh_mixed_read_lengths(gpu, tmp_path):
+    """Reads of 40..3000 bp: waves whose reads exceed the LDS staging capacity walk them from
+    global memory; both paths against the oracle."""
+    from kmer_hasher_amd import api, synth
+    g = synth.iid(200_000, 71)
+    rng = np.random.default_rng(72)
+    recs = []
+    for i in range(3000):
+        ln = int(rng.choice([40, 150, 151, 3000], p=[.3, .4, .2, .1]))
+        st = int(rng.integers(0, len(g) - ln))
+        s = g[st:st + ln].tobytes()
+        q = rng.integers(40, 75, ln).astype(np.uint8).tobytes()
+        recs.append(b"@r%d\n%s\n+\n%s\n" % (i, s, q))
+    p = str(tmp_path / "mixed.fq")
+    open(p, "wb").write(b"".join(recs))
+    for k, mq in [(21, 10), (31, 3)]:
+        ptr = api.count_kmers_fq_sh_rp(p, [k, 20, mq, 1, -1, 1, 1, 0])
+        keys, M = _sorted_table(ptr)
+        ok, om = O.OracleSH(k, 1).add_fastq(p, mq, 2**62, 0).arrays()
+        assert np.array_equal(keys, ok) and np.array_equal(M, om)
+
+
+@pytest.mark.parametrize("seed", range(10, 16))
+def test_sh_fuzz_fastx(gpu, seed, tmp_path):
+    """Random FASTX files (multi-line, CRLF, N runs, random phred, FASTA records first) at
+    several k and thresholds against the oracle: the per-base automaton of the kernel equals
+    the reference's nested iterator."""
+    from kmer_hasher_amd import api
+    p = str(tmp_path / "f.fq")
+    open(p, "wb").write(I.random_fastx(500, seed))
+    for k, mq in [(3, 0), (8, 15), (17, 25), (31, 5)]:
+        ptr = api.count_kmers_fq_sh_rp(p, [k, min(8, 2 * k), mq, 1, -1, 1, 2, 1])
+        keys, M = _sorted_table(ptr)
+        ok, om = O.OracleSH(k, 2).add_fastq(p, mq, 2**62, 1).arrays()
+        assert np.array_equal(keys, ok) and np.array_equal(M, om), (k, mq)
