@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round GPU check through gpurun: gpu tests, smoke, default bench line, rocprof kernel stats.
+#   bash tools/gpu_check.sh <tag>
+set -uo pipefail
+TAG=${1:-rNN}
+REPO=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$REPO/gpurun_out/check_$TAG
+mkdir -p "$OUT"
+cd "$REPO"
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  > "$OUT/pytest_gpu.log" 2>&1 || { echo "gpu tests failed"; tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+tail -3 "$OUT/pytest_gpu.log"
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+  || { echo "smoke failed"; tail -30 "$OUT/smoke.log"; exit 1; }
+cat "$OUT/smoke.log"
+timeout -k 10 300 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
+  || { echo "bench failed"; tail -30 "$OUT/bench.err"; exit 1; }
+cat "$OUT/bench.json"
+echo "check $TAG done"
