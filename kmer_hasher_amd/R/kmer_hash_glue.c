@@ -1,7 +1,7 @@
 /*
  * kmer_hash_glue.c -- R .Call bridge over the libkmhgpu C-ABI (include/kmhgpu.h).
  *
- * Drop-in for the index half of the reference's src/kmer_hash.c: the same three .Call
+ * Drop-in for the index and read-counting halves of the reference's src/kmer_hash.c: the .Call
  * symbols with the same arities (registration as in src/kmer_hash.c:1205-1224), the same
  * argument validation and error() texts, the same externalptr tag "kmer_hash_250930"
  * (src/kmer_hash.c:22) and return shapes:
@@ -11,6 +11,9 @@
  *   sequence_kmer_positions(ptr, seq, k)    src/kmer_hash.c:1151-1172 -> INTSXP 2 x H
  *   kmer_pair_pos(ptr_a, ptr_b)             src/kmer_hash.c:1174-1203 -> INTSXP 2 x M (fixed)
  *   count_kmers(hash_ptr, params, seq)      src/kmer_hash.c:548-591   -> EXTPTRSXP (counts)
+ *   count_kmers_fastq_sh_rp(ptr, params, f) src/kmer_hash.c:810-857   -> EXTPTRSXP (suffix_hash_n)
+ *   seq_kmer_depth_sh(ptr, seq, k)          src/kmer_hash.c:859-879   -> INTSXP counts_n x L
+ *   kmer_spectrum_suffix_hash_n(ptr, ...)   src/kmer_hash.c:1010-1039 -> REALSXP
  *
  * Differences, all deliberate: the finaliser frees the whole payload (the reference leaks the
  * 32-B khash_ptr, src/kmer_hash.c:56-66); a freed pointer is detected instead of dereferenced;
@@ -208,6 +211,101 @@ SEXP count_kmers(SEXP hash_ptr_r, SEXP params_r, SEXP seq_r) {
   return ptr;
 }
 
+/* ---- suffix_hash_n (read counting) ------------------------------------------------------
+ * Same tag as the reference's suffix hashes (src/kmer_hash.c:25), so pointers made here are
+ * refused by kmer.pos exactly as the reference refuses a suffix_hash_n. */
+static const char *suffix_hash_n_tag = "suffix_hash_n_250930";
+
+/* extract_ext_ptr(ptr, suffix_hash_n_tag), src/kmer_hash.c:41-52: NULL for anything else */
+static kmhg_index *gpu_sh_of(SEXP ptr_r) {
+  if (TYPEOF(ptr_r) != EXTPTRSXP) return NULL;
+  SEXP tag = R_ExternalPtrTag(ptr_r);
+  if (TYPEOF(tag) != STRSXP || length(tag) != 1 ||
+      strcmp(CHAR(STRING_ELT(tag, 0)), suffix_hash_n_tag))
+    return NULL;
+  return (kmhg_index *)R_ExternalPtrAddr(ptr_r);
+}
+
+static int gpu_sh_sources(kmhg_index *sh) {
+  kmhg_info info;
+  if (kmhg_index_info(sh, &info) != KMHG_OK) error("%s", kmhg_last_error());
+  return info.sources;
+}
+
+/* count_kmers_fastq_sh_rp, src/kmer_hash.c:810-857 (count.kmers.fq.sh.rp, kmer_hash.R:70-73):
+ * params = (k, prefix_bits, min_q, thread_n, max_reads, max_mem, source_n, source); the
+ * canonical k-mers of the FASTA/FASTQ file the quality iterator accepts, counted on the GPU
+ * into entry `source` of a new or the given suffix hash.  Validation order and texts as the
+ * reference (kmhg_sh_count_fastq repeats the k / source checks). */
+SEXP count_kmers_fastq_sh_rp(SEXP hash_ptr_r, SEXP params_r, SEXP fq_file_r) {
+  if (TYPEOF(fq_file_r) != STRSXP || length(fq_file_r) != 1)
+    error("fq_file should be a character vector of length at least one");
+  if (TYPEOF(params_r) != INTSXP || length(params_r) != 8)
+    error("k_r must be an integer vector of length 6 (k, prefix_bits, min_q, thread_n, "
+          "max_reads, max_mem, source_n, source");
+  const char *fq_file = CHAR(STRING_ELT(fq_file_r, 0));
+  kmhg_index *sh = gpu_sh_of(hash_ptr_r);
+  kmhg_index *out = sh;
+  if (kmhg_sh_count_fastq(&out, fq_file, (const int32_t *)INTEGER(params_r)) != KMHG_OK)
+    error("%s", kmhg_last_error());
+  if (sh) return hash_ptr_r;
+  SEXP tag = PROTECT(allocVector(STRSXP, 1));
+  SET_STRING_ELT(tag, 0, mkChar(suffix_hash_n_tag));
+  SEXP ptr = PROTECT(R_MakeExternalPtr(out, tag, R_NilValue));
+  R_RegisterCFinalizerEx(ptr, finalise_gpu_index, TRUE);
+  UNPROTECT(2);
+  return ptr;
+}
+
+/* seq_kmer_depth_sh, src/kmer_hash.c:859-879 (seq.kmer.depth.sh, kmer_hash.R:75-78):
+ * counts_n x L int matrix of the canonical k-mer counts along seq, written by the GPU. */
+SEXP seq_kmer_depth_sh(SEXP hash_ptr_r, SEXP seq_r, SEXP k_r) {
+  kmhg_index *sh = gpu_sh_of(hash_ptr_r);
+  if (!sh) error("unable to obtain suffix_hash_n from external pointer");
+  if (TYPEOF(k_r) != INTSXP || length(k_r) != 1) error("k_r should be a single integer");
+  const int k = asInteger(k_r);
+  if (TYPEOF(seq_r) != STRSXP || length(seq_r) != 1)
+    error("seq_r should be a character vector of length 1");
+  SEXP s = STRING_ELT(seq_r, 0);
+  const size_t L = (size_t)length(s);
+  SEXP counts_r = PROTECT(allocMatrix(INTSXP, gpu_sh_sources(sh), (int)L));
+  if (kmhg_sh_depth(sh, CHAR(s), L, k, INTEGER(counts_r)) != KMHG_OK) {
+    UNPROTECT(1);
+    error("Receieved error from seq_kmer_counts");
+  }
+  UNPROTECT(1);
+  return counts_r;
+}
+
+/* kmer_spectrum_suffix_hash_n, src/kmer_hash.c:1010-1039 (kmer.spec.sh.n, kmer_hash.R:88-91) */
+SEXP kmer_spectrum_suffix_hash_n(SEXP hash_ptr_r, SEXP max_count_r, SEXP comb_r,
+                                 SEXP comb_inner_r, SEXP source_min_r) {
+  kmhg_index *sh = gpu_sh_of(hash_ptr_r);
+  if (!sh) error("unable to obtain suffix_hash_n from external pointer");
+  if (TYPEOF(max_count_r) != INTSXP || length(max_count_r) != 1)
+    error("max_count_r should be a single integer");
+  if (TYPEOF(comb_r) != INTSXP || length(comb_r) < 1)
+    error("comb_r should be an integer vector of length > 0");
+  if (TYPEOF(comb_inner_r) != INTSXP || length(comb_inner_r) != length(comb_r))
+    error("comb_inner_r should be an integer vector of the same length as comb_r");
+  const int S = gpu_sh_sources(sh);
+  if (TYPEOF(source_min_r) != INTSXP || length(source_min_r) != S)
+    error("source_min_r should be an integer vector of length sh->counts_n");
+  const int max_count = asInteger(max_count_r);
+  if (max_count < 0) error("max_count must be >= 0");
+  const int comb_n = length(comb_r);
+  SEXP counts_r = PROTECT(allocMatrix(REALSXP, comb_n * S, max_count + 1));
+  int status = 1;
+  if (kmhg_sh_spectrum(sh, max_count, INTEGER(comb_r), INTEGER(comb_inner_r), comb_n,
+                       INTEGER(source_min_r), S, REAL(counts_r), &status) != KMHG_OK) {
+    UNPROTECT(1);
+    error("%s", kmhg_last_error());
+  }
+  if (status < 0) Rprintf("sh_count_spectrum_nc returned an error: %d\n", status);
+  UNPROTECT(1);
+  return counts_r;
+}
+
 /* Not in the reference: choose the kmer.pos k-mer order of an index, "first" (first
  * occurrence, the default) or "khash" (the reference's own bucket order, byte-identical
  * output).  KMHG_ROW_ORDER=khash in the environment sets the default for new indices. */
@@ -228,6 +326,9 @@ static const R_CallMethodDef gpu_call_methods[] = {
     {"sequence_kmer_positions", (DL_FUNC)&sequence_kmer_positions, 3},
     {"kmer_pair_pos", (DL_FUNC)&kmer_pair_pos, 2},
     {"count_kmers", (DL_FUNC)&count_kmers, 3},
+    {"count_kmers_fastq_sh_rp", (DL_FUNC)&count_kmers_fastq_sh_rp, 3},
+    {"seq_kmer_depth_sh", (DL_FUNC)&seq_kmer_depth_sh, 3},
+    {"kmer_spectrum_suffix_hash_n", (DL_FUNC)&kmer_spectrum_suffix_hash_n, 5},
     {"kmer_row_order", (DL_FUNC)&kmer_row_order, 2},
     {NULL, NULL, 0}};
 

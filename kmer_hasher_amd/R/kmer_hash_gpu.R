@@ -53,3 +53,23 @@ count.kmers <- function(seq, params, hash.ptr=NULL){
 kmer.row.order <- function(ex.ptr, order="khash"){
     invisible(.Call("kmer_row_order", ex.ptr, as.character(order)))
 }
+
+## canonical k-mer counts of a FASTA/FASTQ file (plain or gzip) into a suffix_hash_n pointer;
+## params = c(k, prefix_bits, min_q, thread_n, max_reads, max_mem, source_n, source)
+## (reference kmer_hash.R:70-73; counted on the GPU, prefix_bits / thread_n / max_mem only
+## change the reference's memory layout and threading, not the counts)
+count.kmers.fq.sh.rp <- function(fq.file, params, hash.ptr=NULL){
+    params <- as.integer(params)
+    .Call("count_kmers_fastq_sh_rp", hash.ptr, params, fq.file)
+}
+
+## counts_n x nchar(seq) matrix of canonical k-mer counts along seq (reference kmer_hash.R:75-78)
+seq.kmer.depth.sh <- function(hash.ptr, seq, k){
+    .Call("seq_kmer_depth_sh", hash.ptr, as.character(seq), as.integer(k))
+}
+
+## k-mer count spectra per source combination (reference kmer_hash.R:88-91)
+kmer.spec.sh.n <- function(ptr, max.count, comb, comb.inner, source.min){
+    .Call("kmer_spectrum_suffix_hash_n", ptr, as.integer(max.count),
+          as.integer(comb), as.integer(comb.inner), as.integer(source.min))
+}
