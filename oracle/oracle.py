@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 import subprocess
 
 import numpy as np
@@ -540,8 +541,19 @@ class RefSH:
 
     def add_fastq(self, path: str, k: int, prefix_bits: int, min_q: int, max_reads: int,
                   source_n: int, source: int, thread_n: int = 1) -> "RefSH":
-        self.h = self.lib.ref_sh_count_fastq(self.h, path.encode(), k, prefix_bits, min_q,
-                                             thread_n, max_reads, source_n, source)
+        # the reference's reader threads printf progress ("thread: 0 exit. ...") to stdout;
+        # send it to stderr so a caller's stdout (bench.py's one JSON line) stays clean
+        libc = C.CDLL(None)
+        sys.stdout.flush()
+        saved = os.dup(1)
+        try:
+            os.dup2(2, 1)
+            self.h = self.lib.ref_sh_count_fastq(self.h, path.encode(), k, prefix_bits, min_q,
+                                                 thread_n, max_reads, source_n, source)
+            libc.fflush(None)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         return self
 
     def arrays(self):
