@@ -703,6 +703,31 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   if (Nw <= 0) return q.release();
   const bool aligned = (reinterpret_cast<uintptr_t>(d_seq) & 15) == 0;
   const uint32_t nt = tiles_for(Nw);
+  // rows are written into a guessed capacity before the total is known (no host round trip
+  // inside the query); a query with more rows than the guess -- heavy repeats -- is redone
+  // by the two-pass path into an exact buffer
+  const uint64_t cap = (uint64_t)Nw + ((uint64_t)Nw >> 3) + 64;
+  q->rows.reset(cap);
+  // default: probe / scan / emit.  KMHG_QUERY=fused: one pass with a decoupled look-back
+  // (k_query_fused) -- measured slower (config 2: 0.403 ms against 0.365 ms for the three
+  // kernels; a tile that has probed waits for its predecessors' totals while holding its CU
+  // slot, and the probe is occupancy/latency bound), kept for A/B and covered by the tests
+  const char* qe = std::getenv("KMHG_QUERY");
+  const bool classic = !(qe && std::string(qe) == "fused");
+  uint64_t H = 0;
+  if (!classic) {
+    // one pass: probe + look-back + emit (k_query_fused); look-back words + ticket zeroed
+    DBuf<uint64_t> status((size_t)nt + 1, s);
+    HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
+    LAUNCH("k_query_fused", s,
+           launch_query_fused(d_seq, L, kq, idx->table.p, idx->geom, w0, w1, aligned,
+                              idx->positions.p, status.p, q->rows.p, cap, s));
+    HIPC(hipMemcpyAsync(&H, status.p + nt - 1, sizeof(H), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    H &= (1ull << 62) - 1;                       // LB_MASK: the last tile's inclusive prefix
+    q->H = (int64_t)H;
+    if (H <= cap) return q.release();
+  }
   DBuf<uint2> qinfo(Nw, s);
   // per-tile rows -> first row; [nt] = total; then the long-scan scratch
   DBuf<uint64_t> tiles((size_t)nt + 1 + scan_u64_scratch(nt), s);
@@ -712,22 +737,19 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
                             tile_row0, s));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, total + 1, s));
-  // emit into a guessed capacity before the total is known (no host round trip between the
-  // kernels); a query with more rows than the guess -- heavy repeats -- is emitted again
-  const uint64_t cap = (uint64_t)Nw + ((uint64_t)Nw >> 3) + 64;
-  q->rows.reset(cap);
-  LAUNCH("k_query_emit", s,
-         launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap, s));
-  uint64_t H = 0;
-  HIPC(hipMemcpyAsync(&H, total, sizeof(H), hipMemcpyDeviceToHost, s));
-  HIPC(hipStreamSynchronize(s));
-  q->H = (int64_t)H;
-  if (H > cap) {
-    q->rows.bind(s);
-    q->rows.reset(H);
+  if (classic) {
     LAUNCH("k_query_emit", s,
-           launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, H, s));
+           launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap,
+                             s));
+    HIPC(hipMemcpyAsync(&H, total, sizeof(H), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    q->H = (int64_t)H;
+    if (H <= cap) return q.release();
   }
+  q->rows.bind(s);
+  q->rows.reset(H);
+  LAUNCH("k_query_emit", s,
+         launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, H, s));
   return q.release();
 }
 

@@ -62,6 +62,11 @@ void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch
 void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
                        uint64_t cap, hipStream_t s);
+// probe + emit in one pass (ticketed tiles, decoupled look-back): `status` = grid_for(w1 - w0,
+// TILE) + 1 zeroed u64; the total row count comes back in status[nt - 1] & LB_MASK
+void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
+                        int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
+                        int2* out, uint64_t cap, hipStream_t s);
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint32_t* F,
                        hipStream_t s);
 void launch_read_order(const uint32_t* F, int64_t L, const Slot* T, uint64_t* st_a,

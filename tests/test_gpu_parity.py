@@ -225,3 +225,45 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr):
     _check_against_oracle(s, 31, pairs=False)
     rr = synth.repeat_rich(300_000, 42, n_gap_every=100_000).tobytes().decode("latin-1")
     _check_against_oracle(rr, 17, qks=[17], pairs=True)
+
+
+@pytest.mark.parametrize("path", ["fused", "classic"])
+def test_query_paths_vs_oracle(gpu, monkeypatch, path):
+    """seq.kmer.pos through the probe / scan / emit kernels (default; also the fused path's redo
+    when a query has more rows than the guessed capacity) and through the one-pass probe +
+    look-back + emit kernel (KMHG_QUERY=fused): ragged sizes around the 2048-window tile, windows
+    with 2-4 hits (lane-written) and > 4 hits (workgroup-dealt) in one slice, thousands of tiles
+    chained by the look-back, a query with far more rows than windows, and a query of another
+    sequence (misses)."""
+    from kmer_hasher_amd import synth
+    monkeypatch.setenv("KMHG_QUERY", path)
+    make, kpos, sqk = _api()
+    rng = np.random.default_rng(77)
+    for n in (40, 2047 + 30, 2048 + 30, 2049 + 30, 3 * 2048 + 7):
+        s = "".join(rng.choice(list("ACGT"), n))
+        oi = O.OracleIndex(s, 8)
+        ptr = make(s, 8)
+        for kq in (8, 6):
+            assert np.array_equal(sqk(ptr, s, kq).reshape(-1), oi.query(s, kq)), (n, kq)
+        ptr.free()
+    rr = synth.add_n_runs(synth.repeat_rich(1_500_000, 23, n_gap_every=300_000), 0.001, 4)
+    rr = rr.tobytes().decode("latin-1")
+    oi = O.OracleIndex(rr, 21)
+    ptr = make(rr, 21)
+    for kq in (21, 13):
+        assert np.array_equal(sqk(ptr, rr, kq).reshape(-1), oi.query(rr, kq)), kq
+    other = synth.iid(400_000, 24).tobytes().decode()
+    assert np.array_equal(sqk(ptr, other, 21).reshape(-1), oi.query(other, 21))
+    ptr.free()
+    s = synth.iid(6_000_000, 25).tobytes().decode()
+    oi = O.OracleIndex(s, 31)
+    ptr = make(s, 31)
+    assert np.array_equal(sqk(ptr, s, 31).reshape(-1), oi.query(s, 31))
+    ptr.free()
+    heavy = "AC" * 3000 + "ACGTTGCA" * 500 + "A" * 5000
+    oi = O.OracleIndex(heavy, 6)
+    ptr = make(heavy, 6)
+    q = sqk(ptr, heavy, 6)
+    assert q.shape[0] > 4 * len(heavy)
+    assert np.array_equal(q.reshape(-1), oi.query(heavy, 6))
+    ptr.free()
