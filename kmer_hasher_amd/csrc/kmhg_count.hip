@@ -95,6 +95,30 @@ k_count_canon(const uint32_t* __restrict__ row_slot, uint32_t U, uint32_t S,
   }
 }
 
+// C_adopt: the first batch merged into an empty counts index.  Every batch key is new, so the
+// batch table itself becomes the counts table: item r (slot perm_b[r], row r; or slot r, whose
+// row the scan of the occupancy flags gave) writes its row's key and count vector, the
+// slot <-> row maps, and rewrites its slot in place with the counts-index fields.  One pass in
+// place of probe / append / table rebuild / C_fix.
+__global__ void __launch_bounds__(BLOCK)
+k_count_adopt(const uint32_t* __restrict__ perm_b, uint32_t n_items, Slot* __restrict__ T,
+              const uint32_t* __restrict__ rank, uint32_t S, uint32_t source,
+              uint64_t* __restrict__ ckeys, int32_t* __restrict__ M,
+              uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot) {
+  const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
+  if (r >= n_items) return;
+  const uint32_t slot = perm_b ? perm_b[r] : r;
+  const uint4 v = *reinterpret_cast<const uint4*>(&T[slot]);
+  if (!v.z) return;                                     // slot walk: an empty slot
+  const uint32_t row = perm_b ? r : rank[r];
+  ckeys[row] = ((uint64_t)v.y << 32) | v.x;
+  int32_t* m = M + (uint64_t)row * S;
+  for (uint32_t j = 0; j < S; ++j) m[j] = j == source ? (int32_t)v.z : 0;
+  slot_row[slot] = row;
+  row_slot[row] = slot;
+  *reinterpret_cast<uint2*>(&T[slot].count) = make_uint2(S, S == 1 ? v.z : (row + 1) * S);
+}
+
 // values base, base + 1, ... of the key stream of a table rebuild
 __global__ void __launch_bounds__(BLOCK) k_iota_u32(uint32_t* __restrict__ a, uint64_t n,
                                                     uint32_t base) {
@@ -143,6 +167,12 @@ void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uin
                          hipStream_t s) {
   hipLaunchKernelGGL(k_count_insert, dim3(grid_of(U)), dim3(BLOCK), 0, s, ckeys, U, T, g, S, M,
                      slot_row, row_slot);
+}
+void launch_count_adopt(const uint32_t* perm_b, uint32_t n_items, Slot* T, const uint32_t* rank,
+                        uint32_t S, uint32_t source, uint64_t* ckeys, int32_t* M,
+                        uint32_t* slot_row, uint32_t* row_slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_count_adopt, dim3(grid_of(n_items)), dim3(BLOCK), 0, s, perm_b, n_items, T,
+                     rank, S, source, ckeys, M, slot_row, row_slot);
 }
 void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s) {
   hipLaunchKernelGGL(k_iota_u32, dim3(grid_cap(n)), dim3(BLOCK), 0, s, a, n, base);

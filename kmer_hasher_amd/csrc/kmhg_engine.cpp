@@ -846,6 +846,42 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_
   }
   const uint64_t ni = n_items;
   const uint32_t nt = tiles_for(ni);
+  // KMHG_COUNT_TABLE (tests): "rebuild" / "probe" take the general merge even for the first batch
+  const char* ct = std::getenv("KMHG_COUNT_TABLE");
+  if (U0 == 0 && !ct) {
+    // first batch into an empty index: every key is new and the batch table becomes the counts
+    // table (k_count_adopt) -- no probe, append, table rebuild or C_fix
+    uint32_t n_new = (uint32_t)Ub;
+    DBuf<uint32_t> rank(perm_b ? 1 : ni + 1, s);
+    if (!perm_b) {               // slot walk: rows = ranks of the occupied slots
+      DBuf<uint64_t> status((size_t)nt + 1, s);
+      HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
+      LAUNCH("k_count_probe", s,
+             launch_count_probe(nullptr, (uint32_t)ni, B->table.p, nullptr, idx->geom, nullptr, S,
+                                source, idx->positions.p, rank.p, s));
+      LAUNCH("k_scan_u32", s, launch_scan_u32(rank.p, ni, status.p, rank.p + ni, s));
+      HIPC(hipMemcpyAsync(&n_new, rank.p + ni, 4, hipMemcpyDeviceToHost, s));
+      HIPC(hipStreamSynchronize(s));
+    }
+    idx->table.bind(s);
+    idx->slot_row.bind(s);
+    idx->row_slot.bind(s);
+    idx->geom = B->geom;
+    idx->table.swap_with(B->table);          // B's release frees the old (empty) table
+    idx->slot_row.reset(idx->slots());
+    idx->row_slot.reset(n_new);
+    LAUNCH("k_count_adopt", s,
+           launch_count_adopt(perm_b, (uint32_t)ni, idx->table.p, rank.p, S, source,
+                              idx->ckeys.p, idx->positions.p, idx->slot_row.p, idx->row_slot.p,
+                              s));
+    idx->U = n_new;
+    idx->N = (uint64_t)n_new * S;
+    idx->P = (uint64_t)n_new * ((uint64_t)S * (S - 1) / 2);
+    idx->max_n = n_new ? S : 0;
+    idx->kmer_count += n_new;
+    idx->canon.ready = false;
+    return;
+  }
   DBuf<uint32_t> rank(ni + 1, s);                 // flags -> ranks of the new keys; [ni] = total
   DBuf<uint64_t> status((size_t)nt + 1, s);
   HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
@@ -866,7 +902,7 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_
   idx->table.bind(s);
   idx->slot_row.bind(s);
   idx->row_slot.bind(s);
-  const char* ct = std::getenv("KMHG_COUNT_TABLE");   // "probe": the fallback (tests)
+  // KMHG_COUNT_TABLE=probe: the fallback (tests)
   const bool probe_only = ct && std::string(ct) == "probe";
   std::unique_ptr<kmhg_index> K;
   bool ovf = true;
@@ -1114,8 +1150,8 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
   }
   const int64_t L = idx->L;
   const uint32_t U = (uint32_t)idx->U;
-  DBuf<uint32_t> F(L, s);
-  HIPC(hipMemsetAsync(F.p, 0xFF, (size_t)L * 4, s));
+  DBuf<uint2> F(L, s);
+  HIPC(hipMemsetAsync(F.p, 0xFF, (size_t)L * 8, s));
   if (U) LAUNCH("k_read_first", s, launch_read_first(idx->table.p, idx->slots(), idx->positions.p,
                                                      F.p, s));
   const uint32_t nt = tiles_for(L);
@@ -1133,7 +1169,7 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
   c.pkeys.reset(idx->N / 2 + 1);
   c.pair_off.reset(idx->N / 2 + 1);
   LAUNCH("k_read_order", s,
-         launch_read_order(F.p, L, idx->table.p, st_a, st_b, st_c, ticket, c.perm.p,
+         launch_read_order(F.p, L, st_a, st_b, st_c, ticket, c.perm.p,
                            c.canon_off.p, c.pkeys.p, c.pair_off.p, rm, s));
   ReadMeta h;
   HIPC(hipMemcpyAsync(&h, rm, sizeof(h), hipMemcpyDeviceToHost, s));

@@ -67,12 +67,12 @@ void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
 void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
                         int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
                         int2* out, uint64_t cap, hipStream_t s);
-void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint32_t* F,
+// F = L entries {slot, count} preset to slot NONE
+void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s);
-void launch_read_order(const uint32_t* F, int64_t L, const Slot* T, uint64_t* st_a,
-                       uint64_t* st_b, uint64_t* st_c, uint32_t* ticket, uint32_t* perm,
-                       uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
-                       ReadMeta* rmeta, hipStream_t s);
+void launch_read_order(const uint2* F, int64_t L, uint64_t* st_a, uint64_t* st_b,
+                       uint64_t* st_c, uint32_t* ticket, uint32_t* perm, uint32_t* canon_off,
+                       uint32_t* pkeys, uint64_t* pair_off, ReadMeta* rmeta, hipStream_t s);
 void launch_read_keys(const uint32_t* perm, uint32_t U, const Slot* T, int k, int32_t* out_counts,
                       char* out_kmers, hipStream_t s);
 void launch_gather_keys(const uint32_t* perm, uint32_t U, const Slot* T, uint64_t* out_keys,
@@ -167,6 +167,9 @@ void launch_count_append(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb,
 void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uint32_t S,
                          const int32_t* M, uint32_t* slot_row, uint32_t* row_slot,
                          hipStream_t s);
+void launch_count_adopt(const uint32_t* perm_b, uint32_t n_items, Slot* T, const uint32_t* rank,
+                        uint32_t S, uint32_t source, uint64_t* ckeys, int32_t* M,
+                        uint32_t* slot_row, uint32_t* row_slot, hipStream_t s);
 void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s);
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s);

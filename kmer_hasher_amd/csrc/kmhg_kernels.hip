@@ -537,14 +537,17 @@ k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
 // positions are [end - count, end).  Canonical k-mer order (first occurrence) is a slot
 // permutation `perm` built once per index (R_first + R_order) and cached.
 
-// R_first: F[first position - 1] = slot, for every occupied slot (positions ascend per key).
+// R_first: F[first position - 1] = {slot, count}, for every occupied slot (positions ascend per
+// key).  The count travels with the slot so that R_order reads F alone, in position order,
+// instead of gathering every key's slot again (a random 16-B read per key).
 __global__ void __launch_bounds__(BLOCK)
 k_read_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions,
-             uint32_t* __restrict__ F) {
+             uint2* __restrict__ F) {
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
        i += (uint64_t)gridDim.x * BLOCK) {
     uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
-    if (v.z) F[(v.z == 1 ? (int32_t)v.w : positions[v.w - v.z]) - 1] = (uint32_t)i;
+    if (v.z)
+      F[(v.z == 1 ? (int32_t)v.w : positions[v.w - v.z]) - 1] = make_uint2((uint32_t)i, v.z);
   }
 }
 
@@ -552,7 +555,7 @@ k_read_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restr
 // canonical pos-row offsets, and the list of keys that own pair rows with their pair offsets.
 // Three look-back chains: {keys, pos rows} packed 31|31, {multi keys}, {pair rows}.
 __global__ void __launch_bounds__(BLOCK)
-k_read_order(const uint32_t* __restrict__ F, int64_t L, const Slot* __restrict__ T,
+k_read_order(const uint2* __restrict__ F, int64_t L,
              uint64_t* __restrict__ st_a, uint64_t* __restrict__ st_b, uint64_t* __restrict__ st_c,
              uint32_t* __restrict__ ticket, uint32_t* __restrict__ perm,
              uint32_t* __restrict__ canon_off, uint32_t* __restrict__ pkeys,
@@ -569,8 +572,9 @@ k_read_order(const uint32_t* __restrict__ F, int64_t L, const Slot* __restrict__
 #pragma unroll
   for (int j = 0; j < WPT; ++j) {
     int64_t p = t0 + (int64_t)threadIdx.x * WPT + j;
-    id[j] = (p < L) ? F[p] : NONE;
-    uint64_t n = (id[j] != NONE) ? T[id[j]].count : 0;
+    const uint2 f = (p < L) ? F[p] : make_uint2(NONE, 0u);
+    id[j] = f.x;
+    uint64_t n = (id[j] != NONE) ? f.y : 0;
     va[j] = (id[j] != NONE) ? ((1ull << 32) | n) : 0;
     vb[j] = (n >= 2) ? 1 : 0;
     vc[j] = n * (n - (n ? 1 : 0)) / 2;
@@ -787,18 +791,17 @@ void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
   hipLaunchKernelGGL(k_query_fused, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, w0, w1,
                      aligned ? 1 : 0, positions, status, nt, out, cap);
 }
-void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint32_t* F,
+void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s) {
   unsigned g = grid_for(nslots, BLOCK);
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(k_read_first, dim3(g), dim3(BLOCK), 0, s, T, nslots, positions, F);
 }
-void launch_read_order(const uint32_t* F, int64_t L, const Slot* T, uint64_t* st_a,
-                       uint64_t* st_b, uint64_t* st_c, uint32_t* ticket, uint32_t* perm,
-                       uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
-                       ReadMeta* rmeta, hipStream_t s) {
+void launch_read_order(const uint2* F, int64_t L, uint64_t* st_a, uint64_t* st_b,
+                       uint64_t* st_c, uint32_t* ticket, uint32_t* perm, uint32_t* canon_off,
+                       uint32_t* pkeys, uint64_t* pair_off, ReadMeta* rmeta, hipStream_t s) {
   uint32_t nt = grid_for(L, TILE);
-  hipLaunchKernelGGL(k_read_order, dim3(nt), dim3(BLOCK), 0, s, F, L, T, st_a, st_b, st_c,
+  hipLaunchKernelGGL(k_read_order, dim3(nt), dim3(BLOCK), 0, s, F, L, st_a, st_b, st_c,
                      ticket, perm, canon_off, pkeys, pair_off, nt, rmeta);
 }
 void launch_read_keys(const uint32_t* perm, uint32_t U, const Slot* T, int k, int32_t* out_counts,

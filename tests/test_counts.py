@@ -148,13 +148,15 @@ def test_gpu_counts_golden_khash_order(gpu, cgold):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["partitioned", "probe"])
+@pytest.mark.parametrize("table", ["adopt", "rebuild", "probe"])
 def test_gpu_counts_first_order_vs_oracle(gpu, cgold, monkeypatch, table):
-    """Both ways of rebuilding the counts table: the partitioned build over the key list (the
-    default) and global linear probing (its overflow fallback, KMHG_COUNT_TABLE=probe)."""
+    """Every way of making the counts table: the first batch's own table adopted (the default
+    for a new pointer), the partitioned build over the key list (KMHG_COUNT_TABLE=rebuild; the
+    default for later batches) and global linear probing (its overflow fallback,
+    KMHG_COUNT_TABLE=probe)."""
     from kmer_hasher_amd import kmer_pos
-    if table == "probe":
-        monkeypatch.setenv("KMHG_COUNT_TABLE", "probe")
+    if table != "adopt":
+        monkeypatch.setenv("KMHG_COUNT_TABLE", table)
     for case, _ in cgold:
         oc = _oracle(case)
         ix = oc.index()

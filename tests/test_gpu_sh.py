@@ -32,9 +32,14 @@ def _sorted_table(ptr):
     return keys[o], M[o]
 
 
+@pytest.mark.parametrize("table", ["adopt", "rebuild"])
 @pytest.mark.parametrize("case", GOLD["cases"], ids=lambda c: c["name"])
-def test_sh_golden(gpu, case, inputs):
+def test_sh_golden(gpu, case, inputs, monkeypatch, table):
+    """`table`: the first batch's table adopted as the suffix hash (default) or rebuilt from
+    the key list (KMHG_COUNT_TABLE=rebuild, the path of every later batch)."""
     from kmer_hasher_amd import api
+    if table != "adopt":
+        monkeypatch.setenv("KMHG_COUNT_TABLE", table)
     files, genome = inputs
     ptr = None
     for f, pb, mq, mr, src in case["calls"]:
