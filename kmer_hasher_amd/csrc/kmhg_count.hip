@@ -95,28 +95,130 @@ k_count_canon(const uint32_t* __restrict__ row_slot, uint32_t U, uint32_t S,
   }
 }
 
-// C_adopt: the first batch merged into an empty counts index.  Every batch key is new, so the
-// batch table itself becomes the counts table: item r (slot perm_b[r], row r; or slot r, whose
-// row the scan of the occupancy flags gave) writes its row's key and count vector, the
-// slot <-> row maps, and rewrites its slot in place with the counts-index fields.  One pass in
-// place of probe / append / table rebuild / C_fix.
+// The first batch of count.kmers into a new pointer, rows in first-occurrence order without a
+// slot permutation: C_first scatters {slot, count, key} to the key's first position, C_order
+// compacts that array in position order straight into the rows (key, count vector, row_slot,
+// slot_row), C_slots rewrites the adopted table's slots in slot order.  The only random
+// accesses left are C_first's 16-B stores and C_order's slot_row stores.
 __global__ void __launch_bounds__(BLOCK)
-k_count_adopt(const uint32_t* __restrict__ perm_b, uint32_t n_items, Slot* __restrict__ T,
-              const uint32_t* __restrict__ rank, uint32_t S, uint32_t source,
+k_count_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions,
+              uint4* __restrict__ F) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
+       i += (uint64_t)gridDim.x * BLOCK) {
+    const uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+    if (v.z)
+      F[(v.z == 1 ? (int32_t)v.w : positions[v.w - v.z]) - 1] =
+          make_uint4((uint32_t)i, v.z, v.x, v.y);
+  }
+}
+
+// Compaction of one tile of TILE elements, element e = j * BLOCK + threadIdx.x (lane-contiguous:
+// every load and store of a step is coalesced).  The flagged elements get consecutive ranks in
+// element order -- (j, wave, lane) -- from per-(j, wave) ballots, offset by the flagged elements
+// of the tiles before (one look-back chain).  `cw` = LDS for WPT * 4 u64.
+__device__ __forceinline__ void tile_compact(const bool (&flag)[WPT], uint64_t (&rk)[WPT],
+                                             uint64_t* cw, uint64_t* status, uint32_t tile) {
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  constexpr int NW = BLOCK / 64;
+  uint64_t m[WPT];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) m[j] = __ballot(flag[j]);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) cw[j * NW + wave] = (uint64_t)__popcll(m[j]);
+  }
+  __syncthreads();
+  if (wave == 0) {                       // lanes 0 .. WPT*NW-1 own one (j, wave) count each
+    const uint64_t c = lane < WPT * NW ? cw[lane] : 0;
+    const uint64_t inc = wave_incl_scan(c);
+    const uint64_t tot = __shfl(inc, 63);
+    const uint64_t x = lookback_excl(status, tile, tot);
+    if (lane < WPT * NW) cw[lane] = x + inc - c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < WPT; ++j)
+    rk[j] = cw[j * NW + wave] + (uint64_t)__popcll(m[j] & lanemask_lt());
+}
+
+// F: L entries in position order, slot NONE where no key starts.  `ticket` orders the tiles.
+__global__ void __launch_bounds__(BLOCK)
+k_count_order(const uint4* __restrict__ F, int64_t L, uint64_t* __restrict__ status,
+              uint32_t* __restrict__ ticket, uint32_t S, uint32_t source,
               uint64_t* __restrict__ ckeys, int32_t* __restrict__ M,
               uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot) {
-  const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
-  if (r >= n_items) return;
-  const uint32_t slot = perm_b ? perm_b[r] : r;
-  const uint4 v = *reinterpret_cast<const uint4*>(&T[slot]);
-  if (!v.z) return;                                     // slot walk: an empty slot
-  const uint32_t row = perm_b ? r : rank[r];
-  ckeys[row] = ((uint64_t)v.y << 32) | v.x;
-  int32_t* m = M + (uint64_t)row * S;
-  for (uint32_t j = 0; j < S; ++j) m[j] = j == source ? (int32_t)v.z : 0;
-  slot_row[slot] = row;
-  row_slot[row] = slot;
-  *reinterpret_cast<uint2*>(&T[slot].count) = make_uint2(S, S == 1 ? v.z : (row + 1) * S);
+  __shared__ uint64_t cw[WPT * (BLOCK / 64)];
+  __shared__ uint32_t tk;
+  const uint32_t tile = take_ticket(ticket, &tk);
+  const int64_t t0 = (int64_t)tile * TILE;
+  uint4 f[WPT];
+  bool fl[WPT];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const int64_t p = t0 + (int64_t)j * BLOCK + threadIdx.x;
+    f[j] = p < L ? F[p] : make_uint4(NONE, 0u, 0u, 0u);
+    fl[j] = f[j].x != NONE;
+  }
+  uint64_t rk[WPT];
+  tile_compact(fl, rk, cw, status, tile);
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (!fl[j]) continue;
+    const uint64_t row = rk[j];
+    ckeys[row] = ((uint64_t)f[j].w << 32) | f[j].z;
+    int32_t* m = M + row * S;
+    for (uint32_t q = 0; q < S; ++q) m[q] = q == source ? (int32_t)f[j].y : 0;
+    row_slot[row] = f[j].x;
+    slot_row[f[j].x] = (uint32_t)row;
+  }
+}
+
+// The first batch into an empty suffix hash (order-free rows: slot order).  One pass over the
+// adopted table in tiles of TILE slots: occupied slots are compacted into rows, each writes its
+// row (key, count vector, row_slot), slot_row and its own slot fields -- every access coalesced.
+__global__ void __launch_bounds__(BLOCK)
+k_count_walk(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ status,
+             uint32_t* __restrict__ ticket, uint32_t S, uint32_t source,
+             uint64_t* __restrict__ ckeys, int32_t* __restrict__ M,
+             uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot) {
+  __shared__ uint64_t cw[WPT * (BLOCK / 64)];
+  __shared__ uint32_t tk;
+  const uint32_t tile = take_ticket(ticket, &tk);
+  const uint64_t t0 = (uint64_t)tile * TILE;
+  uint4 v[WPT];
+  bool fl[WPT];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    v[j] = i < nslots ? *reinterpret_cast<const uint4*>(&T[i]) : make_uint4(0u, 0u, 0u, 0u);
+    fl[j] = v[j].z != 0;
+  }
+  uint64_t rk[WPT];
+  tile_compact(fl, rk, cw, status, tile);
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (!fl[j]) continue;
+    const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    const uint64_t row = rk[j];
+    ckeys[row] = ((uint64_t)v[j].y << 32) | v[j].x;
+    int32_t* m = M + row * S;
+    for (uint32_t q = 0; q < S; ++q) m[q] = q == source ? (int32_t)v[j].z : 0;
+    row_slot[row] = (uint32_t)i;
+    slot_row[i] = (uint32_t)row;
+    *reinterpret_cast<uint2*>(&T[i].count) =
+        make_uint2(S, S == 1 ? v[j].z : ((uint32_t)row + 1) * S);
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_count_slots(Slot* __restrict__ T, uint64_t nslots, uint32_t S,
+              const uint32_t* __restrict__ slot_row) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
+       i += (uint64_t)gridDim.x * BLOCK) {
+    const uint32_t c = T[i].count;
+    if (!c) continue;
+    *reinterpret_cast<uint2*>(&T[i].count) = make_uint2(S, S == 1 ? c : (slot_row[i] + 1) * S);
+  }
 }
 
 // values base, base + 1, ... of the key stream of a table rebuild
@@ -168,11 +270,29 @@ void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uin
   hipLaunchKernelGGL(k_count_insert, dim3(grid_of(U)), dim3(BLOCK), 0, s, ckeys, U, T, g, S, M,
                      slot_row, row_slot);
 }
-void launch_count_adopt(const uint32_t* perm_b, uint32_t n_items, Slot* T, const uint32_t* rank,
-                        uint32_t S, uint32_t source, uint64_t* ckeys, int32_t* M,
-                        uint32_t* slot_row, uint32_t* row_slot, hipStream_t s) {
-  hipLaunchKernelGGL(k_count_adopt, dim3(grid_of(n_items)), dim3(BLOCK), 0, s, perm_b, n_items, T,
-                     rank, S, source, ckeys, M, slot_row, row_slot);
+void launch_count_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint4* F,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_count_first, dim3(grid_cap(nslots)), dim3(BLOCK), 0, s, T, nslots,
+                     positions, F);
+}
+void launch_count_order(const uint4* F, int64_t L, uint64_t* status, uint32_t* ticket, uint32_t S,
+                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
+                        uint32_t* row_slot, hipStream_t s) {
+  const unsigned nt = (unsigned)(((uint64_t)L + TILE - 1) / TILE);
+  hipLaunchKernelGGL(k_count_order, dim3(nt), dim3(BLOCK), 0, s, F, L, status, ticket, S, source,
+                     ckeys, M, slot_row, row_slot);
+}
+void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
+                       uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
+                       uint32_t* row_slot, hipStream_t s) {
+  const unsigned nt = (unsigned)((nslots + TILE - 1) / TILE);
+  hipLaunchKernelGGL(k_count_walk, dim3(nt), dim3(BLOCK), 0, s, T, nslots, status, ticket, S,
+                     source, ckeys, M, slot_row, row_slot);
+}
+void launch_count_slots(Slot* T, uint64_t nslots, uint32_t S, const uint32_t* slot_row,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_count_slots, dim3(grid_cap(nslots)), dim3(BLOCK), 0, s, T, nslots, S,
+                     slot_row);
 }
 void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s) {
   hipLaunchKernelGGL(k_iota_u32, dim3(grid_cap(n)), dim3(BLOCK), 0, s, a, n, base);

@@ -803,6 +803,63 @@ struct Release {                   // a batch index dies in stream order
 void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_t n_items,
                  uint32_t source, hipStream_t s);
 
+// Room for `need` rows in the count matrix (grown geometrically: repeated calls amortise the copy).
+void reserve_rows(kmhg_index* idx, uint64_t need, hipStream_t s) {
+  const uint32_t S = idx->sources;
+  const uint64_t U0 = idx->U;
+  if (need * S > (uint64_t)INT32_MAX)
+    fail(KMHG_EOVERFLOW, "counts index larger than 2^31-1 counts (R vector limit)");
+  if (need <= idx->rows_cap) return;
+  const uint64_t cap = std::max<uint64_t>(need, idx->rows_cap * 2);
+  DBuf<uint64_t> nk(cap);
+  DBuf<int32_t> nm(cap * S);
+  if (U0) {
+    HIPC(hipMemcpyAsync(nk.p, idx->ckeys.p, U0 * 8, hipMemcpyDeviceToDevice, s));
+    HIPC(hipMemcpyAsync(nm.p, idx->positions.p, U0 * S * 4, hipMemcpyDeviceToDevice, s));
+  }
+  idx->ckeys.bind(s);
+  idx->positions.bind(s);
+  idx->ckeys.swap_with(nk);
+  idx->positions.swap_with(nm);
+  idx->rows_cap = cap;
+}
+
+// The first batch into an empty counts index: every key is new, the batch table becomes the
+// counts table, and the rows (first-occurrence order) come from C_first / C_order / C_slots
+// (kmhg_count.hip) -- no slot permutation, probe, append, table rebuild or C_fix.
+void adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, hipStream_t s) {
+  const uint32_t S = idx->sources;
+  const uint64_t Ub = B->U;
+  const int64_t L = B->L;
+  reserve_rows(idx, Ub, s);
+  DBuf<uint4> F(L, s);
+  HIPC(hipMemsetAsync(F.p, 0xFF, (size_t)L * 16, s));
+  LAUNCH("k_count_first", s,
+         launch_count_first(B->table.p, B->slots(), B->positions.p, F.p, s));
+  const uint64_t nt = ((uint64_t)L + TILE - 1) / TILE;
+  DBuf<uint64_t> status(nt + 1, s);                // look-back words + the tile ticket
+  HIPC(hipMemsetAsync(status.p, 0, (nt + 1) * 8, s));
+  idx->table.bind(s);
+  idx->slot_row.bind(s);
+  idx->row_slot.bind(s);
+  idx->geom = B->geom;
+  idx->table.swap_with(B->table);                  // B's release frees the old (empty) table
+  idx->slot_row.reset(idx->slots());
+  idx->row_slot.reset(Ub);
+  LAUNCH("k_count_order", s,
+         launch_count_order(F.p, L, status.p, reinterpret_cast<uint32_t*>(status.p + nt), S,
+                            source, idx->ckeys.p, idx->positions.p, idx->slot_row.p,
+                            idx->row_slot.p, s));
+  LAUNCH("k_count_slots", s,
+         launch_count_slots(idx->table.p, idx->slots(), S, idx->slot_row.p, s));
+  idx->U = Ub;
+  idx->N = Ub * S;
+  idx->P = Ub * ((uint64_t)S * (S - 1) / 2);
+  idx->max_n = Ub ? S : 0;
+  idx->kmer_count += Ub;
+  idx->canon.ready = false;
+}
+
 void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t source,
                   hipStream_t s) {
   idx->stream = s;
@@ -813,8 +870,13 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
   finish_build(B.get());
   B->stream = s;
   if (!B->U) return;
-  prepare_canon(B.get(), s);       // batch keys in first-occurrence order
-  merge_batch(idx, B.get(), B->canon.perm.p, B->U, source, s);
+  // KMHG_COUNT_TABLE (tests): "rebuild" / "probe" take the general merge for the first batch too
+  if (idx->U == 0 && !std::getenv("KMHG_COUNT_TABLE")) {
+    adopt_first_batch(idx, B.get(), source, s);
+  } else {
+    prepare_canon(B.get(), s);     // batch keys in first-occurrence order
+    merge_batch(idx, B.get(), B->canon.perm.p, B->U, source, s);
+  }
   idx->L += L;
 }
 
@@ -827,53 +889,35 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_
   const uint32_t S = idx->sources;
   const uint64_t Ub = B->U;
   const uint64_t U0 = idx->U;
-  const uint64_t need = U0 + Ub;
-  if (need * S > (uint64_t)INT32_MAX)
-    fail(KMHG_EOVERFLOW, "counts index larger than 2^31-1 counts (R vector limit)");
-  if (need > idx->rows_cap) {      // grow geometrically: repeated calls amortise the copy
-    const uint64_t cap = std::max<uint64_t>(need, idx->rows_cap * 2);
-    DBuf<uint64_t> nk(cap);
-    DBuf<int32_t> nm(cap * S);
-    if (U0) {
-      HIPC(hipMemcpyAsync(nk.p, idx->ckeys.p, U0 * 8, hipMemcpyDeviceToDevice, s));
-      HIPC(hipMemcpyAsync(nm.p, idx->positions.p, U0 * S * 4, hipMemcpyDeviceToDevice, s));
-    }
-    idx->ckeys.bind(s);
-    idx->positions.bind(s);
-    idx->ckeys.swap_with(nk);
-    idx->positions.swap_with(nm);
-    idx->rows_cap = cap;
-  }
+  reserve_rows(idx, U0 + Ub, s);
   const uint64_t ni = n_items;
   const uint32_t nt = tiles_for(ni);
   // KMHG_COUNT_TABLE (tests): "rebuild" / "probe" take the general merge even for the first batch
   const char* ct = std::getenv("KMHG_COUNT_TABLE");
-  if (U0 == 0 && !ct) {
-    // first batch into an empty index: every key is new and the batch table becomes the counts
-    // table (k_count_adopt) -- no probe, append, table rebuild or C_fix
-    uint32_t n_new = (uint32_t)Ub;
-    DBuf<uint32_t> rank(perm_b ? 1 : ni + 1, s);
-    if (!perm_b) {               // slot walk: rows = ranks of the occupied slots
-      DBuf<uint64_t> status((size_t)nt + 1, s);
-      HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
-      LAUNCH("k_count_probe", s,
-             launch_count_probe(nullptr, (uint32_t)ni, B->table.p, nullptr, idx->geom, nullptr, S,
-                                source, idx->positions.p, rank.p, s));
-      LAUNCH("k_scan_u32", s, launch_scan_u32(rank.p, ni, status.p, rank.p + ni, s));
-      HIPC(hipMemcpyAsync(&n_new, rank.p + ni, 4, hipMemcpyDeviceToHost, s));
-      HIPC(hipStreamSynchronize(s));
-    }
+  if (U0 == 0 && !ct && !perm_b) {
+    // first batch into an empty suffix hash: every key is new and the batch table becomes the
+    // counts table, its occupied slots compacted into rows in slot order in one pass
+    // (k_count_walk) -- no probe, append, table rebuild or C_fix.  (count.kmers batches take
+    // adopt_first_batch: rows in first-occurrence order.)
+    const uint64_t ns = B->slots();
+    const uint64_t nw = (ns + TILE - 1) / TILE;
+    DBuf<uint64_t> status(nw + 1, s);            // look-back words + the tile ticket
+    HIPC(hipMemsetAsync(status.p, 0, (nw + 1) * 8, s));
     idx->table.bind(s);
     idx->slot_row.bind(s);
     idx->row_slot.bind(s);
     idx->geom = B->geom;
     idx->table.swap_with(B->table);          // B's release frees the old (empty) table
-    idx->slot_row.reset(idx->slots());
-    idx->row_slot.reset(n_new);
-    LAUNCH("k_count_adopt", s,
-           launch_count_adopt(perm_b, (uint32_t)ni, idx->table.p, rank.p, S, source,
-                              idx->ckeys.p, idx->positions.p, idx->slot_row.p, idx->row_slot.p,
-                              s));
+    idx->slot_row.reset(ns);
+    idx->row_slot.reset(Ub);                 // B->U: exact, or an upper bound after an overflow
+    LAUNCH("k_count_walk", s,
+           launch_count_walk(idx->table.p, ns, status.p, reinterpret_cast<uint32_t*>(status.p + nw),
+                             S, source, idx->ckeys.p, idx->positions.p, idx->slot_row.p,
+                             idx->row_slot.p, s));
+    uint64_t last = 0;                       // the last tile's inclusive prefix = rows written
+    HIPC(hipMemcpyAsync(&last, status.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    const uint64_t n_new = last & ((1ull << 62) - 1);   // LB_MASK: payload of a status word
     idx->U = n_new;
     idx->N = (uint64_t)n_new * S;
     idx->P = (uint64_t)n_new * ((uint64_t)S * (S - 1) / 2);

@@ -167,9 +167,20 @@ void launch_count_append(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb,
 void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uint32_t S,
                          const int32_t* M, uint32_t* slot_row, uint32_t* row_slot,
                          hipStream_t s);
-void launch_count_adopt(const uint32_t* perm_b, uint32_t n_items, Slot* T, const uint32_t* rank,
-                        uint32_t S, uint32_t source, uint64_t* ckeys, int32_t* M,
-                        uint32_t* slot_row, uint32_t* row_slot, hipStream_t s);
+// first batch into a new count.kmers pointer: F = L entries {slot, count, key} preset to slot
+// NONE; `status` = ceil(L / TILE) zeroed look-back words, `ticket` a zeroed u32
+void launch_count_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint4* F,
+                        hipStream_t s);
+void launch_count_order(const uint4* F, int64_t L, uint64_t* status, uint32_t* ticket, uint32_t S,
+                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
+                        uint32_t* row_slot, hipStream_t s);
+void launch_count_slots(Slot* T, uint64_t nslots, uint32_t S, const uint32_t* slot_row,
+                        hipStream_t s);
+// first batch into a new suffix hash: rows in slot order; `status` = ceil(nslots / TILE) zeroed
+// look-back words, `ticket` a zeroed u32
+void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
+                       uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
+                       uint32_t* row_slot, hipStream_t s);
 void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s);
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s);
