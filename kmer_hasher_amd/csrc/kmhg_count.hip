@@ -81,14 +81,16 @@ k_count_insert(const uint64_t* __restrict__ ckeys, uint32_t U, Slot* __restrict_
 }
 
 __global__ void __launch_bounds__(BLOCK)
-k_count_canon(const uint32_t* __restrict__ row_slot, uint32_t U, uint32_t S,
-              uint32_t* __restrict__ perm, uint32_t* __restrict__ canon_off,
-              uint32_t* __restrict__ pkeys, uint64_t* __restrict__ pair_off) {
+k_count_canon(const uint32_t* __restrict__ row_slot, const int32_t* __restrict__ M, uint32_t U,
+              uint32_t S, uint32_t* __restrict__ perm, uint32_t* __restrict__ canon_off,
+              uint32_t* __restrict__ pkeys, uint64_t* __restrict__ pair_off,
+              uint2* __restrict__ rinfo) {
   const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
   if (r > U) return;
   canon_off[r] = r * S;
   if (r == U) return;
   perm[r] = row_slot[r];
+  rinfo[r] = make_uint2(S, S == 1 ? (uint32_t)M[r] : (r + 1) * S);   // the slot's {count, aux}
   if (S >= 2) {
     pkeys[r] = r;
     pair_off[r] = (uint64_t)r * ((uint64_t)S * (S - 1) / 2);
@@ -302,11 +304,11 @@ void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, ui
   hipLaunchKernelGGL(k_count_fix, dim3(grid_cap(nslots)), dim3(BLOCK), 0, s, T, nslots, S, M,
                      slot_row, row_slot);
 }
-void launch_count_canon(const uint32_t* row_slot, uint32_t U, uint32_t S, uint32_t* perm,
-                        uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
-                        hipStream_t s) {
+void launch_count_canon(const uint32_t* row_slot, const int32_t* M, uint32_t U, uint32_t S,
+                        uint32_t* perm, uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
+                        uint2* rinfo, hipStream_t s) {
   hipLaunchKernelGGL(k_count_canon, dim3(grid_of((uint64_t)U + 1)), dim3(BLOCK), 0, s, row_slot,
-                     U, S, perm, canon_off, pkeys, pair_off);
+                     M, U, S, perm, canon_off, pkeys, pair_off, rinfo);
 }
 
 }  // namespace kmhg

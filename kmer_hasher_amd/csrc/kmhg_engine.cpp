@@ -377,6 +377,7 @@ struct Canon {              // readout order arrays (first occurrence or khash),
   int order = KMHG_ORDER_FIRST;   // which order the arrays below hold
   DBuf<uint32_t> perm, canon_off, pkeys;
   DBuf<uint64_t> pair_off;
+  DBuf<uint2> rinfo;        // {count, aux} of each row's slot (readout kernels read rows in order)
   uint64_t n_multi = 0;
 };
 
@@ -413,6 +414,7 @@ struct kmhg_index {
   void bind_all(hipStream_t s) {
     table.bind(s); positions.bind(s); ckeys.bind(s); slot_row.bind(s); row_slot.bind(s);
     canon.perm.bind(s); canon.canon_off.bind(s); canon.pkeys.bind(s); canon.pair_off.bind(s);
+    canon.rinfo.bind(s);
   }
 };
 
@@ -1186,8 +1188,10 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
     c.canon_off.reset(U + 1);
     c.pkeys.reset(S >= 2 ? U : 1);
     c.pair_off.reset(S >= 2 ? U : 1);
-    LAUNCH("k_count_canon", s, launch_count_canon(idx->row_slot.p, U, S, c.perm.p, c.canon_off.p,
-                                                  c.pkeys.p, c.pair_off.p, s));
+    c.rinfo.reset(U);
+    LAUNCH("k_count_canon", s, launch_count_canon(idx->row_slot.p, idx->positions.p, U, S, c.perm.p,
+                                                  c.canon_off.p, c.pkeys.p, c.pair_off.p,
+                                                  c.rinfo.p, s));
     c.n_multi = S >= 2 ? U : 0;
     c.ready = true;
     return;
@@ -1209,12 +1213,13 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
   ReadMeta* rm = reinterpret_cast<ReadMeta*>(scratch.p + (size_t)nt * 24 + 64);
   c.perm.reset(U);
   c.canon_off.reset(U + 1);
+  c.rinfo.reset(U);
   // keys with >= 2 positions: at most N/2
   c.pkeys.reset(idx->N / 2 + 1);
   c.pair_off.reset(idx->N / 2 + 1);
   LAUNCH("k_read_order", s,
-         launch_read_order(F.p, L, st_a, st_b, st_c, ticket, c.perm.p,
-                           c.canon_off.p, c.pkeys.p, c.pair_off.p, rm, s));
+         launch_read_order(F.p, L, idx->table.p, st_a, st_b, st_c, ticket, c.perm.p,
+                           c.canon_off.p, c.pkeys.p, c.pair_off.p, c.rinfo.p, rm, s));
   ReadMeta h;
   HIPC(hipMemcpyAsync(&h, rm, sizeof(h), hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -1302,26 +1307,26 @@ void prepare_readout(kmhg_index* idx, hipStream_t s) {
   const uint32_t U = (uint32_t)idx->U;
   std::vector<uint64_t> keys(U);
   std::vector<uint32_t> perm(U);
-  std::vector<int32_t> cnt(U);
+  std::vector<uint2> info(U);
   if (U) {
     DBuf<uint64_t> dk(U, s);
-    DBuf<int32_t> dc(U, s);
     LAUNCH("k_gather_keys", s, launch_gather_keys(c.perm.p, U, idx->table.p, dk.p, s));
-    LAUNCH("k_read_keys", s, launch_read_keys(c.perm.p, U, idx->table.p, idx->k, dc.p, nullptr, s));
     HIPC(hipMemcpyAsync(keys.data(), dk.p, (size_t)U * 8, hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(cnt.data(), dc.p, (size_t)U * 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(info.data(), c.rinfo.p, (size_t)U * 8, hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(perm.data(), c.perm.p, (size_t)U * 4, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
   }
   const std::vector<uint32_t> order = khash_bucket_order(keys);
   if (order.size() != U) fail(KMHG_EDEVICE, "khash order replay lost keys (internal error)");
   std::vector<uint32_t> perm_k(U), off_k(U + 1), pkeys;
+  std::vector<uint2> info_k(U);
   std::vector<uint64_t> pair_off;
   uint64_t rows = 0, pairs = 0;
   for (uint32_t r = 0; r < U; ++r) {
     const uint32_t id = order[r];
-    const uint64_t n = (uint64_t)cnt[id];
+    const uint64_t n = (uint64_t)info[id].x;
     perm_k[r] = perm[id];
+    info_k[r] = info[id];
     off_k[r] = (uint32_t)rows;
     rows += n;
     if (n >= 2) {
@@ -1335,6 +1340,7 @@ void prepare_readout(kmhg_index* idx, hipStream_t s) {
     fail(KMHG_EDEVICE, "khash readout order inconsistent with the index (internal error)");
   if (U) {
     HIPC(hipMemcpyAsync(c.perm.p, perm_k.data(), (size_t)U * 4, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(c.rinfo.p, info_k.data(), (size_t)U * 8, hipMemcpyHostToDevice, s));
     HIPC(hipMemcpyAsync(c.canon_off.p, off_k.data(), (size_t)(U + 1) * 4, hipMemcpyHostToDevice, s));
   }
   if (!pkeys.empty()) {
@@ -1363,17 +1369,21 @@ void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, 
   const uint32_t U = (uint32_t)idx->U;
   if ((opt & (KMHG_OPT_KMER | KMHG_OPT_COUNT)) && U)
     LAUNCH("k_read_keys", s,
-           launch_read_keys(c.perm.p, U, idx->table.p, idx->k,
+           launch_read_keys(c.perm.p, c.rinfo.p, U, idx->table.p, idx->k,
                             (opt & KMHG_OPT_COUNT) ? counts : nullptr,
                             (opt & KMHG_OPT_KMER) ? kmers : nullptr, s));
-  if ((opt & KMHG_OPT_POS) && idx->N)
+  if ((opt & KMHG_OPT_POS) && idx->N) {
+    DBuf<uint32_t> tile_key((size_t)read_pos_tiles(idx->N) + 1, s);
     LAUNCH("k_read_pos", s,
-           launch_read_pos(c.perm.p, c.canon_off.p, U, idx->N, idx->table.p, idx->positions.p,
+           launch_read_pos(c.rinfo.p, c.canon_off.p, U, idx->N, idx->positions.p, tile_key.p,
                            reinterpret_cast<int2*>(pos), s));
-  if ((opt & KMHG_OPT_PAIRS) && idx->P)
+  }
+  if ((opt & KMHG_OPT_PAIRS) && idx->P) {
+    DBuf<uint32_t> tile_key((size_t)read_pairs_tiles(idx->P) + 1, s);
     LAUNCH("k_read_pairs", s,
-           launch_read_pairs(c.pkeys.p, c.pair_off.p, (uint32_t)c.n_multi, idx->P, c.perm.p,
-                             idx->table.p, idx->positions.p, pairs, s));
+           launch_read_pairs(c.pkeys.p, c.pair_off.p, (uint32_t)c.n_multi, idx->P, c.rinfo.p,
+                             idx->positions.p, tile_key.p, pairs, s));
+  }
 }
 
 }  // namespace

@@ -70,18 +70,23 @@ void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
 // F = L entries {slot, count} preset to slot NONE
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s);
-void launch_read_order(const uint2* F, int64_t L, uint64_t* st_a, uint64_t* st_b,
+// rinfo[c] = {count, aux} of row c's slot, so the readout kernels below read rows in order
+// instead of gathering T[perm[c]] (only the k-mer strings need the slot itself)
+void launch_read_order(const uint2* F, int64_t L, const Slot* T, uint64_t* st_a, uint64_t* st_b,
                        uint64_t* st_c, uint32_t* ticket, uint32_t* perm, uint32_t* canon_off,
-                       uint32_t* pkeys, uint64_t* pair_off, ReadMeta* rmeta, hipStream_t s);
-void launch_read_keys(const uint32_t* perm, uint32_t U, const Slot* T, int k, int32_t* out_counts,
-                      char* out_kmers, hipStream_t s);
+                       uint32_t* pkeys, uint64_t* pair_off, uint2* rinfo, ReadMeta* rmeta,
+                       hipStream_t s);
+void launch_read_keys(const uint32_t* perm, const uint2* rinfo, uint32_t U, const Slot* T, int k,
+                      int32_t* out_counts, char* out_kmers, hipStream_t s);
 void launch_gather_keys(const uint32_t* perm, uint32_t U, const Slot* T, uint64_t* out_keys,
                         hipStream_t s);
-void launch_read_pos(const uint32_t* perm, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
-                     const Slot* T, const int32_t* positions, int2* out, hipStream_t s);
+void launch_read_pos(const uint2* rinfo, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
+                     const int32_t* positions, uint32_t* tile_key, int2* out, hipStream_t s);
+uint32_t read_pos_tiles(uint64_t nrows);     // tile_key holds read_pos_tiles(nrows) + 1 u32
 void launch_read_pairs(const uint32_t* pkeys, const uint64_t* pair_off, uint32_t M,
-                       uint64_t nrows, const uint32_t* perm, const Slot* T,
-                       const int32_t* positions, int32_t* out, hipStream_t s);
+                       uint64_t nrows, const uint2* rinfo, const int32_t* positions,
+                       uint32_t* tile_key, int32_t* out, hipStream_t s);
+uint32_t read_pairs_tiles(uint64_t nrows);   // tile_key holds read_pairs_tiles(nrows) + 1 u32
 // radix digit of a bucket id: floor(b / div) mod R via magic multipliers (see digit_of)
 struct Digit {
   uint64_t mdiv;   // ceil(2^64 / div), 0 for div = 1
@@ -184,9 +189,9 @@ void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* tic
 void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s);
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s);
-void launch_count_canon(const uint32_t* row_slot, uint32_t U, uint32_t S, uint32_t* perm,
-                        uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
-                        hipStream_t s);
+void launch_count_canon(const uint32_t* row_slot, const int32_t* M, uint32_t U, uint32_t S,
+                        uint32_t* perm, uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
+                        uint2* rinfo, hipStream_t s);
 
 #ifdef KMHG_STAMPS
 void set_stamp_buffer(uint64_t* p);

@@ -555,11 +555,12 @@ k_read_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restr
 // canonical pos-row offsets, and the list of keys that own pair rows with their pair offsets.
 // Three look-back chains: {keys, pos rows} packed 31|31, {multi keys}, {pair rows}.
 __global__ void __launch_bounds__(BLOCK)
-k_read_order(const uint2* __restrict__ F, int64_t L,
+k_read_order(const uint2* __restrict__ F, int64_t L, const Slot* __restrict__ T,
              uint64_t* __restrict__ st_a, uint64_t* __restrict__ st_b, uint64_t* __restrict__ st_c,
              uint32_t* __restrict__ ticket, uint32_t* __restrict__ perm,
              uint32_t* __restrict__ canon_off, uint32_t* __restrict__ pkeys,
-             uint64_t* __restrict__ pair_off, uint32_t ntiles, ReadMeta* __restrict__ rmeta) {
+             uint64_t* __restrict__ pair_off, uint2* __restrict__ rinfo, uint32_t ntiles,
+             ReadMeta* __restrict__ rmeta) {
   __shared__ uint64_t sh[8];
   __shared__ uint64_t ex_sh[3];
   __shared__ uint32_t tk;
@@ -606,6 +607,11 @@ k_read_order(const uint2* __restrict__ F, int64_t L,
     if (id[j] == NONE) continue;
     perm[ca] = id[j];
     canon_off[ca] = (uint32_t)ra;
+    // the row's slot fields {count, aux}: a key seen once starts here (aux = its position),
+    // only a repeated key's list end needs its slot
+    const uint32_t n = (uint32_t)(va[j] & 0xFFFFFFFFull);
+    rinfo[ca] = make_uint2(n, n == 1 ? (uint32_t)(t0 + (int64_t)threadIdx.x * WPT + j + 1)
+                                     : T[id[j]].aux);
     if (vb[j]) { pkeys[cb] = (uint32_t)ca; pair_off[cb] = cc; ++cb; }
     ++ca; ra += va[j] & 0xFFFFFFFFull; cc += vc[j];
   }
@@ -613,14 +619,14 @@ k_read_order(const uint2* __restrict__ F, int64_t L,
 
 // R_keys: counts (opt 8) and k-mer strings (opt 1) in canonical order.
 __global__ void __launch_bounds__(BLOCK)
-k_read_keys(const uint32_t* __restrict__ perm, uint32_t U, const Slot* __restrict__ T, int k,
-            int32_t* __restrict__ out_counts, char* __restrict__ out_kmers) {
+k_read_keys(const uint32_t* __restrict__ perm, const uint2* __restrict__ rinfo, uint32_t U,
+            const Slot* __restrict__ T, int k, int32_t* __restrict__ out_counts,
+            char* __restrict__ out_kmers) {
   const char NUC[4] = {'A', 'C', 'T', 'G'};             // src/kmer_hash.c:21
   for (uint32_t c = blockIdx.x * BLOCK + threadIdx.x; c < U; c += gridDim.x * BLOCK) {
-    const uint4 v = *reinterpret_cast<const uint4*>(&T[perm[c]]);
-    if (out_counts) out_counts[c] = (int32_t)v.z;
-    if (out_kmers) {
-      uint64_t key = ((uint64_t)v.y << 32) | v.x;
+    if (out_counts) out_counts[c] = (int32_t)rinfo[c].x;
+    if (out_kmers) {                                    // the key needs the slot itself
+      uint64_t key = T[perm[c]].key;
       char* o = out_kmers + (size_t)c * (k + 1);
       for (int i = k - 1; i >= 0; --i) { o[i] = NUC[key & 3]; key >>= 2; }
       o[k] = 0;
@@ -637,78 +643,156 @@ k_gather_keys(const uint32_t* __restrict__ perm, uint32_t U, const Slot* __restr
 }
 
 // R_pos: rows (i, pos) in canonical order.  Each workgroup owns TILE output rows; every key
-// owns >= 1 row so its key range fits the LDS copy of the canonical offsets.
+// owns >= 1 row so its key range fits the LDS copy of the canonical offsets.  The key holding
+// each tile's first row comes from R_tiles (no per-workgroup search of the global offsets);
+// rows are staged in LDS and leave as 16-B stores.
+// R_tiles: tile_key[t] = the key holding row t*tile (every row belongs to one key);
+// tile_key[ntiles] = nkeys - 1.
+template <class Off>
 __global__ void __launch_bounds__(BLOCK)
-k_read_pos(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ canon_off, uint32_t U,
-           uint64_t nrows, const Slot* __restrict__ T, const int32_t* __restrict__ positions,
-           int2* __restrict__ out) {
-  __shared__ uint32_t off[TILE + 1];
-  __shared__ uint32_t cr[2];
-  const uint64_t r0 = (uint64_t)blockIdx.x * TILE;
-  if (r0 >= nrows) return;
-  const uint64_t r1 = min(nrows, r0 + TILE);
-  if (threadIdx.x < 2) {            // key holding row r0 / row r1-1: last c with off[c] <= r
-    uint64_t r = threadIdx.x == 0 ? r0 : r1 - 1;
-    uint32_t lo = 0, hi = U - 1;
-    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (canon_off[mid] <= r) lo = mid; else hi = mid - 1; }
-    cr[threadIdx.x] = lo;
+k_row_tiles(const Off* __restrict__ off, uint32_t nkeys, uint64_t nrows, uint32_t tile,
+            uint32_t* __restrict__ tile_key, uint32_t ntiles) {
+  for (uint32_t m = blockIdx.x * BLOCK + threadIdx.x; m < nkeys; m += gridDim.x * BLOCK) {
+    const uint64_t lo = off[m], hi = m + 1 < nkeys ? (uint64_t)off[m + 1] : nrows;
+    for (uint64_t t = (lo + tile - 1) / tile; t * tile < hi; ++t) tile_key[t] = m;
   }
-  __syncthreads();
-  const uint32_t c0 = cr[0], nk = cr[1] - cr[0] + 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) tile_key[ntiles] = nkeys - 1;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_read_pos(const uint2* __restrict__ rinfo, const uint32_t* __restrict__ canon_off,
+           const uint32_t* __restrict__ tile_key, uint64_t nrows,
+           const int32_t* __restrict__ positions, int2* __restrict__ out) {
+  __shared__ uint32_t off[TILE + 1];
+  __shared__ __attribute__((aligned(16))) int2 stage[TILE];
+  const uint64_t r0 = (uint64_t)blockIdx.x * TILE;
+  const uint64_t r1 = min(nrows, r0 + TILE);
+  const uint32_t c0 = tile_key[blockIdx.x];
+  uint32_t c1 = tile_key[blockIdx.x + 1];
+  if (r1 < nrows && canon_off[c1] == r1) --c1;
+  const uint32_t nk = c1 - c0 + 1;
   for (uint32_t i = threadIdx.x; i < nk; i += BLOCK) off[i] = canon_off[c0 + i];
   __syncthreads();
-  for (uint64_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
+  // thread t: the WPT consecutive rows r0 + t*WPT ...; one binary search, then row by row
+  const uint64_t rb = r0 + (uint64_t)threadIdx.x * WPT;
+  if (rb < r1) {
     uint32_t lo = 0, hi = nk - 1;
-    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (off[mid] <= r) lo = mid; else hi = mid - 1; }
-    const uint32_t c = c0 + lo;
-    const uint4 v = *reinterpret_cast<const uint4*>(&T[perm[c]]);
-    const int32_t p = v.z == 1 ? (int32_t)v.w : positions[v.w - v.z + (uint32_t)(r - off[lo])];
-    out[r] = make_int2((int32_t)(c + 1), p);
+    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (off[mid] <= rb) lo = mid; else hi = mid - 1; }
+    uint2 v = rinfo[c0 + lo];
+    uint32_t t = (uint32_t)(rb - off[lo]);
+    const uint32_t nr = (uint32_t)min<uint64_t>(WPT, r1 - rb);
+    for (uint32_t i = 0; i < nr; ++i) {
+      if (i > 0 && ++t == v.x) { v = rinfo[c0 + ++lo]; t = 0; }
+      const int32_t p = v.x == 1 ? (int32_t)v.y : positions[v.y - v.x + t];
+      stage[threadIdx.x * WPT + i] = make_int2((int32_t)(c0 + lo + 1), p);
+    }
+  }
+  __syncthreads();
+  const uint32_t nrow = (uint32_t)(r1 - r0);
+  int2* dst = out + r0;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {        // two rows per 16-B store
+    for (uint32_t i = threadIdx.x; i < nrow / 2; i += BLOCK)
+      reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(stage)[i];
+    if ((nrow & 1) && threadIdx.x == 0) dst[nrow - 1] = stage[nrow - 1];
+  } else {
+    for (uint32_t i = threadIdx.x; i < nrow; i += BLOCK) dst[i] = stage[i];
   }
 }
 
 // R_pairs: rows (i, x, y), x < y, j-outer / k-inner inside a key (src/kmer_hash.c:1113-1121).
-// Keys without pairs are excluded from pkeys, so again every listed key owns >= 1 row.
+// Keys without pairs are excluded from pkeys, so again every listed key owns >= 1 row.  A
+// workgroup owns PR_TILE rows; R_tiles has recorded the key holding each tile's first row, so
+// no workgroup binary-searches the global offsets.  Thread t produces the PR_PER consecutive
+// rows r0 + t*PR_PER ...: one LDS binary search and one triangular-root inversion for the first,
+// then (j, q) advance row by row; all position loads are issued before any is used; rows are
+// staged in LDS and leave as 16-B stores over the tile's contiguous 12*PR_TILE bytes.
+constexpr int PR_PER = 8;
+constexpr int PR_TILE = BLOCK * PR_PER;
+
 __global__ void __launch_bounds__(BLOCK)
 k_read_pairs(const uint32_t* __restrict__ pkeys, const uint64_t* __restrict__ pair_off,
-             uint32_t M, uint64_t nrows, const uint32_t* __restrict__ perm,
-             const Slot* __restrict__ T, const int32_t* __restrict__ positions,
+             const uint32_t* __restrict__ tile_key, uint64_t nrows,
+             const uint2* __restrict__ rinfo, const int32_t* __restrict__ positions,
              int32_t* __restrict__ out) {
-  __shared__ uint64_t off[TILE + 1];
-  __shared__ uint32_t cr[2];
-  const uint64_t r0 = (uint64_t)blockIdx.x * TILE;
-  if (r0 >= nrows) return;
-  const uint64_t r1 = min(nrows, r0 + TILE);
-  if (threadIdx.x < 2) {
-    uint64_t r = threadIdx.x == 0 ? r0 : r1 - 1;
-    uint32_t lo = 0, hi = M - 1;
-    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (pair_off[mid] <= r) lo = mid; else hi = mid - 1; }
-    cr[threadIdx.x] = lo;
+  __shared__ uint32_t offr[PR_TILE];        // key start rows - r0 (the first key's clamped to 0)
+  __shared__ __attribute__((aligned(16))) int32_t stage[3 * PR_TILE];
+  __shared__ uint64_t first_off;
+  const uint32_t b = blockIdx.x;
+  const uint64_t r0 = (uint64_t)b * PR_TILE;
+  const uint64_t r1 = min(nrows, r0 + PR_TILE);
+  // keys of the tile: m0 holds row r0; the last holds row r1 - 1
+  const uint32_t m0 = tile_key[b];
+  uint32_t m1 = tile_key[b + 1];
+  if (r1 < nrows && pair_off[m1] == r1) --m1;
+  const uint32_t nk = m1 - m0 + 1;
+  for (uint32_t i = threadIdx.x; i < nk; i += BLOCK) {
+    const uint64_t o = pair_off[m0 + i];
+    offr[i] = o > r0 ? (uint32_t)(o - r0) : 0u;
+    if (i == 0) first_off = o;
   }
   __syncthreads();
-  const uint32_t m0 = cr[0], nk = cr[1] - cr[0] + 1;
-  for (uint32_t i = threadIdx.x; i < nk; i += BLOCK) off[i] = pair_off[m0 + i];
-  __syncthreads();
-  for (uint64_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
+  const uint32_t rel = threadIdx.x * PR_PER;
+  const uint64_t rb = r0 + rel;
+  if (rb < r1) {
     uint32_t lo = 0, hi = nk - 1;
-    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (off[mid] <= r) lo = mid; else hi = mid - 1; }
-    const uint32_t c = pkeys[m0 + lo];
-    const uint4 v = *reinterpret_cast<const uint4*>(&T[perm[c]]);
-    const uint64_t n = v.z;
-    const uint64_t t = r - off[lo];
+    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (offr[mid] <= rel) lo = mid; else hi = mid - 1; }
+    uint32_t c = pkeys[m0 + lo];
+    uint2 v = rinfo[c];
+    uint32_t n = v.x;
+    const uint64_t t = lo == 0 ? rb - first_off : (uint64_t)(rel - offr[lo]);
     // largest j with S(j) = j*(2n-j-1)/2 <= t
-    double dn = (double)(2 * n - 1);
+    const uint64_t n64 = n;
+    double dn = (double)(2 * n64 - 1);
     double disc = dn * dn - 8.0 * (double)t;
-    int64_t j = (int64_t)((dn - sqrt(disc > 0 ? disc : 0)) * 0.5);
-    if (j < 0) j = 0;
-    if (j > (int64_t)n - 2) j = (int64_t)n - 2;
-    auto S = [n](int64_t jj) -> uint64_t { return (uint64_t)jj * (2 * n - (uint64_t)jj - 1) / 2; };
-    while (j > 0 && S(j) > t) --j;
-    while (j + 1 <= (int64_t)n - 2 && S(j + 1) <= t) ++j;
-    const uint64_t q = (uint64_t)j + 1 + (t - S(j));
-    const int32_t* a = positions + (v.w - v.z);
-    int32_t* o = out + 3 * r;
-    o[0] = (int32_t)(c + 1); o[1] = a[j]; o[2] = a[q];
+    int64_t jj = (int64_t)((dn - sqrt(disc > 0 ? disc : 0)) * 0.5);
+    if (jj < 0) jj = 0;
+    if (jj > (int64_t)n64 - 2) jj = (int64_t)n64 - 2;
+    auto S = [n64](int64_t x) -> uint64_t { return (uint64_t)x * (2 * n64 - (uint64_t)x - 1) / 2; };
+    while (jj > 0 && S(jj) > t) --jj;
+    while (jj + 1 <= (int64_t)n64 - 2 && S(jj + 1) <= t) ++jj;
+    uint32_t j = (uint32_t)jj;
+    uint32_t q = j + 1 + (uint32_t)(t - S(jj));
+    uint32_t base = v.y - v.x;
+    const uint32_t nr = (uint32_t)min<uint64_t>(PR_PER, r1 - rb);
+    uint32_t ij[PR_PER], iq[PR_PER], cc[PR_PER];
+#pragma unroll
+    for (int i = 0; i < PR_PER; ++i) {
+      if ((uint32_t)i >= nr) break;
+      // advance before every row but the first (no key past this thread's rows is touched)
+      if (i > 0 && ++q == n) {               // next j; past the last pair: the next key
+        if (++j == n - 1) {
+          c = pkeys[m0 + ++lo];
+          v = rinfo[c];
+          n = v.x;
+          base = v.y - v.x;
+          j = 0;
+        }
+        q = j + 1;
+      }
+      ij[i] = base + j;
+      iq[i] = base + q;
+      cc[i] = c + 1;
+    }
+    int32_t pj[PR_PER], pq[PR_PER];
+#pragma unroll
+    for (int i = 0; i < PR_PER; ++i)
+      if ((uint32_t)i < nr) { pj[i] = positions[ij[i]]; pq[i] = positions[iq[i]]; }
+    int32_t* o = stage + 3 * rel;
+#pragma unroll
+    for (int i = 0; i < PR_PER; ++i)
+      if ((uint32_t)i < nr) { o[3 * i] = (int32_t)cc[i]; o[3 * i + 1] = pj[i]; o[3 * i + 2] = pq[i]; }
+  }
+  __syncthreads();
+  // the tile's rows are the contiguous ints [3 r0, 3 r1) of out
+  const uint32_t nint = 3 * (uint32_t)(r1 - r0);
+  int32_t* dst = out + 3 * r0;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+    const uint32_t n4 = nint / 4;
+    for (uint32_t i = threadIdx.x; i < n4; i += BLOCK)
+      reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(stage)[i];
+    for (uint32_t i = 4 * n4 + threadIdx.x; i < nint; i += BLOCK) dst[i] = stage[i];
+  } else {
+    for (uint32_t i = threadIdx.x; i < nint; i += BLOCK) dst[i] = stage[i];
   }
 }
 
@@ -797,18 +881,19 @@ void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions,
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(k_read_first, dim3(g), dim3(BLOCK), 0, s, T, nslots, positions, F);
 }
-void launch_read_order(const uint2* F, int64_t L, uint64_t* st_a, uint64_t* st_b,
+void launch_read_order(const uint2* F, int64_t L, const Slot* T, uint64_t* st_a, uint64_t* st_b,
                        uint64_t* st_c, uint32_t* ticket, uint32_t* perm, uint32_t* canon_off,
-                       uint32_t* pkeys, uint64_t* pair_off, ReadMeta* rmeta, hipStream_t s) {
+                       uint32_t* pkeys, uint64_t* pair_off, uint2* rinfo, ReadMeta* rmeta,
+                       hipStream_t s) {
   uint32_t nt = grid_for(L, TILE);
-  hipLaunchKernelGGL(k_read_order, dim3(nt), dim3(BLOCK), 0, s, F, L, st_a, st_b, st_c,
-                     ticket, perm, canon_off, pkeys, pair_off, nt, rmeta);
+  hipLaunchKernelGGL(k_read_order, dim3(nt), dim3(BLOCK), 0, s, F, L, T, st_a, st_b, st_c,
+                     ticket, perm, canon_off, pkeys, pair_off, rinfo, nt, rmeta);
 }
-void launch_read_keys(const uint32_t* perm, uint32_t U, const Slot* T, int k, int32_t* out_counts,
-                      char* out_kmers, hipStream_t s) {
+void launch_read_keys(const uint32_t* perm, const uint2* rinfo, uint32_t U, const Slot* T, int k,
+                      int32_t* out_counts, char* out_kmers, hipStream_t s) {
   unsigned g = grid_for(U, BLOCK);
   if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(k_read_keys, dim3(g), dim3(BLOCK), 0, s, perm, U, T, k, out_counts,
+  hipLaunchKernelGGL(k_read_keys, dim3(g), dim3(BLOCK), 0, s, perm, rinfo, U, T, k, out_counts,
                      out_kmers);
 }
 void launch_gather_keys(const uint32_t* perm, uint32_t U, const Slot* T, uint64_t* out_keys,
@@ -817,18 +902,26 @@ void launch_gather_keys(const uint32_t* perm, uint32_t U, const Slot* T, uint64_
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(k_gather_keys, dim3(g), dim3(BLOCK), 0, s, perm, U, T, out_keys);
 }
-void launch_read_pos(const uint32_t* perm, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
-                     const Slot* T, const int32_t* positions, int2* out, hipStream_t s) {
+void launch_read_pos(const uint2* rinfo, const uint32_t* canon_off, uint32_t U, uint64_t nrows,
+                     const int32_t* positions, uint32_t* tile_key, int2* out, hipStream_t s) {
   if (!nrows) return;
-  hipLaunchKernelGGL(k_read_pos, dim3(grid_for(nrows, TILE)), dim3(BLOCK), 0, s, perm, canon_off,
-                     U, nrows, T, positions, out);
+  const uint32_t nt = grid_for(nrows, TILE);
+  hipLaunchKernelGGL(k_row_tiles<uint32_t>, dim3(std::min(grid_for(U, BLOCK), 16384u)),
+                     dim3(BLOCK), 0, s, canon_off, U, nrows, (uint32_t)TILE, tile_key, nt);
+  hipLaunchKernelGGL(k_read_pos, dim3(nt), dim3(BLOCK), 0, s, rinfo, canon_off, tile_key, nrows,
+                     positions, out);
 }
+uint32_t read_pos_tiles(uint64_t nrows) { return grid_for(nrows, TILE); }
 void launch_read_pairs(const uint32_t* pkeys, const uint64_t* pair_off, uint32_t M,
-                       uint64_t nrows, const uint32_t* perm, const Slot* T,
-                       const int32_t* positions, int32_t* out, hipStream_t s) {
+                       uint64_t nrows, const uint2* rinfo, const int32_t* positions,
+                       uint32_t* tile_key, int32_t* out, hipStream_t s) {
   if (!nrows) return;
-  hipLaunchKernelGGL(k_read_pairs, dim3(grid_for(nrows, TILE)), dim3(BLOCK), 0, s, pkeys,
-                     pair_off, M, nrows, perm, T, positions, out);
+  const uint32_t nt = grid_for(nrows, PR_TILE);
+  hipLaunchKernelGGL(k_row_tiles<uint64_t>, dim3(std::min(grid_for(M, BLOCK), 16384u)),
+                     dim3(BLOCK), 0, s, pair_off, M, nrows, (uint32_t)PR_TILE, tile_key, nt);
+  hipLaunchKernelGGL(k_read_pairs, dim3(nt), dim3(BLOCK), 0, s, pkeys, pair_off, tile_key, nrows,
+                     rinfo, positions, out);
 }
+uint32_t read_pairs_tiles(uint64_t nrows) { return grid_for(nrows, PR_TILE); }
 
 }  // namespace kmhg
