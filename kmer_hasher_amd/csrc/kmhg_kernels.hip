@@ -552,8 +552,10 @@ k_read_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restr
 }
 
 // R_order: compact F in position order -> perm (canonical order = first occurrence), with the
-// canonical pos-row offsets, and the list of keys that own pair rows with their pair offsets.
-// Three look-back chains: {keys, pos rows} packed 31|31, {multi keys}, {pair rows}.
+// canonical pos-row offsets, the list of keys that own pair rows with their pair offsets, and
+// rinfo.  Three look-back chains: {keys, pos rows} packed 31|31, {multi keys}, {pair rows}.
+// Tiles are lane-contiguous (element j * BLOCK + t: every load and store of a step coalesced);
+// ranks come from per-(j, wave) ballots and wave scans, so compaction order == position order.
 __global__ void __launch_bounds__(BLOCK)
 k_read_order(const uint2* __restrict__ F, int64_t L, const Slot* __restrict__ T,
              uint64_t* __restrict__ st_a, uint64_t* __restrict__ st_b, uint64_t* __restrict__ st_c,
@@ -561,59 +563,78 @@ k_read_order(const uint2* __restrict__ F, int64_t L, const Slot* __restrict__ T,
              uint32_t* __restrict__ canon_off, uint32_t* __restrict__ pkeys,
              uint64_t* __restrict__ pair_off, uint2* __restrict__ rinfo, uint32_t ntiles,
              ReadMeta* __restrict__ rmeta) {
-  __shared__ uint64_t sh[8];
-  __shared__ uint64_t ex_sh[3];
+  constexpr int NW = BLOCK / 64;
+  __shared__ uint64_t wk[WPT * NW], wr[WPT * NW], wm[WPT * NW], wp[WPT * NW];
   __shared__ uint32_t tk;
   const uint32_t tile = take_ticket(ticket, &tk);
   const int64_t t0 = (int64_t)tile * TILE;
-  uint32_t id[WPT];
-  uint64_t va[WPT], vb[WPT], vc[WPT];
-  uint64_t suma = 0, sumb = 0, sumc = 0;
-  // thread-contiguous WPT entries keep the compaction order == position order
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  uint32_t id[WPT], nn[WPT];
+  uint64_t mk[WPT], mm[WPT], rinc[WPT], pinc[WPT];
 #pragma unroll
   for (int j = 0; j < WPT; ++j) {
-    int64_t p = t0 + (int64_t)threadIdx.x * WPT + j;
+    const int64_t p = t0 + (int64_t)j * BLOCK + threadIdx.x;
     const uint2 f = (p < L) ? F[p] : make_uint2(NONE, 0u);
     id[j] = f.x;
-    uint64_t n = (id[j] != NONE) ? f.y : 0;
-    va[j] = (id[j] != NONE) ? ((1ull << 32) | n) : 0;
-    vb[j] = (n >= 2) ? 1 : 0;
-    vc[j] = n * (n - (n ? 1 : 0)) / 2;
-    suma += va[j]; sumb += vb[j]; sumc += vc[j];
-  }
-  uint64_t ta, tb, tc;
-  uint64_t ea = block_excl_scan(suma, sh, ta);
-  uint64_t eb = block_excl_scan(sumb, sh, tb);
-  uint64_t ec = block_excl_scan(sumc, sh, tc);
-  if (threadIdx.x < 64) {
-    uint64_t agga = ((ta >> 32) << 31) | (ta & 0xFFFFFFFFull);
-    uint64_t xa = lookback_excl(st_a, tile, agga);
-    uint64_t xb = lookback_excl(st_b, tile, tb);
-    uint64_t xc = lookback_excl(st_c, tile, tc);
-    if (threadIdx.x == 0) { ex_sh[0] = xa; ex_sh[1] = xb; ex_sh[2] = xc; }
-    if (threadIdx.x == 0 && tile == ntiles - 1) {
-      rmeta->n_keys = (xa + agga) >> 31;
-      rmeta->n_rows = (xa + agga) & ((1ull << 31) - 1);
-      rmeta->n_multi = xb + tb;
-      rmeta->n_pairs = xc + tc;
+    nn[j] = (id[j] != NONE) ? f.y : 0u;
+    const uint64_t n = nn[j];
+    mk[j] = __ballot(id[j] != NONE);
+    mm[j] = __ballot(n >= 2);
+    rinc[j] = wave_incl_scan(n);
+    pinc[j] = wave_incl_scan(n * (n - (n ? 1 : 0)) / 2);
+    if (lane == 63) {
+      wk[j * NW + wave] = (uint64_t)__popcll(mk[j]);
+      wr[j * NW + wave] = rinc[j];
+      wm[j * NW + wave] = (uint64_t)__popcll(mm[j]);
+      wp[j * NW + wave] = pinc[j];
     }
   }
   __syncthreads();
-  uint64_t ga = ex_sh[0], gb = ex_sh[1], gc = ex_sh[2];
-  uint64_t ca = (ga >> 31) + (ea >> 32), ra = (ga & ((1ull << 31) - 1)) + (ea & 0xFFFFFFFFull);
-  uint64_t cb = gb + eb, cc = gc + ec;
+  if (wave == 0) {                          // lanes 0 .. WPT*NW-1: one (j, wave) group each
+    const bool own = lane < WPT * NW;
+    const uint64_t ck = own ? wk[lane] : 0, cr = own ? wr[lane] : 0;
+    const uint64_t cm = own ? wm[lane] : 0, cp = own ? wp[lane] : 0;
+    const uint64_t ik = wave_incl_scan(ck), ir = wave_incl_scan(cr);
+    const uint64_t im = wave_incl_scan(cm), ip = wave_incl_scan(cp);
+    const uint64_t tk_ = __shfl(ik, 63), tr = __shfl(ir, 63), tm = __shfl(im, 63),
+                   tp = __shfl(ip, 63);
+    const uint64_t agga = (tk_ << 31) | tr;
+    const uint64_t xa = lookback_excl(st_a, tile, agga);
+    const uint64_t xb = lookback_excl(st_b, tile, tm);
+    const uint64_t xc = lookback_excl(st_c, tile, tp);
+    if (lane == 0 && tile == ntiles - 1) {
+      rmeta->n_keys = (xa + agga) >> 31;
+      rmeta->n_rows = (xa + agga) & ((1ull << 31) - 1);
+      rmeta->n_multi = xb + tm;
+      rmeta->n_pairs = xc + tp;
+    }
+    if (own) {
+      wk[lane] = (xa >> 31) + ik - ck;
+      wr[lane] = (xa & ((1ull << 31) - 1)) + ir - cr;
+      wm[lane] = xb + im - cm;
+      wp[lane] = xc + ip - cp;
+    }
+  }
+  __syncthreads();
+  const uint64_t lt = lanemask_lt();
 #pragma unroll
   for (int j = 0; j < WPT; ++j) {
     if (id[j] == NONE) continue;
+    const int g = j * NW + wave;
+    const uint32_t n = nn[j];
+    const uint64_t ca = wk[g] + (uint64_t)__popcll(mk[j] & lt);
     perm[ca] = id[j];
-    canon_off[ca] = (uint32_t)ra;
+    canon_off[ca] = (uint32_t)(wr[g] + rinc[j] - n);
     // the row's slot fields {count, aux}: a key seen once starts here (aux = its position),
     // only a repeated key's list end needs its slot
-    const uint32_t n = (uint32_t)(va[j] & 0xFFFFFFFFull);
-    rinfo[ca] = make_uint2(n, n == 1 ? (uint32_t)(t0 + (int64_t)threadIdx.x * WPT + j + 1)
+    rinfo[ca] = make_uint2(n, n == 1 ? (uint32_t)(t0 + (int64_t)j * BLOCK + threadIdx.x + 1)
                                      : T[id[j]].aux);
-    if (vb[j]) { pkeys[cb] = (uint32_t)ca; pair_off[cb] = cc; ++cb; }
-    ++ca; ra += va[j] & 0xFFFFFFFFull; cc += vc[j];
+    if (n >= 2) {
+      const uint64_t cb = wm[g] + (uint64_t)__popcll(mm[j] & lt);
+      const uint64_t c2 = (uint64_t)n * (n - 1) / 2;
+      pkeys[cb] = (uint32_t)ca;
+      pair_off[cb] = wp[g] + pinc[j] - c2;
+    }
   }
 }
 
