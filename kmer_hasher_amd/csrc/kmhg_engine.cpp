@@ -862,6 +862,17 @@ void adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, hipStrea
   idx->canon.ready = false;
 }
 
+// Adopting a batch table keeps its size, set by the batch's windows / k-mer words; the rebuild
+// sizes the table by the distinct keys (~1.5 slots per key).  A batch with heavy repetition
+// (deep read coverage) would leave a sparse, oversized table, so adoption needs <= 6 slots per
+// distinct key (<= 4x the rebuilt table); otherwise the general merge rebuilds a compact one.
+// KMHG_COUNT_TABLE (tests): "adopt" adopts regardless of size, "rebuild" / "probe" never do.
+bool adoptable(const kmhg_index* idx, const kmhg_index* B) {
+  if (idx->U != 0) return false;
+  if (const char* e = std::getenv("KMHG_COUNT_TABLE")) return std::string(e) == "adopt";
+  return B->slots() <= 6 * B->U;
+}
+
 void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t source,
                   hipStream_t s) {
   idx->stream = s;
@@ -872,8 +883,7 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
   finish_build(B.get());
   B->stream = s;
   if (!B->U) return;
-  // KMHG_COUNT_TABLE (tests): "rebuild" / "probe" take the general merge for the first batch too
-  if (idx->U == 0 && !std::getenv("KMHG_COUNT_TABLE")) {
+  if (adoptable(idx, B.get())) {
     adopt_first_batch(idx, B.get(), source, s);
   } else {
     prepare_canon(B.get(), s);     // batch keys in first-occurrence order
@@ -896,7 +906,7 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_
   const uint32_t nt = tiles_for(ni);
   // KMHG_COUNT_TABLE (tests): "rebuild" / "probe" take the general merge even for the first batch
   const char* ct = std::getenv("KMHG_COUNT_TABLE");
-  if (U0 == 0 && !ct && !perm_b) {
+  if (!perm_b && adoptable(idx, B)) {
     // first batch into an empty suffix hash: every key is new and the batch table becomes the
     // counts table, its occupied slots compacted into rows in slot order in one pass
     // (k_count_walk) -- no probe, append, table rebuild or C_fix.  (count.kmers batches take

@@ -155,8 +155,7 @@ def test_gpu_counts_first_order_vs_oracle(gpu, cgold, monkeypatch, table):
     default for later batches) and global linear probing (its overflow fallback,
     KMHG_COUNT_TABLE=probe)."""
     from kmer_hasher_amd import kmer_pos
-    if table != "adopt":
-        monkeypatch.setenv("KMHG_COUNT_TABLE", table)
+    monkeypatch.setenv("KMHG_COUNT_TABLE", table)
     for case, _ in cgold:
         oc = _oracle(case)
         ix = oc.index()

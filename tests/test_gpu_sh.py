@@ -38,8 +38,7 @@ def test_sh_golden(gpu, case, inputs, monkeypatch, table):
     """`table`: the first batch's table adopted as the suffix hash (default) or rebuilt from
     the key list (KMHG_COUNT_TABLE=rebuild, the path of every later batch)."""
     from kmer_hasher_amd import api
-    if table != "adopt":
-        monkeypatch.setenv("KMHG_COUNT_TABLE", table)
+    monkeypatch.setenv("KMHG_COUNT_TABLE", table)
     files, genome = inputs
     ptr = None
     for f, pb, mq, mr, src in case["calls"]:
