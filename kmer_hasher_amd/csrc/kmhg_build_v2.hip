@@ -247,7 +247,10 @@ struct ScatterLDS {
   PStage st;
 };
 
-template <bool FROM_SEQ>
+// KEYS0: the first pass over a caller's key stream (a table rebuilt from keys): `kin` holds
+// exactly n keys (loads clamped, no pad) and positions are implicit (e + 1), so the stream is
+// neither copied nor paired with an iota array first.
+template <bool FROM_SEQ, bool KEYS0 = false>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned,
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
@@ -299,8 +302,13 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
 #pragma unroll
       for (int cc = 0; cc < PER; ++cc) {   // e < ntiles * PTILE <= n_max + pad: in bounds
         const uint64_t e = t0 + wbase + (uint32_t)cc * 64 + lane;
-        nkey[cc] = kin[e];
-        npos[cc] = pin[e];
+        if (KEYS0) {
+          nkey[cc] = kin[e < n ? e : n - 1];
+          npos[cc] = (uint32_t)(e + 1);
+        } else {
+          nkey[cc] = kin[e];
+          npos[cc] = pin[e];
+        }
       }
     }
   };
@@ -1231,6 +1239,13 @@ void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t*
                        uint32_t pad, hipStream_t s) {
   hipLaunchKernelGGL(k_v2_scatter<false>, dim3(scatter_grid(ch)), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
                      (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ch, kout, pout, pad, xcd_map());
+}
+void launch_v2_scatter_keys0(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
+                             const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                             uint32_t pad, hipStream_t s) {
+  hipLaunchKernelGGL((k_v2_scatter<false, true>), dim3(scatter_grid(ch)), dim3(BLOCK), 0, s,
+                     nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D, hist, ch,
+                     kout, pout, pad, xcd_map());
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s) {

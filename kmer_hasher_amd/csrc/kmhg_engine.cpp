@@ -523,6 +523,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   idx->L = L;
   const bool from_keys = d_seq == nullptr;
   const int64_t Nw = from_keys ? n_keys : L - k + 1;
+  if (from_keys && Nw < 1) fail(KMHG_EINVAL, "empty key stream (internal error)");
   // the partition kernels read the sequence as aligned 16-B words: copy an unaligned input
   DBuf<uint8_t> aligned_copy;
   if (!from_keys && (reinterpret_cast<uintptr_t>(d_seq) & 15) != 0) {
@@ -592,9 +593,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = 1;
-  if (from_keys) {   // pass 0 reads the key stream like every later pass
-    HIPC(hipMemcpyAsync(kA.p, d_keys, (size_t)Nw * 8, hipMemcpyDeviceToDevice, s));
-    LAUNCH("k_iota_u32", s, launch_iota_u32(pA.p, (uint64_t)Nw, 1u, s));
+  if (from_keys) {   // pass 0 reads the caller's key stream in place (positions implicit)
     HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(n_valid), (int)Nw, 1, s));
     HIPC(hipMemsetAsync(meta, 0, sizeof(BuildMeta), s));
   } else {
@@ -609,11 +608,18 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   }
   for (uint32_t p = from_keys ? 0 : 1; p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
+    const bool keys0 = from_keys && p == 0;
+    const uint64_t* src = keys0 ? d_keys : kin;
     LAUNCH("k_v2_hist", s,
-           launch_v2_hist(kin, n_valid, g, Dp, hist.p, ch, status, n_status, s));
+           launch_v2_hist(src, n_valid, g, Dp, hist.p, ch, status, n_status, s));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
-    LAUNCH("k_v2_scatter", s,
-           launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ch, kout, pout, pad, s));
+    if (keys0) {
+      LAUNCH("k_v2_scatter", s,
+             launch_v2_scatter_keys0(d_keys, n_valid, g, Dp, hist.p, ch, kout, pout, pad, s));
+    } else {
+      LAUNCH("k_v2_scatter", s,
+             launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ch, kout, pout, pad, s));
+    }
     std::swap(kin, kout);
     std::swap(pin, pout);
     div *= R;

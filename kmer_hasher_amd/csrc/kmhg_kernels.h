@@ -135,6 +135,10 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s);
+// first pass over a caller's key stream of exactly *n_ptr keys (>= 1): positions are e + 1
+void launch_v2_scatter_keys0(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
+                             const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                             uint32_t pad, hipStream_t s);
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s);
