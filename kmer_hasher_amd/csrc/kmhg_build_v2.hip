@@ -249,8 +249,9 @@ struct ScatterLDS {
 
 // KEYS0: the first pass over a caller's key stream (a table rebuilt from keys): `kin` holds
 // exactly n keys (loads clamped, no pad) and positions are implicit (e + 1), so the stream is
-// neither copied nor paired with an iota array first.
-template <bool FROM_SEQ, bool KEYS0 = false>
+// neither copied nor paired with an iota array first.  NOPOS: keys only (count-only builds:
+// nobody reads the positions), 8 B per element in and out instead of 12.
+template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned,
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
@@ -307,7 +308,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
           npos[cc] = (uint32_t)(e + 1);
         } else {
           nkey[cc] = kin[e];
-          npos[cc] = pin[e];
+          npos[cc] = NOPOS ? 0u : pin[e];
         }
       }
     }
@@ -321,7 +322,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
 #pragma unroll
   for (int j = 0; j < PTILE / BLOCK; ++j) {
     kout[pad + threadIdx.x] = 0;
-    pout[pad + threadIdx.x] = 0;
+    if (!NOPOS) pout[pad + threadIdx.x] = 0;
   }
   for (uint32_t it = 0; it < n_iter; ++it) {
     const uint32_t tile = tile_at(it);
@@ -416,7 +417,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       // lanes past the tile's end store into the PTILE-element pad behind the outputs
       const uint32_t dst = i < (uint32_t)tile_n ? S.sdst[i] : pad + threadIdx.x;
       kout[dst] = S.skey[i];
-      pout[dst] = S.spos[i];
+      if (!NOPOS) pout[dst] = S.spos[i];
     }
   }
 }
@@ -669,6 +670,9 @@ __device__ __forceinline__ int lds_find_g(const GroupTable& W, uint64_t key) {
 
 // The CAS build of one group bucket (the body of V_bucket_wg; also the fallback of V_bucket_sort
 // for buckets it does not take).  W, sh, red are the caller's LDS.
+// COUNT_ONLY (occurrence counts of a key stream, kmhg_sh.hip's read counting): pass B -- the
+// positions -- is skipped; slots get {key, count, unspecified aux}.
+template <bool COUNT_ONLY = false>
 __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint32_t (*red)[4],
                                               const uint64_t* __restrict__ keys,
                                               const uint32_t* __restrict__ pos,
@@ -692,7 +696,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     for (int c = 0; c < PER; ++c) {
       const uint32_t i = elem(i0, c);
       key[c] = i < s1 ? keys[i] : 0;
-      ps[c] = i < s1 ? pos[i] : 0;
+      ps[c] = (!COUNT_ONLY && i < s1) ? pos[i] : 0;
     }
   };
   STAMP_WG(b, 0);
@@ -764,7 +768,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   }
   // pass B: keys seen once keep their position inline (cc.y); repeated keys are ranked in
   // position order, the waves taking turns so that wave w follows waves < w
-  for (uint32_t i0 = s0; i0 < s1; i0 += BATCH) {
+  for (uint32_t i0 = s0; i0 < (COUNT_ONLY ? s0 : s1); i0 += BATCH) {
     if (!one_batch) {
       load(i0);
 #pragma unroll
@@ -814,6 +818,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   STAMP_WG(b, 5);
 }
 
+template <bool COUNT_ONLY>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
@@ -822,7 +827,8 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   __shared__ GroupTable W;
   __shared__ uint64_t sh[8];
   __shared__ uint32_t red[3][4];
-  bucket_wg_cas(W, sh, red, keys, pos, start, g, T, positions, bstats, meta, blockIdx.x);
+  bucket_wg_cas<COUNT_ONLY>(W, sh, red, keys, pos, start, g, T, positions, bstats, meta,
+                            blockIdx.x);
 }
 
 // ---------------------------------------------------------------- V_bucket_sort (group per bucket)
@@ -1242,10 +1248,22 @@ void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t*
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
-                             uint32_t pad, hipStream_t s) {
-  hipLaunchKernelGGL((k_v2_scatter<false, true>), dim3(scatter_grid(ch)), dim3(BLOCK), 0, s,
-                     nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D, hist, ch,
-                     kout, pout, pad, xcd_map());
+                             uint32_t pad, bool nopos, hipStream_t s) {
+  if (nopos)
+    hipLaunchKernelGGL((k_v2_scatter<false, true, true>), dim3(scatter_grid(ch)), dim3(BLOCK), 0,
+                       s, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D, hist,
+                       ch, kout, nullptr, pad, xcd_map());
+  else
+    hipLaunchKernelGGL((k_v2_scatter<false, true>), dim3(scatter_grid(ch)), dim3(BLOCK), 0, s,
+                       nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D, hist, ch,
+                       kout, pout, pad, xcd_map());
+}
+void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
+                             const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t pad,
+                             hipStream_t s) {
+  hipLaunchKernelGGL((k_v2_scatter<false, false, true>), dim3(scatter_grid(ch)), dim3(BLOCK), 0,
+                     s, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D, hist,
+                     ch, kout, nullptr, pad, xcd_map());
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s) {
@@ -1267,9 +1285,13 @@ void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_bucket_wg, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
-                     positions, bstats, meta);
+                         bool count_only, hipStream_t s) {
+  if (count_only)
+    hipLaunchKernelGGL(k_v2_bucket_wg<true>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
+                       positions, bstats, meta);
+  else
+    hipLaunchKernelGGL(k_v2_bucket_wg<false>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g,
+                       T, positions, bstats, meta);
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {

@@ -513,8 +513,11 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 // Partitioned build over the windows of a sequence (d_seq), or over a stream of n_keys
 // distinct keys (d_keys, d_seq == nullptr; the counts index's table rebuild): key r is stored
 // with count 1 and aux = r + 1.
+// count_only (a key stream whose positions nobody reads: read counting): the group bucket kernel
+// skips its position pass and no positions array is kept.
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
-                            const uint64_t* d_keys = nullptr, int64_t n_keys = 0) {
+                            const uint64_t* d_keys = nullptr, int64_t n_keys = 0,
+                            bool count_only = false) {
   const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
   idx->stream = s;
@@ -572,7 +575,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const uint64_t nhist = (uint64_t)R * ch.C;
   const uint32_t scan_tiles = tiles_for(nhist);
   DBuf<uint64_t> kA(Nw + PTILE, s), kB(Nw + PTILE, s);   // + pad (launch_v2_scatter)
-  DBuf<uint32_t> pA(Nw + PTILE, s), pB(Nw + PTILE, s);
+  const bool no_pos = count_only && group && !sorted;   // keys only through the passes
+  DBuf<uint32_t> pA(no_pos ? 1 : Nw + PTILE, s), pB(no_pos ? 1 : Nw + PTILE, s);
   const uint32_t pad = (uint32_t)Nw;
   DBuf<uint32_t> hist(nhist, s);
   DBuf<uint32_t> start((uint64_t)nb + 1, s);
@@ -587,7 +591,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint64_t* status = reinterpret_cast<uint64_t*>(sc + off_status);
   idx->rec = PinnedPool::get().take();                     // V_stats writes the totals here
   idx->table.reset(idx->slots());
-  idx->positions.reset(Nw);
+  idx->positions.reset(no_pos ? 1 : Nw);
   DBuf<BucketStats> bstats(nb, s);
 
   uint64_t *kin = kA.p, *kout = kB.p;
@@ -615,7 +619,11 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     if (keys0) {
       LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter_keys0(d_keys, n_valid, g, Dp, hist.p, ch, kout, pout, pad, s));
+             launch_v2_scatter_keys0(d_keys, n_valid, g, Dp, hist.p, ch, kout, pout, pad, no_pos,
+                                     s));
+    } else if (no_pos) {
+      LAUNCH("k_v2_scatter", s,
+             launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ch, kout, pad, s));
     } else {
       LAUNCH("k_v2_scatter", s,
              launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ch, kout, pout, pad, s));
@@ -638,7 +646,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   else if (group)
     LAUNCH("k_v2_bucket_wg", s,
            launch_v2_bucket_wg(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
-                               meta, s));
+                               meta, no_pos, s));
   else
     LAUNCH("k_v2_bucket", s,
            launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
@@ -1077,7 +1085,7 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   LAUNCH("k_read_kmers_emit", s,
          launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
                            keys.p, true, s));
-  std::unique_ptr<kmhg_index> B(build_device_v2(nullptr, 0, k, s, keys.p, (int64_t)total));
+  std::unique_ptr<kmhg_index> B(build_device_v2(nullptr, 0, k, s, keys.p, (int64_t)total, true));
   Release rel{B.get(), s};
   HIPC(hipEventSynchronize(B->rec.ev));
   const BuildMeta hm = *B->rec.meta;

@@ -136,9 +136,13 @@ void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geo
                            const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s);
 // first pass over a caller's key stream of exactly *n_ptr keys (>= 1): positions are e + 1
+// nopos: keys only (count-only builds), pout unused
 void launch_v2_scatter_keys0(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
-                             uint32_t pad, hipStream_t s);
+                             uint32_t pad, bool nopos, hipStream_t s);
+void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
+                             const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t pad,
+                             hipStream_t s);
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s);
@@ -154,9 +158,10 @@ void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t*
 void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint32_t* start,
                            Geom g, Slot* T, int32_t* positions, BucketStats* bstats,
                            BuildMeta* meta, hipStream_t s);
+// count_only: occurrence counts only (no positions written; slot aux unspecified)
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         hipStream_t s);
+                         bool count_only, hipStream_t s);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);
 
