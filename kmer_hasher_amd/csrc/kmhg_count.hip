@@ -118,28 +118,29 @@ k_count_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __rest
 // every load and store of a step is coalesced).  The flagged elements get consecutive ranks in
 // element order -- (j, wave, lane) -- from per-(j, wave) ballots, offset by the flagged elements
 // of the tiles before (one look-back chain).  `cw` = LDS for WPT * 4 u64.
-__device__ __forceinline__ void tile_compact(const bool (&flag)[WPT], uint64_t (&rk)[WPT],
+template <int J = WPT>
+__device__ __forceinline__ void tile_compact(const bool (&flag)[J], uint64_t (&rk)[J],
                                              uint64_t* cw, uint64_t* status, uint32_t tile) {
   const int wave = threadIdx.x >> 6, lane = lane_id();
   constexpr int NW = BLOCK / 64;
-  uint64_t m[WPT];
+  uint64_t m[J];
 #pragma unroll
-  for (int j = 0; j < WPT; ++j) m[j] = __ballot(flag[j]);
+  for (int j = 0; j < J; ++j) m[j] = __ballot(flag[j]);
   if (lane == 0) {
 #pragma unroll
-    for (int j = 0; j < WPT; ++j) cw[j * NW + wave] = (uint64_t)__popcll(m[j]);
+    for (int j = 0; j < J; ++j) cw[j * NW + wave] = (uint64_t)__popcll(m[j]);
   }
   __syncthreads();
-  if (wave == 0) {                       // lanes 0 .. WPT*NW-1 own one (j, wave) count each
-    const uint64_t c = lane < WPT * NW ? cw[lane] : 0;
+  if (wave == 0) {                       // lanes 0 .. J*NW-1 own one (j, wave) count each
+    const uint64_t c = lane < J * NW ? cw[lane] : 0;
     const uint64_t inc = wave_incl_scan(c);
     const uint64_t tot = __shfl(inc, 63);
     const uint64_t x = lookback_excl(status, tile, tot);
-    if (lane < WPT * NW) cw[lane] = x + inc - c;
+    if (lane < J * NW) cw[lane] = x + inc - c;
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < WPT; ++j)
+  for (int j = 0; j < J; ++j)
     rk[j] = cw[j * NW + wave] + (uint64_t)__popcll(m[j] & lanemask_lt());
 }
 
@@ -178,27 +179,33 @@ k_count_order(const uint4* __restrict__ F, int64_t L, uint64_t* __restrict__ sta
 // The first batch into an empty suffix hash (order-free rows: slot order).  One pass over the
 // adopted table in tiles of TILE slots: occupied slots are compacted into rows, each writes its
 // row (key, count vector, row_slot), slot_row and its own slot fields -- every access coalesced.
+// WALK_PER slots per thread: a longer tile halves the look-back chain over the sparse table
+#ifndef KMHG_WALK_PER
+#define KMHG_WALK_PER 16
+#endif
+constexpr int WALK_PER = KMHG_WALK_PER;
+constexpr int WALK_TILE = BLOCK * WALK_PER;
 __global__ void __launch_bounds__(BLOCK)
 k_count_walk(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ status,
              uint32_t* __restrict__ ticket, uint32_t S, uint32_t source,
              uint64_t* __restrict__ ckeys, int32_t* __restrict__ M,
              uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot) {
-  __shared__ uint64_t cw[WPT * (BLOCK / 64)];
+  __shared__ uint64_t cw[WALK_PER * (BLOCK / 64)];
   __shared__ uint32_t tk;
   const uint32_t tile = take_ticket(ticket, &tk);
-  const uint64_t t0 = (uint64_t)tile * TILE;
-  uint4 v[WPT];
-  bool fl[WPT];
+  const uint64_t t0 = (uint64_t)tile * WALK_TILE;
+  uint4 v[WALK_PER];
+  bool fl[WALK_PER];
 #pragma unroll
-  for (int j = 0; j < WPT; ++j) {
+  for (int j = 0; j < WALK_PER; ++j) {
     const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
     v[j] = i < nslots ? *reinterpret_cast<const uint4*>(&T[i]) : make_uint4(0u, 0u, 0u, 0u);
     fl[j] = v[j].z != 0;
   }
-  uint64_t rk[WPT];
-  tile_compact(fl, rk, cw, status, tile);
+  uint64_t rk[WALK_PER];
+  tile_compact<WALK_PER>(fl, rk, cw, status, tile);
 #pragma unroll
-  for (int j = 0; j < WPT; ++j) {
+  for (int j = 0; j < WALK_PER; ++j) {
     if (!fl[j]) continue;
     const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
     const uint64_t row = rk[j];
@@ -284,10 +291,11 @@ void launch_count_order(const uint4* F, int64_t L, uint64_t* status, uint32_t* t
   hipLaunchKernelGGL(k_count_order, dim3(nt), dim3(BLOCK), 0, s, F, L, status, ticket, S, source,
                      ckeys, M, slot_row, row_slot);
 }
+uint64_t count_walk_tiles(uint64_t nslots) { return (nslots + WALK_TILE - 1) / WALK_TILE; }
 void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
                        uint32_t* row_slot, hipStream_t s) {
-  const unsigned nt = (unsigned)((nslots + TILE - 1) / TILE);
+  const unsigned nt = (unsigned)((nslots + WALK_TILE - 1) / WALK_TILE);
   hipLaunchKernelGGL(k_count_walk, dim3(nt), dim3(BLOCK), 0, s, T, nslots, status, ticket, S,
                      source, ckeys, M, slot_row, row_slot);
 }

@@ -926,7 +926,7 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_
     // (k_count_walk) -- no probe, append, table rebuild or C_fix.  (count.kmers batches take
     // adopt_first_batch: rows in first-occurrence order.)
     const uint64_t ns = B->slots();
-    const uint64_t nw = (ns + TILE - 1) / TILE;
+    const uint64_t nw = count_walk_tiles(ns);
     DBuf<uint64_t> status(nw + 1, s);            // look-back words + the tile ticket
     HIPC(hipMemsetAsync(status.p, 0, (nw + 1) * 8, s));
     idx->table.bind(s);

@@ -192,6 +192,7 @@ void launch_count_slots(Slot* T, uint64_t nslots, uint32_t S, const uint32_t* sl
                         hipStream_t s);
 // first batch into a new suffix hash: rows in slot order; `status` = ceil(nslots / TILE) zeroed
 // look-back words, `ticket` a zeroed u32
+uint64_t count_walk_tiles(uint64_t nslots);   // look-back words launch_count_walk needs
 void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
                        uint32_t* row_slot, hipStream_t s);
