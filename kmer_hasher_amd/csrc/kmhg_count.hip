@@ -230,14 +230,6 @@ k_count_slots(Slot* __restrict__ T, uint64_t nslots, uint32_t S,
   }
 }
 
-// values base, base + 1, ... of the key stream of a table rebuild
-__global__ void __launch_bounds__(BLOCK) k_iota_u32(uint32_t* __restrict__ a, uint64_t n,
-                                                    uint32_t base) {
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n;
-       i += (uint64_t)gridDim.x * BLOCK)
-    a[i] = base + (uint32_t)i;
-}
-
 // C_fix: a table rebuilt by the partitioned build from the key list holds {key, 1, row + 1};
 // give every occupied slot its counts-index fields and record the slot <-> row maps.
 __global__ void __launch_bounds__(BLOCK)
@@ -303,9 +295,6 @@ void launch_count_slots(Slot* T, uint64_t nslots, uint32_t S, const uint32_t* sl
                         hipStream_t s) {
   hipLaunchKernelGGL(k_count_slots, dim3(grid_cap(nslots)), dim3(BLOCK), 0, s, T, nslots, S,
                      slot_row);
-}
-void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s) {
-  hipLaunchKernelGGL(k_iota_u32, dim3(grid_cap(n)), dim3(BLOCK), 0, s, a, n, base);
 }
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s) {

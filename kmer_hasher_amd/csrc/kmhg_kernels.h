@@ -196,7 +196,6 @@ uint64_t count_walk_tiles(uint64_t nslots);   // look-back words launch_count_wa
 void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
                        uint32_t* row_slot, hipStream_t s);
-void launch_iota_u32(uint32_t* a, uint64_t n, uint32_t base, hipStream_t s);
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s);
 void launch_count_canon(const uint32_t* row_slot, const int32_t* M, uint32_t U, uint32_t S,
