@@ -160,6 +160,36 @@ def reads_algorithmic_bytes(kernel: str, n_bases: int, n_reads: int, words: int)
     return None
 
 
+def counts_algorithmic_bytes(kernel: str, L: int, U: int, S: int) -> int | None:
+    """Minimum bytes of the count.kmers kernels (first batch into a new pointer): C_first reads
+    each occupied slot (16 B) and scatters {slot, count, key} (16 B); C_order reads the L-entry
+    first-position array (16 B each) and writes a row per key (key 8 B, S counts, row_slot and
+    slot_row 4 B each); C_slots rereads each occupied slot, its row (4 B) and rewrites 8 B."""
+    if kernel == "k_count_first":
+        return 32 * U
+    if kernel == "k_count_order":
+        return 16 * L + U * (8 + 4 * S + 8)
+    if kernel == "k_count_slots":
+        return 28 * U
+    return None
+
+
+def depth_algorithmic_bytes(kernel: str, L: int, S: int) -> int | None:
+    """k_depth_probe: every base read once and one 16-B slot probe per window, S int32 out per
+    base."""
+    if kernel == "k_depth_probe":
+        return L + 16 * L + 4 * S * L
+    return None
+
+
+def _leg_roofline(per: dict, kernel: str, ab) -> dict:
+    ach = ab / (per[kernel] * 1e-3) / 1e9 if ab else None
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(ach, 2) if ach else None,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "algorithmic_bytes": ab,
+            "avg_ms": round(per[kernel], 5)}
+
+
 def cpu_reads_baseline(fq: bytes, seq_bytes: bytes, k: int, depth_bp: int = 2_000_000):
     """count_kmers_fastq_sh_rp (src/kmer_hash.c:810-857, 1 reader thread) and seq_kmer_counts
     (src/kmer_reader.c:155-193) of the reference's own counting core (oracle/_ref) on a bounded
@@ -457,7 +487,12 @@ def main():
                 "ms_per_step": round(t_count / args.steps * 1e3, 4), "distinct_kmers": cU,
                 "kernels_ms_per_step": {n: round(v, 5) for n, v in cper.items()},
                 "note": "count.kmers(seq, c(k, 0, 2)) into a new pointer per step: partitioned "
-                        "build of the batch + merge into the count matrix + table rebuild"}
+                        "build of the batch, whose table the new pointer adopts (first-occurrence "
+                        "rows from k_count_first / k_count_order / k_count_slots)"}
+            cdom = max((n for n in cper if n.startswith("k_count_")), key=cper.get, default=None)
+            if cdom:
+                out["counts"]["roofline"] = _leg_roofline(
+                    cper, cdom, counts_algorithmic_bytes(cdom, L, cU, 2))
         if t_reads:
             dom_r = "k_read_kmers_emit"      # the row's own kernel (the batch build is the index's)
             ab_r = reads_algorithmic_bytes(dom_r, n_bases, READS_N, r_words)
@@ -481,6 +516,9 @@ def main():
                 "ms_per_step": round(t_depth / args.steps * 1e3, 4),
                 "kernels_ms_per_step": {n: round(v, 5) for n, v in dper.items()},
                 "note": "seq.kmer.depth.sh of the bench sequence against that suffix hash"}
+            if "k_depth_probe" in dper:
+                out["depth"]["roofline"] = _leg_roofline(
+                    dper, "k_depth_probe", depth_algorithmic_bytes("k_depth_probe", L, 2))
         if not args.no_cpu and not args.profile:
             out["cpu_baseline"] = cpu_baseline(host_seq.tobytes(), k)
             if t_count:
