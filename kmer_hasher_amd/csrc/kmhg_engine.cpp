@@ -1070,9 +1070,15 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   const double* qll = qll_device(s);
   DBuf<uint32_t> cnt((size_t)n_reads + 1, s);
   const uint32_t nt = tiles_for(n_reads);
-  DBuf<uint64_t> status((size_t)nt + 1, s);
-  HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
-  const uint32_t cap = read_kmers_cap(mean_len);
+  DBuf<uint64_t> status((size_t)nt + 2, s);        // scan look-back + ticket, then the span
+  HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 2) * 8, s));
+  uint32_t* d_span = reinterpret_cast<uint32_t*>(status.p + nt + 1);
+  LAUNCH("k_rk_span", s, launch_rk_span(d_off, n_reads, d_span, s));
+  uint32_t span = 0;
+  HIPC(hipMemcpyAsync(&span, d_span, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  const uint32_t cap = read_kmers_cap_span(span);
+  (void)mean_len;
   LAUNCH("k_read_kmers_count", s,
          launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
                            nullptr, false, s));

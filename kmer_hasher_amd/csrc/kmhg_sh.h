@@ -1,5 +1,6 @@
 // kmhg_sh.h -- launch wrappers of kmhg_sh.hip (read counting, depth, spectrum).
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include "kmhg_common.h"
 
@@ -12,20 +13,24 @@ inline uint32_t depth_tiles(int64_t L) { return (uint32_t)((L + DP_TILE - 1) / D
 // one lane per read of a packed batch: seq / qual bytes (16-B aligned, >= 16 B of padding),
 // read r = [off[r], off[r+1]), hasq[r] = 0 for a FASTA record.  emit = false: cnt[r] = k-mers
 // accepted; emit = true: cnt = exclusive offsets, keys[cnt[r] + t] = canonical k-mer t.
-// cap = LDS bytes per stream staged per wave of 64 reads (read_kmers_cap).
+// cap = LDS bytes per stream staged per wave of 64 reads (read_kmers_cap_span).
 void launch_read_kmers(const uint8_t* seq, const uint8_t* qual, const int64_t* off,
                        const uint8_t* hasq, uint32_t n_reads, int k, double min_ll,
                        const double* qll, uint32_t cap, uint32_t* cnt, uint64_t* keys,
                        bool emit, hipStream_t s);
 // staging capacity for a batch of mean read length `mean_len`: 1.5x the mean span of a wave,
 // 16-B multiple, at most 28 KiB per stream (4+ waves per CU)
-inline uint32_t read_kmers_cap(double mean_len) {
-  double c = mean_len * 64 * 1.5 + 32;
+// *span = the largest byte span a k_read_kmers workgroup stages (atomicMax; zero it first)
+void launch_rk_span(const int64_t* off, uint32_t n_reads, uint32_t* span, hipStream_t s);
+// LDS bytes per staged stream: the measured span, capped (a workgroup whose reads do not fit
+// walks them from global memory)
+inline uint32_t read_kmers_cap_span(uint32_t span) {
+  if (const char* e = std::getenv("KMHG_RK_CAP"))   // A/B knob: LDS bytes per stream (16: global)
+    return ((uint32_t)std::atoi(e) + 15) & ~15u;
+  uint32_t c = span < 1024 ? 1024 : span;
   if (c > 28672) c = 28672;
-  if (c < 1024) c = 1024;
-  return ((uint32_t)c + 15) & ~15u;
+  return (c + 15) & ~15u;
 }
-
 // depth: tcnt = depth_tiles(L) u32 (segment starts per tile, scanned in place by the caller),
 // sstart / send = segment bounds, n_seg = number of segments, stale = per-segment flag
 void launch_depth_seg_count(const uint8_t* seq, int64_t L, uint32_t* tcnt, hipStream_t s);

@@ -154,6 +154,25 @@ k_read_kmers(const uint8_t* __restrict__ seq, const uint8_t* __restrict__ qual,
     walk_read<EMIT>(ByteCursor(seq), ByteCursor(qual), b, e, hq, k, min_ll, qll, cnt, rd, keys);
 }
 
+// The largest byte span one k_read_kmers workgroup stages (RK_READS reads from an aligned-down
+// start): sizing the LDS staging exactly (not by a mean-length guess with headroom) lets more
+// workgroups share a CU -- the walk is latency bound.
+__global__ void __launch_bounds__(BLOCK)
+k_rk_span(const int64_t* __restrict__ off, uint32_t n_reads, uint32_t* __restrict__ span) {
+  const uint32_t w = blockIdx.x * BLOCK + threadIdx.x;
+  const uint32_t r0 = w * RK_READS;
+  if (r0 >= n_reads) return;
+  const uint32_t r1 = min(n_reads, r0 + RK_READS);
+  const int64_t sp = off[r1] - (off[r0] & ~(int64_t)15);
+  atomicMax(span, (uint32_t)min<int64_t>(sp, 0x7FFFFFFF));
+}
+
+void launch_rk_span(const int64_t* off, uint32_t n_reads, uint32_t* span, hipStream_t s) {
+  const uint32_t nw = (n_reads + RK_READS - 1) / RK_READS;
+  hipLaunchKernelGGL(k_rk_span, dim3((nw + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, off, n_reads,
+                     span);
+}
+
 void launch_read_kmers(const uint8_t* seq, const uint8_t* qual, const int64_t* off,
                        const uint8_t* hasq, uint32_t n_reads, int k, double min_ll,
                        const double* qll, uint32_t cap, uint32_t* cnt, uint64_t* keys,
