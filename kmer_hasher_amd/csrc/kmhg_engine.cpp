@@ -5,6 +5,7 @@
 //   * Timing       per-kernel HIP-event pairs on the launch stream (kmhg_timing_*)
 //   * Index/Query  build -> query -> readout pipelines over kmhg_kernels.hip
 // Reference entry points each C function replaces are listed in include/kmhgpu.h.
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -517,7 +518,7 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 // skips its position pass and no positions array is kept.
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
                             const uint64_t* d_keys = nullptr, int64_t n_keys = 0,
-                            bool count_only = false) {
+                            bool count_only = false, int co_spread = 1) {
   const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
   idx->stream = s;
@@ -556,7 +557,16 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // buckets halve the radix (longer digit runs) -- config 2 26.1 vs 24.8 Gbp/s -- and save a pass
   // from ~26 M windows -- config 3 26.3 vs 24.5.  KMHG_BUCKET=wave|group forces one.
   const uint32_t nb_w = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW - 1) / V2_BW);
-  const uint32_t nb_g = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW_WG - 1) / V2_BW_WG);
+  // count-only builds: co_spread (KMHG_CO_SPREAD overrides) x more stream entries per group
+  // bucket -- a read batch's distinct keys are a fraction of its key stream, so fewer buckets
+  // still fit their LDS sub-tables (an overflowing bucket takes the global find-or-insert path)
+  int64_t bw_g = V2_BW_WG;
+  if (count_only) {
+    int f = co_spread;
+    if (const char* e = std::getenv("KMHG_CO_SPREAD")) f = std::atoi(e);
+    bw_g *= std::max(1, std::min(8, f));
+  }
+  const uint32_t nb_g = (uint32_t)std::max<int64_t>(1, (Nw + bw_g - 1) / bw_g);
   uint32_t R_w = 0, R_g = 0;
   const uint32_t passes_w = plan(nb_w, R_w), passes_g = plan(nb_g, R_g);
   bool group = passes_g <= passes_w;
@@ -1091,10 +1101,21 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   LAUNCH("k_read_kmers_emit", s,
          launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
                            keys.p, true, s));
-  std::unique_ptr<kmhg_index> B(build_device_v2(nullptr, 0, k, s, keys.p, (int64_t)total, true));
+  // bucket spread from the distinct / stream ratio the previous count-only build measured
+  // (bench, 3.7x coverage: spread 1/2/3/4 -> 22.6/26.8/28.5/27.6 Gbp/s): mean distinct keys per
+  // group bucket ~900 of its 1536 LDS slots; an overflow resets it to 1
+  static std::atomic<int> co_spread{1};
+  const int spread = co_spread.load(std::memory_order_relaxed);
+  std::unique_ptr<kmhg_index> B(
+      build_device_v2(nullptr, 0, k, s, keys.p, (int64_t)total, true, spread));
   Release rel{B.get(), s};
   HIPC(hipEventSynchronize(B->rec.ev));
   const BuildMeta hm = *B->rec.meta;
+  {
+    const double ratio = hm.overflow ? 1.0 : (double)hm.n_kmers / (double)total;
+    const int f = (int)(900.0 / (V2_BW_WG * std::max(ratio, 1e-3)));
+    co_spread.store(std::max(1, std::min(4, f)), std::memory_order_relaxed);
+  }
   PinnedPool::get().give(B->rec, false);
   B->rec = PinnedRec{};
   B->pending = false;
