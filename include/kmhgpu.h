@@ -206,6 +206,12 @@ int kmhg_sh_count_reads_device(kmhg_index **sh, const void *d_seq, const void *d
                                const int64_t *d_offsets, const uint8_t *d_has_qual,
                                int64_t n_reads, const int32_t params[8], void *stream);
 
+/* Diagnostics of the last batch counted into a suffix hash (no reference counterpart): the HLL
+ * estimate of its distinct canonical k-mers, the bucket spread its count-only build chose
+ * (stream entries per LDS sub-table / 1024), and the path taken: 1 = built at that spread,
+ * 2 = a sub-table overflowed and the batch was rebuilt at spread 1, 3 = global find-or-insert. */
+int kmhg_sh_last_batch(const kmhg_index *sh, double *distinct_est, int *spread, int *path);
+
 /* seq.kmer.depth.sh <- .Call("seq_kmer_depth_sh", hash.ptr, seq, k)  src/kmer_hash.c:859-879
  *        (+ seq_kmer_counts src/kmer_reader.c:155-193)
  * counts = counts_n x L int32 (R column-major): the counts of the canonical k-mer the reference's

@@ -80,6 +80,8 @@ _PROTOS = {
     "kmhg_sh_spectrum": (C.c_int, [vp, C.c_int, vp, vp, C.c_int, vp, C.c_int, vp,
                                    C.POINTER(C.c_int)]),
     "kmhg_counts_export": (C.c_int, [vp, vp, vp]),
+    "kmhg_sh_last_batch": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int),
+                                     C.POINTER(C.c_int)]),
     "kmhg_image_sizes_get": (C.c_int, [vp, C.POINTER(ImageSizes), i64p]),
     "kmhg_image_export": (C.c_int, [vp, vp, vp, vp]),
     "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, C.POINTER(vp)]),

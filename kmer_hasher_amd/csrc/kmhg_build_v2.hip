@@ -71,9 +71,12 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ uint32_t div_magic(uint32_t x, uint64_t m) {
   return m ? (uint32_t)__umul64hi((uint64_t)x, m) : x;
 }
-__device__ __forceinline__ uint32_t digit_of(uint64_t key, uint32_t nb, const Digit& D) {
-  const uint32_t q = div_magic(bucket_of(mix64(key), nb), D.mdiv);
+__device__ __forceinline__ uint32_t digit_of_h(uint64_t h, uint32_t nb, const Digit& D) {
+  const uint32_t q = div_magic(bucket_of(h, nb), D.mdiv);
   return q - div_magic(q, D.mR) * D.R;
+}
+__device__ __forceinline__ uint32_t digit_of(uint64_t key, uint32_t nb, const Digit& D) {
+  return digit_of_h(mix64(key), nb, D);
 }
 
 // Lanes of the wave holding the same `v` (nbits wide) among active lanes: one ballot per bit.
@@ -199,13 +202,27 @@ k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict
 }
 
 // ---------------------------------------------------------------- V_hist (passes >= 1)
+// HLL (count-only builds, first pass): a HyperLogLog sketch of the distinct keys rides on the
+// histogram pass, which hashes every key anyway.  A 1/HLL_SAMPLE key-space sample (h mod 64 == 0)
+// updates register (h >> 6) mod 256 with rho = leading zeros of h's top 50 bits + 1; each
+// workgroup leaves its registers as one 256-B row (bytes), V_hll reduces the rows.
+constexpr uint32_t HLL_SAMPLE_BITS = 6;
+constexpr uint32_t HLL_PART_ROWS = 256;        // V_hll workgroups (partial rows) at most
+static_assert(HLL_PART_WORDS == HLL_PART_ROWS * 64 + 1, "V_hll partial rows + ticket");
+
+template <bool HLL>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
           Digit D, uint32_t* __restrict__ hist, Chunks ch, int remap,
-          uint64_t* __restrict__ scan_status, uint32_t n_status) {
+          uint64_t* __restrict__ scan_status, uint32_t n_status, uint32_t* __restrict__ hll_rows,
+          uint32_t* __restrict__ hll_regs) {
   __shared__ uint32_t lh[V2_MAXR];
+  __shared__ uint32_t hreg[HLL ? HLL_REGS : 1];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
     scan_status[i] = 0;
+  if (HLL) {
+    for (uint32_t i = threadIdx.x; i < HLL_REGS; i += BLOCK) hreg[i] = 0;
+  }
   const uint64_t n = *n_ptr;
   const uint32_t c = remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x;
   const uint64_t e0 = (uint64_t)c * ch.tpc * PTILE;
@@ -219,7 +236,11 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
 #pragma unroll
     for (int j = 0; j < 4; ++j) {                // 4 loads in flight per lane
       in[j] = e + j * BLOCK < e1;
-      dg[j] = in[j] ? digit_of(keys[e + j * BLOCK], g.nb, D) : 0u;
+      const uint64_t h = in[j] ? mix64(keys[e + j * BLOCK]) : 1ull;
+      dg[j] = in[j] ? digit_of_h(h, g.nb, D) : 0u;
+      if (HLL && (h & ((1u << HLL_SAMPLE_BITS) - 1)) == 0)
+        atomicMax(&hreg[(uint32_t)(h >> HLL_SAMPLE_BITS) & (HLL_REGS - 1)],
+                  (uint32_t)__clzll(h | ((1ull << (HLL_SAMPLE_BITS + 8)) - 1)) + 1u);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -227,6 +248,91 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
   }
   __syncthreads();
   for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[(size_t)d * ch.C + c] = lh[d];
+  if (HLL && threadIdx.x < HLL_REGS / 4) {
+    const uint32_t* h4 = hreg + 4 * threadIdx.x;
+    hll_rows[(size_t)blockIdx.x * (HLL_REGS / 4) + threadIdx.x] =
+        h4[0] | (h4[1] << 8) | (h4[2] << 16) | (h4[3] << 24);
+  }
+}
+
+// V_hll: register-wise max of the histogram workgroups' HLL rows.  V_hll_part: workgroup g
+// reduces rows [g * rpw, (g + 1) * rpw) into partial row g (thread t takes packed word t mod 64
+// of every 16th row: each row one coalesced 256-B read, eight rows in flight per thread);
+// V_hll_final (one workgroup) reduces the partial rows and turns the registers into the estimate
+// of distinct keys (Flajolet et al. 2007, linear counting in the small range, x 64 for the
+// sample), published to pinned host memory.  Two launches instead of a last-workgroup ticket:
+// the ticket's release fence per workgroup (an XCD L2 write-back) cost ~35 us.
+__device__ __forceinline__ uint32_t max_u8x4(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r |= max((a >> (8 * j)) & 0xFFu, (b >> (8 * j)) & 0xFFu) << (8 * j);
+  return r;
+}
+
+// rows r0 + q, r0 + q + HLL_RG, ... below r1, word w: eight independent loads per trip
+constexpr uint32_t HLL_T = 1024;               // V_hll threads: 16 row groups x 64 words
+constexpr uint32_t HLL_RG = HLL_T / 64;
+__device__ __forceinline__ uint32_t hll_rows_max(const uint32_t* rows, uint32_t r0, uint32_t r1,
+                                                 uint32_t w, uint32_t q) {
+  uint32_t m = 0;
+  uint32_t r = r0 + q;
+  for (; r + 7 * HLL_RG < r1; r += 8 * HLL_RG) {
+    uint32_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = rows[(size_t)(r + j * HLL_RG) * 64 + w];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = max_u8x4(m, x[j]);
+  }
+  for (; r < r1; r += HLL_RG) m = max_u8x4(m, rows[(size_t)r * 64 + w]);
+  return m;
+}
+
+__global__ void __launch_bounds__(HLL_T)
+k_v2_hll_part(const uint32_t* __restrict__ rows, uint32_t n_rows, uint32_t* __restrict__ part) {
+  __shared__ uint32_t pw[HLL_RG][64];
+  const uint32_t w = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const uint32_t rpw = (n_rows + gridDim.x - 1) / gridDim.x;
+  const uint32_t r0 = blockIdx.x * rpw, r1 = min(n_rows, r0 + rpw);
+  pw[q][w] = hll_rows_max(rows, r0, r1, w, q);
+  __syncthreads();
+  if (q == 0) {
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < HLL_RG; ++j) m = max_u8x4(m, pw[j][w]);
+    part[(size_t)blockIdx.x * 64 + w] = m;
+  }
+}
+
+__global__ void __launch_bounds__(HLL_T)
+k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __restrict__ host_est) {
+  __shared__ uint32_t pw[HLL_RG][64];
+  __shared__ double zs[HLL_REGS / 64];
+  __shared__ uint32_t zc[HLL_REGS / 64];
+  const uint32_t w = threadIdx.x & 63, q = threadIdx.x >> 6;
+  pw[q][w] = hll_rows_max(part, 0, n_part, w, q);
+  __syncthreads();
+  if (threadIdx.x < HLL_REGS) {                // one thread per register
+    const uint32_t reg = threadIdx.x, wr = reg >> 2, sh = 8 * (reg & 3);
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < HLL_RG; ++j) v = max(v, (pw[j][wr] >> sh) & 0xFFu);
+    double z = ldexp(1.0, -(int)v);
+    uint32_t zero = v == 0;
+    for (int d = 32; d >= 1; d >>= 1) {
+      z += __shfl_xor(z, d);
+      zero += __shfl_xor(zero, d);
+    }
+    if (lane_id() == 0) { zs[threadIdx.x >> 6] = z; zc[threadIdx.x >> 6] = zero; }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double mm = HLL_REGS;
+    const double zt = zs[0] + zs[1] + zs[2] + zs[3];
+    const uint32_t zeros = zc[0] + zc[1] + zc[2] + zc[3];
+    double e = 0.7213 / (1.0 + 1.079 / mm) * mm * mm / zt;
+    if (e <= 2.5 * mm && zeros) e = mm * log(mm / (double)zeros);
+    *host_est = e * (double)(1u << HLL_SAMPLE_BITS);
+  }
 }
 
 // ---------------------------------------------------------------- V_scatter (stable)
@@ -1136,6 +1242,7 @@ k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __re
       r.n_small = 0;
       r.n_large = 0;
       r.blocks_done = done + 1;
+      r.distinct_est = 0;
       *host_meta = r;
       __threadfence_system();
     }
@@ -1230,9 +1337,20 @@ void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total,
   }
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
-                    Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_hist, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist, ch,
-                     xcd_map(), scan_status, n_status);
+                    Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
+                    uint32_t* hll_rows, uint32_t* hll_regs) {
+  if (hll_rows)
+    hipLaunchKernelGGL(k_v2_hist<true>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
+                       ch, xcd_map(), scan_status, n_status, hll_rows, hll_regs);
+  else
+    hipLaunchKernelGGL(k_v2_hist<false>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
+                       ch, xcd_map(), scan_status, n_status, nullptr, nullptr);
+}
+void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
+                   hipStream_t s) {
+  const uint32_t g = std::max(1u, std::min(HLL_PART_ROWS, (n_rows + 127) / 128));
+  hipLaunchKernelGGL(k_v2_hll_part, dim3(g), dim3(HLL_T), 0, s, hll_rows, n_rows, hll_regs);
+  hipLaunchKernelGGL(k_v2_hll_final, dim3(1), dim3(HLL_T), 0, s, hll_regs, g, host_est);
 }
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,

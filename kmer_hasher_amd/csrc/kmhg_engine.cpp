@@ -409,6 +409,10 @@ struct kmhg_index {
   uint32_t sources = 0;
   bool canonical = false;         // suffix hash (count.kmers.fq.sh.rp): canonical k-mer counts
   uint64_t rows_cap = 0, kmer_count = 0;
+  bool u_upper = false;           // U is only an upper bound (batch table of the global fallback)
+  // last read batch (kmhg_sh_last_batch): HLL distinct estimate, bucket spread, build path
+  double co_est = 0;
+  int co_spread = 0, co_path = 0;
   DBuf<uint64_t> ckeys;
   DBuf<uint32_t> slot_row, row_slot;
   // stream-ordered release of everything the index holds (work queued on `s` may still read it)
@@ -508,14 +512,33 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   return idx.release();
 }
 
+constexpr double CO_FILL = 0.6;                  // target mean occupancy of a count-only bucket
+
+// Stream entries per group bucket (in units of V2_BW_WG) for a batch of `total` keys with
+// ~`distinct` distinct ones: mean distinct keys per bucket ~CO_FILL x V2_CAPW, at most 4x.
+// KMHG_CO_SPREAD (tests) forces one, rounded down to a divisor of 12 (build_device_v2).
+int co_spread_for(double distinct, uint64_t total) {
+  if (const char* e = std::getenv("KMHG_CO_SPREAD")) {
+    int f = std::max(1, std::min(12, std::atoi(e)));
+    while (12 % f) --f;
+    return f;
+  }
+  const double ratio = std::max(std::min(distinct / std::max<double>((double)total, 1.0), 1.0), 1e-3);
+  const int f = (int)(CO_FILL * V2_CAPW / (V2_BW_WG * ratio));
+  return std::max(1, std::min(4, f));
+}
+
 // Partitioned build (kmhg_build_v2.hip): LSD radix partition of the windows by hash bucket,
 // then one wave per bucket builds its sub-table in LDS.  Falls back to v1 if a bucket's LDS
-// sub-table overflows (never observed: distinct keys per bucket ~ Binomial, mean <= V2_BW).
+// sub-table overflows (position builds: never observed -- distinct keys per bucket ~ Binomial,
+// mean <= V2_BW; count-only builds retry at spread 1 instead, sh_count_reads_device).
 // Partitioned build over the windows of a sequence (d_seq), or over a stream of n_keys
 // distinct keys (d_keys, d_seq == nullptr; the counts index's table rebuild): key r is stored
 // with count 1 and aux = r + 1.
 // count_only (a key stream whose positions nobody reads: read counting): the group bucket kernel
 // skips its position pass and no positions array is kept.
+// count_only with co_spread = 0: the spread is chosen from the key stream's own HLL estimate
+// (co_spread_for), read back while the radix passes run.
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
                             const uint64_t* d_keys = nullptr, int64_t n_keys = 0,
                             bool count_only = false, int co_spread = 1) {
@@ -557,16 +580,19 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // buckets halve the radix (longer digit runs) -- config 2 26.1 vs 24.8 Gbp/s -- and save a pass
   // from ~26 M windows -- config 3 26.3 vs 24.5.  KMHG_BUCKET=wave|group forces one.
   const uint32_t nb_w = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW - 1) / V2_BW);
-  // count-only builds: co_spread (KMHG_CO_SPREAD overrides) x more stream entries per group
-  // bucket -- a read batch's distinct keys are a fraction of its key stream, so fewer buckets
-  // still fit their LDS sub-tables (an overflowing bucket takes the global find-or-insert path)
+  // count-only builds: co_spread x more stream entries per group bucket -- a read batch's
+  // distinct keys are a fraction of its key stream, so fewer buckets still fit their LDS
+  // sub-tables (co_spread_for); one overflowing bucket fails the whole build (meta->overflow)
+  // and sh_count_reads_device rebuilds at spread 1.  With co_spread = 0 the radix passes sort
+  // by the bucket b1 among nb1 = 12 * ceil(Nw / (12 * V2_BW_WG)): the bucket among nb1 / s is
+  // b1 / s exactly (floor(floor(h nb1 / 2^64) / s) = floor(h (nb1 / s) / 2^64)), so one sorted
+  // stream serves every spread s in {1, 2, 3, 4}, and s is picked only before the bucket stage.
+  const bool co_auto = count_only && co_spread == 0;
   int64_t bw_g = V2_BW_WG;
-  if (count_only) {
-    int f = co_spread;
-    if (const char* e = std::getenv("KMHG_CO_SPREAD")) f = std::atoi(e);
-    bw_g *= std::max(1, std::min(8, f));
-  }
-  const uint32_t nb_g = (uint32_t)std::max<int64_t>(1, (Nw + bw_g - 1) / bw_g);
+  if (count_only && !co_auto) bw_g *= std::max(1, std::min(8, co_spread));
+  const uint32_t nb_g =
+      co_auto ? (uint32_t)(12 * std::max<int64_t>(1, (Nw + 12 * V2_BW_WG - 1) / (12 * V2_BW_WG)))
+              : (uint32_t)std::max<int64_t>(1, (Nw + bw_g - 1) / bw_g);
   uint32_t R_w = 0, R_g = 0;
   const uint32_t passes_w = plan(nb_w, R_w), passes_g = plan(nb_g, R_g);
   bool group = passes_g <= passes_w;
@@ -576,6 +602,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     if (std::string(e) == "sort") group = sorted = true;
     if (std::string(e) == "wave") group = false;
   }
+  if (count_only) { group = true; sorted = false; }   // the keys-only group bucket build
   const uint32_t nb = group ? nb_g : nb_w;
   const uint32_t passes = group ? passes_g : passes_w;
   const uint32_t R = group ? R_g : R_w;
@@ -600,9 +627,14 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   BuildMeta* meta = reinterpret_cast<BuildMeta*>(sc + off_meta);
   uint64_t* status = reinterpret_cast<uint64_t*>(sc + off_status);
   idx->rec = PinnedPool::get().take();                     // V_stats writes the totals here
-  idx->table.reset(idx->slots());
+  if (!co_auto) idx->table.reset(idx->slots());
   idx->positions.reset(no_pos ? 1 : Nw);
   DBuf<BucketStats> bstats(nb, s);
+  // co_auto: HLL rows of the first histogram pass, V_hll's registers + ticket, its pinned record
+  DBuf<uint32_t> hll_rows(co_auto ? (size_t)ch.C * (HLL_REGS / 4) : 1, s);
+  DBuf<uint32_t> hll_regs(co_auto ? HLL_PART_WORDS : 1, s);
+  PinnedRec hrec;
+  if (co_auto) hrec = PinnedPool::get().take();
 
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
@@ -624,8 +656,15 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const Digit Dp = make_digit(div, R);
     const bool keys0 = from_keys && p == 0;
     const uint64_t* src = keys0 ? d_keys : kin;
+    const bool hll = co_auto && p == 0;
     LAUNCH("k_v2_hist", s,
-           launch_v2_hist(src, n_valid, g, Dp, hist.p, ch, status, n_status, s));
+           launch_v2_hist(src, n_valid, g, Dp, hist.p, ch, status, n_status, s,
+                          hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr));
+    if (hll) {
+      LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ch.C, hll_regs.p,
+                                          &hrec.meta->distinct_est, s));
+      HIPC(hipEventRecord(hrec.ev, s));
+    }
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     if (keys0) {
       LAUNCH("k_v2_scatter", s,
@@ -642,7 +681,18 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     std::swap(pin, pout);
     div *= R;
   }
-  LAUNCH("k_v2_bounds", s, launch_v2_bounds(kin, n_valid, g, start.p, (uint64_t)Nw, s));
+  Geom gb = g;                     // the bucket stage's geometry
+  if (co_auto) {
+    // the estimate landed while the later radix passes were still queued on the device
+    HIPC(hipEventSynchronize(hrec.ev));
+    idx->co_est = hrec.meta->distinct_est;
+    PinnedPool::get().give(hrec, false);
+    idx->co_spread = co_spread_for(idx->co_est, (uint64_t)Nw);
+    gb = Geom{nb / (uint32_t)idx->co_spread, V2_CAPW};
+    idx->geom = gb;
+    idx->table.reset(idx->slots());
+  }
+  LAUNCH("k_v2_bounds", s, launch_v2_bounds(kin, n_valid, gb, start.p, (uint64_t)Nw, s));
 #ifdef KMHG_STAMPS
   static uint64_t* stamps = nullptr;
   if (!stamps) HIPC(hipMallocManaged(&stamps, sizeof(uint64_t) * 8 * (1u << 22)));
@@ -655,13 +705,13 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
                                  meta, s));
   else if (group)
     LAUNCH("k_v2_bucket_wg", s,
-           launch_v2_bucket_wg(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
+           launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, bstats.p,
                                meta, no_pos, s));
   else
     LAUNCH("k_v2_bucket", s,
            launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
                             meta, s));
-  LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, nb, n_valid, meta, idx->rec.meta, s));
+  LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, gb.nb, n_valid, meta, idx->rec.meta, s));
   HIPC(hipEventRecord(idx->rec.ev, s));
 #ifdef KMHG_STAMPS
   if (const char* f = std::getenv("KMHG_STAMP_FILE")) {
@@ -687,7 +737,8 @@ kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) 
 }
 
 // Wait for a pending build and collect its totals.  If a bucket's LDS sub-table overflowed
-// (never observed: distinct keys per bucket ~ Binomial with mean <= V2_BW), the index is rebuilt
+// (position builds: never observed -- distinct keys per bucket ~ Binomial with mean <= V2_BW;
+// count-only builds do not come here), the index is rebuilt
 // with the global-atomic build from the retained input.
 void finish_build(kmhg_index* idx) {
   if (!idx->pending) return;
@@ -892,7 +943,7 @@ void adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, hipStrea
 // distinct key (<= 4x the rebuilt table); otherwise the general merge rebuilds a compact one.
 // KMHG_COUNT_TABLE (tests): "adopt" adopts regardless of size, "rebuild" / "probe" never do.
 bool adoptable(const kmhg_index* idx, const kmhg_index* B) {
-  if (idx->U != 0) return false;
+  if (idx->U != 0 || B->u_upper) return false;   // a table sized by a key stream: rebuild
   if (const char* e = std::getenv("KMHG_COUNT_TABLE")) return std::string(e) == "adopt";
   return B->slots() <= 6 * B->U;
 }
@@ -978,7 +1029,7 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_
   const uint64_t U1 = U0 + n_new;
   // rebuild the table for U1 keys (aux of a source_n = 1 index carries the count itself, so
   // even a batch of known keys changes the slots): the partitioned build over the key list,
-  // or global linear probing should a bucket overflow (never observed: distinct keys)
+  // or global linear probing should a bucket overflow (never observed: a key list is distinct)
   idx->table.bind(s);
   idx->slot_row.bind(s);
   idx->row_slot.bind(s);
@@ -1055,6 +1106,25 @@ double qll_host(int q) {   // the same table on the host (the iterator's thresho
   return std::strtod(buf, nullptr);
 }
 
+// The count-only partitioned build of a key stream at `spread` (0: from its HLL estimate),
+// waited for.  `overflow`: a bucket's LDS sub-table filled up -- the table is unusable and the
+// caller retries at spread 1 (the index still reports the spread and estimate it tried).
+std::unique_ptr<kmhg_index> count_only_build(const uint64_t* keys, uint32_t total, int k,
+                                             int spread, hipStream_t s, bool& overflow) {
+  std::unique_ptr<kmhg_index> B(
+      build_device_v2(nullptr, 0, k, s, keys, (int64_t)total, true, spread));
+  HIPC(hipEventSynchronize(B->rec.ev));
+  const BuildMeta hm = *B->rec.meta;
+  PinnedPool::get().give(B->rec, false);
+  B->rec = PinnedRec{};
+  B->pending = false;
+  B->stream = s;
+  if (!B->co_spread) B->co_spread = spread;
+  overflow = hm.overflow != 0;
+  B->U = overflow ? 0 : hm.n_kmers;
+  return B;
+}
+
 kmhg_index* new_sh_index(int k, int counts_n, hipStream_t s) {
   auto idx = std::make_unique<kmhg_index>();
   HIPC(hipGetDevice(&idx->device));
@@ -1101,35 +1171,46 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   LAUNCH("k_read_kmers_emit", s,
          launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
                            keys.p, true, s));
-  // bucket spread from the distinct / stream ratio the previous count-only build measured
-  // (bench, 3.7x coverage: spread 1/2/3/4 -> 22.6/26.8/28.5/27.6 Gbp/s): mean distinct keys per
-  // group bucket ~900 of its 1536 LDS slots; an overflow resets it to 1
-  static std::atomic<int> co_spread{1};
-  const int spread = co_spread.load(std::memory_order_relaxed);
-  std::unique_ptr<kmhg_index> B(
-      build_device_v2(nullptr, 0, k, s, keys.p, (int64_t)total, true, spread));
-  Release rel{B.get(), s};
-  HIPC(hipEventSynchronize(B->rec.ev));
-  const BuildMeta hm = *B->rec.meta;
-  {
-    const double ratio = hm.overflow ? 1.0 : (double)hm.n_kmers / (double)total;
-    const int f = (int)(900.0 / (V2_BW_WG * std::max(ratio, 1e-3)));
-    co_spread.store(std::max(1, std::min(4, f)), std::memory_order_relaxed);
+  // The count-only build gives each group bucket `spread` x V2_BW_WG stream entries, so that the
+  // batch's distinct keys -- not its key stream -- fill the LDS sub-tables (bench, 3.7x
+  // coverage: spread 1/2/3/4 -> 22.6/26.8/28.5/27.6 Gbp/s).  The spread comes from THIS
+  // batch's HLL estimate of its distinct keys (build_device_v2, co_spread = 0).
+  // KMHG_CO_GLOBAL=1 (tests): straight to the global fallback below
+  const bool force_global = std::getenv("KMHG_CO_GLOBAL") != nullptr;
+  std::unique_ptr<kmhg_index> B;
+  bool ovf = true;
+  int path = 1;
+  double est = 0.0;
+  int spread = 0;
+  if (!force_global) {
+    B = count_only_build(keys.p, total, k, 0, s, ovf);
+    est = B->co_est;
+    spread = B->co_spread;
+    if (ovf && spread > 1) {                     // a sub-table overflowed: spread 1 (mean 1024)
+      path = 2;
+      B->bind_all(s);
+      B = count_only_build(keys.p, total, k, 1, s, ovf);
+    }
   }
-  PinnedPool::get().give(B->rec, false);
-  B->rec = PinnedRec{};
-  B->pending = false;
-  B->stream = s;
-  if (hm.overflow) {                             // never observed: global find-or-insert
+  if (ovf) {                                     // still overflowing: global find-or-insert
+    path = 3;
+    if (B) B->bind_all(s);
+    B = std::make_unique<kmhg_index>();
+    HIPC(hipGetDevice(&B->device));
+    B->k = k;
+    B->stream = s;
     B->geom = Geom{1u, (uint32_t)table_capacity((int64_t)total)};
     B->table.reset(B->slots());
     LAUNCH("k_table_init", s, launch_table_init(B->table.p, B->slots(), s));
     LAUNCH("k_key_count_insert", s,
            launch_key_count_insert(keys.p, total, B->table.p, B->geom, s));
     B->U = total;                                // an upper bound (row capacity only)
-  } else {
-    B->U = hm.n_kmers;
+    B->u_upper = true;                           // sized by the stream: never adopted
   }
+  Release rel{B.get(), s};
+  idx->co_est = est;
+  idx->co_spread = spread;
+  idx->co_path = path;
   merge_batch(idx, B.get(), nullptr, B->slots(), source, s);
 }
 
@@ -1859,6 +1940,15 @@ int kmhg_counts_export(kmhg_index* idx, uint64_t* keys, int32_t* counts) {
       HIPC(hipMemcpyAsync(counts, idx->positions.p, idx->U * idx->sources * 4,
                           hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+  });
+}
+
+int kmhg_sh_last_batch(const kmhg_index* sh, double* distinct_est, int* spread, int* path) {
+  return guarded([&] {
+    if (!sh || !sh->canonical) fail(KMHG_EINVAL, "not a suffix hash");
+    if (distinct_est) *distinct_est = sh->co_est;
+    if (spread) *spread = sh->co_spread;
+    if (path) *path = sh->co_path;
   });
 }
 

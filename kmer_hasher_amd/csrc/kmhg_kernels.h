@@ -29,6 +29,7 @@ struct BuildMeta {              // written by the build kernels, read once by th
   uint32_t n_large;             // keys with n >= LARGE_MIN
   uint32_t overflow;            // partitioned build: a bucket's LDS sub-table filled up
   uint32_t blocks_done;         // V_stats arrival counter (last block publishes to the host)
+  double distinct_est;          // count-only builds: V_hll's estimate of the distinct keys
 };
 
 struct ReadMeta {               // canonical-order readout preparation
@@ -129,8 +130,17 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
 // reduce-then-scan (status = tile sums) beyond.
 constexpr uint32_t LB_SCAN_MAX_TILES = 256;
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s);
+// hll_rows (count-only builds, first pass): the histogram workgroups also sketch the distinct
+// keys (HyperLogLog, HLL_REGS registers, 1/64 key-space sample) into one 256-B row each (ch.C
+// rows, HLL_REGS / 4 u32); launch_v2_hll reduces the rows (through hll_regs = HLL_PART_WORDS u32
+// of partial rows) and writes the distinct-key estimate to *host_est (pinned host memory)
+constexpr uint32_t HLL_REGS = 256;
+constexpr uint32_t HLL_PART_WORDS = 256 * 64 + 1;
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
-                    Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s);
+                    Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
+                    uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr);
+void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
+                   hipStream_t s);
 // the sequence must be 16-B aligned (the engine copies an unaligned input)
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,

@@ -198,3 +198,75 @@ def test_sh_fuzz_fastx(gpu, seed, tmp_path):
         keys, M = _sorted_table(ptr)
         ok, om = O.OracleSH(k, 2).add_fastq(p, mq, 2**62, 1).arrays()
         assert np.array_equal(keys, ok) and np.array_equal(M, om), (k, mq)
+
+
+def _last_batch(ptr):
+    from kmer_hasher_amd import _lib
+    est, sp, path = C.c_double(), C.c_int(), C.c_int()
+    _lib.check(_lib.lib().kmhg_sh_last_batch(ptr.handle, C.byref(est), C.byref(sp),
+                                             C.byref(path)))
+    return est.value, sp.value, path.value
+
+
+def _count_packed(torch, seq, qual, k, mq, ptr=None, source=0, S=1):
+    from kmer_hasher_amd import _lib, api
+    ds, dq, do, dh = _pack(torch, seq, qual)
+    h = C.c_void_p(ptr.handle.value if ptr is not None else None)
+    prm = (C.c_int32 * 8)(k, 10, mq, 1, -1, 1, S, source)
+    _lib.check(_lib.lib().kmhg_sh_count_reads_device(C.byref(h), ds.data_ptr(), dq.data_ptr(),
+                                                     do.data_ptr(), dh.data_ptr(), len(seq), prm,
+                                                     None))
+    torch.cuda.synchronize()
+    return ptr if ptr is not None else api.ExtPtr(h.value, tag=api.SUFFIX_HASH_N_TAG)
+
+
+@pytest.mark.parametrize("table", ["adopt", "rebuild"])
+@pytest.mark.parametrize("env,want_path", [({}, 1), ({"KMHG_CO_SPREAD": "8"}, 2),
+                                           ({"KMHG_CO_GLOBAL": "1"}, 3)])
+def test_sh_count_only_build_paths(gpu, monkeypatch, env, want_path, table):
+    """Every path of the count-only batch build, forced, against the oracle: the spread chosen
+    from the batch's own HLL estimate (1), a spread too wide for low-coverage reads (distinct /
+    stream ~ 0.9: KMHG_CO_SPREAD=8 overflows a sub-table -> the batch is rebuilt at spread 1)
+    (2), and the global find-or-insert fallback (3), whose stream-sized table is never adopted."""
+    torch = gpu
+    from kmer_hasher_amd import synth
+    monkeypatch.setenv("KMHG_COUNT_TABLE", table)
+    for kk, v in env.items():
+        monkeypatch.setenv(kk, v)
+    g = synth.iid(3_000_000, 81)
+    seq, qual = synth.reads(g, 20_000, 150, 82)
+    k, mq = 31, 10
+    ptr = _count_packed(torch, seq, qual, k, mq)
+    est, sp, path = _last_batch(ptr)
+    assert path == want_path, (est, sp, path)
+    keys, M = _sorted_table(ptr)
+    uk, cnt = _oracle_counts(seq, qual, np.ones(len(seq), np.uint8), k, mq)
+    assert np.array_equal(keys, uk) and np.array_equal(M[:, 0], cnt)
+
+
+def test_sh_spread_per_batch(gpu):
+    """The spread comes from each batch's own distinct / stream estimate, not from an earlier
+    batch: a deep-coverage batch (spread > 1) followed by a low-coverage batch of another genome
+    into the same hash builds at spread 1 without an overflow; the HLL estimate (256 registers:
+    standard error 1.04 / 16 = 6.5 %) is within 25 % of the true number of distinct k-mers;
+    counts equal the oracle's after both batches."""
+    torch = gpu
+    from kmer_hasher_amd import synth
+    k, mq = 31, 10
+    g1 = synth.iid(500_000, 91)
+    s1, q1 = synth.reads(g1, 40_000, 150, 92)                 # ~12x coverage
+    ptr = _count_packed(torch, s1, q1, k, mq)
+    est1, sp1, path1 = _last_batch(ptr)
+    u1 = len(_oracle_counts(s1, q1, np.ones(len(s1), np.uint8), k, mq)[0])
+    assert sp1 > 1 and path1 == 1
+    assert abs(est1 - u1) < 0.25 * u1, (est1, u1)
+    g2 = synth.iid(4_000_000, 93)
+    s2, q2 = synth.reads(g2, 20_000, 150, 94)                 # ~0.75x coverage
+    _count_packed(torch, s2, q2, k, mq, ptr)
+    est2, sp2, path2 = _last_batch(ptr)
+    assert sp2 == 1 and path2 == 1, (est2, sp2, path2)
+    keys, M = _sorted_table(ptr)
+    seq = np.concatenate([s1, s2])
+    qual = np.concatenate([q1, q2])
+    uk, cnt = _oracle_counts(seq, qual, np.ones(len(seq), np.uint8), k, mq)
+    assert np.array_equal(keys, uk) and np.array_equal(M[:, 0], cnt)
