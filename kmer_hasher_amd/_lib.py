@@ -115,6 +115,8 @@ def lib():
             pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _PROTOS.items():
+            if os.environ.get("KMHG_LIB_VARIANT") and not hasattr(L, name):
+                continue              # an older A/B build may predate an entry point
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
