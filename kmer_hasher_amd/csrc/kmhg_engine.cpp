@@ -66,6 +66,13 @@ int guarded(F&& f) {
 // ============================================================================ device pool
 // Caching allocator: blocks are kept per (device, rounded size) and reused, so repeated builds
 // and queries (bench steps, many queries against one index) pay hipMalloc once.
+// Stream-ordered releases inside one host call (one build, query, ...) share ONE event: every
+// ordered release on the group's stream is deferred to the group's end, where a single event is
+// recorded for all of them.  (Each event record is a marker packet the command processor
+// drains the stream for; a build used to record ~14 of them back to back.)
+struct ReleaseGroup;
+thread_local ReleaseGroup* tl_release_group = nullptr;
+
 class DevicePool {
  public:
   static DevicePool& get() {
@@ -97,7 +104,7 @@ class DevicePool {
         g.unlock();
         (void)hipEventSynchronize(pd.ev);
         g.lock();
-        events_.push_back(pd.ev);
+        if (pd.owns_ev) events_.push_back(pd.ev);
         live_[pd.p] = pd.key;
         return pd.p;
       }
@@ -116,7 +123,35 @@ class DevicePool {
   }
   // Stream-ordered release: the block returns to the free list once the work queued on
   // `stream` up to now has completed (an event is recorded and polled on later allocations).
-  void release(void* p, hipStream_t stream = nullptr, bool ordered = false) {
+  void release(void* p, hipStream_t stream = nullptr, bool ordered = false);
+  // the group's blocks: one event recorded on `stream` for all of them
+  void release_batch(const std::vector<void*>& ps, hipStream_t stream) {
+    if (ps.empty()) return;
+    hipEvent_t ev = nullptr;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!events_.empty()) { ev = events_.back(); events_.pop_back(); }
+    }
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+    if (!ev || hipEventRecord(ev, stream) != hipSuccess) {
+      (void)hipStreamSynchronize(stream);
+      if (ev) { std::lock_guard<std::mutex> g(mu_); events_.push_back(ev); }
+      ev = nullptr;
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t i = 0; i < ps.size(); ++i) {
+      auto it = live_.find(ps[i]);
+      if (it == live_.end()) continue;
+      if (ev) {
+        pending_.push_back({ps[i], it->second, ev, i + 1 == ps.size()});
+      } else {
+        free_[it->second].push_back(ps[i]);
+        cached_ += it->second.second;
+      }
+      live_.erase(it);
+    }
+  }
+  void release_one(void* p, hipStream_t stream, bool ordered) {
     if (!p) return;
     hipEvent_t ev = nullptr;
     if (ordered) {
@@ -135,7 +170,7 @@ class DevicePool {
     auto it = live_.find(p);
     if (it == live_.end()) return;
     if (ev) {
-      pending_.push_back({p, it->second, ev});
+      pending_.push_back({p, it->second, ev, true});
     } else {
       free_[it->second].push_back(p);
       cached_ += it->second.second;
@@ -146,7 +181,7 @@ class DevicePool {
     std::lock_guard<std::mutex> g(mu_);
     for (auto& pd : pending_) {
       (void)hipEventSynchronize(pd.ev);
-      events_.push_back(pd.ev);
+      if (pd.owns_ev) events_.push_back(pd.ev);
       free_[pd.key].push_back(pd.p);
     }
     pending_.clear();
@@ -166,11 +201,14 @@ class DevicePool {
   }
 
  private:
-  struct Pending { void* p; std::pair<int, size_t> key; hipEvent_t ev; };
+  // owns_ev: the one entry of a batch that recycles the shared event.  An entry polled after
+  // its batch's event was recycled and recorded again only waits for later work (safe).
+  struct Pending { void* p; std::pair<int, size_t> key; hipEvent_t ev; bool owns_ev; };
   void poll_pending() {
     for (size_t i = 0; i < pending_.size();) {
       if (hipEventQuery(pending_[i].ev) == hipSuccess) {
-        events_.push_back(pending_[i].ev);          // recycled: no create/destroy per release
+        if (pending_[i].owns_ev)
+          events_.push_back(pending_[i].ev);        // recycled: no create/destroy per release
         free_[pending_[i].key].push_back(pending_[i].p);
         cached_ += pending_[i].key.second;
         pending_[i] = pending_.back();
@@ -196,6 +234,30 @@ class DevicePool {
   std::vector<hipEvent_t> events_;
   size_t cached_ = 0;
 };
+
+struct ReleaseGroup {
+  hipStream_t s;
+  std::vector<void*> ps;
+  ReleaseGroup* prev;
+  explicit ReleaseGroup(hipStream_t stream) : s(stream), prev(tl_release_group) {
+    tl_release_group = this;
+  }
+  ~ReleaseGroup() {
+    tl_release_group = prev;
+    DevicePool::get().release_batch(ps, s);
+  }
+  ReleaseGroup(const ReleaseGroup&) = delete;
+  ReleaseGroup& operator=(const ReleaseGroup&) = delete;
+};
+
+void DevicePool::release(void* p, hipStream_t stream, bool ordered) {
+  if (!p) return;
+  if (ordered && tl_release_group && tl_release_group->s == stream) {
+    tl_release_group->ps.push_back(p);          // deferred to the group's one event
+    return;
+  }
+  release_one(p, stream, ordered);
+}
 
 // RAII device buffer from the pool.  A buffer bound to a stream is released stream-ordered
 // (kernels still queued on that stream may use it after the C++ object dies).
@@ -465,6 +527,7 @@ void check_query_args(size_t L, int k) {
 
 // ---------------------------------------------------------------------------- build
 kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
+  ReleaseGroup rg(s);
   auto idx = std::make_unique<kmhg_index>();
   idx->stream = s;
   HIPC(hipGetDevice(&idx->device));
@@ -542,6 +605,7 @@ int co_spread_for(double distinct, uint64_t total) {
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
                             const uint64_t* d_keys = nullptr, int64_t n_keys = 0,
                             bool count_only = false, int co_spread = 1) {
+  ReleaseGroup rg(s);             // the scratch buffers below: one release event
   const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
   idx->stream = s;
@@ -770,6 +834,7 @@ void finish_build(kmhg_index* idx) {
 // end, so shards of consecutive window ranges concatenate to the unsharded result.
 kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int kq, int64_t w0,
                          int64_t w1, hipStream_t s) {
+  ReleaseGroup rg(s);
   if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
   finish_build(idx);
   auto q = std::make_unique<kmhg_query>();
@@ -836,6 +901,7 @@ void prepare_readout(kmhg_index* idx, hipStream_t s);
 // Rows (a, b) for the k-mers both indices hold, a's k-mers in a's kmer.pos row order
 // (kmhg_join.hip).  Same two-phase shape as the query: probe + tile totals, one read-back, emit.
 kmhg_query* pairs_device(kmhg_index* a, kmhg_index* b, hipStream_t s) {
+  ReleaseGroup rg(s);
   if (a->canonical || b->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
   finish_build(a);
   finish_build(b);
@@ -905,6 +971,7 @@ void reserve_rows(kmhg_index* idx, uint64_t need, hipStream_t s) {
 // counts table, and the rows (first-occurrence order) come from C_first / C_order / C_slots
 // (kmhg_count.hip) -- no slot permutation, probe, append, table rebuild or C_fix.
 void adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, hipStream_t s) {
+  ReleaseGroup rg(s);
   const uint32_t S = idx->sources;
   const uint64_t Ub = B->U;
   const int64_t L = B->L;
@@ -950,6 +1017,7 @@ bool adoptable(const kmhg_index* idx, const kmhg_index* B) {
 
 void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t source,
                   hipStream_t s) {
+  ReleaseGroup rg(s);
   idx->stream = s;
   const int k = idx->k;
   if (L <= k) return;
@@ -972,6 +1040,7 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
 // empty slots skipped).  New keys get rows in item order.
 void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_t n_items,
                  uint32_t source, hipStream_t s) {
+  ReleaseGroup rg(s);
   const int k = idx->k;
   const uint32_t S = idx->sources;
   const uint64_t Ub = B->U;
@@ -1144,6 +1213,7 @@ kmhg_index* new_sh_index(int k, int counts_n, hipStream_t s) {
 void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t* d_qual,
                            const int64_t* d_off, const uint8_t* d_hasq, uint32_t n_reads,
                            double mean_len, double min_ll, uint32_t source, hipStream_t s) {
+  ReleaseGroup rg(s);
   idx->stream = s;
   if (!n_reads) return;
   const int k = idx->k;
@@ -1274,6 +1344,7 @@ int64_t read_fastx(const char* path, uint64_t max_reads, int k, ReadsHost& r,
 
 void sh_depth_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k, int32_t* d_out,
                      hipStream_t s) {
+  ReleaseGroup rg(s);
   idx->stream = s;
   const uint32_t S = idx->sources;
   if (L > 0)
@@ -1311,6 +1382,7 @@ void check_sh(const kmhg_index* idx) {
 
 // ---------------------------------------------------------------------------- readout
 void prepare_canon(kmhg_index* idx, hipStream_t s) {
+  ReleaseGroup rg(s);
   idx->stream = s;
   Canon& c = idx->canon;
   if (c.ready) return;
@@ -1429,6 +1501,7 @@ std::vector<uint32_t> khash_bucket_order(const std::vector<uint64_t>& keys) {
 // order is replayed there (inherently sequential, ~0.1 us per key), and the permuted arrays
 // come back.  The readout kernels then run unchanged.
 void prepare_readout(kmhg_index* idx, hipStream_t s) {
+  ReleaseGroup rg(s);
   finish_build(idx);
   Canon& c = idx->canon;
   if (c.ready && c.order == idx->row_order) return;
@@ -1495,6 +1568,7 @@ void positions_sizes(kmhg_index* idx, uint32_t opt, int64_t* nk, int64_t* np, in
 
 void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, int32_t* pairs,
                       int32_t* counts, hipStream_t s) {
+  ReleaseGroup rg(s);
   if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
   prepare_readout(idx, s);
   Canon& c = idx->canon;
@@ -1562,6 +1636,7 @@ int kmhg_free(kmhg_index* idx) {
     }
     // stream-ordered release: the buffers return to the pool once work queued on the index's
     // last stream has finished (queries on other streams are synchronised by their callers)
+    ReleaseGroup rg(idx->stream);
     idx->bind_all(idx->stream);
     delete idx;
   });
