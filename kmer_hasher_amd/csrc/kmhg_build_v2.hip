@@ -125,6 +125,51 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
   for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) hist[(size_t)d * ch.C + c] = lh[d];
 }
 
+// Persistent form for the interleaved schedule (one histogram column per tile): workgroup w
+// walks virtual tiles w, w + G, ... (XCD-contiguous like the scatter) and loads the next tile's
+// chars into registers while it encodes the current one, so the load latency of all but the
+// first tile is hidden behind the encode.
+__global__ void __launch_bounds__(BLOCK)
+k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
+            uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
+            uint32_t n_status, BuildMeta* __restrict__ meta) {
+  __shared__ PStage st;
+  __shared__ uint32_t lh[V2_MAXR];
+  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
+    scan_status[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < sizeof(BuildMeta) / 4)
+    reinterpret_cast<uint32_t*>(meta)[threadIdx.x] = 0u;
+  const uint32_t G = gridDim.x;
+  const uint32_t n_iter = (ch.ntiles - blockIdx.x + G - 1) / G;
+  auto tile_at = [&](uint32_t i) -> uint32_t {
+    const uint32_t v = blockIdx.x + i * G;
+    return remap ? xcd_remap(v, ch.ntiles) : v;
+  };
+  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) lh[d] = 0;
+  StageRegs<PSTAGE_W16> regs;
+  stage_load<PSTAGE_W16, true>(regs, seq, L, (int64_t)tile_at(0) * PTILE - HALO, true);
+  for (uint32_t it = 0; it < n_iter; ++it) {
+    const uint32_t tile = tile_at(it);
+    const int64_t tile0 = (int64_t)tile * PTILE;
+    stage_pack(regs, st);                      // the previous tile's reads of st are done
+    if (it + 1 < n_iter)
+      stage_load<PSTAGE_W16, true>(regs, seq, L, (int64_t)tile_at(it + 1) * PTILE - HALO, true);
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < PWPT; ++j) {
+      const int w = j * BLOCK + threadIdx.x;
+      const int64_t s = tile0 + w;
+      uint64_t key = 0;
+      if (s < Nw && window_key(st, HALO + w, s, L, k, key)) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) {
+      hist[(size_t)d * ch.C + tile] = lh[d];
+      lh[d] = 0;                               // next tile's atomics follow a barrier
+    }
+  }
+}
+
 // ---------------------------------------------------------------- V_scan (u32, exclusive)
 // Single pass: tiles in ticket order, decoupled look-back (kmhg_device.h) for the tile base.
 // `status` holds one look-back word per tile and the ticket at status[ntiles]; the preceding
@@ -215,11 +260,15 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
           Digit D, uint32_t* __restrict__ hist, Chunks ch, int remap,
           uint64_t* __restrict__ scan_status, uint32_t n_status, uint32_t* __restrict__ hll_rows,
-          uint32_t* __restrict__ hll_regs) {
+          uint32_t* __restrict__ hll_regs, uint32_t* __restrict__ save_col0) {
   __shared__ uint32_t lh[V2_MAXR];
   __shared__ uint32_t hreg[HLL ? HLL_REGS : 1];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
     scan_status[i] = 0;
+  // the previous pass's scanned column 0 (digit starts), kept for V_bounds_lo before this
+  // workgroup -- the only writer of column 0 -- overwrites it
+  if (save_col0 && (remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x) == 0)
+    for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) save_col0[d] = hist[(size_t)d * ch.C];
   if (HLL) {
     for (uint32_t i = threadIdx.x; i < HLL_REGS; i += BLOCK) hreg[i] = 0;
   }
@@ -343,6 +392,8 @@ k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __res
 // ones; later passes read the (key, pos) stream.  The tile is re-ordered by digit in LDS first
 // and written out run by run, so each wave store covers a few contiguous runs instead of 64
 // scattered addresses.
+// (Measured: 320-digit arrays and u16 digits instead of sdst, 48 -> 37 KB, change nothing --
+// the kernel is held to 3 waves / SIMD by its 164 VGPRs; forcing 4 spills and runs 35 % slower.)
 struct ScatterLDS {
   uint32_t wc[4][V2_MAXR];     // per-wave digit counts -> per-wave tile-local cursors
   uint32_t tstart[V2_MAXR];    // tile-local start of each digit
@@ -566,6 +617,43 @@ k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_pt
       }
     }
   }
+}
+
+// ---------------------------------------------------------------- V_bounds_lo (at most 2 passes)
+// Bucket starts from the radix histograms instead of a pass over the sorted keys.  With LSD
+// passes the last pass's input is sorted by lo = b mod div (div = R^(passes-1)) and that pass
+// places elements by hi = b / div, stably, so
+//   start[hi * div + lo] = #(digit < hi) + #(digit == hi and lo' < lo)
+//                        = hist[hi][t] + #(digit hi among input [t * PTILE, P_lo))
+// where P_lo = #(lo' < lo) is the previous pass's start of digit lo (its scanned column 0, saved
+// by V_hist) and t = P_lo / PTILE: one workgroup per lo value counts at most one partial tile.
+// Interleaved schedule only (one histogram column per tile).  `spread` (count-only builds):
+// start[b / spread] for the buckets b that are multiples of spread.
+__global__ void __launch_bounds__(BLOCK)
+k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ n_ptr, Geom g,
+               Digit Dlast, uint32_t div, const uint32_t* __restrict__ hist, uint32_t C,
+               const uint32_t* __restrict__ lo_start, uint32_t spread,
+               uint32_t* __restrict__ start) {
+  __shared__ uint32_t cnt[V2_MAXR];
+  const uint32_t lo = blockIdx.x;
+  const uint32_t R = Dlast.R;
+  const uint32_t n = *n_ptr;
+  const uint32_t P = lo_start ? lo_start[lo] : 0u;
+  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) cnt[d] = 0;
+  __syncthreads();
+  const uint32_t tile = P / PTILE;
+  for (uint32_t i = tile * PTILE + threadIdx.x; i < P; i += BLOCK)
+    atomicAdd(&cnt[digit_of(kprev[i], g.nb, Dlast)], 1u);
+  __syncthreads();
+  for (uint32_t hi = threadIdx.x; hi < R; hi += BLOCK) {
+    const uint64_t b = (uint64_t)hi * div + lo;
+    if (b >= g.nb || b % spread) continue;
+    // P == n on a tile boundary past the last column: the end of digit hi
+    const uint32_t base = tile < C ? hist[(size_t)hi * C + tile]
+                                   : (hi + 1 < R ? hist[(size_t)(hi + 1) * C] : n);
+    start[b / spread] = base + cnt[hi];
+  }
+  if (lo == 0 && threadIdx.x == 0) start[g.nb / spread] = n;
 }
 
 // ---------------------------------------------------------------- V_bucket (wave per bucket)
@@ -1335,6 +1423,17 @@ static unsigned scatter_grid(const Chunks& ch) {
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
                      BuildMeta* meta, hipStream_t s) {
+  static const int persist = [] {
+    const char* e = std::getenv("KMHG_HIST0P");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  if (ch.interleaved && persist) {
+    static const unsigned cap = resident_blocks((const void*)k_v2_hist0p);
+    const unsigned G = std::min<unsigned>(ch.ntiles, cap);
+    hipLaunchKernelGGL(k_v2_hist0p, dim3(G), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
+                       xcd_map(), scan_status, n_status, meta);
+    return;
+  }
   hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
                      xcd_map(), scan_status, n_status, meta);
 }
@@ -1351,13 +1450,19 @@ void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total,
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
-                    uint32_t* hll_rows, uint32_t* hll_regs) {
+                    uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0) {
   if (hll_rows)
     hipLaunchKernelGGL(k_v2_hist<true>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
-                       ch, xcd_map(), scan_status, n_status, hll_rows, hll_regs);
+                       ch, xcd_map(), scan_status, n_status, hll_rows, hll_regs, save_col0);
   else
     hipLaunchKernelGGL(k_v2_hist<false>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
-                       ch, xcd_map(), scan_status, n_status, nullptr, nullptr);
+                       ch, xcd_map(), scan_status, n_status, nullptr, nullptr, save_col0);
+}
+void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
+                         uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
+                         uint32_t spread, uint32_t* start, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_bounds_lo, dim3(div), dim3(BLOCK), 0, s, kprev, n_ptr, g, Dlast, div,
+                     hist, C, lo_start, spread, start);
 }
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    hipStream_t s) {

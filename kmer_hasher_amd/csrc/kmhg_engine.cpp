@@ -700,6 +700,12 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   PinnedRec hrec;
   if (co_auto) hrec = PinnedPool::get().take();
 
+  // bucket starts straight from the histograms (V_bounds_lo) for one or two passes;
+  // KMHG_BOUNDS=scan (tests) forces the pass over the sorted keys (V_bounds)
+  const char* be = std::getenv("KMHG_BOUNDS");
+  const bool bounds_scan = be && std::string(be) == "scan";
+  const bool bounds_lo = ch.interleaved && passes <= 2 && !bounds_scan;
+  DBuf<uint32_t> lo_start(bounds_lo && passes == 2 ? R : 1, s);
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = 1;
@@ -721,9 +727,11 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const bool keys0 = from_keys && p == 0;
     const uint64_t* src = keys0 ? d_keys : kin;
     const bool hll = co_auto && p == 0;
+    const bool save = bounds_lo && passes == 2 && p == 1;
     LAUNCH("k_v2_hist", s,
            launch_v2_hist(src, n_valid, g, Dp, hist.p, ch, status, n_status, s,
-                          hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr));
+                          hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
+                          save ? lo_start.p : nullptr));
     if (hll) {
       LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ch.C, hll_regs.p,
                                           &hrec.meta->distinct_est, s));
@@ -756,7 +764,17 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     idx->geom = gb;
     idx->table.reset(idx->slots());
   }
-  LAUNCH("k_v2_bounds", s, launch_v2_bounds(kin, n_valid, gb, start.p, (uint64_t)Nw, s));
+  if (bounds_lo) {
+    // the last pass's input: kout after the final swap (pass 0 of a sequence build reads chars,
+    // pass 0 of a key stream the caller's keys: one pass has no partial tile to count)
+    const uint32_t div_last = passes == 2 ? R : 1u;
+    LAUNCH("k_v2_bounds", s,
+           launch_v2_bounds_lo(passes == 2 ? kout : nullptr, n_valid, g, make_digit(div_last, R),
+                               div_last, hist.p, ch.C, passes == 2 ? lo_start.p : nullptr,
+                               g.nb / gb.nb, start.p, s));
+  } else {
+    LAUNCH("k_v2_bounds", s, launch_v2_bounds(kin, n_valid, gb, start.p, (uint64_t)Nw, s));
+  }
 #ifdef KMHG_STAMPS
   static uint64_t* stamps = nullptr;
   if (!stamps) HIPC(hipMallocManaged(&stamps, sizeof(uint64_t) * 8 * (1u << 22)));

@@ -138,7 +138,15 @@ constexpr uint32_t HLL_REGS = 256;
 constexpr uint32_t HLL_PART_WORDS = 256 * 64 + 1;
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
-                    uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr);
+                    uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr,
+                    uint32_t* save_col0 = nullptr);
+// bucket starts from the histograms (passes <= 2, interleaved schedule): one workgroup per lo
+// value (div of them); kprev = the last pass's input keys, lo_start = the previous pass's digit
+// starts (saved by launch_v2_hist's save_col0; nullptr for one pass); start[b / spread] for
+// buckets b that are multiples of spread, start[nb / spread] = n
+void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
+                         uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
+                         uint32_t spread, uint32_t* start, hipStream_t s);
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    hipStream_t s);
 // the sequence must be 16-B aligned (the engine copies an unaligned input)

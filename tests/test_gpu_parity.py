@@ -214,17 +214,25 @@ def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     _check_against_oracle("G" * 40, 32, qks=[31])
 
 
-@pytest.mark.parametrize("maxr", ["6", "12", "40"])
-def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr):
-    """More radix passes than the input needs (KMHG_MAXR caps the radix): 2-4 passes, so the
-    last pass's bucket counts (which replace a bounds search) are exercised with 1, 2 and 3
-    low digits below the last one, chunks spanning many low values, and N-runs."""
+@pytest.mark.parametrize("bounds", ["lo", "scan"])
+@pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
+def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds):
+    """More radix passes than the input needs (KMHG_MAXR caps the radix): 1-4 passes with N-runs
+    and repeat-rich input.  Bucket starts come from the radix histograms for one or two passes
+    (k_v2_bounds_lo: the partial-tile count at each low digit's first element; a zero-width
+    tile at a tile boundary) and from a pass over the sorted keys otherwise or with
+    KMHG_BOUNDS=scan; both against the oracle."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_MAXR", maxr)
+    monkeypatch.setenv("KMHG_BOUNDS", bounds)
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
     _check_against_oracle(s, 31, pairs=False)
     rr = synth.repeat_rich(300_000, 42, n_gap_every=100_000).tobytes().decode("latin-1")
     _check_against_oracle(rr, 17, qks=[17], pairs=True)
+    # tiny inputs (one pass, a few buckets) and a window count that is a multiple of the tile
+    rng = np.random.default_rng(43)
+    for L in (40, 2047 + 30, 4096 + 30, 3 * 2048 + 30):
+        _check_against_oracle("".join(rng.choice(list("ACGT"), L)), 31, pairs=False)
 
 
 @pytest.mark.parametrize("path", ["fused", "classic"])
