@@ -477,9 +477,14 @@ struct kmhg_index {
   int co_spread = 0, co_path = 0;
   DBuf<uint64_t> ckeys;
   DBuf<uint32_t> slot_row, row_slot;
+  // seq.kmer.pos diagonal path: the slot of every indexed window by position (built on the
+  // first eligible query, kept with the index)
+  DBuf<Slot> pslot;
+  bool ps_ready = false;
   // stream-ordered release of everything the index holds (work queued on `s` may still read it)
   void bind_all(hipStream_t s) {
     table.bind(s); positions.bind(s); ckeys.bind(s); slot_row.bind(s); row_slot.bind(s);
+    pslot.bind(s);
     canon.perm.bind(s); canon.canon_off.bind(s); canon.pkeys.bind(s); canon.pair_off.bind(s);
     canon.rinfo.bind(s);
   }
@@ -893,9 +898,22 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   DBuf<uint64_t> tiles((size_t)nt + 1 + scan_u64_scratch(nt), s);
   uint64_t* tile_row0 = tiles.p;
   uint64_t* total = tiles.p + nt;
+  // diagonal path (k_query_probe): a position index queried at its own k
+  const int64_t nA = idx->L - idx->k + 1;
+  const char* de = std::getenv("KMHG_QUERY_DIAG");
+  const bool diag = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
+                    idx->U > 0;
+  if (diag && !idx->ps_ready) {
+    idx->pslot.reset((size_t)nA);
+    idx->pslot.bind(s);
+    HIPC(hipMemsetAsync(idx->pslot.p, 0xFF, (size_t)nA * sizeof(Slot), s));
+    LAUNCH("k_pos_slots", s, launch_pos_slots(idx->table.p, idx->slots(), idx->positions.p,
+                                              idx->pslot.p, s));
+    idx->ps_ready = true;
+  }
   LAUNCH("k_query_probe", s,
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
-                            tile_row0, s));
+                            tile_row0, s, diag ? idx->pslot.p : nullptr, nA));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, total + 1, s));
   if (classic) {
     LAUNCH("k_query_emit", s,

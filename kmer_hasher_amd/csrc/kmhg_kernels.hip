@@ -270,14 +270,75 @@ k_inline_singles(Slot* __restrict__ T, uint64_t nslots, const int32_t* __restric
 }
 
 // ================================================================== query kernels
+// Position-indexed slots (the diagonal path of Q_probe): PS[s] = the table slot of the index's
+// window s (0-based start), EMPTY key where the window is not indexed (PS preset to 0xFF).  One
+// thread per slot; a key with more than PS_LANE positions is written by the whole wave.
+constexpr uint32_t PS_LANE = 16;
+__global__ void __launch_bounds__(BLOCK)
+k_pos_slots(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions,
+            Slot* __restrict__ PS) {
+  const int lane = lane_id();
+  for (uint64_t i0 = (uint64_t)blockIdx.x * BLOCK; i0 < nslots; i0 += (uint64_t)gridDim.x * BLOCK) {
+    const uint64_t i = i0 + threadIdx.x;
+    Slot sl;
+    sl.key = EMPTY_KEY; sl.count = 0; sl.aux = 0;
+    if (i < nslots) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+      sl.key = ((uint64_t)v.y << 32) | v.x; sl.count = v.z; sl.aux = v.w;
+    }
+    const uint4 out = make_uint4((uint32_t)sl.key, (uint32_t)(sl.key >> 32), sl.count, sl.aux);
+    if (sl.count == 1) {
+      *reinterpret_cast<uint4*>(&PS[sl.aux - 1]) = out;
+    } else if (sl.count > 1 && sl.count <= PS_LANE) {
+      for (uint32_t q = sl.aux - sl.count; q < sl.aux; ++q)
+        *reinterpret_cast<uint4*>(&PS[positions[q] - 1]) = out;
+    }
+    uint64_t heavy = __ballot(sl.count > PS_LANE);
+    while (heavy) {                            // long lists: the wave strides over them
+      const int src = __ffsll((unsigned long long)heavy) - 1;
+      heavy &= heavy - 1;
+      const uint32_t c = __shfl(sl.count, src), a = __shfl(sl.aux, src);
+      const uint4 o = make_uint4(__shfl(out.x, src), __shfl(out.y, src), c, a);
+      for (uint32_t q = a - c + lane; q < a; q += 64)
+        *reinterpret_cast<uint4*>(&PS[positions[q] - 1]) = o;
+    }
+  }
+}
+
+void launch_pos_slots(const Slot* T, uint64_t nslots, const int32_t* positions, Slot* PS,
+                      hipStream_t s) {
+  uint64_t g = (nslots + BLOCK - 1) / BLOCK;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(k_pos_slots, dim3((unsigned)(g ? g : 1)), dim3(BLOCK), 0, s, T, nslots,
+                     positions, PS);
+}
+
 // Q_probe: per query window (query k) probe the table; qinfo[s] = {count, start}; per-tile row
 // totals go through the look-back so each tile learns its first output row.
+// Diagonal path (PS != nullptr: query k = index k, a position index): dot plots hit along
+// diagonals, so a window whose predecessor matched index position j usually matches j + 1.  Every
+// DG_STRIDE-th window of the tile ("anchor") probes the table; an anchor with a unique hit at j
+// predicts j + d for the window d after it, and the later windows of the tile follow the last
+// anchor that predicted.  A prediction is VERIFIED by reading PS[j + d - 1] -- consecutive windows
+// read consecutive 16-B entries, coalesced -- and taken only if its key equals the window's key,
+// in which case its {count, aux} ARE the key's slot (exact); otherwise the window probes the
+// table as before.  Queries unrelated to the index pay the anchors and one failed check.
+#ifndef KMHG_DG_STRIDE
+#define KMHG_DG_STRIDE 16
+#endif
+constexpr int DG_STRIDE = KMHG_DG_STRIDE;
+constexpr int DG_ANCHORS = TILE / DG_STRIDE;
+static_assert(DG_ANCHORS <= BLOCK && DG_ANCHORS % 64 == 0, "anchors: one thread each");
+
 __global__ void __launch_bounds__(BLOCK)
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
-              uint64_t* __restrict__ tile_rows) {
+              uint64_t* __restrict__ tile_rows, const Slot* __restrict__ PS, int64_t nA) {
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
+  __shared__ uint32_t anc[DG_ANCHORS];         // anchor's unique hit (1-based index position), 0 none
+  __shared__ int32_t last_anc[DG_ANCHORS];     // last anchor <= a that predicts, -1 none
+  __shared__ uint2 anc_info[DG_ANCHORS];       // anchor's {count, aux}
   const uint32_t tile = blockIdx.x;
   // windows [w0, w1) of the FULL sequence: halo chars come from the real neighbours, so the
   // N / end-of-sequence rules at a shard boundary are those of the unsharded walk
@@ -286,6 +347,33 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   const int o0 = (int)(t_start - base);
   stage_tile(seq, L, base, st, aligned != 0);
   __syncthreads();
+  if (PS) {
+    if (threadIdx.x < DG_ANCHORS) {
+      const int w = threadIdx.x * DG_STRIDE;
+      const int64_t s = t_start + w;
+      uint64_t key = 0;
+      uint32_t count = 0, aux = 0;
+      if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
+      anc[threadIdx.x] = count == 1 ? aux : 0u;
+      anc_info[threadIdx.x] = make_uint2(count, aux);
+      // last predicting anchor at or before this one: max-scan over the anchor indices
+      int32_t v = count == 1 ? (int32_t)threadIdx.x : -1;
+      const int lane = lane_id();
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int32_t u = __shfl_up(v, d);
+        if (lane >= d) v = max(v, u);
+      }
+      last_anc[threadIdx.x] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64 && threadIdx.x < DG_ANCHORS) {   // carry across the anchor waves
+      const int32_t carry = last_anc[(threadIdx.x & ~63) - 1];
+      // waves > 1 would need the carry of every earlier wave: DG_ANCHORS = 128 has two
+      if (last_anc[threadIdx.x] < 0) last_anc[threadIdx.x] = carry;
+    }
+    __syncthreads();
+  }
   uint64_t rows = 0;
   // (measured: issuing all WPT home-slot loads before resolving any cost occupancy -- 94
   // VGPRs, 5 waves/SIMD -- and ran 15 % slower than this two-deep loop; a per-lane state
@@ -300,8 +388,27 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
-    if (s < w1 && window_key(st, o0 + w, s, L, kq, key))
-      table_find(T, g, key, count, aux);
+    if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) {
+      bool found = false;
+      if (PS) {
+        const int a = w / DG_STRIDE;
+        if (w % DG_STRIDE == 0) {              // an anchor: its probe is done
+          const uint2 ai = anc_info[a];
+          count = ai.x; aux = ai.y;
+          found = true;
+        } else {
+          const int la = last_anc[a];
+          if (la >= 0) {
+            const int64_t pj = (int64_t)anc[la] + (w - la * DG_STRIDE);   // 1-based
+            if (pj <= nA) {
+              const uint4 v = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
+              if ((((uint64_t)v.y << 32) | v.x) == key) { count = v.z; aux = v.w; found = true; }
+            }
+          }
+        }
+      }
+      if (!found) table_find(T, g, key, count, aux);
+    }
     // {count, position} for a key seen once, {count, first index} otherwise
     if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
     rows += count;
@@ -864,10 +971,10 @@ void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, h
 }
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
-                        hipStream_t s) {
+                        hipStream_t s, const Slot* PS, int64_t nA) {
   uint32_t nt = grid_for(w1 - w0, TILE);
   hipLaunchKernelGGL(k_query_probe, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo, w0,
-                     w1, aligned ? 1 : 0, tile_rows);
+                     w1, aligned ? 1 : 0, tile_rows, PS, nA);
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);

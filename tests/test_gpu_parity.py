@@ -235,7 +235,7 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds):
         _check_against_oracle("".join(rng.choice(list("ACGT"), L)), 31, pairs=False)
 
 
-@pytest.mark.parametrize("path", ["fused", "classic"])
+@pytest.mark.parametrize("path", ["fused", "classic", "nodiag"])
 def test_query_paths_vs_oracle(gpu, monkeypatch, path):
     """seq.kmer.pos through the probe / scan / emit kernels (default; also the fused path's redo
     when a query has more rows than the guessed capacity) and through the one-pass probe +
@@ -244,7 +244,10 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
     chained by the look-back, a query with far more rows than windows, and a query of another
     sequence (misses)."""
     from kmer_hasher_amd import synth
-    monkeypatch.setenv("KMHG_QUERY", path)
+    if path == "nodiag":
+        monkeypatch.setenv("KMHG_QUERY_DIAG", "0")
+    else:
+        monkeypatch.setenv("KMHG_QUERY", path)
     make, kpos, sqk = _api()
     rng = np.random.default_rng(77)
     for n in (40, 2047 + 30, 2048 + 30, 2049 + 30, 3 * 2048 + 7):
@@ -275,3 +278,52 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
     assert q.shape[0] > 4 * len(heavy)
     assert np.array_equal(q.reshape(-1), oi.query(heavy, 6))
     ptr.free()
+
+
+def test_query_diagonal_path_vs_oracle(gpu):
+    """The diagonal path of k_query_probe (anchors every 16th window; later windows follow the
+    last anchor with a unique hit and take a position-indexed slot only when its key equals
+    theirs) against the oracle: the index's own sequence, a related sequence (1 % SNVs,
+    inversions, translocations, N-runs), its reverse complement, an unrelated one, repeat-rich
+    input (multi-hit anchors predict nothing; keys with > 16 positions get their position slots
+    from a whole wave), shards of the window range that start inside a diagonal, and a query k
+    different from the index k (path off)."""
+    import torch
+    from kmer_hasher_amd import device as D, synth
+    make, kpos, sqk = _api()
+    A = synth.add_n_runs(synth.iid(300_000, 61), 0.0005, 62, max_run=40)
+    B = synth.derived(A, 63)
+    comp = np.zeros(256, np.uint8)
+    for a, b in zip(b"ACGTN", b"TGCAN"):
+        comp[a] = b
+    RC = comp[A[::-1]]
+    U = synth.iid(200_000, 64)
+    sa = A.tobytes().decode("latin-1")
+    for k in (31, 17):
+        oi = O.OracleIndex(sa, k)
+        ptr = make(sa, k)
+        for q in (A, B, RC, U):
+            qs = q.tobytes().decode("latin-1")
+            assert np.array_equal(sqk(ptr, qs, k).reshape(-1), oi.query(qs, k)), k
+        qs = B.tobytes().decode("latin-1")
+        assert np.array_equal(sqk(ptr, qs, k - 4).reshape(-1), oi.query(qs, k - 4))
+        ptr.free()
+    rr = synth.add_n_runs(synth.repeat_rich(600_000, 65, n_gap_every=150_000), 0.001, 66)
+    for k in (21, 9):
+        srr = rr.tobytes().decode("latin-1")
+        oi = O.OracleIndex(srr, k)
+        ptr = make(srr, k)
+        assert np.array_equal(sqk(ptr, srr, k).reshape(-1), oi.query(srr, k)), k
+        ptr.free()
+    # shards: window ranges cut mid-diagonal concatenate to the whole query
+    dA = torch.from_numpy(A).cuda()
+    dB = torch.from_numpy(B).cuda()
+    idx = D.DeviceIndex.build(dA, 31)
+    full = idx.query(dB, 31).rows().cpu().numpy()
+    nw = len(B) - 31 + 1
+    cuts = [0, 1, 2047, 2049, 100_003, nw]
+    parts = [idx.query_range(dB, 31, a, b).rows().cpu().numpy() for a, b in zip(cuts, cuts[1:])]
+    assert np.array_equal(np.concatenate(parts), full)
+    oi = O.OracleIndex(sa, 31)
+    assert np.array_equal(full.reshape(-1), oi.query(B.tobytes().decode("latin-1"), 31))
+    idx.free()
