@@ -880,25 +880,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   const char* qe = std::getenv("KMHG_QUERY");
   const bool classic = !(qe && std::string(qe) == "fused");
   uint64_t H = 0;
-  if (!classic) {
-    // one pass: probe + look-back + emit (k_query_fused); look-back words + ticket zeroed
-    DBuf<uint64_t> status((size_t)nt + 1, s);
-    HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
-    LAUNCH("k_query_fused", s,
-           launch_query_fused(d_seq, L, kq, idx->table.p, idx->geom, w0, w1, aligned,
-                              idx->positions.p, status.p, q->rows.p, cap, s));
-    HIPC(hipMemcpyAsync(&H, status.p + nt - 1, sizeof(H), hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
-    H &= (1ull << 62) - 1;                       // LB_MASK: the last tile's inclusive prefix
-    q->H = (int64_t)H;
-    if (H <= cap) return q.release();
-  }
-  DBuf<uint2> qinfo(Nw, s);
-  // per-tile rows -> first row; [nt] = total; then the long-scan scratch
-  DBuf<uint64_t> tiles((size_t)nt + 1 + scan_u64_scratch(nt), s);
-  uint64_t* tile_row0 = tiles.p;
-  uint64_t* total = tiles.p + nt;
-  // diagonal path (k_query_probe): a position index queried at its own k
+  // diagonal path (k_query_probe / k_query_fused): a position index queried at its own k
   const int64_t nA = idx->L - idx->k + 1;
   const char* de = std::getenv("KMHG_QUERY_DIAG");
   const bool diag = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
@@ -911,18 +893,47 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
                                               idx->pslot.p, s));
     idx->ps_ready = true;
   }
+
+  if (!classic) {
+    // one pass: probe + look-back + emit (k_query_fused); look-back words + ticket zeroed
+    DBuf<uint64_t> status((size_t)nt + 1, s);
+    HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
+    LAUNCH("k_query_fused", s,
+           launch_query_fused(d_seq, L, kq, idx->table.p, idx->geom, w0, w1, aligned,
+                              idx->positions.p, status.p, q->rows.p, cap, s,
+                              diag ? idx->pslot.p : nullptr, nA));
+    HIPC(hipMemcpyAsync(&H, status.p + nt - 1, sizeof(H), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    H &= (1ull << 62) - 1;                       // LB_MASK: the last tile's inclusive prefix
+    q->H = (int64_t)H;
+    if (H <= cap) return q.release();
+  }
+  DBuf<uint2> qinfo(Nw, s);
+  // per-tile rows -> first row; then the long-scan scratch.  The row total goes straight into
+  // pinned host memory (no copy launch before the host reads it).
+  DBuf<uint64_t> tiles((size_t)nt + scan_u64_scratch(nt), s);
+  uint64_t* tile_row0 = tiles.p;
+  PinnedRec hrec = PinnedPool::get().take();
+  struct GiveBack {
+    PinnedRec& r;
+    ~GiveBack() { PinnedPool::get().give(r, false); }
+  } give_back{hrec};
+  uint64_t* total = &hrec.meta->n_kmers;
   LAUNCH("k_query_probe", s,
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
                             tile_row0, s, diag ? idx->pslot.p : nullptr, nA));
-  LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, total + 1, s));
+  LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, tiles.p + nt, s));
   if (classic) {
     LAUNCH("k_query_emit", s,
            launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap,
                              s));
-    HIPC(hipMemcpyAsync(&H, total, sizeof(H), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
+    H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
     q->H = (int64_t)H;
     if (H <= cap) return q.release();
+  } else {
+    HIPC(hipStreamSynchronize(s));
+    H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
   }
   q->rows.bind(s);
   q->rows.reset(H);

@@ -324,21 +324,89 @@ void launch_pos_slots(const Slot* T, uint64_t nslots, const int32_t* positions, 
 // in which case its {count, aux} ARE the key's slot (exact); otherwise the window probes the
 // table as before.  Queries unrelated to the index pay the anchors and one failed check.
 #ifndef KMHG_DG_STRIDE
-#define KMHG_DG_STRIDE 16
-#endif
+#define KMHG_DG_STRIDE 64        // A/B (config 2 self dot plot, probe): 16 / 32 / 64 / 128 ->
+#endif                           //   97 / 86 / 82 / 76 us; 64 keeps misses after a tile start short
 constexpr int DG_STRIDE = KMHG_DG_STRIDE;
 constexpr int DG_ANCHORS = TILE / DG_STRIDE;
-static_assert(DG_ANCHORS <= BLOCK && DG_ANCHORS % 64 == 0, "anchors: one thread each");
+constexpr int DG_SCAN = (DG_ANCHORS + 63) / 64 * 64;   // whole waves run the anchor scan
+static_assert(DG_SCAN <= BLOCK && DG_SCAN <= 128, "anchors: one thread each, at most two waves");
 
+struct DiagAnchors {
+  uint32_t anc[DG_ANCHORS];      // anchor's unique hit (1-based index position), 0 none
+  int32_t last[DG_ANCHORS];      // last anchor <= a that predicts, -1 none
+  uint2 info[DG_ANCHORS];        // anchor's {count, aux}
+};
+
+// Anchor probes of a staged tile (threads < DG_ANCHORS) and the last-predicting-anchor scan;
+// called by every thread of the block (two barriers inside).
+template <class ST>
+__device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_start, int64_t w1,
+                                             int64_t L, int kq, const Slot* __restrict__ T,
+                                             Geom g, DiagAnchors& A) {
+  if (threadIdx.x < DG_SCAN) {
+    const bool is_anchor = threadIdx.x < DG_ANCHORS;
+    const int w = threadIdx.x * DG_STRIDE;
+    const int64_t s = t_start + w;
+    uint64_t key = 0;
+    uint32_t count = 0, aux = 0;
+    if (is_anchor && s < w1 && window_key(st, o0 + w, s, L, kq, key))
+      table_find(T, g, key, count, aux);
+    if (is_anchor) {
+      A.anc[threadIdx.x] = count == 1 ? aux : 0u;
+      A.info[threadIdx.x] = make_uint2(count, aux);
+    }
+    int32_t v = count == 1 ? (int32_t)threadIdx.x : -1;   // max-scan over the anchor indices
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t u = __shfl_up(v, d);
+      if (lane >= d) v = max(v, u);
+    }
+    if (is_anchor) A.last[threadIdx.x] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 64 && threadIdx.x < DG_ANCHORS) {   // carry across the (two) anchor waves
+    const int32_t carry = A.last[(threadIdx.x & ~63) - 1];
+    if (A.last[threadIdx.x] < 0) A.last[threadIdx.x] = carry;
+  }
+  __syncthreads();
+}
+
+// count / aux of tile window w with key `key` (a valid window): the anchor's own probe or a
+// verified diagonal prediction; false = the window still needs its table probe.  (Written
+// without early returns around table_find: the probe loop keeps two windows' table probes in
+// flight only when the probe stays a straight-line call -- an early-return helper around it ran
+// the table-only path 0.31 -> 0.44 ms.)
+__device__ __forceinline__ bool diag_window(int w, uint64_t key, const Slot* __restrict__ PS,
+                                            int64_t nA, const DiagAnchors& A, uint32_t& count,
+                                            uint32_t& aux) {
+  const int a = w / DG_STRIDE;
+  bool hit = false;
+  if (w % DG_STRIDE == 0) {
+    const uint2 ai = A.info[a];
+    count = ai.x; aux = ai.y;
+    hit = true;
+  } else {
+    const int la = A.last[a];
+    if (la >= 0) {
+      const int64_t pj = (int64_t)A.anc[la] + (w - la * DG_STRIDE);   // 1-based
+      if (pj <= nA) {
+        const uint4 v = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
+        if ((((uint64_t)v.y << 32) | v.x) == key) { count = v.z; aux = v.w; hit = true; }
+      }
+    }
+  }
+  return hit;
+}
+
+template <bool DIAG>
 __global__ void __launch_bounds__(BLOCK)
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
               uint64_t* __restrict__ tile_rows, const Slot* __restrict__ PS, int64_t nA) {
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
-  __shared__ uint32_t anc[DG_ANCHORS];         // anchor's unique hit (1-based index position), 0 none
-  __shared__ int32_t last_anc[DG_ANCHORS];     // last anchor <= a that predicts, -1 none
-  __shared__ uint2 anc_info[DG_ANCHORS];       // anchor's {count, aux}
+  __shared__ DiagAnchors A;
   const uint32_t tile = blockIdx.x;
   // windows [w0, w1) of the FULL sequence: halo chars come from the real neighbours, so the
   // N / end-of-sequence rules at a shard boundary are those of the unsharded walk
@@ -347,33 +415,7 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   const int o0 = (int)(t_start - base);
   stage_tile(seq, L, base, st, aligned != 0);
   __syncthreads();
-  if (PS) {
-    if (threadIdx.x < DG_ANCHORS) {
-      const int w = threadIdx.x * DG_STRIDE;
-      const int64_t s = t_start + w;
-      uint64_t key = 0;
-      uint32_t count = 0, aux = 0;
-      if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
-      anc[threadIdx.x] = count == 1 ? aux : 0u;
-      anc_info[threadIdx.x] = make_uint2(count, aux);
-      // last predicting anchor at or before this one: max-scan over the anchor indices
-      int32_t v = count == 1 ? (int32_t)threadIdx.x : -1;
-      const int lane = lane_id();
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int32_t u = __shfl_up(v, d);
-        if (lane >= d) v = max(v, u);
-      }
-      last_anc[threadIdx.x] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x >= 64 && threadIdx.x < DG_ANCHORS) {   // carry across the anchor waves
-      const int32_t carry = last_anc[(threadIdx.x & ~63) - 1];
-      // waves > 1 would need the carry of every earlier wave: DG_ANCHORS = 128 has two
-      if (last_anc[threadIdx.x] < 0) last_anc[threadIdx.x] = carry;
-    }
-    __syncthreads();
-  }
+  if (DIAG) diag_anchors(st, o0, t_start, w1, L, kq, T, g, A);
   uint64_t rows = 0;
   // (measured: issuing all WPT home-slot loads before resolving any cost occupancy -- 94
   // VGPRs, 5 waves/SIMD -- and ran 15 % slower than this two-deep loop; a per-lane state
@@ -388,27 +430,9 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
-    if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) {
-      bool found = false;
-      if (PS) {
-        const int a = w / DG_STRIDE;
-        if (w % DG_STRIDE == 0) {              // an anchor: its probe is done
-          const uint2 ai = anc_info[a];
-          count = ai.x; aux = ai.y;
-          found = true;
-        } else {
-          const int la = last_anc[a];
-          if (la >= 0) {
-            const int64_t pj = (int64_t)anc[la] + (w - la * DG_STRIDE);   // 1-based
-            if (pj <= nA) {
-              const uint4 v = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
-              if ((((uint64_t)v.y << 32) | v.x) == key) { count = v.z; aux = v.w; found = true; }
-            }
-          }
-        }
-      }
-      if (!found) table_find(T, g, key, count, aux);
-    }
+    if (s < w1 && window_key(st, o0 + w, s, L, kq, key) &&
+        !(DIAG && diag_window(w, key, PS, nA, A, count, aux)))
+      table_find(T, g, key, count, aux);
     // {count, position} for a key seen once, {count, first index} otherwise
     if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
     rows += count;
@@ -562,7 +586,8 @@ k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
 __global__ void __launch_bounds__(BLOCK)
 k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, int64_t w0, int64_t w1, int aligned, const int32_t* __restrict__ positions,
-              uint64_t* __restrict__ status, uint32_t nt, int2* __restrict__ out, uint64_t cap) {
+              uint64_t* __restrict__ status, uint32_t nt, int2* __restrict__ out, uint64_t cap,
+              const Slot* __restrict__ PS, int64_t nA) {
   // LDS ~19 KB -> 8 workgroups per CU, as Q_probe: per-window {count, first} records (the
   // registers would hold them only with all WPT probes unrolled: 100 VGPRs, half the waves), and
   // the stage shares its bytes with the emit's heavy-window list
@@ -575,12 +600,14 @@ k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   __shared__ uint32_t tk;
   __shared__ uint64_t r0_sh;
   __shared__ uint32_t n_heavy;
+  __shared__ DiagAnchors A;
   const uint32_t tile = take_ticket(reinterpret_cast<uint32_t*>(status + nt), &tk);
   const int64_t t_start = w0 + (int64_t)tile * TILE;
   const int64_t base = (t_start & ~15ll) - HALO;
   const int o0 = (int)(t_start - base);
   stage_tile(seq, L, base, u.st, aligned != 0);
   __syncthreads();
+  if (PS) diag_anchors(u.st, o0, t_start, w1, L, kq, T, g, A);
   uint64_t rows = 0;
 #pragma unroll KMHG_PROBE_UNROLL
   for (int j = 0; j < WPT; ++j) {
@@ -588,7 +615,8 @@ k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
-    if (s < w1 && window_key(u.st, o0 + w, s, L, kq, key))
+    if (s < w1 && window_key(u.st, o0 + w, s, L, kq, key) &&
+        !(PS && diag_window(w, key, PS, nA, A, count, aux)))
       table_find(T, g, key, count, aux);
     qi[w] = make_uint2(count, count == 1 ? aux : aux - count);   // position, or list start
     rows += count;
@@ -973,8 +1001,12 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
                         hipStream_t s, const Slot* PS, int64_t nA) {
   uint32_t nt = grid_for(w1 - w0, TILE);
-  hipLaunchKernelGGL(k_query_probe, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo, w0,
-                     w1, aligned ? 1 : 0, tile_rows, PS, nA);
+  if (PS)
+    hipLaunchKernelGGL(k_query_probe<true>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo,
+                       w0, w1, aligned ? 1 : 0, tile_rows, PS, nA);
+  else
+    hipLaunchKernelGGL(k_query_probe<false>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo,
+                       w0, w1, aligned ? 1 : 0, tile_rows, nullptr, (int64_t)0);
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
@@ -998,10 +1030,11 @@ void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
 }
 void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
                         int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
-                        int2* out, uint64_t cap, hipStream_t s) {
+                        int2* out, uint64_t cap, hipStream_t s,
+                        const Slot* PS, int64_t nA) {
   const uint32_t nt = grid_for(w1 - w0, TILE);
   hipLaunchKernelGGL(k_query_fused, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, w0, w1,
-                     aligned ? 1 : 0, positions, status, nt, out, cap);
+                     aligned ? 1 : 0, positions, status, nt, out, cap, PS, nA);
 }
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s) {

@@ -281,7 +281,7 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
 
 
 def test_query_diagonal_path_vs_oracle(gpu):
-    """The diagonal path of k_query_probe (anchors every 16th window; later windows follow the
+    """The diagonal path of k_query_probe (anchors every 64th window; later windows follow the
     last anchor with a unique hit and take a position-indexed slot only when its key equals
     theirs) against the oracle: the index's own sequence, a related sequence (1 % SNVs,
     inversions, translocations, N-runs), its reverse complement, an unrelated one, repeat-rich
