@@ -302,6 +302,40 @@ __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom 
   }
 }
 
+// The same probe reading FOUR consecutive slots per round trip (a miss walks its run of
+// occupied slots to an empty one: at load 0.67 ~5 slots, one 64-B span instead of 5 dependent
+// loads).  Used where misses dominate (the diagonal query path sends only anchors, unpredicted
+// windows and misses here).
+__device__ __forceinline__ uint32_t table_find4(const Slot* __restrict__ T, Geom g, uint64_t key,
+                                                uint32_t& count, uint32_t& aux) {
+  if (key == EMPTY_KEY) return table_find(T, g, key, count, aux);
+  const uint64_t h = mix64(key);
+  const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
+  uint32_t j = local_home(h, g.capb);
+  for (;;) {
+    uint4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t jq = j + q;
+      if (jq >= g.capb) jq -= g.capb;
+      v[q] = *reinterpret_cast<const uint4*>(&T[b0 + jq]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t cur = ((uint64_t)v[q].y << 32) | v[q].x;
+      if (cur == key) {
+        count = v[q].z; aux = v[q].w;
+        uint32_t jq = j + q;
+        if (jq >= g.capb) jq -= g.capb;
+        return (uint32_t)(b0 + jq);
+      }
+      if (cur == EMPTY_KEY) { count = 0; aux = 0; return NONE; }
+    }
+    j += 4;
+    if (j >= g.capb) j -= g.capb;
+  }
+}
+
 // Wave-aggregated atomicAdd on a per-slot u32 counter.  Lanes that hold the same slot are
 // grouped behind the first active lane (readfirstlane + ballot); one atomic per group.  The
 // loop stops as soon as a group of one appears (i.i.d. data: one iteration), leaving the rest

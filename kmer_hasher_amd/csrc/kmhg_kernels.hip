@@ -431,8 +431,13 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
     if (s < w1 && window_key(st, o0 + w, s, L, kq, key) &&
-        !(DIAG && diag_window(w, key, PS, nA, A, count, aux)))
-      table_find(T, g, key, count, aux);
+        !(DIAG && diag_window(w, key, PS, nA, A, count, aux))) {
+#ifndef KMHG_NO_FIND4
+      if (DIAG) table_find4(T, g, key, count, aux);
+      else
+#endif
+        table_find(T, g, key, count, aux);
+    }
     // {count, position} for a key seen once, {count, first index} otherwise
     if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
     rows += count;
