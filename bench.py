@@ -54,7 +54,8 @@ CONFIGS = {
 # HIP-event labels (kmhg_timing_*) -> kernel names as rocprofv3 reports them
 PMC_NAME = {"k_v2_scatter_seq": "k_v2_scatter<true, false, false>",
             "k_v2_scatter": "k_v2_scatter<false, false, false>",
-            "k_v2_bucket_wg": "k_v2_bucket_wg<false>"}
+            "k_v2_bucket_wg": "k_v2_bucket_wg<false>",
+            "k_query_probe": "k_query_probe<true>"}
 
 
 def pmc_traffic(pmc: dict, kernel: str):
@@ -360,19 +361,21 @@ def main():
     # the same index queried with an unrelated sequence of the same length (seed + 100): almost
     # every window misses, so the diagonal path's anchors predict nothing and every window
     # probes the table -- the path's worst case, reported beside the self dot plot
-    other = torch.from_numpy(synth.iid(L, seed + 100)).to(dev)
-    H_other, n_other = 0, max(1, min(args.steps, 5))
-    q = idx.query(other, k, stream)
-    q.free()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(n_other):
+    H_other, t_other = 0, 0.0
+    if not args.profile:        # (the profile's per-kernel PMC averages stay self-query only)
+        other = torch.from_numpy(synth.iid(L, seed + 100)).to(dev)
+        n_other = max(1, min(args.steps, 5))
         q = idx.query(other, k, stream)
-        H_other = q.n_rows
         q.free()
-    barrier()
-    t_other = (time.perf_counter() - t0) / n_other
-    del other
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(n_other):
+            q = idx.query(other, k, stream)
+            H_other = q.n_rows
+            q.free()
+        barrier()
+        t_other = (time.perf_counter() - t0) / n_other
+        del other
     idx.free()
 
     # ---------------- count.kmers (SURVEY.md §8 f next-4) of the same sequence: one call per step
@@ -517,7 +520,8 @@ def main():
                       "first_call_ms": round(t_query_first * 1e3, 3),
                       "kernels_ms": {n: round(v, 5) for n, v in qper.items()},
                       "roofline": query_roofline(qper, L, Nw, H, pmc),
-                      "unrelated": {"value": round(L * world / 1e6 / t_other, 2), "unit": "Mbp/s",
+                      "unrelated": {"value": round(L * world / 1e6 / t_other, 2) if t_other
+                                    else None, "unit": "Mbp/s",
                                     "ms_per_step": round(t_other * 1e3, 4), "rows": H_other,
                                     "note": "index queried with an unrelated iid sequence "
                                             "(seed + 100): every window probes the table"},
