@@ -480,7 +480,8 @@ struct kmhg_index {
   // seq.kmer.pos diagonal path: the slot of every indexed window by position (built on the
   // first eligible query, kept with the index)
   DBuf<Slot> pslot;
-  bool ps_ready = false;
+  bool ps_ready = false, ps_failed = false;
+  std::mutex ps_mu;
   // stream-ordered release of everything the index holds (work queued on `s` may still read it)
   void bind_all(hipStream_t s) {
     table.bind(s); positions.bind(s); ckeys.bind(s); slot_row.bind(s); row_slot.bind(s);
@@ -883,16 +884,31 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   // diagonal path (k_query_probe / k_query_fused): a position index queried at its own k
   const int64_t nA = idx->L - idx->k + 1;
   const char* de = std::getenv("KMHG_QUERY_DIAG");
-  const bool diag = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
-                    idx->U > 0;
+  const bool diag_ok = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
+                       idx->U > 0;
+  bool diag = diag_ok;
   if (diag && !idx->ps_ready) {
-    idx->pslot.reset((size_t)nA);
-    idx->pslot.bind(s);
-    HIPC(hipMemsetAsync(idx->pslot.p, 0xFF, (size_t)nA * sizeof(Slot), s));
-    LAUNCH("k_pos_slots", s, launch_pos_slots(idx->table.p, idx->slots(), idx->positions.p,
-                                              idx->pslot.p, s));
-    idx->ps_ready = true;
+    std::lock_guard<std::mutex> lk(idx->ps_mu);
+    if (!idx->ps_ready && !idx->ps_failed) {
+      try {
+        idx->pslot.reset((size_t)nA);
+      } catch (const Error& e) {           // no room for 16 B per window: table probes only
+        if (e.code != KMHG_ENOMEM) throw;
+        idx->ps_failed = true;
+        (void)hipGetLastError();
+      }
+      if (!idx->ps_failed) {
+        idx->pslot.bind(s);
+        HIPC(hipMemsetAsync(idx->pslot.p, 0xFF, (size_t)nA * sizeof(Slot), s));
+        LAUNCH("k_pos_slots", s, launch_pos_slots(idx->table.p, idx->slots(),
+                                                  idx->positions.p, idx->pslot.p, s));
+        // once per index: later queries may run on other streams
+        HIPC(hipStreamSynchronize(s));
+        idx->ps_ready = true;
+      }
+    }
   }
+  diag = diag && idx->ps_ready;
 
   if (!classic) {
     // one pass: probe + look-back + emit (k_query_fused); look-back words + ticket zeroed
