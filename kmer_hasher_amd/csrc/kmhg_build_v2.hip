@@ -385,44 +385,70 @@ k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __res
 }
 
 // ---------------------------------------------------------------- V_scatter (stable)
-// Tile t = elements [t*PTILE, (t+1)*PTILE); wave w owns the contiguous PTILE/4 elements
-// [t*PTILE + w*PTILE/4, +PTILE/4), lane l holds element 64c + l of them.  Element order
-// inside the tile = (wave, c, lane) = input order, so ranks assigned in that order keep the
-// pass stable.  FROM_SEQ (pass 0) encodes the windows from LDS-staged chars and drops invalid
-// ones; later passes read the (key, pos) stream.  The tile is re-ordered by digit in LDS first
-// and written out run by run, so each wave store covers a few contiguous runs instead of 64
-// scattered addresses.
-// (Measured: 320-digit arrays and u16 digits instead of sdst, 48 -> 37 KB, change nothing --
-// the kernel is held to 3 waves / SIMD by its 164 VGPRs; forcing 4 spills and runs 35 % slower.)
+// Tile t = elements [t*PTILE, (t+1)*PTILE); wave w of the NWV waves owns the contiguous
+// PTILE/NWV elements [t*PTILE + w*PTILE/NWV, ...), lane l holds element 64c + l of them.
+// Element order inside the tile = (wave, c, lane) = input order, so ranks assigned in that
+// order keep the pass stable.  FROM_SEQ (pass 0) encodes the windows from LDS-staged chars and
+// drops invalid ones; later passes read the (key, pos) stream.  The tile is re-ordered by digit
+// in LDS first and written out run by run, so each wave store covers a few contiguous runs
+// instead of 64 scattered addresses.
+// NWV = 8 (512 threads, the default up to V2_MAXR_IL digits): 4 elements per lane instead of 8,
+// so a lane's keys, positions, digits and the next tile's prefetch fit half the registers and
+// the CU holds twice the waves (4 waves / 256 threads were held to 3 waves / SIMD by 164 VGPRs
+// and 48 KB of LDS; 320-digit arrays alone, or forcing 4 waves with spills, did not help).
+template <int NWV>
 struct ScatterLDS {
-  uint32_t wc[4][V2_MAXR];     // per-wave digit counts -> per-wave tile-local cursors
-  uint32_t tstart[V2_MAXR];    // tile-local start of each digit
-  uint32_t gbase[V2_MAXR];     // global start of each digit for this tile (scanned histogram)
+  static constexpr uint32_t MAXR = NWV == 4 ? V2_MAXR : V2_MAXR_IL;
+  uint32_t wc[NWV][MAXR];      // per-wave digit counts -> per-wave tile-local cursors
+  uint32_t tstart[MAXR];       // tile-local start of each digit
+  uint32_t gbase[MAXR];        // global start of each digit for this tile (scanned histogram)
   uint64_t skey[PTILE];
   uint32_t spos[PTILE];
   uint32_t sdst[PTILE];
   PStage st;
 };
 
+// Exclusive scan over the NWV * 64 threads of a block (one value per thread), lds >= NWV u64.
+template <int NWV>
+__device__ __forceinline__ uint64_t block_excl_scan_n(uint64_t v, uint64_t* lds, uint64_t& total) {
+  const int wid = threadIdx.x >> 6;
+  const uint64_t inc = wave_incl_scan(v);
+  if (lane_id() == 63) lds[wid] = inc;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) {
+    const uint64_t x = lds[w];
+    if (w < wid) off += x;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return off + inc - v;
+}
+
 // KEYS0: the first pass over a caller's key stream (a table rebuilt from keys): `kin` holds
 // exactly n keys (loads clamped, no pad) and positions are implicit (e + 1), so the stream is
 // neither copied nor paired with an iota array first.  NOPOS: keys only (count-only builds:
 // nobody reads the positions), 8 B per element in and out instead of 12.
-template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false>
-__global__ void __launch_bounds__(BLOCK)
+template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false, int NWV = 4>
+__global__ void __launch_bounds__(NWV * 64)
 k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned,
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, Chunks ch,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad, int remap) {
-  __shared__ ScatterLDS S;
+  using SL = ScatterLDS<NWV>;
+  constexpr int TB = NWV * 64;                  // threads per workgroup
+  constexpr int PER = PTILE / NWV / 64;         // elements per lane
+  constexpr int DPT = (int)((SL::MAXR + TB - 1) / TB);   // digits owned per thread
+  __shared__ SL S;
   __shared__ uint64_t sh[8];
   const uint32_t R = D.R;
-  constexpr int PER = PTILE / 4 / 64;    // elements per lane
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const uint32_t wbase = (uint32_t)wave * (PTILE / 4);
+  const uint32_t wbase = (uint32_t)wave * (PTILE / NWV);
   const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
-  // Two tile schedules (Chunks, kmhg_kernels.h); thread t owns digits 4t..4t+3 either way.
+  // Two tile schedules (Chunks, kmhg_kernels.h); thread t owns digits [DPT t, DPT t + DPT).
   //  interleaved (ch.interleaved): persistent workgroup b walks virtual tiles b, b + G, ...;
   //    with `remap` every XCD owns one contiguous tile range, so the tiles running at the same
   //    time on an XCD are neighbours and their partial output lines merge in that XCD's L2.
@@ -439,11 +465,11 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
     const uint32_t v = blockIdx.x + i * G;
     return remap ? xcd_remap(v, ch.ntiles) : v;
   };
-  uint32_t cursor[4], ngb[4];
+  uint32_t cursor[DPT], ngb[DPT];
   auto load_bases = [&](uint32_t tv) {     // unconditional (clamped) loads: static count
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t d = min(threadIdx.x * 4 + q, R - 1);
+    for (int q = 0; q < DPT; ++q) {
+      const uint32_t d = min(threadIdx.x * DPT + q, R - 1);
       ngb[q] = hist[(size_t)d * ch.C + (ch.interleaved ? tv : chunk)];
     }
   };
@@ -470,14 +496,14 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       }
     }
   };
-  // Every path into the loop top has [prefetch loads][PTILE/BLOCK x 2 stores] in flight, so the
+  // Every path into the loop top has [prefetch loads][PTILE/TB x 2 stores] in flight, so the
   // compiler waits for the prefetch with a counted vmcnt: the pad stores below stand in for the
   // previous tile's write-out on the first iteration.
   prefetch(tile_at(0));
 #pragma unroll
-  for (int q = 0; q < 4; ++q) cursor[q] = ngb[q];
+  for (int q = 0; q < DPT; ++q) cursor[q] = ngb[q];
 #pragma unroll
-  for (int j = 0; j < PTILE / BLOCK; ++j) {
+  for (int j = 0; j < PTILE / TB; ++j) {
     kout[pad + threadIdx.x] = 0;
     if (!NOPOS) pout[pad + threadIdx.x] = 0;
   }
@@ -489,7 +515,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
     bool act[PER];
     if (ch.interleaved) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) cursor[q] = ngb[q];
+      for (int q = 0; q < DPT; ++q) cursor[q] = ngb[q];
     }
     if (FROM_SEQ) {
       stage_pack(nchars, S.st);
@@ -517,27 +543,32 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
     for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
       if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
     __syncthreads();
-    // tile-local digit starts: thread t owns digits [4t, 4t+4)
-    uint32_t dsum[4];
+    // tile-local digit starts: thread t owns digits [DPT t, DPT t + DPT)
+    uint32_t dsum[DPT];
     uint64_t own = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t d = threadIdx.x * 4 + q;
-      dsum[q] = d < R ? S.wc[0][d] + S.wc[1][d] + S.wc[2][d] + S.wc[3][d] : 0u;
-      own += dsum[q];
+    for (int q = 0; q < DPT; ++q) {
+      const uint32_t d = threadIdx.x * DPT + q;
+      uint32_t sum = 0;
+      if (d < R) {
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) sum += S.wc[w][d];
+      }
+      dsum[q] = sum;
+      own += sum;
     }
     uint64_t tile_n;
-    uint32_t run = (uint32_t)block_excl_scan(own, sh, tile_n);
+    uint32_t run = (uint32_t)block_excl_scan_n<NWV>(own, sh, tile_n);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t d = threadIdx.x * 4 + q;
+    for (int q = 0; q < DPT; ++q) {
+      const uint32_t d = threadIdx.x * DPT + q;
       if (d < R) {
         S.tstart[d] = run;
         S.gbase[d] = cursor[q];
         cursor[q] += dsum[q];
         uint32_t cur = run;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NWV; ++w) {
           const uint32_t t = S.wc[w][d];
           S.wc[w][d] = cur;
           cur += t;
@@ -569,8 +600,8 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
     // the next tile's prefetched loads at the loop top is vmcnt(#stores), not vmcnt(0): the
     // prefetch was issued before these stores and must not queue behind their completion
 #pragma unroll
-    for (int j = 0; j < PTILE / BLOCK; ++j) {
-      const uint32_t i = (uint32_t)(j * BLOCK) + threadIdx.x;
+    for (int j = 0; j < PTILE / TB; ++j) {
+      const uint32_t i = (uint32_t)(j * TB) + threadIdx.x;
       // lanes past the tile's end store into the PTILE-element pad behind the outputs
       const uint32_t dst = i < (uint32_t)tile_n ? S.sdst[i] : pad + threadIdx.x;
       kout[dst] = S.skey[i];
@@ -1357,11 +1388,12 @@ void set_stamp_buffer(uint64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps
 // ---------------------------------------------------------------- launchers
 // Persistent grids: as many workgroups as are resident at once (CUs x the occupancy the
 // kernel's VGPR/LDS budget allows), so no workgroup waits for another to finish.
-static unsigned resident_blocks(const void* kernel) {
+static unsigned resident_blocks(const void* kernel, int threads = BLOCK) {
   int dev = 0, cus = 256, per = 1;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, BLOCK, 0) != hipSuccess || per < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess ||
+      per < 1)
     per = 1;
   return (unsigned)(cus > 0 ? cus : 256) * (unsigned)per;
 }
@@ -1391,7 +1423,7 @@ static inline unsigned grid_of(uint64_t n, unsigned per) {
 }
 
 static unsigned scatter_cap() {
-  static unsigned cap = resident_blocks((const void*)k_v2_scatter<true>);
+  static unsigned cap = resident_blocks((const void*)k_v2_scatter<true, false, false, 4>);
   return cap;
 }
 
@@ -1419,6 +1451,28 @@ Chunks make_chunks(uint32_t ntiles) {
 static unsigned scatter_grid(const Chunks& ch) {
   return ch.interleaved ? std::min<unsigned>(ch.ntiles, scatter_cap()) : ch.C;
 }
+
+// 8-wave scatter workgroups (interleaved schedule, R <= V2_MAXR_IL) unless KMHG_SC8=0
+static bool scatter8(const Chunks& ch, const Digit& D) {
+  static const int on = [] {
+    const char* e = std::getenv("KMHG_SC8");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on && ch.interleaved && D.R <= V2_MAXR_IL;
+}
+static unsigned scatter8_grid(const Chunks& ch) {
+  static const unsigned cap = resident_blocks((const void*)k_v2_scatter<true, false, false, 8>, 512);
+  return std::min<unsigned>(ch.ntiles, cap);
+}
+#define KMHG_SCATTER(FS, K0, NP, ...)                                                       \
+  do {                                                                                      \
+    if (scatter8(ch, D))                                                                    \
+      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, 8>), dim3(scatter8_grid(ch)), dim3(512), \
+                         0, s, __VA_ARGS__);                                                \
+    else                                                                                    \
+      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, 4>), dim3(scatter_grid(ch)), dim3(BLOCK),\
+                         0, s, __VA_ARGS__);                                                \
+  } while (0)
 
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
@@ -1473,33 +1527,30 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_scatter<true>, dim3(scatter_grid(ch)), dim3(BLOCK), 0, s, seq, L, k, Nw, 1,
-                     nullptr, nullptr, nullptr, g, D, hist, ch, kout, pout, pad, xcd_map());
+  KMHG_SCATTER(true, false, false, seq, L, k, Nw, 1, nullptr, nullptr, nullptr, g, D, hist, ch,
+               kout, pout, pad, xcd_map());
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_scatter<false>, dim3(scatter_grid(ch)), dim3(BLOCK), 0, s, nullptr, (int64_t)0, 0,
-                     (int64_t)0, 0, kin, pin, n_ptr, g, D, hist, ch, kout, pout, pad, xcd_map());
+  KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, pin, n_ptr, g, D,
+               hist, ch, kout, pout, pad, xcd_map());
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                              uint32_t pad, bool nopos, hipStream_t s) {
   if (nopos)
-    hipLaunchKernelGGL((k_v2_scatter<false, true, true>), dim3(scatter_grid(ch)), dim3(BLOCK), 0,
-                       s, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D, hist,
-                       ch, kout, nullptr, pad, xcd_map());
+    KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g,
+                 D, hist, ch, kout, nullptr, pad, xcd_map());
   else
-    hipLaunchKernelGGL((k_v2_scatter<false, true>), dim3(scatter_grid(ch)), dim3(BLOCK), 0, s,
-                       nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D, hist, ch,
-                       kout, pout, pad, xcd_map());
+    KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g,
+                 D, hist, ch, kout, pout, pad, xcd_map());
 }
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t pad,
                              hipStream_t s) {
-  hipLaunchKernelGGL((k_v2_scatter<false, false, true>), dim3(scatter_grid(ch)), dim3(BLOCK), 0,
-                     s, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D, hist,
-                     ch, kout, nullptr, pad, xcd_map());
+  KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D,
+               hist, ch, kout, nullptr, pad, xcd_map());
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s) {
