@@ -392,10 +392,10 @@ k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __res
 // drops invalid ones; later passes read the (key, pos) stream.  The tile is re-ordered by digit
 // in LDS first and written out run by run, so each wave store covers a few contiguous runs
 // instead of 64 scattered addresses.
-// NWV = 8 (512 threads, the default up to V2_MAXR_IL digits): 4 elements per lane instead of 8,
-// so a lane's keys, positions, digits and the next tile's prefetch fit half the registers and
-// the CU holds twice the waves (4 waves / 256 threads were held to 3 waves / SIMD by 164 VGPRs
-// and 48 KB of LDS; 320-digit arrays alone, or forcing 4 waves with spills, did not help).
+// NWV = 8 (512 threads, KMHG_SC8=1, up to V2_MAXR_IL digits): 4 elements per lane instead of 8
+// (84-96 VGPRs, 24 waves / CU instead of 12).  More waves did not make the pass faster (config 2
+// neutral, config 3 +10 %): it is bound by the digit-run write pattern, not by latency hiding.
+// (Also measured: 320-digit arrays alone, or forcing 4 waves of the 4-wave kernel with spills.)
 template <int NWV>
 struct ScatterLDS {
   static constexpr uint32_t MAXR = NWV == 4 ? V2_MAXR : V2_MAXR_IL;
@@ -1452,13 +1452,12 @@ static unsigned scatter_grid(const Chunks& ch) {
   return ch.interleaved ? std::min<unsigned>(ch.ntiles, scatter_cap()) : ch.C;
 }
 
-// 8-wave scatter workgroups (interleaved schedule, R <= V2_MAXR_IL) unless KMHG_SC8=0
+// 8-wave scatter workgroups only with KMHG_SC8=1 (interleaved schedule, R <= V2_MAXR_IL):
+// measured neutral at config 2 (R = 99), -3 % on the read-counting passes, +10 % slower at
+// config 3 (R = 313), so the 4-wave kernel stays the default
 static bool scatter8(const Chunks& ch, const Digit& D) {
-  static const int on = [] {
-    const char* e = std::getenv("KMHG_SC8");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on && ch.interleaved && D.R <= V2_MAXR_IL;
+  const char* e = std::getenv("KMHG_SC8");       // read per launch: the tests switch it
+  return e && e[0] == '1' && ch.interleaved && D.R <= V2_MAXR_IL;
 }
 static unsigned scatter8_grid(const Chunks& ch) {
   static const unsigned cap = resident_blocks((const void*)k_v2_scatter<true, false, false, 8>, 512);

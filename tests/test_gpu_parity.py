@@ -214,7 +214,7 @@ def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     _check_against_oracle("G" * 40, 32, qks=[31])
 
 
-@pytest.mark.parametrize("bounds", ["lo", "scan"])
+@pytest.mark.parametrize("bounds", ["lo", "scan", "sc8"])
 @pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
 def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds):
     """More radix passes than the input needs (KMHG_MAXR caps the radix): 1-4 passes with N-runs
@@ -224,7 +224,10 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds):
     KMHG_BOUNDS=scan; both against the oracle."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_MAXR", maxr)
-    monkeypatch.setenv("KMHG_BOUNDS", bounds)
+    if bounds == "sc8":                    # the 8-wave radix scatter (KMHG_SC8=1)
+        monkeypatch.setenv("KMHG_SC8", "1")
+    else:
+        monkeypatch.setenv("KMHG_BOUNDS", bounds)
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
     _check_against_oracle(s, 31, pairs=False)
     rr = synth.repeat_rich(300_000, 42, n_gap_every=100_000).tobytes().decode("latin-1")
