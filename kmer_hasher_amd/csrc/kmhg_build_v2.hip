@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
           Digit D, uint32_t* __restrict__ hist, Chunks ch, int remap,
           uint64_t* __restrict__ scan_status, uint32_t n_status, uint32_t* __restrict__ hll_rows,
-          uint32_t* __restrict__ hll_regs, uint32_t* __restrict__ save_col0) {
+          uint32_t* __restrict__ hll_regs, uint32_t* __restrict__ save_col0, int skip_empty) {
   __shared__ uint32_t lh[V2_MAXR];
   __shared__ uint32_t hreg[HLL ? HLL_REGS : 1];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
@@ -285,7 +285,9 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
 #pragma unroll
     for (int j = 0; j < 4; ++j) {                // 4 loads in flight per lane
       in[j] = e + j * BLOCK < e1;
-      const uint64_t h = in[j] ? mix64(keys[e + j * BLOCK]) : 1ull;
+      const uint64_t key = in[j] ? keys[e + j * BLOCK] : 0ull;
+      if (skip_empty && key == EMPTY_KEY) in[j] = false;      // a padded read's unused slot
+      const uint64_t h = in[j] ? mix64(key) : 1ull;
       dg[j] = in[j] ? digit_of_h(h, g.nb, D) : 0u;
       if (HLL && (h & ((1u << HLL_SAMPLE_BITS) - 1)) == 0)
         atomicMax(&hreg[(uint32_t)(h >> HLL_SAMPLE_BITS) & (HLL_REGS - 1)],
@@ -353,7 +355,8 @@ k_v2_hll_part(const uint32_t* __restrict__ rows, uint32_t n_rows, uint32_t* __re
 }
 
 __global__ void __launch_bounds__(HLL_T)
-k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __restrict__ host_est) {
+k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __restrict__ host_est,
+               const uint32_t* __restrict__ n_valid, uint64_t* __restrict__ host_n) {
   __shared__ uint32_t pw[HLL_RG][64];
   __shared__ double zs[HLL_REGS / 64];
   __shared__ uint32_t zc[HLL_REGS / 64];
@@ -381,6 +384,7 @@ k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __res
     double e = 0.7213 / (1.0 + 1.079 / mm) * mm * mm / zt;
     if (e <= 2.5 * mm && zeros) e = mm * log(mm / (double)zeros);
     *host_est = e * (double)(1u << HLL_SAMPLE_BITS);
+    if (host_n) *host_n = *n_valid;            // the keys the estimate is set against
   }
 }
 
@@ -437,7 +441,8 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, Chunks ch,
-             uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad, int remap) {
+             uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad, int remap,
+             int skip_empty) {
   using SL = ScatterLDS<NWV>;
   constexpr int TB = NWV * 64;                  // threads per workgroup
   constexpr int PER = PTILE / NWV / 64;         // elements per lane
@@ -447,7 +452,9 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
   const uint32_t R = D.R;
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const uint32_t wbase = (uint32_t)wave * (PTILE / NWV);
-  const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
+  // elements to read: every window (FROM_SEQ) or the caller's whole key stream (KEYS0, passed
+  // as Nw: with skip_empty it is longer than the valid count the scan left in *n_ptr)
+  const uint64_t n = (FROM_SEQ || KEYS0) ? (uint64_t)Nw : (uint64_t)*n_ptr;
   // Two tile schedules (Chunks, kmhg_kernels.h); thread t owns digits [DPT t, DPT t + DPT).
   //  interleaved (ch.interleaved): persistent workgroup b walks virtual tiles b, b + G, ...;
   //    with `remap` every XCD owns one contiguous tile range, so the tiles running at the same
@@ -535,7 +542,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
         act[c] = e < n && window_key(S.st, HALO + (int)w, (int64_t)e, L, k, key[c]);
         ps[c] = (uint32_t)(e + 1);
       } else {
-        act[c] = e < n;
+        act[c] = e < n && !(KEYS0 && skip_empty && key[c] == EMPTY_KEY);
       }
       dg[c] = act[c] ? digit_of(key[c], g.nb, D) : 0;
     }
@@ -1503,13 +1510,15 @@ void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total,
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
-                    uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0) {
+                    uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0, bool skip_empty) {
   if (hll_rows)
     hipLaunchKernelGGL(k_v2_hist<true>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
-                       ch, xcd_map(), scan_status, n_status, hll_rows, hll_regs, save_col0);
+                       ch, xcd_map(), scan_status, n_status, hll_rows, hll_regs, save_col0,
+                       skip_empty ? 1 : 0);
   else
     hipLaunchKernelGGL(k_v2_hist<false>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
-                       ch, xcd_map(), scan_status, n_status, nullptr, nullptr, save_col0);
+                       ch, xcd_map(), scan_status, n_status, nullptr, nullptr, save_col0,
+                       skip_empty ? 1 : 0);
 }
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
@@ -1518,38 +1527,40 @@ void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, D
                      hist, C, lo_start, spread, start);
 }
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
-                   hipStream_t s) {
+                   const uint32_t* n_valid, uint64_t* host_n, hipStream_t s) {
   const uint32_t g = std::max(1u, std::min(HLL_PART_ROWS, (n_rows + 127) / 128));
   hipLaunchKernelGGL(k_v2_hll_part, dim3(g), dim3(HLL_T), 0, s, hll_rows, n_rows, hll_regs);
-  hipLaunchKernelGGL(k_v2_hll_final, dim3(1), dim3(HLL_T), 0, s, hll_regs, g, host_est);
+  hipLaunchKernelGGL(k_v2_hll_final, dim3(1), dim3(HLL_T), 0, s, hll_regs, g, host_est, n_valid,
+                     host_n);
 }
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s) {
   KMHG_SCATTER(true, false, false, seq, L, k, Nw, 1, nullptr, nullptr, nullptr, g, D, hist, ch,
-               kout, pout, pad, xcd_map());
+               kout, pout, pad, xcd_map(), 0);
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s) {
   KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, pin, n_ptr, g, D,
-               hist, ch, kout, pout, pad, xcd_map());
+               hist, ch, kout, pout, pad, xcd_map(), 0);
 }
-void launch_v2_scatter_keys0(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
-                             const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
-                             uint32_t pad, bool nopos, hipStream_t s) {
+void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
+                             Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout,
+                             uint32_t* pout, uint32_t pad, bool nopos, bool skip_empty,
+                             hipStream_t s) {
   if (nopos)
-    KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g,
-                 D, hist, ch, kout, nullptr, pad, xcd_map());
+    KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)n_keys, 0, kin, nullptr, n_ptr,
+                 g, D, hist, ch, kout, nullptr, pad, xcd_map(), skip_empty ? 1 : 0);
   else
-    KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g,
-                 D, hist, ch, kout, pout, pad, xcd_map());
+    KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)n_keys, 0, kin, nullptr,
+                 n_ptr, g, D, hist, ch, kout, pout, pad, xcd_map(), skip_empty ? 1 : 0);
 }
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t pad,
                              hipStream_t s) {
   KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D,
-               hist, ch, kout, nullptr, pad, xcd_map());
+               hist, ch, kout, nullptr, pad, xcd_map(), 0);
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s) {

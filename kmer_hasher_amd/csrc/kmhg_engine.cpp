@@ -344,6 +344,11 @@ class PinnedPool {
   std::mutex mu_;
   std::vector<PinnedRec> free_, pending_;
 };
+// returns a record taken for a host round trip that the scope waited for (any exit path)
+struct GiveBack {
+  PinnedRec& r;
+  ~GiveBack() { PinnedPool::get().give(r, false); }
+};
 
 // ============================================================================ timing
 struct Timing {
@@ -608,9 +613,11 @@ int co_spread_for(double distinct, uint64_t total) {
 // skips its position pass and no positions array is kept.
 // count_only with co_spread = 0: the spread is chosen from the key stream's own HLL estimate
 // (co_spread_for), read back while the radix passes run.
+// skip_empty (count-only key streams of k <= 31): EMPTY_KEY entries are padding, not keys --
+// the first pass drops them, and the valid count comes from its scan.
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
                             const uint64_t* d_keys = nullptr, int64_t n_keys = 0,
-                            bool count_only = false, int co_spread = 1) {
+                            bool count_only = false, int co_spread = 1, bool skip_empty = false) {
   ReleaseGroup rg(s);             // the scratch buffers below: one release event
   const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
@@ -621,6 +628,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const bool from_keys = d_seq == nullptr;
   const int64_t Nw = from_keys ? n_keys : L - k + 1;
   if (from_keys && Nw < 1) fail(KMHG_EINVAL, "empty key stream (internal error)");
+  if (skip_empty && !(from_keys && count_only && k < 32))
+    fail(KMHG_EINVAL, "padded key stream outside a count-only build (internal error)");
   // the partition kernels read the sequence as aligned 16-B words: copy an unaligned input
   DBuf<uint8_t> aligned_copy;
   if (!from_keys && (reinterpret_cast<uintptr_t>(d_seq) & 15) != 0) {
@@ -737,17 +746,18 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     LAUNCH("k_v2_hist", s,
            launch_v2_hist(src, n_valid, g, Dp, hist.p, ch, status, n_status, s,
                           hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
-                          save ? lo_start.p : nullptr));
-    if (hll) {
+                          save ? lo_start.p : nullptr, keys0 && skip_empty));
+    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
+    if (hll) {   // after the scan: the estimate travels with the valid key count
       LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ch.C, hll_regs.p,
-                                          &hrec.meta->distinct_est, s));
+                                          &hrec.meta->distinct_est, n_valid,
+                                          &hrec.meta->n_positions, s));
       HIPC(hipEventRecord(hrec.ev, s));
     }
-    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     if (keys0) {
       LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter_keys0(d_keys, n_valid, g, Dp, hist.p, ch, kout, pout, pad, no_pos,
-                                     s));
+             launch_v2_scatter_keys0(d_keys, (uint64_t)Nw, n_valid, g, Dp, hist.p, ch, kout, pout,
+                                     pad, no_pos, skip_empty, s));
     } else if (no_pos) {
       LAUNCH("k_v2_scatter", s,
              launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ch, kout, pad, s));
@@ -764,8 +774,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     // the estimate landed while the later radix passes were still queued on the device
     HIPC(hipEventSynchronize(hrec.ev));
     idx->co_est = hrec.meta->distinct_est;
+    const uint64_t n_keys_valid = hrec.meta->n_positions;
     PinnedPool::get().give(hrec, false);
-    idx->co_spread = co_spread_for(idx->co_est, (uint64_t)Nw);
+    idx->co_spread = co_spread_for(idx->co_est, n_keys_valid);
     gb = Geom{nb / (uint32_t)idx->co_spread, V2_CAPW};
     idx->geom = gb;
     idx->table.reset(idx->slots());
@@ -930,10 +941,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   DBuf<uint64_t> tiles((size_t)nt + scan_u64_scratch(nt), s);
   uint64_t* tile_row0 = tiles.p;
   PinnedRec hrec = PinnedPool::get().take();
-  struct GiveBack {
-    PinnedRec& r;
-    ~GiveBack() { PinnedPool::get().give(r, false); }
-  } give_back{hrec};
+  GiveBack give_back{hrec};
   uint64_t* total = &hrec.meta->n_kmers;
   LAUNCH("k_query_probe", s,
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
@@ -1241,10 +1249,11 @@ double qll_host(int q) {   // the same table on the host (the iterator's thresho
 // The count-only partitioned build of a key stream at `spread` (0: from its HLL estimate),
 // waited for.  `overflow`: a bucket's LDS sub-table filled up -- the table is unusable and the
 // caller retries at spread 1 (the index still reports the spread and estimate it tried).
+// `keys` is a padded stream (EMPTY_KEY entries skipped, k <= 31).
 std::unique_ptr<kmhg_index> count_only_build(const uint64_t* keys, uint32_t total, int k,
                                              int spread, hipStream_t s, bool& overflow) {
   std::unique_ptr<kmhg_index> B(
-      build_device_v2(nullptr, 0, k, s, keys, (int64_t)total, true, spread));
+      build_device_v2(nullptr, 0, k, s, keys, (int64_t)total, true, spread, true));
   HIPC(hipEventSynchronize(B->rec.ev));
   const BuildMeta hm = *B->rec.meta;
   PinnedPool::get().give(B->rec, false);
@@ -1270,9 +1279,12 @@ kmhg_index* new_sh_index(int k, int counts_n, hipStream_t s) {
   return idx.release();
 }
 
-// One batch of packed reads (device-resident) merged into the suffix hash: R_kmers count ->
-// scan -> R_kmers emit -> partitioned build of the key stream (occurrence counts per distinct
-// key) -> merge over the batch table's slots.
+// One batch of packed reads (device-resident) merged into the suffix hash: per-read upper
+// bounds (R_ub) -> scan -> R_kmers emit, padded with EMPTY_KEY up to each read's bound ->
+// partitioned build of the key stream, padding skipped (occurrence counts per distinct key) ->
+// merge over the batch table's slots.  The padding (quality- or N-rejected windows) costs its
+// 8 B per window in the build's first pass; the exact count pass it replaces re-walked every
+// read and cost a second host round trip (reads leg: see DESIGN.md).
 void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t* d_qual,
                            const int64_t* d_off, const uint8_t* d_hasq, uint32_t n_reads,
                            double mean_len, double min_ll, uint32_t source, hipStream_t s) {
@@ -1287,23 +1299,23 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 2) * 8, s));
   uint32_t* d_span = reinterpret_cast<uint32_t*>(status.p + nt + 1);
   LAUNCH("k_rk_span", s, launch_rk_span(d_off, n_reads, d_span, s));
-  uint32_t span = 0;
-  HIPC(hipMemcpyAsync(&span, d_span, 4, hipMemcpyDeviceToHost, s));
+  LAUNCH("k_read_ub", s, launch_read_ub(d_off, n_reads, k, cnt.p, s));
+  LAUNCH("k_scan_u32", s, launch_scan_u32(cnt.p, n_reads, status.p, cnt.p + n_reads, s));
+  // one round trip for the staging span and the stream length (pinned: the GiveBack returns it)
+  PinnedRec hr = PinnedPool::get().take();
+  GiveBack hr_back{hr};
+  HIPC(hipMemcpyAsync(&hr.meta->n_pairs, d_span, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipMemcpyAsync(&hr.meta->max_count, cnt.p + n_reads, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  const uint32_t span = (uint32_t)__atomic_load_n(&hr.meta->n_pairs, __ATOMIC_ACQUIRE);
+  const uint32_t total = __atomic_load_n(&hr.meta->max_count, __ATOMIC_ACQUIRE);
   const uint32_t cap = read_kmers_cap_span(span);
   (void)mean_len;
-  LAUNCH("k_read_kmers_count", s,
-         launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
-                           nullptr, false, s));
-  LAUNCH("k_scan_u32", s, launch_scan_u32(cnt.p, n_reads, status.p, cnt.p + n_reads, s));
-  uint32_t total = 0;
-  HIPC(hipMemcpyAsync(&total, cnt.p + n_reads, 4, hipMemcpyDeviceToHost, s));
-  HIPC(hipStreamSynchronize(s));
   if (!total) return;
   DBuf<uint64_t> keys(total, s);
   LAUNCH("k_read_kmers_emit", s,
          launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
-                           keys.p, true, s));
+                           keys.p, true, s, true));
   // The count-only build gives each group bucket `spread` x V2_BW_WG stream entries, so that the
   // batch's distinct keys -- not its key stream -- fill the LDS sub-tables (bench, 3.7x
   // coverage: spread 1/2/3/4 -> 22.6/26.8/28.5/27.6 Gbp/s).  The spread comes from THIS

@@ -144,7 +144,7 @@ constexpr uint32_t HLL_PART_WORDS = 256 * 64 + 1;
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr,
-                    uint32_t* save_col0 = nullptr);
+                    uint32_t* save_col0 = nullptr, bool skip_empty = false);
 // bucket starts from the histograms (passes <= 2, interleaved schedule): one workgroup per lo
 // value (div of them); kprev = the last pass's input keys, lo_start = the previous pass's digit
 // starts (saved by launch_v2_hist's save_col0; nullptr for one pass); start[b / spread] for
@@ -152,17 +152,20 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
                          uint32_t spread, uint32_t* start, hipStream_t s);
+// also copies *n_valid (launch it after the pass's scan) to *host_n
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
-                   hipStream_t s);
+                   const uint32_t* n_valid, uint64_t* host_n, hipStream_t s);
 // the sequence must be 16-B aligned (the engine copies an unaligned input)
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s);
-// first pass over a caller's key stream of exactly *n_ptr keys (>= 1): positions are e + 1
-// nopos: keys only (count-only builds), pout unused
-void launch_v2_scatter_keys0(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
-                             const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
-                             uint32_t pad, bool nopos, hipStream_t s);
+// first pass over a caller's key stream of n_keys keys (>= 1): positions are e + 1; nopos:
+// keys only (count-only builds), pout unused; skip_empty: EMPTY_KEY entries are not keys (padded
+// read k-mer streams, k <= 31)
+void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
+                             Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout,
+                             uint32_t* pout, uint32_t pad, bool nopos, bool skip_empty,
+                             hipStream_t s);
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t pad,
                              hipStream_t s);

@@ -17,7 +17,10 @@ inline uint32_t depth_tiles(int64_t L) { return (uint32_t)((L + DP_TILE - 1) / D
 void launch_read_kmers(const uint8_t* seq, const uint8_t* qual, const int64_t* off,
                        const uint8_t* hasq, uint32_t n_reads, int k, double min_ll,
                        const double* qll, uint32_t cap, uint32_t* cnt, uint64_t* keys,
-                       bool emit, hipStream_t s);
+                       bool emit, hipStream_t s, bool pad = false);
+// pad (emit only): cnt holds exclusive offsets of per-read UPPER BOUNDS (launch_read_ub), and
+// each read's unused tail of its range is filled with EMPTY_KEY (skipped by the count-only build)
+void launch_read_ub(const int64_t* off, uint32_t n_reads, int k, uint32_t* cnt, hipStream_t s);
 // staging capacity for a batch of mean read length `mean_len`: 1.5x the mean span of a wave,
 // 16-B multiple, at most 28 KiB per stream (4+ waves per CU)
 // *span = the largest byte span a k_read_kmers workgroup stages (atomicMax; zero it first)

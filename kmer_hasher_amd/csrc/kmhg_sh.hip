@@ -58,7 +58,7 @@ struct LdsBytes {
 template <bool EMIT, class Acc>
 __device__ __forceinline__ void walk_read(Acc s, Acc q, int64_t x, int64_t e, bool hasq, int k,
                                           double min_ll, const double* qll, uint32_t* cnt,
-                                          uint32_t rd, uint64_t* keys) {
+                                          uint32_t rd, uint64_t* keys, bool pad) {
   enum : int { SEEK = 0, SKIP = 1, RUN = 2 };
   const uint64_t mask = (1ull << (2 * k)) - 1;
   const int shift = 64 - 2 * k;
@@ -107,6 +107,10 @@ __device__ __forceinline__ void walk_read(Acc s, Acc q, int64_t x, int64_t e, bo
     ++n;
   }
   if (!EMIT) cnt[rd] = n;
+  // padded emit (offsets from per-read upper bounds, no count pass): the rest of the read's
+  // range holds EMPTY_KEY, which the count-only build skips (k <= 31: never a real key)
+  if (EMIT && pad)
+    for (uint32_t i = n, ub = cnt[rd + 1] - cnt[rd]; i < ub; ++i) out[i] = EMPTY_KEY;
 }
 
 // One wave per RK_READS consecutive reads, one lane per read.  The wave's bases and qualities
@@ -119,7 +123,7 @@ __global__ void __launch_bounds__(RK_READS)
 k_read_kmers(const uint8_t* __restrict__ seq, const uint8_t* __restrict__ qual,
              const int64_t* __restrict__ off, const uint8_t* __restrict__ hasq, uint32_t n_reads,
              int k, double min_ll, const double* __restrict__ qll_g, uint32_t cap,
-             uint32_t* __restrict__ cnt, uint64_t* __restrict__ keys) {
+             uint32_t* __restrict__ cnt, uint64_t* __restrict__ keys, int pad) {
   extern __shared__ uint4 rk_smem[];
   double* qll = reinterpret_cast<double*>(rk_smem);
   uint8_t* ls = reinterpret_cast<uint8_t*>(rk_smem) + 256 * sizeof(double);
@@ -149,9 +153,24 @@ k_read_kmers(const uint8_t* __restrict__ seq, const uint8_t* __restrict__ qual,
   const bool hq = hasq[rd] != 0;
   if (fits)
     walk_read<EMIT>(LdsBytes{ls, base}, LdsBytes{lq, base}, b, e, hq, k, min_ll, qll, cnt, rd,
-                    keys);
+                    keys, pad != 0);
   else
-    walk_read<EMIT>(ByteCursor(seq), ByteCursor(qual), b, e, hq, k, min_ll, qll, cnt, rd, keys);
+    walk_read<EMIT>(ByteCursor(seq), ByteCursor(qual), b, e, hq, k, min_ll, qll, cnt, rd, keys,
+                    pad != 0);
+}
+
+// Per-read upper bound of the k-mers the iterator can accept: max(0, length - k + 1).
+__global__ void __launch_bounds__(BLOCK)
+k_read_ub(const int64_t* __restrict__ off, uint32_t n_reads, int k, uint32_t* __restrict__ cnt) {
+  const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
+  if (r >= n_reads) return;
+  const int64_t len = off[r + 1] - off[r];
+  cnt[r] = len >= k ? (uint32_t)(len - k + 1) : 0u;
+}
+
+void launch_read_ub(const int64_t* off, uint32_t n_reads, int k, uint32_t* cnt, hipStream_t s) {
+  hipLaunchKernelGGL(k_read_ub, dim3((n_reads + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, off,
+                     n_reads, k, cnt);
 }
 
 // The largest byte span one k_read_kmers workgroup stages (RK_READS reads from an aligned-down
@@ -176,15 +195,15 @@ void launch_rk_span(const int64_t* off, uint32_t n_reads, uint32_t* span, hipStr
 void launch_read_kmers(const uint8_t* seq, const uint8_t* qual, const int64_t* off,
                        const uint8_t* hasq, uint32_t n_reads, int k, double min_ll,
                        const double* qll, uint32_t cap, uint32_t* cnt, uint64_t* keys,
-                       bool emit, hipStream_t s) {
+                       bool emit, hipStream_t s, bool pad) {
   const dim3 grid((n_reads + RK_READS - 1) / RK_READS);
   const size_t smem = 256 * sizeof(double) + 2 * (size_t)cap;
   if (emit)
     hipLaunchKernelGGL(k_read_kmers<true>, grid, dim3(RK_READS), smem, s, seq, qual, off, hasq,
-                       n_reads, k, min_ll, qll, cap, cnt, keys);
+                       n_reads, k, min_ll, qll, cap, cnt, keys, pad ? 1 : 0);
   else
     hipLaunchKernelGGL(k_read_kmers<false>, grid, dim3(RK_READS), smem, s, seq, qual, off, hasq,
-                       n_reads, k, min_ll, qll, cap, cnt, keys);
+                       n_reads, k, min_ll, qll, cap, cnt, keys, 0);
 }
 
 // ------------------------------------------------------------------ depth: N-free segments
@@ -504,7 +523,9 @@ __global__ void __launch_bounds__(BLOCK)
 k_key_count_insert(const uint64_t* __restrict__ keys, uint64_t n, Slot* __restrict__ T, Geom g) {
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * BLOCK) {
-    const uint32_t slot = table_insert(T, g, keys[i]);
+    const uint64_t key = keys[i];
+    if (key == EMPTY_KEY) continue;              // padding (suffix-hash k <= 31: never a key)
+    const uint32_t slot = table_insert(T, g, key);
     atomicAdd(&T[slot].count, 1u);
   }
 }
