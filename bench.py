@@ -159,11 +159,10 @@ READS_N, READS_LEN, READS_MINQ, READS_CPU = 400_000, 150, 10, 40_000
 
 
 def reads_algorithmic_bytes(kernel: str, n_bases: int, n_reads: int, words: int) -> int | None:
-    """Minimum bytes of the read-counting kernels: the iterator reads every base and quality
-    once (2 B/base) and its read's offset (8 B) and count/offset (4 B); the emit pass also writes
-    8 B per accepted k-mer (`words`, the k-mer occurrences counted)."""
-    if kernel == "k_read_kmers_count":
-        return 2 * n_bases + 12 * n_reads
+    """Minimum bytes of the read-counting iterator (one walk): every base and quality read once
+    (2 B/base), its read's offset (8 B) and output offset (4 B), and 8 B written per accepted
+    k-mer (`words`, the k-mer occurrences counted; the EMPTY_KEY padding of rejected windows is
+    not counted)."""
     if kernel == "k_read_kmers_emit":
         return 2 * n_bases + 12 * n_reads + 8 * words
     return None

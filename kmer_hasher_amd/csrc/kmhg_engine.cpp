@@ -1315,7 +1315,7 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   DBuf<uint64_t> keys(total, s);
   LAUNCH("k_read_kmers_emit", s,
          launch_read_kmers(d_seq, d_qual, d_off, d_hasq, n_reads, k, min_ll, qll, cap, cnt.p,
-                           keys.p, true, s, true));
+                           keys.p, s));
   // The count-only build gives each group bucket `spread` x V2_BW_WG stream entries, so that the
   // batch's distinct keys -- not its key stream -- fill the LDS sub-tables (bench, 3.7x
   // coverage: spread 1/2/3/4 -> 22.6/26.8/28.5/27.6 Gbp/s).  The spread comes from THIS

@@ -11,15 +11,15 @@ constexpr int DP_TILE = BLOCK * DP_CPT;      // depth: chars per workgroup
 inline uint32_t depth_tiles(int64_t L) { return (uint32_t)((L + DP_TILE - 1) / DP_TILE); }
 
 // one lane per read of a packed batch: seq / qual bytes (16-B aligned, >= 16 B of padding),
-// read r = [off[r], off[r+1]), hasq[r] = 0 for a FASTA record.  emit = false: cnt[r] = k-mers
-// accepted; emit = true: cnt = exclusive offsets, keys[cnt[r] + t] = canonical k-mer t.
-// cap = LDS bytes per stream staged per wave of 64 reads (read_kmers_cap_span).
+// read r = [off[r], off[r+1]), hasq[r] = 0 for a FASTA record.  cnt = exclusive offsets of the
+// per-read UPPER bounds (launch_read_ub + scan, n_reads + 1 entries): keys[cnt[r] + t] =
+// canonical k-mer t accepted from read r, EMPTY_KEY after the last (the count-only build skips
+// it).  cap = LDS bytes per stream staged per wave of 64 reads (read_kmers_cap_span).
 void launch_read_kmers(const uint8_t* seq, const uint8_t* qual, const int64_t* off,
                        const uint8_t* hasq, uint32_t n_reads, int k, double min_ll,
-                       const double* qll, uint32_t cap, uint32_t* cnt, uint64_t* keys,
-                       bool emit, hipStream_t s, bool pad = false);
-// pad (emit only): cnt holds exclusive offsets of per-read UPPER BOUNDS (launch_read_ub), and
-// each read's unused tail of its range is filled with EMPTY_KEY (skipped by the count-only build)
+                       const double* qll, uint32_t cap, const uint32_t* cnt, uint64_t* keys,
+                       hipStream_t s);
+// cnt[r] = max(0, length of read r - k + 1)
 void launch_read_ub(const int64_t* off, uint32_t n_reads, int k, uint32_t* cnt, hipStream_t s);
 // staging capacity for a batch of mean read length `mean_len`: 1.5x the mean span of a wave,
 // 16-B multiple, at most 28 KiB per stream (4+ waves per CU)

@@ -55,14 +55,17 @@ struct LdsBytes {
 // exactly one position, so the lanes of a wave stay in step -- the nested restart loops of
 // ReadIter serialise a wave whenever any one lane restarts (measured: 4.6x slower).  States:
 // SEEK (= kmer_iterator_begin accumulating i < k bases), SKIP (its skip loop), RUN (_next).
-template <bool EMIT, class Acc>
+// Read rd's range of keys is [cnt[rd], cnt[rd + 1]), sized by its upper bound (k_read_ub): the
+// accepted k-mers, then EMPTY_KEY to the end, which the count-only build skips (k <= 31: never a
+// real key) -- one walk, no exact count pass.
+template <class Acc>
 __device__ __forceinline__ void walk_read(Acc s, Acc q, int64_t x, int64_t e, bool hasq, int k,
-                                          double min_ll, const double* qll, uint32_t* cnt,
-                                          uint32_t rd, uint64_t* keys, bool pad) {
+                                          double min_ll, const double* qll,
+                                          const uint32_t* cnt, uint32_t rd, uint64_t* keys) {
   enum : int { SEEK = 0, SKIP = 1, RUN = 2 };
   const uint64_t mask = (1ull << (2 * k)) - 1;
   const int shift = 64 - 2 * k;
-  uint64_t* out = EMIT ? keys + cnt[rd] : nullptr;
+  uint64_t* out = keys + cnt[rd];
   uint32_t n = 0;
   int st = SEEK, i = 0;
   uint64_t f = 0, r = 0;
@@ -100,17 +103,10 @@ __device__ __forceinline__ void walk_read(Acc s, Acc q, int64_t x, int64_t e, bo
       if (restart) { st = SEEK; i = 0; f = 0; r = 0; kl = 0; pv = 0; continue; }
       f = fwd_push(f, c); r = rev_push(r, c);
     }
-    if (EMIT) {
-      const uint64_t a = f & mask, bb = r >> shift;
-      out[n] = a < bb ? a : bb;
-    }
-    ++n;
+    const uint64_t a = f & mask, bb = r >> shift;
+    out[n++] = a < bb ? a : bb;
   }
-  if (!EMIT) cnt[rd] = n;
-  // padded emit (offsets from per-read upper bounds, no count pass): the rest of the read's
-  // range holds EMPTY_KEY, which the count-only build skips (k <= 31: never a real key)
-  if (EMIT && pad)
-    for (uint32_t i = n, ub = cnt[rd + 1] - cnt[rd]; i < ub; ++i) out[i] = EMPTY_KEY;
+  for (uint32_t i = n, ub = cnt[rd + 1] - cnt[rd]; i < ub; ++i) out[i] = EMPTY_KEY;
 }
 
 // One wave per RK_READS consecutive reads, one lane per read.  The wave's bases and qualities
@@ -118,12 +114,11 @@ __device__ __forceinline__ void walk_read(Acc s, Acc q, int64_t x, int64_t e, bo
 // HBM); a wave whose reads span more than `cap` bytes walks them from global memory instead.
 constexpr int RK_READS = 64;
 
-template <bool EMIT>
 __global__ void __launch_bounds__(RK_READS)
 k_read_kmers(const uint8_t* __restrict__ seq, const uint8_t* __restrict__ qual,
              const int64_t* __restrict__ off, const uint8_t* __restrict__ hasq, uint32_t n_reads,
              int k, double min_ll, const double* __restrict__ qll_g, uint32_t cap,
-             uint32_t* __restrict__ cnt, uint64_t* __restrict__ keys, int pad) {
+             const uint32_t* __restrict__ cnt, uint64_t* __restrict__ keys) {
   extern __shared__ uint4 rk_smem[];
   double* qll = reinterpret_cast<double*>(rk_smem);
   uint8_t* ls = reinterpret_cast<uint8_t*>(rk_smem) + 256 * sizeof(double);
@@ -152,11 +147,9 @@ k_read_kmers(const uint8_t* __restrict__ seq, const uint8_t* __restrict__ qual,
   const int64_t b = off[rd], e = off[rd + 1];
   const bool hq = hasq[rd] != 0;
   if (fits)
-    walk_read<EMIT>(LdsBytes{ls, base}, LdsBytes{lq, base}, b, e, hq, k, min_ll, qll, cnt, rd,
-                    keys, pad != 0);
+    walk_read(LdsBytes{ls, base}, LdsBytes{lq, base}, b, e, hq, k, min_ll, qll, cnt, rd, keys);
   else
-    walk_read<EMIT>(ByteCursor(seq), ByteCursor(qual), b, e, hq, k, min_ll, qll, cnt, rd, keys,
-                    pad != 0);
+    walk_read(ByteCursor(seq), ByteCursor(qual), b, e, hq, k, min_ll, qll, cnt, rd, keys);
 }
 
 // Per-read upper bound of the k-mers the iterator can accept: max(0, length - k + 1).
@@ -194,16 +187,12 @@ void launch_rk_span(const int64_t* off, uint32_t n_reads, uint32_t* span, hipStr
 
 void launch_read_kmers(const uint8_t* seq, const uint8_t* qual, const int64_t* off,
                        const uint8_t* hasq, uint32_t n_reads, int k, double min_ll,
-                       const double* qll, uint32_t cap, uint32_t* cnt, uint64_t* keys,
-                       bool emit, hipStream_t s, bool pad) {
+                       const double* qll, uint32_t cap, const uint32_t* cnt, uint64_t* keys,
+                       hipStream_t s) {
   const dim3 grid((n_reads + RK_READS - 1) / RK_READS);
   const size_t smem = 256 * sizeof(double) + 2 * (size_t)cap;
-  if (emit)
-    hipLaunchKernelGGL(k_read_kmers<true>, grid, dim3(RK_READS), smem, s, seq, qual, off, hasq,
-                       n_reads, k, min_ll, qll, cap, cnt, keys, pad ? 1 : 0);
-  else
-    hipLaunchKernelGGL(k_read_kmers<false>, grid, dim3(RK_READS), smem, s, seq, qual, off, hasq,
-                       n_reads, k, min_ll, qll, cap, cnt, keys, 0);
+  hipLaunchKernelGGL(k_read_kmers, grid, dim3(RK_READS), smem, s, seq, qual, off, hasq, n_reads, k,
+                     min_ll, qll, cap, cnt, keys);
 }
 
 // ------------------------------------------------------------------ depth: N-free segments
