@@ -1356,6 +1356,7 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   idx->co_est = est;
   idx->co_spread = spread;
   idx->co_path = path;
+  if (B->U == 0) return;                         // every window of the batch rejected
   merge_batch(idx, B.get(), nullptr, B->slots(), source, s);
 }
 

@@ -372,6 +372,14 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
   __syncthreads();
 }
 
+// A position slot holds `key`'s table slot.  Any entry whose key equals the window's is a copy
+// of that key's slot, whichever position it was loaded from; entries of windows the index does
+// not hold keep the 0xFF preset, key ~0, which no query window has (query k <= 31,
+// src/kmer_hash.c:1163-1164).
+__device__ __forceinline__ bool ps_match(uint4 v, uint64_t key) {
+  return (((uint64_t)v.y << 32) | v.x) == key;
+}
+
 // count / aux of tile window w with key `key` (a valid window): the anchor's own probe or a
 // verified diagonal prediction; false = the window still needs its table probe.  (Written
 // without early returns around table_find: the probe loop keeps two windows' table probes in
@@ -392,7 +400,7 @@ __device__ __forceinline__ bool diag_window(int w, uint64_t key, const Slot* __r
       const int64_t pj = (int64_t)A.anc[la] + (w - la * DG_STRIDE);   // 1-based
       if (pj <= nA) {
         const uint4 v = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
-        if ((((uint64_t)v.y << 32) | v.x) == key) { count = v.z; aux = v.w; hit = true; }
+        if (ps_match(v, key)) { count = v.z; aux = v.w; hit = true; }
       }
     }
   }
@@ -417,13 +425,64 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   __syncthreads();
   if (DIAG) diag_anchors(st, o0, t_start, w1, L, kq, T, g, A);
   uint64_t rows = 0;
+#ifndef KMHG_DIAG_PRELOAD
+#define KMHG_DIAG_PRELOAD 1
+#endif
+#ifndef KMHG_PROBE_UNROLL
+#define KMHG_PROBE_UNROLL 2
+#endif
+  if (DIAG && KMHG_DIAG_PRELOAD) {
+    // Diagonal path: the WPT predicted position slots of this thread's windows are loaded
+    // first, all in flight at once (coalesced across the wave; a window without a prediction
+    // loads PS[0], one shared line, so every lane issues a static WPT loads), then resolved;
+    // windows whose prediction fails probe the table as below.  (The resolve-as-you-go loop
+    // kept at most two PS loads in flight per lane behind its branches.)
+    uint4 pv[WPT];
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+      const int w = j * BLOCK + threadIdx.x;
+      const int la = A.last[w / DG_STRIDE];
+      int64_t pj = la >= 0 ? (int64_t)A.anc[la] + (w - la * DG_STRIDE) : 1;
+      if (pj > nA || w % DG_STRIDE == 0) pj = 1;
+      pv[j] = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
+    }
+#pragma unroll                 // static indices into pv (a partial unroll put it in scratch)
+    for (int j = 0; j < WPT; ++j) {
+      const int w = j * BLOCK + threadIdx.x;
+      const int64_t s = t_start + w;
+      uint64_t key = 0;
+      uint32_t count = 0, aux = 0;
+      if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) {
+        bool hit;
+        if (w % DG_STRIDE == 0) {
+          const uint2 ai = A.info[w / DG_STRIDE];
+          count = ai.x; aux = ai.y;
+          hit = true;
+        } else {
+          hit = A.last[w / DG_STRIDE] >= 0 && ps_match(pv[j], key);
+          count = pv[j].z; aux = pv[j].w;
+        }
+        if (!hit) {
+          count = 0; aux = 0;
+#ifndef KMHG_NO_FIND4
+          table_find4(T, g, key, count, aux);
+#else
+          table_find(T, g, key, count, aux);
+#endif
+        }
+      }
+      if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
+      rows += count;
+    }
+    uint64_t tot;
+    block_excl_scan(rows, sh, tot);
+    if (threadIdx.x == 0) tile_rows[tile] = tot;
+    return;
+  }
   // (measured: issuing all WPT home-slot loads before resolving any cost occupancy -- 94
   // VGPRs, 5 waves/SIMD -- and ran 15 % slower than this two-deep loop; a per-lane state
   // machine walking two probe streams one slot per step ran 30 % slower, and compacting the
   // windows not resolved at their home slot into LDS queue rounds 40 % slower)
-#ifndef KMHG_PROBE_UNROLL
-#define KMHG_PROBE_UNROLL 2
-#endif
 #pragma unroll KMHG_PROBE_UNROLL
   for (int j = 0; j < WPT; ++j) {
     const int w = j * BLOCK + threadIdx.x;

@@ -270,3 +270,30 @@ def test_sh_spread_per_batch(gpu):
     qual = np.concatenate([q1, q2])
     uk, cnt = _oracle_counts(seq, qual, np.ones(len(seq), np.uint8), k, mq)
     assert np.array_equal(keys, uk) and np.array_equal(M[:, 0], cnt)
+
+
+def test_sh_padded_stream_edges(gpu):
+    """The iterator writes each read's k-mers into a range sized by its upper bound
+    (length - k + 1) and pads the rest with EMPTY_KEY, which the count-only build skips: a batch
+    with 90 % of its reads rejected by quality (mostly padding), and a batch with every window
+    rejected (no key at all), fresh and into an existing hash, against the oracle."""
+    torch = gpu
+    from kmer_hasher_amd import synth
+    k, mq = 25, 10
+    g = synth.iid(1_000_000, 101)
+    seq, qual = synth.reads(g, 30_000, 150, 102)
+    bad = qual.copy()
+    bad[np.arange(len(seq)) % 10 != 0] = ord("!")        # q = 0: every window rejected
+    ptr = _count_packed(torch, seq, bad, k, mq)
+    keys, M = _sorted_table(ptr)
+    uk, cnt = _oracle_counts(seq, bad, np.ones(len(seq), np.uint8), k, mq)
+    assert len(uk) > 0 and np.array_equal(keys, uk) and np.array_equal(M[:, 0], cnt)
+    est, sp, path = _last_batch(ptr)
+    assert path == 1 and abs(est - len(uk)) < 0.25 * len(uk), (est, len(uk))
+    # every window rejected: nothing counted, fresh or into the existing hash
+    none = np.full_like(qual, ord("!"))
+    empty = _count_packed(torch, seq, none, k, mq)
+    assert empty.info().n_kmers == 0
+    _count_packed(torch, seq, none, k, mq, ptr)
+    keys2, M2 = _sorted_table(ptr)
+    assert np.array_equal(keys2, keys) and np.array_equal(M2, M)
