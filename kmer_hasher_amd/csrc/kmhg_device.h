@@ -336,6 +336,58 @@ __device__ __forceinline__ uint32_t table_find4(const Slot* __restrict__ T, Geom
   }
 }
 
+// Slot tags, the diagonal query path's filter for windows that miss (built with the position
+// slots, kmhg_kernels.hip k_pos_slots): one byte per table slot, 0 for an empty slot, else the
+// low byte of the key's hash (the bucket takes the high word, the home bits 16..31), 0 -> 1.
+__device__ __forceinline__ uint8_t slot_tag(uint64_t h) {
+  const uint32_t t = (uint32_t)h & 0xFFu;
+  return (uint8_t)(t ? t : 1u);
+}
+// bit q (q < 8) set iff byte q of v is 0, exact for the lowest zero byte (bits above it may be
+// spurious); the caller keeps only bits below the first one
+__device__ __forceinline__ uint32_t zero_bytes8(uint64_t v) {
+  const uint64_t x = (v - 0x0101010101010101ull) & ~v & 0x8080808080808080ull;
+  return (uint32_t)(((x >> 7) * 0x0102040810204080ull) >> 56);
+}
+
+// table_find through the tags: a miss reads the 16 tags of its home's aligned group (one 16-B
+// load from an array 1/16 the table's size) and usually stops at an empty tag without touching
+// the table; the table is read only at slots whose tag equals the key's.  Needs g.capb % 16 == 0.
+__device__ __forceinline__ uint32_t table_find_tag(const Slot* __restrict__ T,
+                                                   const uint8_t* __restrict__ TG, Geom g,
+                                                   uint64_t key, uint32_t& count, uint32_t& aux) {
+  count = 0; aux = 0;
+  if (key == EMPTY_KEY) return table_find(T, g, key, count, aux);
+  const uint64_t h = mix64(key);
+  const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
+  const uint32_t j = local_home(h, g.capb);
+  const uint64_t tt = 0x0101010101010101ull * slot_tag(h);
+  uint32_t grp = j & ~15u, off = j & 15u;
+  for (uint32_t n = 0; n <= g.capb / 16; ++n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(TG + b0 + grp);
+    uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
+    // bytes before the home read as 0xFF: no zero there, so no borrow into the bytes above
+    const uint64_t lo0 = off >= 8 ? ~0ull : (off ? ((1ull << (8 * off)) - 1) : 0ull);
+    const uint64_t lo1 = off > 8 ? ((1ull << (8 * (off - 8))) - 1) : 0ull;
+    w0 |= lo0; w1 |= lo1;
+    const uint32_t zm = zero_bytes8(w0) | (zero_bytes8(w1) << 8);
+    const uint32_t below = zm ? (1u << (__ffs(zm) - 1)) - 1 : 0xFFFFu;
+    uint32_t cand = (zero_bytes8(w0 ^ tt) | (zero_bytes8(w1 ^ tt) << 8)) & below & (0xFFFFu << off);
+    while (cand) {                              // tag hits: the full key decides
+      const uint32_t q = __ffs(cand) - 1;
+      cand &= cand - 1;
+      const uint64_t i = b0 + grp + q;
+      const uint4 sv = *reinterpret_cast<const uint4*>(&T[i]);
+      if ((((uint64_t)sv.y << 32) | sv.x) == key) { count = sv.z; aux = sv.w; return (uint32_t)i; }
+    }
+    if (zm) return NONE;
+    grp += 16;
+    if (grp >= g.capb) grp = 0;
+    off = 0;
+  }
+  return NONE;
+}
+
 // Wave-aggregated atomicAdd on a per-slot u32 counter.  Lanes that hold the same slot are
 // grouped behind the first active lane (readfirstlane + ballot); one atomic per group.  The
 // loop stops as soon as a group of one appears (i.i.d. data: one iteration), leaving the rest

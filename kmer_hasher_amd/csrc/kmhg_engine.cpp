@@ -485,12 +485,13 @@ struct kmhg_index {
   // seq.kmer.pos diagonal path: the slot of every indexed window by position (built on the
   // first eligible query, kept with the index)
   DBuf<Slot> pslot;
+  DBuf<uint8_t> ptag;             // one tag byte per table slot (0 = empty), built with pslot
   bool ps_ready = false, ps_failed = false;
   std::mutex ps_mu;
   // stream-ordered release of everything the index holds (work queued on `s` may still read it)
   void bind_all(hipStream_t s) {
     table.bind(s); positions.bind(s); ckeys.bind(s); slot_row.bind(s); row_slot.bind(s);
-    pslot.bind(s);
+    pslot.bind(s); ptag.bind(s);
     canon.perm.bind(s); canon.canon_off.bind(s); canon.pkeys.bind(s); canon.pair_off.bind(s);
     canon.rinfo.bind(s);
   }
@@ -824,6 +825,12 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   return idx.release();
 }
 
+// the tag filter of the diagonal query path (per call: tests switch it)
+bool tags_on() {
+  const char* e = std::getenv("KMHG_QUERY_TAGS");
+  return !(e && e[0] == '0');
+}
+
 int build_version() {   // read per build so tests can exercise the fallback (KMHG_BUILD=v1)
   const char* e = std::getenv("KMHG_BUILD");
   return (e && std::string(e) == "v1") ? 1 : 2;
@@ -903,16 +910,20 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
     if (!idx->ps_ready && !idx->ps_failed) {
       try {
         idx->pslot.reset((size_t)nA);
+        idx->ptag.reset(idx->slots() + 32);  // + the 32-B span the last probe group reads
       } catch (const Error& e) {           // no room for 16 B per window: table probes only
         if (e.code != KMHG_ENOMEM) throw;
         idx->ps_failed = true;
+        idx->pslot.free();
         (void)hipGetLastError();
       }
       if (!idx->ps_failed) {
         idx->pslot.bind(s);
+        idx->ptag.bind(s);
         HIPC(hipMemsetAsync(idx->pslot.p, 0xFF, (size_t)nA * sizeof(Slot), s));
         LAUNCH("k_pos_slots", s, launch_pos_slots(idx->table.p, idx->slots(),
-                                                  idx->positions.p, idx->pslot.p, s));
+                                                  idx->positions.p, idx->pslot.p,
+                                                  idx->ptag.p, s));
         // once per index: later queries may run on other streams
         HIPC(hipStreamSynchronize(s));
         idx->ps_ready = true;
@@ -945,7 +956,8 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   uint64_t* total = &hrec.meta->n_kmers;
   LAUNCH("k_query_probe", s,
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
-                            tile_row0, s, diag ? idx->pslot.p : nullptr, nA));
+                            tile_row0, s, diag ? idx->pslot.p : nullptr, nA,
+                            diag && tags_on() ? idx->ptag.p : nullptr));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, tiles.p + nt, s));
   if (classic) {
     LAUNCH("k_query_emit", s,

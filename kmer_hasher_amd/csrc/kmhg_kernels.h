@@ -50,13 +50,16 @@ void launch_sort_small(const uint32_t* small_ids, const BuildMeta* meta, const u
 void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const uint32_t* counts,
                        const uint32_t* offsets, int32_t* positions, int32_t* tmp, hipStream_t s);
 void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, hipStream_t s);
-// PS (optional, the diagonal path): position-indexed slots of the index's nA windows
+// PS (optional, the diagonal path): position-indexed slots of the index's nA windows; TG
+// (optional, with PS, g.capb % 16 == 0): slot tags for the windows the path does not resolve
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
-                        hipStream_t s, const Slot* PS = nullptr, int64_t nA = 0);
-// PS[s] = the slot of the index's window s (PS preset to 0xFF bytes: EMPTY key elsewhere)
+                        hipStream_t s, const Slot* PS = nullptr, int64_t nA = 0,
+                        const uint8_t* TG = nullptr);
+// PS[s] = the slot of the index's window s (PS preset to 0xFF bytes: EMPTY key elsewhere);
+// TG[i] = slot_tag of slot i (0 empty), all nslots slots
 void launch_pos_slots(const Slot* T, uint64_t nslots, const int32_t* positions, Slot* PS,
-                      hipStream_t s);
+                      uint8_t* TG, hipStream_t s);
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
 // exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
 // reduce-then-scan with `scratch` = scan_u64_scratch(n) u64

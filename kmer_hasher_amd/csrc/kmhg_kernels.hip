@@ -276,7 +276,7 @@ k_inline_singles(Slot* __restrict__ T, uint64_t nslots, const int32_t* __restric
 constexpr uint32_t PS_LANE = 16;
 __global__ void __launch_bounds__(BLOCK)
 k_pos_slots(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions,
-            Slot* __restrict__ PS) {
+            Slot* __restrict__ PS, uint8_t* __restrict__ TG) {
   const int lane = lane_id();
   for (uint64_t i0 = (uint64_t)blockIdx.x * BLOCK; i0 < nslots; i0 += (uint64_t)gridDim.x * BLOCK) {
     const uint64_t i = i0 + threadIdx.x;
@@ -287,6 +287,7 @@ k_pos_slots(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restri
       sl.key = ((uint64_t)v.y << 32) | v.x; sl.count = v.z; sl.aux = v.w;
     }
     const uint4 out = make_uint4((uint32_t)sl.key, (uint32_t)(sl.key >> 32), sl.count, sl.aux);
+    if (i < nslots) TG[i] = sl.key == EMPTY_KEY ? (uint8_t)0 : slot_tag(mix64(sl.key));
     if (sl.count == 1) {
       *reinterpret_cast<uint4*>(&PS[sl.aux - 1]) = out;
     } else if (sl.count > 1 && sl.count <= PS_LANE) {
@@ -306,11 +307,11 @@ k_pos_slots(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restri
 }
 
 void launch_pos_slots(const Slot* T, uint64_t nslots, const int32_t* positions, Slot* PS,
-                      hipStream_t s) {
+                      uint8_t* TG, hipStream_t s) {
   uint64_t g = (nslots + BLOCK - 1) / BLOCK;
   if (g > 65536) g = 65536;
   hipLaunchKernelGGL(k_pos_slots, dim3((unsigned)(g ? g : 1)), dim3(BLOCK), 0, s, T, nslots,
-                     positions, PS);
+                     positions, PS, TG);
 }
 
 // Q_probe: per query window (query k) probe the table; qinfo[s] = {count, start}; per-tile row
@@ -411,7 +412,8 @@ template <bool DIAG>
 __global__ void __launch_bounds__(BLOCK)
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
-              uint64_t* __restrict__ tile_rows, const Slot* __restrict__ PS, int64_t nA) {
+              uint64_t* __restrict__ tile_rows, const Slot* __restrict__ PS, int64_t nA,
+              const uint8_t* __restrict__ TG) {
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
   __shared__ DiagAnchors A;
@@ -464,10 +466,12 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
         }
         if (!hit) {
           count = 0; aux = 0;
+          if (TG) table_find_tag(T, TG, g, key, count, aux);   // mostly misses here
+          else
 #ifndef KMHG_NO_FIND4
-          table_find4(T, g, key, count, aux);
+            table_find4(T, g, key, count, aux);
 #else
-          table_find(T, g, key, count, aux);
+            table_find(T, g, key, count, aux);
 #endif
         }
       }
@@ -1063,14 +1067,15 @@ void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, h
 }
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
-                        hipStream_t s, const Slot* PS, int64_t nA) {
+                        hipStream_t s, const Slot* PS, int64_t nA, const uint8_t* TG) {
   uint32_t nt = grid_for(w1 - w0, TILE);
+  if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
   if (PS)
     hipLaunchKernelGGL(k_query_probe<true>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo,
-                       w0, w1, aligned ? 1 : 0, tile_rows, PS, nA);
+                       w0, w1, aligned ? 1 : 0, tile_rows, PS, nA, TG);
   else
     hipLaunchKernelGGL(k_query_probe<false>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo,
-                       w0, w1, aligned ? 1 : 0, tile_rows, nullptr, (int64_t)0);
+                       w0, w1, aligned ? 1 : 0, tile_rows, nullptr, (int64_t)0, nullptr);
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);

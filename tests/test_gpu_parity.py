@@ -238,7 +238,7 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds):
         _check_against_oracle("".join(rng.choice(list("ACGT"), L)), 31, pairs=False)
 
 
-@pytest.mark.parametrize("path", ["fused", "classic", "nodiag"])
+@pytest.mark.parametrize("path", ["fused", "classic", "nodiag", "notags"])
 def test_query_paths_vs_oracle(gpu, monkeypatch, path):
     """seq.kmer.pos through the probe / scan / emit kernels (default; also the fused path's redo
     when a query has more rows than the guessed capacity) and through the one-pass probe +
@@ -249,6 +249,8 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
     from kmer_hasher_amd import synth
     if path == "nodiag":
         monkeypatch.setenv("KMHG_QUERY_DIAG", "0")
+    elif path == "notags":
+        monkeypatch.setenv("KMHG_QUERY_TAGS", "0")
     else:
         monkeypatch.setenv("KMHG_QUERY", path)
     make, kpos, sqk = _api()
@@ -283,16 +285,19 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
     ptr.free()
 
 
-def test_query_diagonal_path_vs_oracle(gpu):
+@pytest.mark.parametrize("tags", ["1", "0"])
+def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags):
     """The diagonal path of k_query_probe (anchors every 64th window; later windows follow the
     last anchor with a unique hit and take a position-indexed slot only when its key equals
-    theirs) against the oracle: the index's own sequence, a related sequence (1 % SNVs,
+    theirs; the rest probe through the slot tags, or the table alone with KMHG_QUERY_TAGS=0)
+    against the oracle: the index's own sequence, a related sequence (1 % SNVs,
     inversions, translocations, N-runs), its reverse complement, an unrelated one, repeat-rich
     input (multi-hit anchors predict nothing; keys with > 16 positions get their position slots
     from a whole wave), shards of the window range that start inside a diagonal, and a query k
     different from the index k (path off)."""
     import torch
     from kmer_hasher_amd import device as D, synth
+    monkeypatch.setenv("KMHG_QUERY_TAGS", tags)
     make, kpos, sqk = _api()
     A = synth.add_n_runs(synth.iid(300_000, 61), 0.0005, 62, max_run=40)
     B = synth.derived(A, 63)

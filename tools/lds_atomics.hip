@@ -51,6 +51,17 @@ __global__ void __launch_bounds__(256) k(uint64_t* out, uint32_t seed) {
       acc += atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)r);
     } else if (MODE == 5) {
       acc += atomicAdd(&cc[j].x, 1u);
+    } else if (MODE == 6) {            // CAS rtn fails, only 8 lanes of each wave active
+      if ((threadIdx.x & 63) < 8)
+        acc += atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)r);
+    } else if (MODE == 7) {            // CAS rtn fails, one lane per wave
+      if ((threadIdx.x & 63) == 0)
+        acc += atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)r);
+    } else if (MODE == 9) {            // 32-bit CAS rtn fails, 64 lanes
+      acc += atomicCAS(&cc[j].y, 0xFFFFFFFFu, r);
+    } else if (MODE == 8) {            // CAS rtn fails, 32 lanes
+      if ((threadIdx.x & 63) < 32)
+        acc += atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)r);
     }
   }
   __syncthreads();
@@ -92,6 +103,49 @@ __global__ void __launch_bounds__(256) kpa(uint64_t* out, uint32_t seed, int rep
         }
         slot[c] = j;
         atomicAdd(&cc[j].x, 1u);
+      }
+    } else if (VARIANT == 2) {
+      uint32_t hm[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hm[q] = homek(mixk(kv[q]));
+      int c = 0;
+      uint64_t kk = kv[0];
+      uint32_t j = hm[0];
+      bool live = true;
+      while (live) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kk);
+        if (prev == ~0ull || prev == kk) {
+          atomicAdd(&cc[j].x, 1u);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) if (q == c) slot[q] = j;
+          if (++c == 4) live = false;
+          else {
+#pragma unroll
+            for (int q = 1; q < 4; ++q) if (q == c) { kk = kv[q]; j = hm[q]; }
+          }
+        } else if (++j == CAP) j = 0;
+      }
+    } else if (VARIANT == 3) {
+      // home round for every element, then the failures alone, element by element
+      uint32_t hm[4];
+      bool pend[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hm[q] = homek(mixk(kv[q]));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&key[hm[q]], ~0ull, (unsigned long long)kv[q]);
+        pend[q] = !(prev == ~0ull || prev == kv[q]);
+        if (!pend[q]) { slot[q] = hm[q]; atomicAdd(&cc[hm[q]].x, 1u); }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!__any(pend[q])) continue;
+        uint32_t j = hm[q];
+        while (pend[q]) {
+          if (++j == CAP) j = 0;
+          const uint64_t prev = atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kv[q]);
+          if (prev == ~0ull || prev == kv[q]) { pend[q] = false; slot[q] = j; atomicAdd(&cc[j].x, 1u); }
+        }
       }
     } else {
       int c = 0;
@@ -172,5 +226,11 @@ int main() {
   run<3>("CAS64 chain (1 WG/CU)", 1);
   run_pa<0>("pass A, element by element");
   run_pa<1>("pass A, per-lane state machine");
+  run_pa<2>("pass A, state machine, homes first");
+  run_pa<3>("pass A, home round then failures");
+  run<6>("CAS64 rtn fails, 8 lanes", 6);
+  run<7>("CAS64 rtn fails, 1 lane", 6);
+  run<8>("CAS64 rtn fails, 32 lanes", 6);
+  run<9>("CAS32 rtn fails, 64 lanes", 6);
   return 0;
 }
