@@ -939,7 +939,8 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
     LAUNCH("k_query_fused", s,
            launch_query_fused(d_seq, L, kq, idx->table.p, idx->geom, w0, w1, aligned,
                               idx->positions.p, status.p, q->rows.p, cap, s,
-                              diag ? idx->pslot.p : nullptr, nA));
+                              diag ? idx->pslot.p : nullptr, nA,
+                              diag && tags_on() ? idx->ptag.p : nullptr));
     HIPC(hipMemcpyAsync(&H, status.p + nt - 1, sizeof(H), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     H &= (1ull << 62) - 1;                       // LB_MASK: the last tile's inclusive prefix

@@ -75,7 +75,8 @@ void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
 void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
                         int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
                         int2* out, uint64_t cap, hipStream_t s,
-                        const Slot* PS = nullptr, int64_t nA = 0);
+                        const Slot* PS = nullptr, int64_t nA = 0,
+                        const uint8_t* TG = nullptr);
 // F = L entries {slot, count} preset to slot NONE
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s);

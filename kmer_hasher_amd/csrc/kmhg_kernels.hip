@@ -381,31 +381,58 @@ __device__ __forceinline__ bool ps_match(uint4 v, uint64_t key) {
   return (((uint64_t)v.y << 32) | v.x) == key;
 }
 
-// count / aux of tile window w with key `key` (a valid window): the anchor's own probe or a
-// verified diagonal prediction; false = the window still needs its table probe.  (Written
-// without early returns around table_find: the probe loop keeps two windows' table probes in
-// flight only when the probe stays a straight-line call -- an early-return helper around it ran
-// the table-only path 0.31 -> 0.44 ms.)
-__device__ __forceinline__ bool diag_window(int w, uint64_t key, const Slot* __restrict__ PS,
-                                            int64_t nA, const DiagAnchors& A, uint32_t& count,
-                                            uint32_t& aux) {
-  const int a = w / DG_STRIDE;
-  bool hit = false;
-  if (w % DG_STRIDE == 0) {
-    const uint2 ai = A.info[a];
-    count = ai.x; aux = ai.y;
-    hit = true;
-  } else {
-    const int la = A.last[a];
-    if (la >= 0) {
-      const int64_t pj = (int64_t)A.anc[la] + (w - la * DG_STRIDE);   // 1-based
-      if (pj <= nA) {
-        const uint4 v = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
-        if (ps_match(v, key)) { count = v.z; aux = v.w; hit = true; }
+// The diagonal path of a staged tile, every lane's WPT windows: the predicted position slots
+// are loaded first, all in flight at once (coalesced across the wave; a window without a
+// prediction loads PS[0], one shared line, so every lane issues a static WPT loads), then
+// resolved; windows whose prediction fails probe through the slot tags (TG) or the table.  (The
+// resolve-as-you-go loop kept at most two PS loads in flight per lane behind its branches.)
+// `out(w, s, count, aux)` receives every window of the tile, s = t_start + w (s >= w1: none).
+template <class ST, class Out>
+__device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_start, int64_t w0,
+                                             int64_t w1, int64_t L, int kq,
+                                             const Slot* __restrict__ T, Geom g,
+                                             const Slot* __restrict__ PS, int64_t nA,
+                                             const uint8_t* __restrict__ TG,
+                                             const DiagAnchors& A, Out out) {
+  (void)w0;
+  uint4 pv[WPT];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const int w = j * BLOCK + threadIdx.x;
+    const int la = A.last[w / DG_STRIDE];
+    int64_t pj = la >= 0 ? (int64_t)A.anc[la] + (w - la * DG_STRIDE) : 1;
+    if (pj > nA || w % DG_STRIDE == 0) pj = 1;
+    pv[j] = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
+  }
+#pragma unroll                 // static indices into pv (a partial unroll put it in scratch)
+  for (int j = 0; j < WPT; ++j) {
+    const int w = j * BLOCK + threadIdx.x;
+    const int64_t s = t_start + w;
+    uint64_t key = 0;
+    uint32_t count = 0, aux = 0;
+    if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) {
+      bool hit;
+      if (w % DG_STRIDE == 0) {
+        const uint2 ai = A.info[w / DG_STRIDE];
+        count = ai.x; aux = ai.y;
+        hit = true;
+      } else {
+        hit = A.last[w / DG_STRIDE] >= 0 && ps_match(pv[j], key);
+        count = pv[j].z; aux = pv[j].w;
+      }
+      if (!hit) {
+        count = 0; aux = 0;
+        if (TG) table_find_tag(T, TG, g, key, count, aux);   // mostly misses here
+        else
+#ifndef KMHG_NO_FIND4
+          table_find4(T, g, key, count, aux);
+#else
+          table_find(T, g, key, count, aux);
+#endif
       }
     }
+    out(w, s, count, aux);
   }
-  return hit;
 }
 
 template <bool DIAG>
@@ -427,57 +454,15 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   __syncthreads();
   if (DIAG) diag_anchors(st, o0, t_start, w1, L, kq, T, g, A);
   uint64_t rows = 0;
-#ifndef KMHG_DIAG_PRELOAD
-#define KMHG_DIAG_PRELOAD 1
-#endif
 #ifndef KMHG_PROBE_UNROLL
 #define KMHG_PROBE_UNROLL 2
 #endif
-  if (DIAG && KMHG_DIAG_PRELOAD) {
-    // Diagonal path: the WPT predicted position slots of this thread's windows are loaded
-    // first, all in flight at once (coalesced across the wave; a window without a prediction
-    // loads PS[0], one shared line, so every lane issues a static WPT loads), then resolved;
-    // windows whose prediction fails probe the table as below.  (The resolve-as-you-go loop
-    // kept at most two PS loads in flight per lane behind its branches.)
-    uint4 pv[WPT];
-#pragma unroll
-    for (int j = 0; j < WPT; ++j) {
-      const int w = j * BLOCK + threadIdx.x;
-      const int la = A.last[w / DG_STRIDE];
-      int64_t pj = la >= 0 ? (int64_t)A.anc[la] + (w - la * DG_STRIDE) : 1;
-      if (pj > nA || w % DG_STRIDE == 0) pj = 1;
-      pv[j] = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
-    }
-#pragma unroll                 // static indices into pv (a partial unroll put it in scratch)
-    for (int j = 0; j < WPT; ++j) {
-      const int w = j * BLOCK + threadIdx.x;
-      const int64_t s = t_start + w;
-      uint64_t key = 0;
-      uint32_t count = 0, aux = 0;
-      if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) {
-        bool hit;
-        if (w % DG_STRIDE == 0) {
-          const uint2 ai = A.info[w / DG_STRIDE];
-          count = ai.x; aux = ai.y;
-          hit = true;
-        } else {
-          hit = A.last[w / DG_STRIDE] >= 0 && ps_match(pv[j], key);
-          count = pv[j].z; aux = pv[j].w;
-        }
-        if (!hit) {
-          count = 0; aux = 0;
-          if (TG) table_find_tag(T, TG, g, key, count, aux);   // mostly misses here
-          else
-#ifndef KMHG_NO_FIND4
-            table_find4(T, g, key, count, aux);
-#else
-            table_find(T, g, key, count, aux);
-#endif
-        }
-      }
-      if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
-      rows += count;
-    }
+  if (DIAG) {
+    diag_resolve(st, o0, t_start, w0, w1, L, kq, T, g, PS, nA, TG, A,
+                 [&](int w, int64_t s, uint32_t count, uint32_t aux) {
+                   if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
+                   rows += count;
+                 });
     uint64_t tot;
     block_excl_scan(rows, sh, tot);
     if (threadIdx.x == 0) tile_rows[tile] = tot;
@@ -493,14 +478,7 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
-    if (s < w1 && window_key(st, o0 + w, s, L, kq, key) &&
-        !(DIAG && diag_window(w, key, PS, nA, A, count, aux))) {
-#ifndef KMHG_NO_FIND4
-      if (DIAG) table_find4(T, g, key, count, aux);
-      else
-#endif
-        table_find(T, g, key, count, aux);
-    }
+    if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
     // {count, position} for a key seen once, {count, first index} otherwise
     if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
     rows += count;
@@ -655,7 +633,7 @@ __global__ void __launch_bounds__(BLOCK)
 k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, int64_t w0, int64_t w1, int aligned, const int32_t* __restrict__ positions,
               uint64_t* __restrict__ status, uint32_t nt, int2* __restrict__ out, uint64_t cap,
-              const Slot* __restrict__ PS, int64_t nA) {
+              const Slot* __restrict__ PS, int64_t nA, const uint8_t* __restrict__ TG) {
   // LDS ~19 KB -> 8 workgroups per CU, as Q_probe: per-window {count, first} records (the
   // registers would hold them only with all WPT probes unrolled: 100 VGPRs, half the waves), and
   // the stage shares its bytes with the emit's heavy-window list
@@ -677,17 +655,23 @@ k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   __syncthreads();
   if (PS) diag_anchors(u.st, o0, t_start, w1, L, kq, T, g, A);
   uint64_t rows = 0;
+  if (PS) {
+    diag_resolve(u.st, o0, t_start, w0, w1, L, kq, T, g, PS, nA, TG, A,
+                 [&](int w, int64_t, uint32_t count, uint32_t aux) {
+                   qi[w] = make_uint2(count, count == 1 ? aux : aux - count);
+                   rows += count;
+                 });
+  } else {
 #pragma unroll KMHG_PROBE_UNROLL
-  for (int j = 0; j < WPT; ++j) {
-    const int w = j * BLOCK + threadIdx.x;
-    const int64_t s = t_start + w;
-    uint64_t key = 0;
-    uint32_t count = 0, aux = 0;
-    if (s < w1 && window_key(u.st, o0 + w, s, L, kq, key) &&
-        !(PS && diag_window(w, key, PS, nA, A, count, aux)))
-      table_find(T, g, key, count, aux);
-    qi[w] = make_uint2(count, count == 1 ? aux : aux - count);   // position, or list start
-    rows += count;
+    for (int j = 0; j < WPT; ++j) {
+      const int w = j * BLOCK + threadIdx.x;
+      const int64_t s = t_start + w;
+      uint64_t key = 0;
+      uint32_t count = 0, aux = 0;
+      if (s < w1 && window_key(u.st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
+      qi[w] = make_uint2(count, count == 1 ? aux : aux - count);   // position, or list start
+      rows += count;
+    }
   }
   uint64_t agg;
   block_excl_scan(rows, sh, agg);              // (its barriers also retire the stage reads)
@@ -1100,10 +1084,11 @@ void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
 void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
                         int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
                         int2* out, uint64_t cap, hipStream_t s,
-                        const Slot* PS, int64_t nA) {
+                        const Slot* PS, int64_t nA, const uint8_t* TG) {
   const uint32_t nt = grid_for(w1 - w0, TILE);
+  if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
   hipLaunchKernelGGL(k_query_fused, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, w0, w1,
-                     aligned ? 1 : 0, positions, status, nt, out, cap, PS, nA);
+                     aligned ? 1 : 0, positions, status, nt, out, cap, PS, nA, TG);
 }
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s) {
