@@ -151,6 +151,17 @@ class DevicePool {
       live_.erase(it);
     }
   }
+  // blocks no queued work uses any more (their stream was synchronized)
+  void release_now(const std::vector<void*>& ps) {
+    std::lock_guard<std::mutex> g(mu_);
+    for (void* p : ps) {
+      auto it = live_.find(p);
+      if (it == live_.end()) continue;
+      free_[it->second].push_back(p);
+      cached_ += it->second.second;
+      live_.erase(it);
+    }
+  }
   void release_one(void* p, hipStream_t stream, bool ordered) {
     if (!p) return;
     hipEvent_t ev = nullptr;
@@ -239,12 +250,16 @@ struct ReleaseGroup {
   hipStream_t s;
   std::vector<void*> ps;
   ReleaseGroup* prev;
+  // set after a synchronize of `s` with no launch behind it: the blocks go straight back to the
+  // pool, no event (a synchronous call's last step)
+  bool synced = false;
   explicit ReleaseGroup(hipStream_t stream) : s(stream), prev(tl_release_group) {
     tl_release_group = this;
   }
   ~ReleaseGroup() {
     tl_release_group = prev;
-    DevicePool::get().release_batch(ps, s);
+    if (synced) DevicePool::get().release_now(ps);
+    else DevicePool::get().release_batch(ps, s);
   }
   ReleaseGroup(const ReleaseGroup&) = delete;
   ReleaseGroup& operator=(const ReleaseGroup&) = delete;
@@ -967,7 +982,10 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
     HIPC(hipStreamSynchronize(s));
     H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
     q->H = (int64_t)H;
-    if (H <= cap) return q.release();
+    if (H <= cap) {
+      rg.synced = true;                          // nothing queued behind the synchronize
+      return q.release();
+    }
   } else {
     HIPC(hipStreamSynchronize(s));
     H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
@@ -2321,6 +2339,7 @@ int kmhg_query_free(kmhg_query* q) {
     if (!q) return;
     DeviceGuard g(q->device);
     HIPC(hipStreamSynchronize(q->stream));   // the caller keeps its stream alive until here
+    q->rows.ordered = false;                 // its stream is idle: straight back to the pool
     delete q;
   });
 }
