@@ -237,15 +237,18 @@ int kmhg_sh_spectrum(kmhg_index *sh, int max_count, const int32_t *comb,
 int kmhg_counts_export(kmhg_index *idx, uint64_t *keys, int32_t *counts);
 
 /* Index replication for the multi-GPU query (the index is broadcast once over RCCL/xGMI by the
- * caller): the device image is the hash table (16-B slots {key, count, end}) + the positions;
- * export copies it into caller device buffers, import rebuilds an index on the current device. */
+ * caller): the device image is the hash table (16-B slots {key, count, end}) + the positions +
+ * (codes_bytes > 0) the index sequence's 2-bit code words and N flags that the diagonal
+ * query path verifies against (0.5 B per window; NULL / 0 = table probes only); export copies
+ * it into caller device buffers, import rebuilds an index on the current device. */
 typedef struct {
-  int64_t table_bytes, positions_bytes;
+  int64_t table_bytes, positions_bytes, codes_bytes;
 } kmhg_image_sizes;
 int kmhg_image_sizes_get(const kmhg_index *idx, kmhg_image_sizes *sz, int64_t header[8]);
-int kmhg_image_export(const kmhg_index *idx, void *d_table, void *d_positions, void *stream);
+int kmhg_image_export(const kmhg_index *idx, void *d_table, void *d_positions, void *d_codes,
+                      void *stream);
 int kmhg_image_import(const int64_t header[8], const void *d_table, const void *d_positions,
-                      void *stream, kmhg_index **out);
+                      const void *d_codes, void *stream, kmhg_index **out);
 
 /* Per-kernel HIP-event timing (KMHG_TIMING=1 also enables it).  The report is JSON:
  * {"kernel": [launches, total_ms], ...}; events are recorded on the kernels' own stream. */

@@ -33,7 +33,8 @@ class Info(C.Structure):
 
 
 class ImageSizes(C.Structure):
-    _fields_ = [("table_bytes", C.c_int64), ("positions_bytes", C.c_int64)]
+    _fields_ = [("table_bytes", C.c_int64), ("positions_bytes", C.c_int64),
+                ("codes_bytes", C.c_int64)]
 
 
 _LIB = None
@@ -83,8 +84,8 @@ _PROTOS = {
     "kmhg_sh_last_batch": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int),
                                      C.POINTER(C.c_int)]),
     "kmhg_image_sizes_get": (C.c_int, [vp, C.POINTER(ImageSizes), i64p]),
-    "kmhg_image_export": (C.c_int, [vp, vp, vp, vp]),
-    "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, C.POINTER(vp)]),
+    "kmhg_image_export": (C.c_int, [vp, vp, vp, vp, vp]),
+    "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, vp, C.POINTER(vp)]),
     "kmhg_timing_enable": (C.c_int, [C.c_int]),
     "kmhg_timing_select": (C.c_int, [C.c_char_p]),
     "kmhg_timing_reset": (C.c_int, []),

@@ -90,6 +90,24 @@ __device__ __forceinline__ uint64_t match_bits(uint32_t v, int nbits, bool act) 
   return m;
 }
 
+// The diagonal query path's copy of the index sequence (DiagBlock, kmhg_kernels.h), written by
+// V_hist0 from its stage: the tile's PTILE / 16 code words and N-flag words (the last tile also
+// the words its last windows reach into).  Thread t stores the word it packed itself (stage word
+// t), so no barrier is needed first.  ~0.4 B per window against the build's ~17.
+constexpr int DIAG_TW = PTILE / 16;             // code words per tile
+constexpr int DIAG_EXTRA = 3;                   // ... beyond the last tile's own
+static_assert(PSTAGE_W16 <= BLOCK && HALO % 16 == 0 && HALO / 16 + DIAG_TW + DIAG_EXTRA <= PSTAGE_W16,
+              "one stage word per thread; the last tile's extra words are staged");
+__device__ __forceinline__ void diag_words_out(const PStage& st, uint32_t tile, uint32_t ntiles,
+                                               uint32_t* __restrict__ code,
+                                               uint16_t* __restrict__ nbit) {
+  const int w = (int)threadIdx.x - HALO / 16;
+  if (w >= 0 && w < (tile + 1 == ntiles ? DIAG_TW + DIAG_EXTRA : DIAG_TW)) {
+    code[(uint64_t)tile * DIAG_TW + w] = st.code[threadIdx.x];
+    nbit[(uint64_t)tile * DIAG_TW + w] = (uint16_t)st.nbit[threadIdx.x];
+  }
+}
+
 // ---------------------------------------------------------------- V_hist0 (from the sequence)
 // LDS-staged 2-bit encode + N mask of every window of the tile (as K_insert) and the tile's
 // histogram of the first radix digit of the windows' buckets.  Nothing else is written: the
@@ -97,7 +115,8 @@ __device__ __forceinline__ uint64_t match_bits(uint32_t v, int nbits, bool act) 
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
            uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
-           uint32_t n_status, BuildMeta* __restrict__ meta) {
+           uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
+           uint16_t* __restrict__ nbit) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
   // zero the next scan's look-back words + ticket and the build meta (no memset launches)
@@ -113,6 +132,7 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
     __syncthreads();                           // previous tile's stage reads done
     stage_tile<true>(seq, L, tile0 - HALO, st, true);
     __syncthreads();
+    if (code) diag_words_out(st, tile, ch.ntiles, code, nbit);
 #pragma unroll 4
     for (int j = 0; j < PWPT; ++j) {
       const int w = j * BLOCK + threadIdx.x;
@@ -129,10 +149,17 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
 // walks virtual tiles w, w + G, ... (XCD-contiguous like the scatter) and loads the next tile's
 // chars into registers while it encodes the current one, so the load latency of all but the
 // first tile is hidden behind the encode.
+// CODES (position indices): the diagonal query path's code and N-flag words ride along, each
+// thread storing the words it packed right after the pack, BEFORE the next tile's loads are
+// issued, so the wait for those loads never waits on these stores.  (A/B, config 2: validity
+// ballots kept in the window loop and stored per tile cost 24 -> 30-41 us; a kernel of its own
+// 18 us; these stores ~1 us.)
+template <bool CODES>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
             uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
-            uint32_t n_status, BuildMeta* __restrict__ meta) {
+            uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
+            uint16_t* __restrict__ nbit) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
@@ -152,6 +179,7 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
     const uint32_t tile = tile_at(it);
     const int64_t tile0 = (int64_t)tile * PTILE;
     stage_pack(regs, st);                      // the previous tile's reads of st are done
+    if (CODES) diag_words_out(st, tile, ch.ntiles, code, nbit);
     if (it + 1 < n_iter)
       stage_load<PSTAGE_W16, true>(regs, seq, L, (int64_t)tile_at(it + 1) * PTILE - HALO, true);
     __syncthreads();
@@ -1482,20 +1510,26 @@ static unsigned scatter8_grid(const Chunks& ch) {
 
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
-                     BuildMeta* meta, hipStream_t s) {
+                     BuildMeta* meta, hipStream_t s, uint32_t* code, uint16_t* nbit) {
   static const int persist = [] {
     const char* e = std::getenv("KMHG_HIST0P");
     return (e && e[0] == '0') ? 0 : 1;
   }();
   if (ch.interleaved && persist) {
-    static const unsigned cap = resident_blocks((const void*)k_v2_hist0p);
-    const unsigned G = std::min<unsigned>(ch.ntiles, cap);
-    hipLaunchKernelGGL(k_v2_hist0p, dim3(G), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
-                       xcd_map(), scan_status, n_status, meta);
+    static const unsigned cap_c = resident_blocks((const void*)k_v2_hist0p<true>);
+    static const unsigned cap_n = resident_blocks((const void*)k_v2_hist0p<false>);
+    if (code && nbit)
+      hipLaunchKernelGGL(k_v2_hist0p<true>, dim3(std::min<unsigned>(ch.ntiles, cap_c)), dim3(BLOCK),
+                         0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status, n_status,
+                         meta, code, nbit);
+    else
+      hipLaunchKernelGGL(k_v2_hist0p<false>, dim3(std::min<unsigned>(ch.ntiles, cap_n)), dim3(BLOCK),
+                         0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status, n_status,
+                         meta, nullptr, nullptr);
     return;
   }
   hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
-                     xcd_map(), scan_status, n_status, meta);
+                     xcd_map(), scan_status, n_status, meta, code, nbit);
 }
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);

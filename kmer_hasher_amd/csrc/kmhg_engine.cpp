@@ -497,16 +497,22 @@ struct kmhg_index {
   int co_spread = 0, co_path = 0;
   DBuf<uint64_t> ckeys;
   DBuf<uint32_t> slot_row, row_slot;
-  // seq.kmer.pos diagonal path: the slot of every indexed window by position (built on the
-  // first eligible query, kept with the index)
-  DBuf<Slot> pslot;
-  DBuf<uint8_t> ptag;             // one tag byte per table slot (0 = empty), built with pslot
+  // seq.kmer.pos diagonal path (DiagIdx, kmhg_kernels.h): the index sequence's 2-bit code words
+  // and window bits, written by the build (V_hist0); the bits of repeated keys' windows are
+  // cleared and the slot tags built on the first eligible query (V_diag_prep)
+  DBuf<uint64_t> dcodes;
+  DBuf<uint8_t> ptag;             // one tag byte per table slot (0 = empty)
   bool ps_ready = false, ps_failed = false;
   std::mutex ps_mu;
+  DiagBlock diag_block_of() const { return diag_block(dcodes.p, L - k + 1); }
+  DiagIdx diag_view() const {
+    const DiagBlock b = diag_block_of();
+    return DiagIdx{b.code, b.uniq, L - k + 1};
+  }
   // stream-ordered release of everything the index holds (work queued on `s` may still read it)
   void bind_all(hipStream_t s) {
     table.bind(s); positions.bind(s); ckeys.bind(s); slot_row.bind(s); row_slot.bind(s);
-    pslot.bind(s); ptag.bind(s);
+    dcodes.bind(s); ptag.bind(s);
     canon.perm.bind(s); canon.canon_off.bind(s); canon.pkeys.bind(s); canon.pair_off.bind(s);
     canon.rinfo.bind(s);
   }
@@ -633,7 +639,8 @@ int co_spread_for(double distinct, uint64_t total) {
 // the first pass drops them, and the valid count comes from its scan.
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
                             const uint64_t* d_keys = nullptr, int64_t n_keys = 0,
-                            bool count_only = false, int co_spread = 1, bool skip_empty = false) {
+                            bool count_only = false, int co_spread = 1, bool skip_empty = false,
+                            bool codes = false) {
   ReleaseGroup rg(s);             // the scratch buffers below: one release event
   const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
@@ -744,9 +751,16 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(n_valid), (int)Nw, 1, s));
     HIPC(hipMemsetAsync(meta, 0, sizeof(BuildMeta), s));
   } else {
+    // a position index keeps its sequence's code words + window bits for the diagonal query
+    // path (code words + N flags, 0.5 B per window with the first query's bits; V_hist0 writes them)
+    DiagBlock db{nullptr, nullptr, nullptr};
+    if (codes) {
+      idx->dcodes.reset(diag_block_words(Nw));
+      db = idx->diag_block_of();
+    }
     LAUNCH("k_v2_hist0", s,
            launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, status, n_status,
-                           meta, s));
+                           meta, s, db.code, db.nbit));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     LAUNCH("k_v2_scatter_seq", s,
            launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, kA.p, pA.p,
@@ -852,8 +866,13 @@ int build_version() {   // read per build so tests can exercise the fallback (KM
 }
 
 // Returns a possibly pending index (partitioned build); finish_build() completes it.
-kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s) {
-  if (build_version() == 2) return build_device_v2(d_seq, L, k, s);
+// codes: keep the sequence's code words for the diagonal query path (position indices; a
+// count.kmers batch index has no use for them)
+kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s, bool codes = true) {
+  if (const char* e = std::getenv("KMHG_DIAG_CODES"))   // tests / A/B: no code block
+    if (e[0] == '0') codes = false;
+  if (build_version() == 2)
+    return build_device_v2(d_seq, L, k, s, nullptr, 0, false, 1, false, codes);
   return build_device_v1(d_seq, L, k, s);
 }
 
@@ -918,27 +937,25 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   const int64_t nA = idx->L - idx->k + 1;
   const char* de = std::getenv("KMHG_QUERY_DIAG");
   const bool diag_ok = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
-                       idx->U > 0;
+                       idx->U > 0 && idx->dcodes.p;
   bool diag = diag_ok;
   if (diag && !idx->ps_ready) {
     std::lock_guard<std::mutex> lk(idx->ps_mu);
     if (!idx->ps_ready && !idx->ps_failed) {
       try {
-        idx->pslot.reset((size_t)nA);
         idx->ptag.reset(idx->slots() + 32);  // + the 32-B span the last probe group reads
-      } catch (const Error& e) {           // no room for 16 B per window: table probes only
+      } catch (const Error& e) {           // no room for the tags: table probes only
         if (e.code != KMHG_ENOMEM) throw;
         idx->ps_failed = true;
-        idx->pslot.free();
         (void)hipGetLastError();
       }
       if (!idx->ps_failed) {
-        idx->pslot.bind(s);
         idx->ptag.bind(s);
-        HIPC(hipMemsetAsync(idx->pslot.p, 0xFF, (size_t)nA * sizeof(Slot), s));
-        LAUNCH("k_pos_slots", s, launch_pos_slots(idx->table.p, idx->slots(),
-                                                  idx->positions.p, idx->pslot.p,
-                                                  idx->ptag.p, s));
+        idx->dcodes.bind(s);
+        const DiagBlock db = idx->diag_block_of();
+        LAUNCH("k_diag_prep", s,
+               launch_diag_prep(db.nbit, idx->L, idx->k, db.uniq, idx->table.p, idx->slots(),
+                                idx->positions.p, idx->ptag.p, s));
         // once per index: later queries may run on other streams
         HIPC(hipStreamSynchronize(s));
         idx->ps_ready = true;
@@ -954,7 +971,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
     LAUNCH("k_query_fused", s,
            launch_query_fused(d_seq, L, kq, idx->table.p, idx->geom, w0, w1, aligned,
                               idx->positions.p, status.p, q->rows.p, cap, s,
-                              diag ? idx->pslot.p : nullptr, nA,
+                              diag ? idx->diag_view() : DiagIdx{nullptr, nullptr, 0},
                               diag && tags_on() ? idx->ptag.p : nullptr));
     HIPC(hipMemcpyAsync(&H, status.p + nt - 1, sizeof(H), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
@@ -972,7 +989,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   uint64_t* total = &hrec.meta->n_kmers;
   LAUNCH("k_query_probe", s,
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
-                            tile_row0, s, diag ? idx->pslot.p : nullptr, nA,
+                            tile_row0, s, diag ? idx->diag_view() : DiagIdx{nullptr, nullptr, 0},
                             diag && tags_on() ? idx->ptag.p : nullptr));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, tiles.p + nt, s));
   if (classic) {
@@ -1123,7 +1140,7 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
   idx->stream = s;
   const int k = idx->k;
   if (L <= k) return;
-  std::unique_ptr<kmhg_index> B(build_device(d_seq, L, k, s));
+  std::unique_ptr<kmhg_index> B(build_device(d_seq, L, k, s, false));
   Release rel{B.get(), s};
   finish_build(B.get());
   B->stream = s;
@@ -2353,6 +2370,7 @@ int kmhg_image_sizes_get(const kmhg_index* cidx, kmhg_image_sizes* sz, int64_t h
     finish_build(idx);
     sz->table_bytes = (int64_t)(idx->slots() * sizeof(Slot));
     sz->positions_bytes = (int64_t)(idx->N * 4);
+    sz->codes_bytes = idx->dcodes.p ? (int64_t)(diag_block_words(idx->L - idx->k + 1) * 8) : 0;
     header[0] = idx->k; header[1] = idx->L;
     header[2] = ((int64_t)idx->geom.nb << 32) | idx->geom.capb;
     header[3] = (int64_t)idx->U; header[4] = (int64_t)idx->N; header[5] = (int64_t)idx->P;
@@ -2360,7 +2378,8 @@ int kmhg_image_sizes_get(const kmhg_index* cidx, kmhg_image_sizes* sz, int64_t h
   });
 }
 
-int kmhg_image_export(const kmhg_index* cidx, void* d_table, void* d_positions, void* stream) {
+int kmhg_image_export(const kmhg_index* cidx, void* d_table, void* d_positions, void* d_codes,
+                      void* stream) {
   return guarded([&] {
     if (!cidx) fail(KMHG_EINVAL, "null index");
     kmhg_index* idx = const_cast<kmhg_index*>(cidx);
@@ -2372,12 +2391,15 @@ int kmhg_image_export(const kmhg_index* cidx, void* d_table, void* d_positions, 
                                      hipMemcpyDeviceToDevice, s));
     if (d_positions && idx->N)
       HIPC(hipMemcpyAsync(d_positions, idx->positions.p, idx->N * 4, hipMemcpyDeviceToDevice, s));
+    if (d_codes && idx->dcodes.p)
+      HIPC(hipMemcpyAsync(d_codes, idx->dcodes.p, diag_block_words(idx->L - idx->k + 1) * 8,
+                          hipMemcpyDeviceToDevice, s));
     HIPC(hipStreamSynchronize(s));
   });
 }
 
 int kmhg_image_import(const int64_t header[8], const void* d_table, const void* d_positions,
-                      void* stream, kmhg_index** out) {
+                      const void* d_codes, void* stream, kmhg_index** out) {
   return guarded([&] {
     if (!header || !out || header[7] != 0x6B6D6867) fail(KMHG_EINVAL, "bad index image header");
     auto idx = std::make_unique<kmhg_index>();
@@ -2394,6 +2416,11 @@ int kmhg_image_import(const int64_t header[8], const void* d_table, const void* 
                         hipMemcpyDeviceToDevice, s));
     if (idx->N)
       HIPC(hipMemcpyAsync(idx->positions.p, d_positions, idx->N * 4, hipMemcpyDeviceToDevice, s));
+    if (d_codes) {   // the diagonal query path's code block (its uniq bits are derived on first use)
+      const uint64_t w = diag_block_words(idx->L - idx->k + 1);
+      idx->dcodes.reset(w);
+      HIPC(hipMemcpyAsync(idx->dcodes.p, d_codes, w * 8, hipMemcpyDeviceToDevice, s));
+    }
     HIPC(hipStreamSynchronize(s));
     *out = idx.release();
   });

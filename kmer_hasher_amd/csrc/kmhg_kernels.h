@@ -50,16 +50,47 @@ void launch_sort_small(const uint32_t* small_ids, const BuildMeta* meta, const u
 void launch_sort_large(const uint32_t* large_ids, const BuildMeta* meta, const uint32_t* counts,
                        const uint32_t* offsets, int32_t* positions, int32_t* tmp, hipStream_t s);
 void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, hipStream_t s);
-// PS (optional, the diagonal path): position-indexed slots of the index's nA windows; TG
-// (optional, with PS, g.capb % 16 == 0): slot tags for the windows the path does not resolve
+// The diagonal query path's view of the INDEX sequence.  The build (V_hist0) keeps its 2-bit
+// codes, 16 chars per u32 MSB-first (char c in word c / 16, the LDS stage's format), and its N
+// flags, 16 chars per u16 (same order); the first diagonal query derives `uniq` from them and
+// the table (V_diag_valid, V_diag_prep): one bit per index window j (0-based, u32 word j / 32,
+// bit j % 32) set iff window j is indexed and its key occurs once -- so a set bit says "window
+// j's key has count 1 and its slot's aux is j + 1".
+struct DiagIdx {
+  const uint32_t* code;
+  const uint32_t* uniq;
+  int64_t nA;            // index windows (L - k + 1)
+};
+// ceil(Nw / PTILE) partition tiles; PTILE / 16 code (and N-flag) words each, + the words the
+// last windows reach into
+inline uint64_t diag_tiles(int64_t Nw) { return (uint64_t)((Nw + PTILE - 1) / PTILE); }
+inline uint64_t diag_code_words(int64_t Nw) { return diag_tiles(Nw) * (PTILE / 16) + 4; }
+inline uint64_t diag_uniq_words(int64_t Nw) { return diag_tiles(Nw) * (PTILE / 32); }   // u32
+// the block, in u64 words: code words (u32), N-flag words (u16), uniq words (u32)
+inline uint64_t diag_block_words(int64_t Nw) {
+  return diag_code_words(Nw) / 2 + diag_code_words(Nw) / 4 + diag_uniq_words(Nw) / 2;
+}
+struct DiagBlock {
+  uint32_t* code;
+  uint16_t* nbit;
+  uint32_t* uniq;
+};
+inline DiagBlock diag_block(uint64_t* p, int64_t Nw) {
+  uint32_t* c = reinterpret_cast<uint32_t*>(p);
+  const uint64_t cw = diag_code_words(Nw);
+  return DiagBlock{c, reinterpret_cast<uint16_t*>(c + cw), c + cw + cw / 2};
+}
+// X.code == nullptr: table probes only.  TG (optional, with X, g.capb % 16 == 0): slot tags for
+// the windows the diagonal path does not resolve
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
-                        hipStream_t s, const Slot* PS = nullptr, int64_t nA = 0,
+                        hipStream_t s, DiagIdx X = DiagIdx{nullptr, nullptr, 0},
                         const uint8_t* TG = nullptr);
-// PS[s] = the slot of the index's window s (PS preset to 0xFF bytes: EMPTY key elsewhere);
-// TG[i] = slot_tag of slot i (0 empty), all nslots slots
-void launch_pos_slots(const Slot* T, uint64_t nslots, const int32_t* positions, Slot* PS,
-                      uint8_t* TG, hipStream_t s);
+// Once per index, before its first diagonal query: `uniq` = the indexed windows (from the N
+// flags: the reference's window rule), then TG[i] = slot_tag of slot i (0 empty), all nslots
+// slots, and the `uniq` bits of every position of a key seen more than once cleared
+void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, const Slot* T,
+                      uint64_t nslots, const int32_t* positions, uint8_t* TG, hipStream_t s);
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
 // exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
 // reduce-then-scan with `scratch` = scan_u64_scratch(n) u64
@@ -75,8 +106,7 @@ void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
 void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
                         int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
                         int2* out, uint64_t cap, hipStream_t s,
-                        const Slot* PS = nullptr, int64_t nA = 0,
-                        const uint8_t* TG = nullptr);
+                        DiagIdx X = DiagIdx{nullptr, nullptr, 0}, const uint8_t* TG = nullptr);
 // F = L entries {slot, count} preset to slot NONE
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s);
@@ -129,9 +159,12 @@ struct Chunks {
 };
 Chunks make_chunks(uint32_t ntiles);
 // V_hist0 also zeroes the look-back words of the scan that follows (n_status u64) and `meta`
+// code / nbit (optional, position indices: the diagonal query path, DiagBlock): the sequence's
+// 2-bit code words and N-flag words
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
-                     BuildMeta* meta, hipStream_t s);
+                     BuildMeta* meta, hipStream_t s, uint32_t* code = nullptr,
+                     uint16_t* nbit = nullptr);
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
 // exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the histogram kernel

@@ -270,60 +270,92 @@ k_inline_singles(Slot* __restrict__ T, uint64_t nslots, const int32_t* __restric
 }
 
 // ================================================================== query kernels
-// Position-indexed slots (the diagonal path of Q_probe): PS[s] = the table slot of the index's
-// window s (0-based start), EMPTY key where the window is not indexed (PS preset to 0xFF).  One
-// thread per slot; a key with more than PS_LANE positions is written by the whole wave.
-constexpr uint32_t PS_LANE = 16;
+// V_diag_valid (once per index, before its first diagonal query): uniq word a = the indexed
+// windows among [32a, 32a + 32), from the N flags the build kept -- no N in [s, s + k), s < Nw,
+// and the end-drop rule of the last window (src/kmer_pos.c:81-83).  One
+// thread per word: u16 flag words 2a .. 2a + 3 hold chars [32a, 32a + 64), char 32a at bit 63.
 __global__ void __launch_bounds__(BLOCK)
-k_pos_slots(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions,
-            Slot* __restrict__ PS, uint8_t* __restrict__ TG) {
+k_diag_valid(const uint16_t* __restrict__ nbit, int64_t L, int k, uint32_t* __restrict__ uniq,
+             uint64_t n_words) {
+  const uint64_t a = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (a >= n_words) return;
+  const int64_t Nw = L - k + 1;
+  const uint64_t x = ((uint64_t)nbit[2 * a] << 48) | ((uint64_t)nbit[2 * a + 1] << 32) |
+                     ((uint64_t)nbit[2 * a + 2] << 16) | (uint64_t)nbit[2 * a + 3];
+  uint32_t u = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const int64_t s = (int64_t)(32 * a) + i;
+    bool v = s < Nw && ((x << i) >> (64 - k)) == 0;
+    if (v && s == Nw - 1 && s + k == L) {      // the end-drop rule
+      const int64_t p = s - 1;
+      v = p >= 0 && !((nbit[p >> 4] >> (15 - (p & 15))) & 1u);
+    }
+    u |= (v ? 1u : 0u) << i;
+  }
+  uniq[a] = u;
+}
+
+// V_diag_prep (after V_diag_valid): the slot tags TG, one byte per table slot, and the `uniq`
+// bits (DiagIdx) of every position of a key seen more than once cleared.  One thread per slot;
+// a key with more than DP_LANE positions is cleared by the whole wave.  Keys seen once (all but
+// a few of an i.i.d. sequence's) cost one 16-B slot read and one tag byte.
+constexpr uint32_t DP_LANE = 16;
+__device__ __forceinline__ void uniq_clear(uint32_t* uniq, int32_t pos) {
+  const uint32_t j = (uint32_t)(pos - 1);
+  atomicAnd(&uniq[j >> 5], ~(1u << (j & 31)));
+}
+__global__ void __launch_bounds__(BLOCK)
+k_diag_prep(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions,
+            uint32_t* __restrict__ uniq, uint8_t* __restrict__ TG) {
   const int lane = lane_id();
   for (uint64_t i0 = (uint64_t)blockIdx.x * BLOCK; i0 < nslots; i0 += (uint64_t)gridDim.x * BLOCK) {
     const uint64_t i = i0 + threadIdx.x;
-    Slot sl;
-    sl.key = EMPTY_KEY; sl.count = 0; sl.aux = 0;
+    uint64_t key = EMPTY_KEY;
+    uint32_t count = 0, aux = 0;
     if (i < nslots) {
       const uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
-      sl.key = ((uint64_t)v.y << 32) | v.x; sl.count = v.z; sl.aux = v.w;
+      key = ((uint64_t)v.y << 32) | v.x; count = v.z; aux = v.w;
     }
-    const uint4 out = make_uint4((uint32_t)sl.key, (uint32_t)(sl.key >> 32), sl.count, sl.aux);
-    if (i < nslots) TG[i] = sl.key == EMPTY_KEY ? (uint8_t)0 : slot_tag(mix64(sl.key));
-    if (sl.count == 1) {
-      *reinterpret_cast<uint4*>(&PS[sl.aux - 1]) = out;
-    } else if (sl.count > 1 && sl.count <= PS_LANE) {
-      for (uint32_t q = sl.aux - sl.count; q < sl.aux; ++q)
-        *reinterpret_cast<uint4*>(&PS[positions[q] - 1]) = out;
-    }
-    uint64_t heavy = __ballot(sl.count > PS_LANE);
+    if (i < nslots) TG[i] = key == EMPTY_KEY ? (uint8_t)0 : slot_tag(mix64(key));
+    if (count > 1 && count <= DP_LANE)
+      for (uint32_t q = aux - count; q < aux; ++q) uniq_clear(uniq, positions[q]);
+    uint64_t heavy = __ballot(count > DP_LANE);
     while (heavy) {                            // long lists: the wave strides over them
       const int src = __ffsll((unsigned long long)heavy) - 1;
       heavy &= heavy - 1;
-      const uint32_t c = __shfl(sl.count, src), a = __shfl(sl.aux, src);
-      const uint4 o = make_uint4(__shfl(out.x, src), __shfl(out.y, src), c, a);
-      for (uint32_t q = a - c + lane; q < a; q += 64)
-        *reinterpret_cast<uint4*>(&PS[positions[q] - 1]) = o;
+      const uint32_t c = __shfl(count, src), a = __shfl(aux, src);
+      for (uint32_t q = a - c + lane; q < a; q += 64) uniq_clear(uniq, positions[q]);
     }
   }
 }
 
-void launch_pos_slots(const Slot* T, uint64_t nslots, const int32_t* positions, Slot* PS,
-                      uint8_t* TG, hipStream_t s) {
+void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, const Slot* T,
+                      uint64_t nslots, const int32_t* positions, uint8_t* TG, hipStream_t s) {
+  const uint64_t nw = diag_uniq_words(L - k + 1);
+  hipLaunchKernelGGL(k_diag_valid, dim3((unsigned)((nw + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                     nbit, L, k, uniq, nw);
   uint64_t g = (nslots + BLOCK - 1) / BLOCK;
   if (g > 65536) g = 65536;
-  hipLaunchKernelGGL(k_pos_slots, dim3((unsigned)(g ? g : 1)), dim3(BLOCK), 0, s, T, nslots,
-                     positions, PS, TG);
+  hipLaunchKernelGGL(k_diag_prep, dim3((unsigned)(g ? g : 1)), dim3(BLOCK), 0, s, T, nslots,
+                     positions, uniq, TG);
 }
 
 // Q_probe: per query window (query k) probe the table; qinfo[s] = {count, start}; per-tile row
 // totals go through the look-back so each tile learns its first output row.
-// Diagonal path (PS != nullptr: query k = index k, a position index): dot plots hit along
+// Diagonal path (X.code != nullptr: query k = index k, a position index): dot plots hit along
 // diagonals, so a window whose predecessor matched index position j usually matches j + 1.  Every
 // DG_STRIDE-th window of the tile ("anchor") probes the table; an anchor with a unique hit at j
 // predicts j + d for the window d after it, and the later windows of the tile follow the last
-// anchor that predicted.  A prediction is VERIFIED by reading PS[j + d - 1] -- consecutive windows
-// read consecutive 16-B entries, coalesced -- and taken only if its key equals the window's key,
-// in which case its {count, aux} ARE the key's slot (exact); otherwise the window probes the
-// table as before.  Queries unrelated to the index pay the anchors and one failed check.
+// anchor that predicted.  A prediction p is VERIFIED against the index sequence itself (DiagIdx):
+// if index window p - 1 is indexed with a key seen once (its `uniq` bit) and that key -- read from
+// the index's 2-bit code words -- equals the window's key, the window's slot is {count 1, aux p}
+// (exact: the only slot of that key holds exactly that); otherwise the window probes the table
+// as before.  Consecutive windows read the same few code and bit words, so a wave's verification
+// loads touch one or two cache lines: ~0.4 B per window, where the position-indexed slot copy
+// this replaced streamed 16 B per window (and took 16 B per index window of HBM, built by a
+// random scatter on the first query).  Queries unrelated to the index pay the anchors and one
+// failed check.
 #ifndef KMHG_DG_STRIDE
 #define KMHG_DG_STRIDE 64        // A/B (config 2 self dot plot, probe): 16 / 32 / 64 / 128 ->
 #endif                           //   97 / 86 / 82 / 76 us; 64 keeps misses after a tile start short
@@ -373,38 +405,42 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
   __syncthreads();
 }
 
-// A position slot holds `key`'s table slot.  Any entry whose key equals the window's is a copy
-// of that key's slot, whichever position it was loaded from; entries of windows the index does
-// not hold keep the 0xFF preset, key ~0, which no query window has (query k <= 31,
-// src/kmer_hash.c:1163-1164).
-__device__ __forceinline__ bool ps_match(uint4 v, uint64_t key) {
-  return (((uint64_t)v.y << 32) | v.x) == key;
+// The key of index window j (0-based) from the index's code words: the stage's window_key
+// extraction on global words (qw = j / 16, three consecutive words).
+__device__ __forceinline__ uint64_t code_key(uint32_t a, uint32_t b, uint32_t c, int64_t j, int k) {
+  const int sh = (int)(j & 15) * 2;
+  const uint64_t x = ((uint64_t)a << 32) | b;
+  const uint64_t y = c;
+  const uint64_t t = (x << sh) | ((y << sh) >> 32);
+  return t >> (64 - 2 * k);
 }
 
-// The diagonal path of a staged tile, every lane's WPT windows: the predicted position slots
-// are loaded first, all in flight at once (coalesced across the wave; a window without a
-// prediction loads PS[0], one shared line, so every lane issues a static WPT loads), then
-// resolved; windows whose prediction fails probe through the slot tags (TG) or the table.  (The
-// resolve-as-you-go loop kept at most two PS loads in flight per lane behind its branches.)
+// The diagonal path of a staged tile, every lane's WPT windows: the verification words of every
+// prediction are loaded first, all in flight at once (a window without a prediction loads word
+// 0, so every lane issues a static number of loads), then resolved; windows whose prediction
+// fails probe through the slot tags (TG) or the table.
 // `out(w, s, count, aux)` receives every window of the tile, s = t_start + w (s >= w1: none).
 template <class ST, class Out>
 __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_start, int64_t w0,
                                              int64_t w1, int64_t L, int kq,
-                                             const Slot* __restrict__ T, Geom g,
-                                             const Slot* __restrict__ PS, int64_t nA,
+                                             const Slot* __restrict__ T, Geom g, DiagIdx X,
                                              const uint8_t* __restrict__ TG,
                                              const DiagAnchors& A, Out out) {
   (void)w0;
-  uint4 pv[WPT];
+  uint32_t ca[WPT], cb[WPT], cc[WPT], ub[WPT];
 #pragma unroll
   for (int j = 0; j < WPT; ++j) {
     const int w = j * BLOCK + threadIdx.x;
     const int la = A.last[w / DG_STRIDE];
     int64_t pj = la >= 0 ? (int64_t)A.anc[la] + (w - la * DG_STRIDE) : 1;
-    if (pj > nA || w % DG_STRIDE == 0) pj = 1;
-    pv[j] = *reinterpret_cast<const uint4*>(&PS[pj - 1]);
+    if (pj > X.nA || w % DG_STRIDE == 0) pj = 1;
+    const uint64_t q0 = (uint64_t)(pj - 1) >> 4;
+    ca[j] = X.code[q0];
+    cb[j] = X.code[q0 + 1];
+    cc[j] = X.code[q0 + 2];
+    ub[j] = X.uniq[(uint64_t)(pj - 1) >> 5];
   }
-#pragma unroll                 // static indices into pv (a partial unroll put it in scratch)
+#pragma unroll                 // static indices into the loaded words
   for (int j = 0; j < WPT; ++j) {
     const int w = j * BLOCK + threadIdx.x;
     const int64_t s = t_start + w;
@@ -417,8 +453,11 @@ __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_sta
         count = ai.x; aux = ai.y;
         hit = true;
       } else {
-        hit = A.last[w / DG_STRIDE] >= 0 && ps_match(pv[j], key);
-        count = pv[j].z; aux = pv[j].w;
+        const int la = A.last[w / DG_STRIDE];
+        const int64_t pj = la >= 0 ? (int64_t)A.anc[la] + (w - la * DG_STRIDE) : 0;
+        hit = la >= 0 && pj <= X.nA && ((ub[j] >> ((pj - 1) & 31)) & 1u) &&
+              code_key(ca[j], cb[j], cc[j], pj - 1, kq) == key;
+        count = 1; aux = (uint32_t)pj;
       }
       if (!hit) {
         count = 0; aux = 0;
@@ -439,8 +478,7 @@ template <bool DIAG>
 __global__ void __launch_bounds__(BLOCK)
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
-              uint64_t* __restrict__ tile_rows, const Slot* __restrict__ PS, int64_t nA,
-              const uint8_t* __restrict__ TG) {
+              uint64_t* __restrict__ tile_rows, DiagIdx X, const uint8_t* __restrict__ TG) {
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
   __shared__ DiagAnchors A;
@@ -458,7 +496,7 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
 #define KMHG_PROBE_UNROLL 2
 #endif
   if (DIAG) {
-    diag_resolve(st, o0, t_start, w0, w1, L, kq, T, g, PS, nA, TG, A,
+    diag_resolve(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
                  [&](int w, int64_t s, uint32_t count, uint32_t aux) {
                    if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
                    rows += count;
@@ -633,7 +671,7 @@ __global__ void __launch_bounds__(BLOCK)
 k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, int64_t w0, int64_t w1, int aligned, const int32_t* __restrict__ positions,
               uint64_t* __restrict__ status, uint32_t nt, int2* __restrict__ out, uint64_t cap,
-              const Slot* __restrict__ PS, int64_t nA, const uint8_t* __restrict__ TG) {
+              DiagIdx X, const uint8_t* __restrict__ TG) {
   // LDS ~19 KB -> 8 workgroups per CU, as Q_probe: per-window {count, first} records (the
   // registers would hold them only with all WPT probes unrolled: 100 VGPRs, half the waves), and
   // the stage shares its bytes with the emit's heavy-window list
@@ -653,10 +691,10 @@ k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   const int o0 = (int)(t_start - base);
   stage_tile(seq, L, base, u.st, aligned != 0);
   __syncthreads();
-  if (PS) diag_anchors(u.st, o0, t_start, w1, L, kq, T, g, A);
+  if (X.code) diag_anchors(u.st, o0, t_start, w1, L, kq, T, g, A);
   uint64_t rows = 0;
-  if (PS) {
-    diag_resolve(u.st, o0, t_start, w0, w1, L, kq, T, g, PS, nA, TG, A,
+  if (X.code) {
+    diag_resolve(u.st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
                  [&](int w, int64_t, uint32_t count, uint32_t aux) {
                    qi[w] = make_uint2(count, count == 1 ? aux : aux - count);
                    rows += count;
@@ -1051,15 +1089,15 @@ void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, h
 }
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
-                        hipStream_t s, const Slot* PS, int64_t nA, const uint8_t* TG) {
+                        hipStream_t s, DiagIdx X, const uint8_t* TG) {
   uint32_t nt = grid_for(w1 - w0, TILE);
   if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
-  if (PS)
+  if (X.code)
     hipLaunchKernelGGL(k_query_probe<true>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo,
-                       w0, w1, aligned ? 1 : 0, tile_rows, PS, nA, TG);
+                       w0, w1, aligned ? 1 : 0, tile_rows, X, TG);
   else
     hipLaunchKernelGGL(k_query_probe<false>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo,
-                       w0, w1, aligned ? 1 : 0, tile_rows, nullptr, (int64_t)0, nullptr);
+                       w0, w1, aligned ? 1 : 0, tile_rows, DiagIdx{nullptr, nullptr, 0}, nullptr);
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
@@ -1084,11 +1122,11 @@ void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
 void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
                         int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
                         int2* out, uint64_t cap, hipStream_t s,
-                        const Slot* PS, int64_t nA, const uint8_t* TG) {
+                        DiagIdx X, const uint8_t* TG) {
   const uint32_t nt = grid_for(w1 - w0, TILE);
   if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
   hipLaunchKernelGGL(k_query_fused, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, w0, w1,
-                     aligned ? 1 : 0, positions, status, nt, out, cap, PS, nA, TG);
+                     aligned ? 1 : 0, positions, status, nt, out, cap, X, TG);
 }
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s) {

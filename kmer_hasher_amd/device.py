@@ -164,10 +164,13 @@ class DeviceIndex:
     @classmethod
     def import_image(cls, meta: torch.Tensor, bufs: list[torch.Tensor], stream=None):
         hdr = (C.c_int64 * 8)(*[int(x) for x in meta[:8].tolist()])
+        sizes = [int(x) for x in meta[8:].tolist()]
         out = C.c_void_p()
+        # a buffer of size 0 (no positions, no code block) is passed as NULL
+        ptrs = [C.c_void_p(b.data_ptr() if i >= len(sizes) or sizes[i] else None)
+                for i, b in enumerate(bufs)]
         with torch.cuda.device(bufs[0].device):
-            _lib.check(_lib.lib().kmhg_image_import(hdr, *[C.c_void_p(b.data_ptr()) for b in bufs],
-                                                    _stream_ptr(stream), C.byref(out)))
+            _lib.check(_lib.lib().kmhg_image_import(hdr, *ptrs, _stream_ptr(stream), C.byref(out)))
         return cls(out.value)
 
     def free(self):

@@ -54,12 +54,28 @@ def test_image_export_import_roundtrip(gpu):
     s, t = _seq(torch, 150_000, 10)
     a = DeviceIndex.build(t, 25)
     meta, bufs = a.export_image()
+    assert int(meta[10]) > 0                 # the diagonal path's code block travels too
     b = DeviceIndex.import_image(meta, [x.clone() for x in bufs])
     qa, qb = a.query(t, 25), b.query(t, 25)
     assert torch.equal(qa.rows(), qb.rows())
     pa, pb = a.positions(15), b.positions(15)
     for f in ("count", "pos", "pair.pos", "kmer"):
         assert torch.equal(pa[f], pb[f])
+    # an image without the code block (codes_bytes 0): the importer probes the table only
+    meta0 = meta.clone()
+    meta0[10] = 0
+    c = DeviceIndex.import_image(meta0, [x.clone() for x in bufs])
+    assert torch.equal(c.query(t, 25).rows(), qa.rows())
+    # an image exported after the first query (unique bits already cleared) imports the same
+    meta2, bufs2 = a.export_image()
+    d = DeviceIndex.import_image(meta2, [x.clone() for x in bufs2])
+    assert torch.equal(d.query(t, 25).rows(), qa.rows())
+    # a related query (SNVs) through the imported index vs the oracle
+    from kmer_hasher_amd import synth
+    B = synth.derived(s, 11)
+    want = O.OracleIndex(s.tobytes(), 25).query(B.tobytes(), 25)
+    got = d.query(torch.from_numpy(B).cuda(), 25).rows().cpu().numpy().reshape(-1)
+    assert np.array_equal(got, want)
 
 
 def test_full_size_self_query_properties(gpu):

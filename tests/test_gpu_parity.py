@@ -288,13 +288,14 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
 @pytest.mark.parametrize("tags", ["1", "0"])
 def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags):
     """The diagonal path of k_query_probe (anchors every 64th window; later windows follow the
-    last anchor with a unique hit and take a position-indexed slot only when its key equals
+    last anchor with a unique hit and take {count 1, aux = predicted position} only when the
+    index window there is unique and its key, read from the index's own code words, equals
     theirs; the rest probe through the slot tags, or the table alone with KMHG_QUERY_TAGS=0)
     against the oracle: the index's own sequence, a related sequence (1 % SNVs,
     inversions, translocations, N-runs), its reverse complement, an unrelated one, repeat-rich
-    input (multi-hit anchors predict nothing; keys with > 16 positions get their position slots
-    from a whole wave), shards of the window range that start inside a diagonal, and a query k
-    different from the index k (path off)."""
+    input (multi-hit anchors predict nothing; keys with > 16 positions have their windows'
+    unique bits cleared by a whole wave), shards of the window range that start inside a
+    diagonal, and a query k different from the index k (path off)."""
     import torch
     from kmer_hasher_amd import device as D, synth
     monkeypatch.setenv("KMHG_QUERY_TAGS", tags)
