@@ -474,8 +474,19 @@ __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_sta
   }
 }
 
+// At least 6 waves per SIMD: the diagonal probe needs 81 VGPRs unconstrained (5 waves / SIMD);
+// capped it fits 72 with no spill (7 waves).  A/B in one run, config 2: self query 87.0 / 90.0 ->
+// 90.9 / 95.4 Gbp/s, unrelated 41.4 -> 44.3; 8 waves (64 VGPRs) spills 44 B / lane and is slower.
+#ifndef KMHG_PROBE_WAVES
+#define KMHG_PROBE_WAVES 6
+#endif
+#if KMHG_PROBE_WAVES
+#define PROBE_BOUNDS __launch_bounds__(BLOCK, KMHG_PROBE_WAVES)
+#else
+#define PROBE_BOUNDS __launch_bounds__(BLOCK)
+#endif
 template <bool DIAG>
-__global__ void __launch_bounds__(BLOCK)
+__global__ void PROBE_BOUNDS
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
               uint64_t* __restrict__ tile_rows, DiagIdx X, const uint8_t* __restrict__ TG) {
