@@ -609,7 +609,9 @@ k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
              int2* __restrict__ out, uint64_t cap) {
   __shared__ uint64_t incl[TILE];
   __shared__ uint32_t start[TILE];
-  __shared__ uint32_t heavy[TILE];
+  using HeavyT = uint16_t;            // a window of the tile (< TILE): 28.7 KB of LDS, 5 groups / CU
+  static_assert(TILE <= 65536, "heavy[] holds tile-local window indices");
+  __shared__ HeavyT heavy[TILE];
   __shared__ uint32_t n_heavy;
   __shared__ uint64_t sh[8];
   const int64_t tile0 = (int64_t)blockIdx.x * TILE;
@@ -642,7 +644,7 @@ k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
     const uint64_t n = incl[w] - before;
     if (n == 0) continue;
     if (n > EMIT_DIRECT) {
-      heavy[atomicAdd(&n_heavy, 1u)] = (uint32_t)w;
+      heavy[atomicAdd(&n_heavy, 1u)] = (HeavyT)w;
       continue;
     }
     const uint64_t r = r0 + before;

@@ -27,6 +27,9 @@ for line in open(sys.argv[1]):
     if line.startswith("{"):
         d = json.loads(line)
         km = d.get("kernels_ms", {})
+        rd = d.get("reads", {})
         print(cur, "value", d["value"], "ms", d["ms_per_step"], "q", d.get("query", {}).get("value"), "qu", d.get("query", {}).get("unrelated", {}).get("value"),
+              "reads", rd.get("value"), "walk", rd.get("kernels_ms_per_step", {}).get("k_count_walk"),
+              "counts", d.get("counts", {}).get("value"),
               " ".join(f"{k}={v:.4f}" for k, v in sorted(km.items())))
 PY
