@@ -336,3 +336,39 @@ def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags):
     oi = O.OracleIndex(sa, 31)
     assert np.array_equal(full.reshape(-1), oi.query(B.tobytes().decode("latin-1"), 31))
     idx.free()
+
+
+@pytest.mark.parametrize("codes", ["1", "0"])
+def test_query_diagonal_edges_vs_oracle(gpu, monkeypatch, codes):
+    """Edges of the diagonal path's verification against the index's own code words and unique-
+    window bits: the reference's end-drop rule (a final N-free run of exactly k chars is not
+    indexed, so a query window with that key must probe and miss even when an anchor predicts
+    it), index windows ending at a tile boundary and in the last tile's extra code words, keys
+    seen twice (their bits are cleared: the window probes the table), lower case and IUPAC codes
+    in the index, and an index built without the code block (KMHG_DIAG_CODES=0: table probes)."""
+    from kmer_hasher_amd import synth
+    monkeypatch.setenv("KMHG_DIAG_CODES", codes)
+    make, kpos, sqk = _api()
+    rng = np.random.default_rng(91)
+
+    def rand(n):
+        return "".join(rng.choice(list("ACGT"), n))
+    for k in (31, 12, 5):
+        body = rand(5000)
+        cases = [body + "N" + rand(k),                  # final run of exactly k: dropped
+                 body + "N" + rand(k + 1),              # final run of k + 1: both windows kept
+                 rand(2048 + k - 1),                    # windows end exactly at a tile boundary
+                 rand(4096 + k + 2),                    # the last tile's extra code words
+                 body + body[100:900] + rand(300),      # keys seen twice (bits cleared)
+                 (body[:2000].lower() + "RYKMSWBDHV" + body[2000:])]
+        for s in cases:
+            oi = O.OracleIndex(s, k)
+            ptr = make(s, k)
+            for q in (s, s[1:] + "A", s[:len(s) // 2] + rand(40) + s[len(s) // 2:]):
+                assert np.array_equal(sqk(ptr, q, k).reshape(-1), oi.query(q, k)), (k, len(s))
+            ptr.free()
+    s = synth.iid(200_000, 92).tobytes().decode()
+    oi = O.OracleIndex(s, 31)
+    ptr = make(s, 31)
+    assert np.array_equal(sqk(ptr, s, 31).reshape(-1), oi.query(s, 31))
+    ptr.free()
