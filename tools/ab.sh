@@ -30,6 +30,7 @@ for line in open(sys.argv[1]):
         rd = d.get("reads", {})
         print(cur, "value", d["value"], "ms", d["ms_per_step"], "q", d.get("query", {}).get("value"), "qu", d.get("query", {}).get("unrelated", {}).get("value"),
               "reads", rd.get("value"), "walk", rd.get("kernels_ms_per_step", {}).get("k_count_walk"),
+              "rk", rd.get("kernels_ms_per_step", {}).get("k_read_kmers_emit"),
               "counts", d.get("counts", {}).get("value"),
               " ".join(f"{k}={v:.4f}" for k, v in sorted(km.items())))
 PY
