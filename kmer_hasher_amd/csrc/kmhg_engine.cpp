@@ -979,7 +979,8 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
     q->H = (int64_t)H;
     if (H <= cap) return q.release();
   }
-  DBuf<uint2> qinfo(Nw, s);
+  DBuf<uint32_t> qrec(Nw, s);         // per window: 0, the one hit's position, or multi
+  DBuf<uint2> qmulti(Nw, s);          // {count, first index}: written for multi-hit windows only
   // per-tile rows -> first row; then the long-scan scratch.  The row total goes straight into
   // pinned host memory (no copy launch before the host reads it).
   DBuf<uint64_t> tiles((size_t)nt + scan_u64_scratch(nt), s);
@@ -988,13 +989,13 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   GiveBack give_back{hrec};
   uint64_t* total = &hrec.meta->n_kmers;
   LAUNCH("k_query_probe", s,
-         launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qinfo.p, w0, w1, aligned,
+         launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qrec.p, qmulti.p, w0, w1, aligned,
                             tile_row0, s, diag ? idx->diag_view() : DiagIdx{nullptr, nullptr, 0},
                             diag && tags_on() ? idx->ptag.p : nullptr));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, tiles.p + nt, s));
   if (classic) {
     LAUNCH("k_query_emit", s,
-           launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap,
+           launch_query_emit(qrec.p, qmulti.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap,
                              s));
     HIPC(hipStreamSynchronize(s));
     H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
@@ -1010,7 +1011,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   q->rows.bind(s);
   q->rows.reset(H);
   LAUNCH("k_query_emit", s,
-         launch_query_emit(qinfo.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, H, s));
+         launch_query_emit(qrec.p, qmulti.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, H, s));
   return q.release();
 }
 

@@ -83,7 +83,8 @@ inline DiagBlock diag_block(uint64_t* p, int64_t Nw) {
 // X.code == nullptr: table probes only.  TG (optional, with X, g.capb % 16 == 0): slot tags for
 // the windows the diagonal path does not resolve
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
-                        uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
+                        uint32_t* qrec, uint2* qmulti, int64_t w0, int64_t w1, bool aligned,
+                        uint64_t* tile_rows,
                         hipStream_t s, DiagIdx X = DiagIdx{nullptr, nullptr, 0},
                         const uint8_t* TG = nullptr);
 // Once per index, before its first diagonal query: `uniq` = the indexed windows (from the N
@@ -98,7 +99,7 @@ constexpr uint64_t SCAN1_MAX = 16384;
 inline uint64_t scan_u64_scratch(uint64_t n) { return (n + TILE - 1) / TILE + 1; }
 void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch, hipStream_t s);
 // rows >= cap are dropped (the caller re-runs the emit into an exact buffer if the total exceeds cap)
-void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
+void launch_query_emit(const uint32_t* qrec, const uint2* qmulti, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
                        uint64_t cap, hipStream_t s);
 // probe + emit in one pass (ticketed tiles, decoupled look-back): `status` = grid_for(w1 - w0,

@@ -341,7 +341,18 @@ void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, co
                      positions, uniq, TG);
 }
 
-// Q_probe: per query window (query k) probe the table; qinfo[s] = {count, start}; per-tile row
+// A window's probe result as Q_emit reads it: qrec[s] = 0 (no hit), the 1-based index position
+// (one hit: a key seen once keeps its position inline, < 2^31), or QREC_MULTI with qmulti[s] =
+// {count, first index into positions} -- 4 B per window written and read back instead of 8 (only
+// windows with several hits, rare outside repeats, touch qmulti).
+constexpr uint32_t QREC_MULTI = 0x80000000u;
+__device__ __forceinline__ void put_qrec(uint32_t* qrec, uint2* qmulti, int64_t i, uint32_t count,
+                                         uint32_t aux) {
+  qrec[i] = count == 0 ? 0u : (count == 1 ? aux : QREC_MULTI);
+  if (count > 1) qmulti[i] = make_uint2(count, aux - count);
+}
+
+// Q_probe: per query window (query k) probe the table; qrec / qmulti (put_qrec); per-tile row
 // totals go through the look-back so each tile learns its first output row.
 // Diagonal path (X.code != nullptr: query k = index k, a position index): dot plots hit along
 // diagonals, so a window whose predecessor matched index position j usually matches j + 1.  Every
@@ -488,7 +499,8 @@ __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_sta
 template <bool DIAG>
 __global__ void PROBE_BOUNDS
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
-              Geom g, uint2* __restrict__ qinfo, int64_t w0, int64_t w1, int aligned,
+              Geom g, uint32_t* __restrict__ qrec, uint2* __restrict__ qmulti, int64_t w0,
+              int64_t w1, int aligned,
               uint64_t* __restrict__ tile_rows, DiagIdx X, const uint8_t* __restrict__ TG) {
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
@@ -509,7 +521,7 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   if (DIAG) {
     diag_resolve(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
                  [&](int w, int64_t s, uint32_t count, uint32_t aux) {
-                   if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
+                   if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
                    rows += count;
                  });
     uint64_t tot;
@@ -529,7 +541,7 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     uint32_t count = 0, aux = 0;
     if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
     // {count, position} for a key seen once, {count, first index} otherwise
-    if (s < w1) qinfo[s - w0] = make_uint2(count, count == 1 ? aux : aux - count);
+    if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
     rows += count;
   }
   uint64_t tot;
@@ -604,7 +616,8 @@ k_block_scan_u64(uint64_t* __restrict__ a, uint64_t n, const uint64_t* __restric
 // re-runs it into an exact-size buffer in the rare case the guess was short.
 constexpr uint32_t EMIT_DIRECT = 4;
 __global__ void __launch_bounds__(BLOCK)
-k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
+k_query_emit(const uint32_t* __restrict__ qrec, const uint2* __restrict__ qmulti, int64_t Nw,
+             int64_t w0, int kq,
              const int32_t* __restrict__ positions, const uint64_t* __restrict__ tile_row0,
              int2* __restrict__ out, uint64_t cap) {
   __shared__ uint64_t incl[TILE];
@@ -620,7 +633,9 @@ k_query_emit(const uint2* __restrict__ qinfo, int64_t Nw, int64_t w0, int kq,
   for (int j = 0; j < WPT; ++j) {
     int w = j * BLOCK + threadIdx.x;
     int64_t s = tile0 + w;
-    uint2 v = (s < Nw) ? qinfo[s] : make_uint2(0u, 0u);
+    const uint32_t rc = (s < Nw) ? qrec[s] : 0u;
+    uint2 v = make_uint2(rc ? 1u : 0u, rc);
+    if (rc == QREC_MULTI) v = qmulti[s];
     incl[w] = v.x;
     start[w] = v.y;
   }
@@ -1101,15 +1116,16 @@ void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, h
   hipLaunchKernelGGL(k_inline_singles, dim3(g), dim3(BLOCK), 0, s, T, nslots, positions);
 }
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
-                        uint2* qinfo, int64_t w0, int64_t w1, bool aligned, uint64_t* tile_rows,
+                        uint32_t* qrec, uint2* qmulti, int64_t w0, int64_t w1, bool aligned,
+                        uint64_t* tile_rows,
                         hipStream_t s, DiagIdx X, const uint8_t* TG) {
   uint32_t nt = grid_for(w1 - w0, TILE);
   if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
   if (X.code)
-    hipLaunchKernelGGL(k_query_probe<true>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo,
+    hipLaunchKernelGGL(k_query_probe<true>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti,
                        w0, w1, aligned ? 1 : 0, tile_rows, X, TG);
   else
-    hipLaunchKernelGGL(k_query_probe<false>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qinfo,
+    hipLaunchKernelGGL(k_query_probe<false>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti,
                        w0, w1, aligned ? 1 : 0, tile_rows, DiagIdx{nullptr, nullptr, 0}, nullptr);
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
@@ -1126,10 +1142,10 @@ void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch
   hipLaunchKernelGGL(k_block_scan_u64, dim3(nb), dim3(BLOCK), 0, s, a, n,
                      (const uint64_t*)scratch);
 }
-void launch_query_emit(const uint2* qinfo, int64_t Nw, int64_t w0, int kq,
+void launch_query_emit(const uint32_t* qrec, const uint2* qmulti, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
                        uint64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qinfo, Nw, w0,
+  hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qrec, qmulti, Nw, w0,
                      kq, positions, tile_row0, out, cap);
 }
 void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
