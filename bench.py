@@ -78,10 +78,10 @@ def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) 
         return 12 * U + 16 * U
     if kernel == "k_build_scatter":     # slot id read + position write per window
         return 8 * N
-    if kernel == "k_query_probe":       # read L chars; one 16-B slot probe + 8-B record per window
-        return L + 24 * Nw
-    if kernel == "k_query_emit":        # window record read + 8-B row write (positions of keys
-        return 8 * Nw + 8 * H             # seen once are inline in the record)
+    if kernel == "k_query_probe":       # read L chars; one 16-B slot probe + 4-B record per window
+        return L + 20 * Nw
+    if kernel == "k_query_emit":        # 4-B window record read + 8-B row write (positions of keys
+        return 4 * Nw + 8 * H             # seen once are inline in the record)
     return None
 
 
