@@ -1,0 +1,85 @@
+"""Multi-rank seq.kmer.pos with the HIP engine, rehearsed on ONE GPU: two ranks
+share cuda:0 over gloo (RCCL refuses two ranks on one device).  Rank 0 builds the index; its device
+image goes to rank 1 by broadcast of HBM buffers (kmer_hasher_amd/dist.py broadcast_index); each
+rank queries its window range with libkmhgpu; the rows are gathered in rank order and must equal
+the oracle's unsharded seq.kmer.pos rows.  gloo moves device tensors for broadcast/all_gather but
+not for point-to-point, so the per-rank rows are handed to gather_rows on the host here; on the
+8-GPU node the same code runs over RCCL with the rows left in HBM."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _HostRows:
+    def __init__(self, eng):
+        self.eng = eng
+
+    def query_range(self, seq, k, w0, w1):
+        return self.eng.query_range(seq, k, w0, w1).cpu()
+
+
+def _worker(rank, world, port, seq_bytes, k_index, kq, out_q):
+    import torch
+    import torch.distributed as dist
+    from kmer_hasher_amd import dist as kd
+    from kmer_hasher_amd.device import DeviceIndex
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()).to(dev)
+        built = DeviceIndex.build(seq, k_index) if rank == 0 else None
+        idx = kd.broadcast_index(built, dev, src=0)
+        info = idx.info()
+        rows = kd.sharded_query(_HostRows(kd.HipQueryEngine(idx)), seq, kq, dst=0)
+        torch.cuda.synchronize()
+        if rank == 0:
+            out_q.put(((info["n_kmers"], info["n_positions"]),
+                       rows.numpy().reshape(-1).tolist()))
+        dist.barrier()
+        idx.free()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k_index,kq", [(2, 31, 31), (2, 21, 19)])
+def test_two_ranks_one_gpu_sharded_query(gpu, world, k_index, kq):
+    import torch.multiprocessing as mp
+    from kmer_hasher_amd import synth
+    from oracle import oracle as O
+    s = synth.add_n_runs(synth.repeat_rich(120_000, 5, n_gap_every=9_001), 0.005, 3)
+    s[-k_index - 2] = ord("N")          # an end-drop case in the last shard
+    seq_bytes = s.tobytes()
+    oi = O.OracleIndex(seq_bytes, k_index)
+    want = oi.query(seq_bytes, kq).tolist()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, seq_bytes, k_index, kq, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        (nk, npos), got = q.get(timeout=100)
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert (nk, npos) == (oi.U, oi.N)
+    assert got == want
