@@ -32,5 +32,7 @@ for line in open(sys.argv[1]):
               "reads", rd.get("value"), "walk", rd.get("kernels_ms_per_step", {}).get("k_count_walk"),
               "rk", rd.get("kernels_ms_per_step", {}).get("k_read_kmers_emit"),
               "counts", d.get("counts", {}).get("value"),
+              "depth", d.get("depth", {}).get("value"),
+              "dprobe", d.get("depth", {}).get("kernels_ms_per_step", {}).get("k_depth_probe"),
               " ".join(f"{k}={v:.4f}" for k, v in sorted(km.items())))
 PY
