@@ -106,6 +106,33 @@ def query_roofline(qper: dict, L: int, Nw: int, H: int, pmc: dict) -> dict | Non
                     "(PMC bytes / the same duration) is the HBM rate actually sustained"}
 
 
+def host_boundary(seq_bytes: bytes, k: int, calls: int = 10) -> dict:
+    """The R-API rate: make.kmer.hash / seq.kmer.pos through the host-pointer C-ABI entries
+    (kmhg_build: pageable host sequence -> H2D -> build -> synchronize; kmhg_query_run +
+    kmhg_query_fill: H2D -> query -> rows D2H into host memory), i.e. PCIe-inclusive.  Reported
+    beside `value`, never as it."""
+    from kmer_hasher_amd import api
+    api.make_kmer_hash(seq_bytes, k).free()            # first call: pool, code objects
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        api.make_kmer_hash(seq_bytes, k).free()
+    t_b = (time.perf_counter() - t0) / calls
+    ptr = api.make_kmer_hash(seq_bytes, k)
+    rows = api.seq_kmer_pos(ptr, seq_bytes, k)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        rows = api.seq_kmer_pos(ptr, seq_bytes, k)
+    t_q = (time.perf_counter() - t0) / calls
+    ptr.free()
+    mbp = len(seq_bytes) / 1e6
+    return {"build": {"value": round(mbp / t_b, 2), "unit": "Mbp/s", "ms": round(t_b * 1e3, 3)},
+            "query": {"value": round(mbp / t_q, 2), "unit": "Mbp/s", "ms": round(t_q * 1e3, 3),
+                      "rows": int(rows.shape[0])},
+            "calls": calls,
+            "note": "PCIe-inclusive: host sequence in (pageable), host rows out, synchronous "
+                    "per call (the R API); not `value`"}
+
+
 def cpu_baseline(seq_bytes: bytes, k: int, budget_s: float = 20.0) -> dict | None:
     """Reference C core (compiled from the reference's own sources into oracle/_ref) timed on
     the host, single-threaded, on a bounded prefix sample of the workload."""
@@ -585,6 +612,8 @@ def main():
             if "k_depth_probe" in dper:
                 out["depth"]["roofline"] = _leg_roofline(
                     dper, "k_depth_probe", depth_algorithmic_bytes("k_depth_probe", L, 2))
+        if not args.profile:
+            out["host_boundary"] = host_boundary(host_seq.tobytes(), k)
         if not args.no_cpu and not args.profile:
             out["cpu_baseline"] = cpu_baseline(host_seq.tobytes(), k)
             if t_count:

@@ -19,6 +19,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kmhg_common.h"
@@ -440,6 +441,69 @@ hipStream_t lib_stream() {
   HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   streams[dev] = s;
   return s;
+}
+
+// Device -> pageable host copy for the host-pointer entry points (R matrices, numpy arrays):
+// results above D2H_STAGE_MIN go through two pinned chunks, the DMA of chunk i + 1 overlapping
+// the host copy of chunk i, which d2h_threads() threads split (they also take the destination's
+// first-touch page faults in parallel).  Synchronous: returns once dst holds the bytes.
+constexpr size_t D2H_CHUNK = 16u << 20;
+constexpr size_t D2H_STAGE_MIN = 4u << 20;
+static int d2h_threads() {                           // KMHG_D2H_THREADS (A/B), default 4
+  static const int n = [] {
+    const char* e = std::getenv("KMHG_D2H_THREADS");
+    return e ? std::max(1, std::min(16, std::atoi(e))) : 4;
+  }();
+  return n;
+}
+
+static void host_copy_par(char* dst, const char* src, size_t n) {
+  const int T = d2h_threads();
+  const size_t stripe = ((n + T - 1) / T + 4095) & ~(size_t)4095;
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) {
+    const size_t a = std::min(n, t * stripe), b = std::min(n, a + stripe);
+    if (a < b) th.emplace_back([=] { std::memcpy(dst + a, src + a, b - a); });
+  }
+  std::memcpy(dst, src, std::min(n, stripe));
+  for (auto& x : th) x.join();
+}
+
+void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (!bytes) return;
+  static const bool staged = [] {
+    const char* e = std::getenv("KMHG_D2H");          // A/B knob: "direct" = one hipMemcpy
+    return !(e && std::string(e) == "direct");
+  }();
+  if (!staged || bytes < D2H_STAGE_MIN) {
+    HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    return;
+  }
+  static std::mutex mu;
+  static char* pin[2] = {nullptr, nullptr};
+  std::lock_guard<std::mutex> g(mu);
+  if (!pin[0])
+    for (auto& b : pin)
+      HIPC(hipHostMalloc(reinterpret_cast<void**>(&b), D2H_CHUNK, hipHostMallocPortable));
+  hipEvent_t ev[2];
+  for (auto& e : ev) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  const size_t nch = (bytes + D2H_CHUNK - 1) / D2H_CHUNK;
+  auto issue = [&](size_t i) {
+    const size_t off = i * D2H_CHUNK, n = std::min(D2H_CHUNK, bytes - off);
+    HIPC(hipMemcpyAsync(pin[i & 1], static_cast<const char*>(src) + off, n,
+                        hipMemcpyDeviceToHost, s));
+    HIPC(hipEventRecord(ev[i & 1], s));
+  };
+  issue(0);
+  if (nch > 1) issue(1);
+  for (size_t i = 0; i < nch; ++i) {
+    HIPC(hipEventSynchronize(ev[i & 1]));
+    const size_t off = i * D2H_CHUNK, n = std::min(D2H_CHUNK, bytes - off);
+    host_copy_par(static_cast<char*>(dst) + off, pin[i & 1], n);
+    if (i + 2 < nch) issue(i + 2);
+  }
+  for (auto& e : ev) HIPC(hipEventDestroy(e));
 }
 
 // The hash table is sized from the number of windows (an upper bound on distinct k-mers) for a
@@ -2062,7 +2126,7 @@ int kmhg_sh_depth(kmhg_index* sh, const char* seq, size_t L, int k, int32_t* cou
     if (L > n)   // past a NUL: never written (NA)
       HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(out.p + n * S), (int)INT_MIN,
                              (L - n) * S, s));
-    if (L) HIPC(hipMemcpyAsync(counts, out.p, L * S * 4, hipMemcpyDeviceToHost, s));
+    if (L) d2h_host(counts, out.p, L * S * 4, s);
     HIPC(hipStreamSynchronize(s));
   });
 }
@@ -2240,13 +2304,13 @@ int kmhg_positions_fill(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos
     DBuf<int32_t> dc((opt & KMHG_OPT_COUNT) ? U : 0, s);
     positions_device(idx, opt, dk.p, dp.p, dpp.p, dc.p, s);
     if ((opt & KMHG_OPT_KMER) && U && kmers)
-      HIPC(hipMemcpyAsync(kmers, dk.p, dk.bytes(), hipMemcpyDeviceToHost, s));
+      d2h_host(kmers, dk.p, dk.bytes(), s);
     if ((opt & KMHG_OPT_POS) && idx->N && pos)
-      HIPC(hipMemcpyAsync(pos, dp.p, dp.bytes(), hipMemcpyDeviceToHost, s));
+      d2h_host(pos, dp.p, dp.bytes(), s);
     if ((opt & KMHG_OPT_PAIRS) && idx->P && pairs)
-      HIPC(hipMemcpyAsync(pairs, dpp.p, dpp.bytes(), hipMemcpyDeviceToHost, s));
+      d2h_host(pairs, dpp.p, dpp.bytes(), s);
     if ((opt & KMHG_OPT_COUNT) && U && counts)
-      HIPC(hipMemcpyAsync(counts, dc.p, dc.bytes(), hipMemcpyDeviceToHost, s));
+      d2h_host(counts, dc.p, dc.bytes(), s);
     HIPC(hipStreamSynchronize(s));
   });
 }
@@ -2322,8 +2386,7 @@ int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
     if (!rows) fail(KMHG_EINVAL, "null output");
     DeviceGuard g(q->device);
     hipStream_t s = lib_stream();
-    HIPC(hipMemcpyAsync(rows, q->rows.p, (size_t)q->H * 8, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
+    d2h_host(rows, q->rows.p, (size_t)q->H * 8, s);
   });
 }
 
