@@ -85,25 +85,99 @@ def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) 
     return None
 
 
-def query_roofline(qper: dict, L: int, Nw: int, H: int, pmc: dict) -> dict | None:
-    """Roofline of the dominant query kernel from its HIP-event average duration."""
+def survey_bytes(kind: str, L: int = 0, U: int = 0, N: int = 0, Nq: int = 0, H: int = 0,
+                 P: int = 0, opt: int = 0) -> int:
+    """SURVEY.md §8(d) / BASELINE.md §3 algorithmic bytes of one unit of work (one build, one
+    query, one readout): the per-unit figures times the units one launch processes.
+      build    B = L + 12 U + 4 N           (read chars; key + count/offset per distinct k-mer;
+                                             4 B per position)
+      query    B = L_q + 12 N_q + 12 H      (read chars; 8-B key + 4-B offset per window; 4 B
+                                             position read + 8 B (i, j) row written per hit)
+      readout  B = 4U + 4N + 8N[opt&2] + 12P[opt&4] + 4U[opt&8]"""
+    if kind == "build":
+        return L + 12 * U + 4 * N
+    if kind == "query":
+        return L + 12 * Nq + 12 * H
+    if kind == "readout":
+        return (4 * U + 4 * N + (8 * N if opt & 2 else 0) + (12 * P if opt & 4 else 0)
+                + (4 * U if opt & 8 else 0))
+    raise ValueError(kind)
+
+
+def pmc_step_traffic(pmc: dict, kernels) -> int | None:
+    """Summed PMC HBM bytes of one step's kernels (per-launch averages x launches per step)."""
+    if not pmc:
+        return None
+    tot, seen = 0, False
+    for name, launches in kernels.items():
+        t = pmc_traffic(pmc, name)
+        if t is not None:
+            tot += t * launches
+            seen = True
+    return tot if seen else None
+
+
+def roofline(B: int, dom: str, dom_ms: float, step_ms: float, pmc: dict,
+             model_bytes: int | None = None, step_kernels: dict | None = None) -> dict:
+    """The contract's roofline object for the dominant kernel of one unit of work:
+    achieved = B (SURVEY.md §8(d) bytes of the unit) / the dominant kernel's HIP-event average;
+    frac_of_step = B / the whole step's wall time per unit; traffic = PMC HBM bytes per launch
+    of the dominant kernel (profiles/pmc_config<c>.json); traffic_step = the summed PMC bytes of
+    every kernel of the step.  kernel_model prices the dominant kernel by the bytes it alone must
+    move (secondary)."""
+    ach = B / (dom_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(pmc, dom)
+    out = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "algorithmic_bytes": B, "avg_ms": round(dom_ms, 5),
+           "frac_of_step": round(B / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "bytes_source": "SURVEY.md §8(d)"}
+    if traffic:
+        out["traffic_gbs"] = round(traffic / (dom_ms * 1e-3) / 1e9, 2)
+    if step_kernels:
+        ts = pmc_step_traffic(pmc, step_kernels)
+        if ts:
+            out["traffic_step"] = ts
+            out["traffic_step_over_B"] = round(ts / B, 3)
+    if model_bytes:
+        ma = model_bytes / (dom_ms * 1e-3) / 1e9
+        out["kernel_model"] = {"algorithmic_bytes": model_bytes, "achieved": round(ma, 2),
+                               "frac": round(ma / HBM_PEAK_GBS, 4),
+                               "note": "bytes the dominant kernel alone must move (bench.py "
+                                       "algorithmic_bytes)"}
+    return out
+
+
+def host_info() -> dict:
+    """nproc / CPU model of the host the CPU baseline runs on."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model}
+
+
+def query_roofline(qper: dict, L: int, Nw: int, H: int, pmc: dict, step_ms: float,
+                   launches: dict | None = None) -> dict | None:
+    """Roofline of the dominant query kernel from its HIP-event average duration, priced with
+    SURVEY.md §8(d)'s query bytes."""
     if not qper:
         return None
     dom = max(qper, key=qper.get)
-    ab = algorithmic_bytes(dom, L, Nw, 0, 0, H)
-    if not ab:
-        return None
-    ach = ab / (qper[dom] * 1e-3) / 1e9
-    traffic = pmc_traffic(pmc, dom)
-    return {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": traffic, "algorithmic_bytes": ab,
-            "traffic_gbs": round(traffic / (qper[dom] * 1e-3) / 1e9, 2) if traffic else None,
-            "avg_ms": round(qper[dom], 5),
-            "note": "algorithmic bytes price one 16-B slot probe per window (the general lookup; "
-                    "a random probe moves >= 64 B); a self dot plot resolves most windows on the "
-                    "diagonal against the index's code words and moves less, so traffic_gbs "
-                    "(PMC bytes / the same duration) is the HBM rate actually sustained"}
+    out = roofline(survey_bytes("query", L=L, Nq=Nw, H=H), dom, qper[dom], step_ms, pmc,
+                   algorithmic_bytes(dom, L, Nw, 0, 0, H), launches or {n: 1 for n in qper})
+    out["note"] = ("a self dot plot resolves most windows on the diagonal against the index's "
+                   "code words, so the probe moves fewer bytes than 12 per window; traffic_gbs "
+                   "(PMC bytes / the same duration) is the HBM rate actually sustained")
+    return out
 
 
 def host_boundary(seq_bytes: bytes, k: int, calls: int = 10) -> dict:
@@ -133,35 +207,64 @@ def host_boundary(seq_bytes: bytes, k: int, calls: int = 10) -> dict:
                     "per call (the R API); not `value`"}
 
 
-def cpu_baseline(seq_bytes: bytes, k: int, budget_s: float = 20.0) -> dict | None:
+class _pinned_one_core:
+    """Pin this process to one of its allowed CPUs for a CPU-baseline leg (taskset -c, as
+    BASELINE.md §3 asks), restoring the previous affinity afterwards."""
+
+    def __enter__(self):
+        try:
+            self.prev = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, {min(self.prev)})
+        except (AttributeError, OSError):
+            self.prev = None
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev:
+            os.sched_setaffinity(0, self.prev)
+
+
+def cpu_baseline(seq_bytes: bytes, k: int, sample_bp: int = 10_000_000, reps_max: int = 3,
+                 budget_s: float = 20.0) -> dict | None:
     """Reference C core (compiled from the reference's own sources into oracle/_ref) timed on
-    the host, single-threaded, on a bounded prefix sample of the workload."""
+    the host, single-threaded and pinned to one core, on a prefix sample of the workload: build
+    (seq_to_hash) and self query (seq_kmer_positions) timed separately, teardown (clear_kmer_h,
+    the finaliser) on its own line."""
     try:
         from oracle import oracle as O
         if not O.ref_available():
             return None
-        sample = seq_bytes[: min(len(seq_bytes), 10_000_000)]
-        t_build, t_query, reps, n = 0.0, 0.0, 0, 0
+        sample = seq_bytes[: min(len(seq_bytes), sample_bp)]
+        t_build, t_query, t_free, reps, n = 0.0, 0.0, 0.0, 0, 0
         t_start = time.perf_counter()
-        while time.perf_counter() - t_start < budget_s / 2 or reps == 0:
-            t0 = time.perf_counter()
-            r = O.RefIndex(sample, k)
-            t1 = time.perf_counter()
-            q = r.query(sample, k)
-            t2 = time.perf_counter()
-            r.close()
-            t_build += t1 - t0
-            t_query += t2 - t1
-            reps += 1
-            n = q.size // 2
-            if reps >= 3:
-                break
+        with _pinned_one_core():
+            while time.perf_counter() - t_start < budget_s / 2 or reps == 0:
+                t0 = time.perf_counter()
+                r = O.RefIndex(sample, k)
+                t1 = time.perf_counter()
+                q = r.query(sample, k)
+                t2 = time.perf_counter()
+                n = q.size // 2
+                del q
+                t3 = time.perf_counter()
+                r.close()
+                t_free += time.perf_counter() - t3
+                t_build += t1 - t0
+                t_query += t2 - t1
+                reps += 1
+                if reps >= reps_max:
+                    break
         mbp = len(sample) / 1e6
+        whole = len(sample) == len(seq_bytes)
         return {"value": round(mbp * reps / t_build, 3), "unit": "Mbp/s", "cores": 1,
                 "kind": "reference",
-                "sample": f"{mbp:.1f} Mbp prefix of the same sequence, k={k}, {reps} build(s) "
-                          f"of src/kmer_pos.c seq_to_hash via oracle/_ref (gcc -O2, 1 thread)",
-                "query_value": round(mbp * reps / t_query, 3), "query_rows": n}
+                "sample": (f"the whole {mbp:.1f} Mbp sequence" if whole else
+                           f"{mbp:.1f} Mbp prefix of the same sequence") +
+                          f", k={k}, {reps} build(s) of src/kmer_pos.c seq_to_hash + "
+                          "seq_kmer_positions via oracle/_ref (gcc -O2, 1 thread pinned)",
+                "build_s": round(t_build / reps, 3),
+                "query_value": round(mbp * reps / t_query, 3), "query_s": round(t_query / reps, 3),
+                "query_rows": n, "teardown_s": round(t_free / reps, 3), "host": host_info()}
     except Exception as e:  # the baseline is reported, never required
         return {"value": None, "unit": "Mbp/s", "cores": 1, "kind": "reference",
                 "sample": f"unavailable: {e}"}
@@ -410,7 +513,12 @@ def main():
         barrier()
         t_other = (time.perf_counter() - t0) / n_other
         del other
+    # teardown (the finaliser, src/kmer_hash.c:56-66; the reference's takes 2.56 s at 10 Mbp)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     idx.free()
+    torch.cuda.synchronize()
+    t_free = time.perf_counter() - t0
 
     # ---------------- count.kmers (SURVEY.md §8 f next-4) of the same sequence: one call per step
     # into a new counts pointer (k, source 0 of 2)
@@ -514,8 +622,6 @@ def main():
         per = all_kernels
         tot = per_step
         dom_ms = ktimes[dom][1] / ktimes[dom][0] if ktimes.get(dom, [0])[0] else per[dom]
-        ab = algorithmic_bytes(dom, L, Nw, U, N)
-        achieved = ab / (dom_ms * 1e-3) / 1e9 if ab else None
         pmc = {}
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_config{args.config}.json")
         if os.path.exists(pmc_path):
@@ -523,7 +629,9 @@ def main():
                 pmc = json.load(open(pmc_path))
             except Exception:
                 pmc = {}
-        traffic = pmc_traffic(pmc, dom)
+        step_ms = t_build / args.steps * 1e3
+        launches = {n: v[0] / n_id for n, v in wt.items() if v[0]}
+        B = survey_bytes("build", L=L, U=U, N=N)
         out = {
             "metric": "Mbp/s indexed (make.kmer.hash k=31) at 1/2/4/8 GPUs; "
                       "seq.kmer.pos query Mbp/s",
@@ -540,12 +648,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": cfg["workload"], "seq_len": L, "k": k,
                        "distinct_kmers": U, "positions": N, "parallelism": f"replicas{world}"},
-            "roofline": {"bound": "hbm", "kernel": dom,
-                         "achieved": round(achieved, 2) if achieved else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": traffic, "algorithmic_bytes": ab,
-                         "avg_ms": round(dom_ms, 5)},
+            "roofline": roofline(B, dom, dom_ms, step_ms, pmc,
+                                 algorithmic_bytes(dom, L, Nw, U, N), launches),
             "synchronous": {"value": round(mbp_total * args.steps / t_sync, 2), "unit": "Mbp/s",
                             "ms_per_step": round(t_sync / args.steps * 1e3, 4),
                             "note": "same steps, host waits for each build (R-API semantics)"},
@@ -553,7 +657,8 @@ def main():
                       "ms_per_step": round(t_query / leg_steps * 1e3, 4),
                       "first_call_ms": round(t_query_first * 1e3, 3),
                       "kernels_ms": {n: round(v, 5) for n, v in qper.items()},
-                      "roofline": query_roofline(qper, L, Nw, H, pmc),
+                      "roofline": query_roofline(qper, L, Nw, H, pmc,
+                                                 t_query / leg_steps * 1e3),
                       "unrelated": {"value": round(L * world / 1e6 / t_other, 2) if t_other
                                     else None, "unit": "Mbp/s",
                                     "ms_per_step": round(t_other * 1e3, 4), "rows": H_other,
@@ -564,11 +669,8 @@ def main():
                               "one-time diagonal-path preparation (unique-window bits, slot "
                               "tags) and the process's first launch of those kernels"},
             "kernels_ms": {n: round(v, 5) for n, v in per.items()},
-            "build_roofline": {"algorithmic_bytes": L + 12 * U + 4 * N,
-                               "kernel_ms_per_step": round(sum(tot.values()), 5),
-                               "frac_of_step": round((L + 12 * U + 4 * N) /
-                                                     (t_build / args.steps) / 1e9 / HBM_PEAK_GBS, 5),
-                               "note": "whole build, SURVEY.md §8(d): B = L + 12U + 4N"},
+            "kernel_ms_per_step": round(sum(tot.values()), 5),
+            "teardown_ms": round(t_free * 1e3, 4),
         }
         if t_count:
             out["counts"] = {
@@ -615,7 +717,10 @@ def main():
         if not args.profile:
             out["host_boundary"] = host_boundary(host_seq.tobytes(), k)
         if not args.no_cpu and not args.profile:
-            out["cpu_baseline"] = cpu_baseline(host_seq.tobytes(), k)
+            # config 3: the whole 100 Mbp (≈ 60 s of CPU: the verdict's full-size baseline)
+            out["cpu_baseline"] = cpu_baseline(
+                host_seq.tobytes(), k, sample_bp=L if args.config == 3 else 10_000_000,
+                reps_max=1 if args.config == 3 else 3)
             if t_count:
                 out["counts"]["cpu_baseline"] = cpu_counts_baseline(host_seq.tobytes(), k)
             if t_reads and sample_fq is not None:
@@ -642,7 +747,7 @@ def bench_readout(args, cfg, dev, world, rank):
     from kmer_hasher_amd import device as D
     from kmer_hasher_amd import synth
     L, k = cfg["L"], cfg["k"]
-    host = synth.repeat_rich(L, 3 + rank)
+    host = synth.config4(L, 3 + rank)
     seq = torch.from_numpy(host).to(dev)
     t0 = time.perf_counter()
     idx = D.DeviceIndex.build(seq, k)
@@ -685,9 +790,14 @@ def bench_readout(args, cfg, dev, world, rank):
     if rank == 0:
         P, N, U = info["n_pairs"], info["n_positions"], info["n_kmers"]
         per = {n: v[1] / v[0] for n, v in kt.items() if v[0]}
+        launches = {n: v[0] / args.steps for n, v in kt.items() if v[0]}
         dom = max(per, key=per.get)
         ab = {"k_read_pairs": 12 * P + 8 * P, "k_read_pos": 8 * N + 4 * N}.get(dom)
-        ach = ab / (per[dom] * 1e-3) / 1e9 if ab else None
+        pmc = _load_pmc(4)
+        B = survey_bytes("readout", U=U, N=N, P=P, opt=opt)
+        cpu = None
+        if not args.no_cpu and not args.profile:
+            cpu = cpu_readout_baseline(host.tobytes(), k, opt)
         _emit({"metric": "kmer.pos pair.pos rows/s (config 4)", "value": round(P * world * args.steps / t / 1e9, 4),
                "unit": "G pair rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(t / args.steps * 1e3, 3), "higher_is_better": True,
@@ -698,16 +808,56 @@ def bench_readout(args, cfg, dev, world, rank):
                           "first_call_ms": round(t_first * 1e3, 3),
                           "first_call_prepare_ms": {n: round(v[1] / v[0], 4) for n, v in kt_first.items()
                                                     if v[0] and n in ("k_read_first", "k_read_order")}},
-               "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2) if ach else None,
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": None,
-                            "algorithmic_bytes": ab, "avg_ms": round(per[dom], 4)},
+               "roofline": roofline(B, dom, per[dom], t / args.steps * 1e3, pmc, ab, launches),
+               "cpu_baseline": cpu,
                "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
     idx.free()
 
 
+def _load_pmc(config: int) -> dict:
+    path = os.path.join(ROOT, "profiles", f"pmc_config{config}.json")
+    try:
+        return json.load(open(path))
+    except (OSError, ValueError):
+        return {}
+
+
+def cpu_readout_baseline(seq_bytes: bytes, k: int, opt: int) -> dict:
+    """kmer_positions(opt) of the compiled reference (oracle/_ref: the bucket walk of
+    src/kmer_hash.c:1096-1124 restated over the reference's khash core) on the whole config-4
+    index, 1 thread pinned: build and readout timed separately, teardown on its own line."""
+    try:
+        from oracle import oracle as O
+        with _pinned_one_core():
+            t0 = time.perf_counter()
+            r = O.RefIndex(seq_bytes, k)
+            t_build = time.perf_counter() - t0
+            t_read, npos, npair = r.time_positions(opt)
+            t0 = time.perf_counter()
+            r.close()
+            t_free = time.perf_counter() - t0
+        return {"value": round(npair / t_read / 1e9, 5), "unit": "G pair rows/s", "cores": 1,
+                "kind": "reference",
+                "sample": f"the whole {len(seq_bytes) / 1e6:.0f} Mbp config-4 sequence, k={k}: "
+                          f"kmer_positions(opt={opt}) into flat arrays (the R matrices' data), "
+                          "oracle/_ref gcc -O2, 1 thread pinned",
+                "readout_s": round(t_read, 3), "build_s": round(t_build, 3),
+                "build_value": round(len(seq_bytes) / 1e6 / t_build, 3),
+                "build_unit": "Mbp/s", "teardown_s": round(t_free, 3), "pos_rows": npos,
+                "pair_rows": npair, "host": host_info()}
+    except Exception as e:  # reported, never required
+        return {"value": None, "unit": "G pair rows/s", "cores": 1, "kind": "reference",
+                "sample": f"unavailable: {e}"}
+
+
 def bench_sharded_query(args, cfg, dev, world, rank):
-    """Config 5: B (500 Mbp) queried against index(A); B's windows sharded over the ranks."""
+    """Config 5: B (500 Mbp) queried against index(A); B's windows sharded over the ranks.
+
+    The index is built on rank 0 and its image broadcast once (timed, outside the steps).  A
+    step is one seq.kmer.pos of B as the R session issues it: B sits on rank 0, is broadcast to
+    every rank (C1), each rank queries its window range with the HIP engine, and the rows are
+    gathered to rank 0 in rank order (= the reference's row order).  The phases are timed
+    separately (synchronized on each rank, max over ranks)."""
     import torch
     import torch.distributed as dist
     from kmer_hasher_amd import device as D
@@ -715,14 +865,25 @@ def bench_sharded_query(args, cfg, dev, world, rank):
     from kmer_hasher_amd import synth
     L, k = cfg["L"], cfg["k"]
     A = synth.iid(L, 4)
-    B = synth.derived(A, 5)
-    tb = torch.from_numpy(B).to(dev)
-    if world > 1:
+    B = synth.derived(A, 5) if rank == 0 else None
+    cpu_sample = None
+    if rank == 0 and not args.no_cpu and not args.profile:
+        cpu_sample = (A[:CONFIG5_CPU_BP].tobytes(), B[:CONFIG5_CPU_BP].tobytes())
+    tb = torch.from_numpy(B).to(dev) if rank == 0 else None
+    t_build = 0.0
+    if rank == 0:
+        ta = torch.from_numpy(A).to(dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        index = D.DeviceIndex.build(ta, k)
+        index.wait()
+        t_build = time.perf_counter() - t0
+        del ta
+    else:
         index = None
-        if rank == 0:
-            ta = torch.from_numpy(A).to(dev)
-            index = D.DeviceIndex.build(ta, k)
-            del ta
+    del A, B
+    t_bcast = 0.0
+    if world > 1:
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -730,21 +891,32 @@ def bench_sharded_query(args, cfg, dev, world, rank):
         dist.barrier()
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - t0
-    else:
-        ta = torch.from_numpy(A).to(dev)
-        index = D.DeviceIndex.build(ta, k)
-        del ta
-        t_bcast = 0.0
-    del A
+    info = index.info()
     eng = kd.HipQueryEngine(index)
 
-    def step():
+    def step(timings=None):
         if world > 1:
-            return kd.sharded_query(eng, tb, k, dst=0)
-        return eng.query_range(tb, k, 0, tb.numel() - k + 1)
+            return kd.sharded_query(eng, tb, k, dst=0, src=0, timings=timings)
+        t0 = time.perf_counter()
+        r = eng.query_range(tb, k, 0, tb.numel() - k + 1)
+        if timings is not None:
+            torch.cuda.synchronize()
+            timings["query"] = timings.get("query", 0.0) + time.perf_counter() - t0
+        return r
 
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    rows = step()                      # first query: the index's diagonal-path preparation
+    torch.cuda.synchronize()
+    t_first = time.perf_counter() - t0
+    del rows
     for _ in range(args.warmup):
         rows = step()
+        del rows
+    # per-phase times in separate (synchronized) steps, then the timed steps without syncs
+    phases = {}
+    for _ in range(2):
+        rows = step(phases)
         del rows
     D.timing_enable(True)
     D.timing_reset()
@@ -752,6 +924,7 @@ def bench_sharded_query(args, cfg, dev, world, rank):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    H = 0
     for _ in range(args.steps):
         rows = step()
         H = rows.shape[0] if rows is not None else 0
@@ -762,29 +935,73 @@ def bench_sharded_query(args, cfg, dev, world, rank):
     t = time.perf_counter() - t0
     kt = D.timing_report()
     D.timing_enable(False)
-    tt = torch.tensor([t], dtype=torch.float64, device=dev)
+    tt = torch.tensor([t] + [phases.get(p, 0.0) / 2 for p in ("broadcast", "query", "gather")],
+                      dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t = tt.item()
+    t, p_b, p_q, p_g = tt.tolist()
     if rank == 0:
         per = {n: v[1] / v[0] for n, v in kt.items() if v[0]}
+        launches = {n: v[0] / args.steps for n, v in kt.items() if v[0]}
         dom = max(per, key=per.get)
         Nw_rank = (L - k + 1) // world
         ab = algorithmic_bytes(dom, L // world, Nw_rank, 0, 0, H // world)
-        ach = ab / (per[dom] * 1e-3) / 1e9 if ab else None
+        B_rank = survey_bytes("query", L=L // world, Nq=Nw_rank, H=H // world)
+        cpu = cpu_query_baseline(*cpu_sample, k) if cpu_sample else None
         _emit({"metric": "seq.kmer.pos query Mbp/s (config 5, sharded)",
                "value": round(L / 1e6 * args.steps / t, 2), "unit": "Mbp/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(t / args.steps * 1e3, 3), "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
                "config": {"workload": cfg["workload"], "seq_len": L, "k": k, "rows": H,
-                          "index_broadcast_s": round(t_bcast, 4), "parallelism": f"shard{world}"},
-               "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2) if ach else None,
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": None,
-                            "algorithmic_bytes": ab, "avg_ms": round(per[dom], 4)},
+                          "distinct_kmers": info["n_kmers"],
+                          "index_build_s": round(t_build, 4),
+                          "index_broadcast_s": round(t_bcast, 4),
+                          "first_query_ms": round(t_first * 1e3, 3),
+                          "phases_ms": {"query_broadcast": round(p_b * 1e3, 3),
+                                        "range_query": round(p_q * 1e3, 3),
+                                        "row_gather": round(p_g * 1e3, 3),
+                                        "note": "separate synchronized steps, max over ranks"},
+                          "parallelism": f"shard{world}"},
+               "roofline": roofline(B_rank, dom, per[dom], t / args.steps * 1e3, _load_pmc(5),
+                                    ab, launches),
+               "cpu_baseline": cpu,
                "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
     index.free()
+
+
+# config 5's CPU baseline: the reference on a prefix of A and of B (the whole 500 Mbp index needs
+# ~65 GB and minutes of one core)
+CONFIG5_CPU_BP = 20_000_000
+
+
+def cpu_query_baseline(a: bytes, b: bytes, k: int) -> dict:
+    """seq_kmer_positions (src/kmer_pos.c:110-136) of the compiled reference (oracle/_ref): B's
+    prefix queried against the index of A's prefix, 1 thread pinned."""
+    try:
+        from oracle import oracle as O
+        with _pinned_one_core():
+            t0 = time.perf_counter()
+            r = O.RefIndex(a, k)
+            t_build = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            q = r.query(b, k)
+            t_q = time.perf_counter() - t0
+            n = q.size // 2
+            del q
+            t0 = time.perf_counter()
+            r.close()
+            t_free = time.perf_counter() - t0
+        return {"value": round(len(b) / 1e6 / t_q, 3), "unit": "Mbp/s", "cores": 1,
+                "kind": "reference",
+                "sample": f"{len(b) / 1e6:.0f} Mbp prefix of B against the index of the "
+                          f"{len(a) / 1e6:.0f} Mbp prefix of A, k={k}, oracle/_ref gcc -O2, "
+                          "1 thread pinned",
+                "query_s": round(t_q, 3), "query_rows": n, "build_s": round(t_build, 3),
+                "teardown_s": round(t_free, 3), "host": host_info()}
+    except Exception as e:  # reported, never required
+        return {"value": None, "unit": "Mbp/s", "cores": 1, "kind": "reference",
+                "sample": f"unavailable: {e}"}
 
 
 if __name__ == "__main__":

@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <map>
 #include <memory>
@@ -140,16 +141,22 @@ class DevicePool {
       ev = nullptr;
     }
     std::lock_guard<std::mutex> g(mu_);
+    size_t owner = SIZE_MAX;            // the last entry actually queued recycles the event
     for (size_t i = 0; i < ps.size(); ++i) {
       auto it = live_.find(ps[i]);
       if (it == live_.end()) continue;
       if (ev) {
-        pending_.push_back({ps[i], it->second, ev, i + 1 == ps.size()});
+        owner = pending_.size();
+        pending_.push_back({ps[i], it->second, ev, false});
       } else {
         free_[it->second].push_back(ps[i]);
         cached_ += it->second.second;
       }
       live_.erase(it);
+    }
+    if (ev) {
+      if (owner != SIZE_MAX) pending_[owner].owns_ev = true;
+      else events_.push_back(ev);       // nothing queued: the event goes straight back
     }
   }
   // blocks no queued work uses any more (their stream was synchronized)
@@ -361,9 +368,15 @@ class PinnedPool {
   std::vector<PinnedRec> free_, pending_;
 };
 // returns a record taken for a host round trip that the scope waited for (any exit path)
+// On an exception path the device may still write into the record (a queued scan's total), so
+// the stream is drained first: a record back in the free list is never a DMA target.
 struct GiveBack {
   PinnedRec& r;
-  ~GiveBack() { PinnedPool::get().give(r, false); }
+  hipStream_t s;
+  ~GiveBack() {
+    if (std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(s);
+    PinnedPool::get().give(r, false);
+  }
 };
 
 // ============================================================================ timing
@@ -480,14 +493,38 @@ void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
     HIPC(hipStreamSynchronize(s));
     return;
   }
-  static std::mutex mu;
-  static char* pin[2] = {nullptr, nullptr};
-  std::lock_guard<std::mutex> g(mu);
+  // two pinned chunks per device, so the parts of a multi-device query copy out concurrently
+  struct Stage {
+    std::mutex mu;
+    char* pin[2] = {nullptr, nullptr};
+  };
+  static std::mutex map_mu;
+  static std::map<int, Stage> stages;
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  Stage* st;
+  {
+    std::lock_guard<std::mutex> g(map_mu);
+    st = &stages[dev];
+  }
+  std::lock_guard<std::mutex> g(st->mu);
+  char** pin = st->pin;
   if (!pin[0])
-    for (auto& b : pin)
-      HIPC(hipHostMalloc(reinterpret_cast<void**>(&b), D2H_CHUNK, hipHostMallocPortable));
-  hipEvent_t ev[2];
-  for (auto& e : ev) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (int i = 0; i < 2; ++i)
+      HIPC(hipHostMalloc(reinterpret_cast<void**>(&pin[i]), D2H_CHUNK, hipHostMallocPortable));
+  // the two events, destroyed on every exit; on an exception the stream is drained first so no
+  // DMA into the static pinned chunks is still in flight when the next caller takes them
+  struct Ev2 {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    hipStream_t s;
+    ~Ev2() {
+      if (std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(s);
+      for (auto x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } evs{{nullptr, nullptr}, s};
+  hipEvent_t* ev = evs.e;
+  for (int i = 0; i < 2; ++i) HIPC(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
   const size_t nch = (bytes + D2H_CHUNK - 1) / D2H_CHUNK;
   auto issue = [&](size_t i) {
     const size_t off = i * D2H_CHUNK, n = std::min(D2H_CHUNK, bytes - off);
@@ -503,7 +540,6 @@ void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
     host_copy_par(static_cast<char*>(dst) + off, pin[i & 1], n);
     if (i + 2 < nch) issue(i + 2);
   }
-  for (auto& e : ev) HIPC(hipEventDestroy(e));
 }
 
 // The hash table is sized from the number of windows (an upper bound on distinct k-mers) for a
@@ -566,7 +602,14 @@ struct kmhg_index {
   // cleared and the slot tags built on the first eligible query (V_diag_prep)
   DBuf<uint64_t> dcodes;
   DBuf<uint8_t> ptag;             // one tag byte per table slot (0 = empty)
-  bool ps_ready = false, ps_failed = false;
+  // ps_ready: published (release) after the preparing query's synchronize; read (acquire) by
+  // later queries, possibly on other threads, before they use ptag / the uniq bits
+  std::atomic<bool> ps_ready{false};
+  // copies of this index on other devices for multi-device queries (KMHG_DEVICES), keyed by
+  // the query part they serve; made on first use by peer copies over xGMI, freed with the index
+  std::map<int, kmhg_index*> replicas;
+  std::mutex rep_mu;
+  bool ps_failed = false;                 // guarded by ps_mu
   std::mutex ps_mu;
   DiagBlock diag_block_of() const { return diag_block(dcodes.p, L - k + 1); }
   DiagIdx diag_view() const {
@@ -587,6 +630,12 @@ struct kmhg_query {
   hipStream_t stream = nullptr;
   int64_t H = 0;
   DBuf<int2> rows;
+  // multi-device query (KMHG_DEVICES): one part per device, each holding the rows of its
+  // contiguous window range in its own HBM; part i's rows start at row part_off[i].  `rows`
+  // then stays empty until a device-side reader asks for them on `device` (gathered once).
+  std::vector<kmhg_query*> parts;
+  std::vector<int64_t> part_off;
+  bool gathered = false;
 };
 
 namespace {
@@ -1003,9 +1052,9 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   const bool diag_ok = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
                        idx->U > 0 && idx->dcodes.p;
   bool diag = diag_ok;
-  if (diag && !idx->ps_ready) {
+  if (diag && !idx->ps_ready.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> lk(idx->ps_mu);
-    if (!idx->ps_ready && !idx->ps_failed) {
+    if (!idx->ps_ready.load(std::memory_order_relaxed) && !idx->ps_failed) {
       try {
         idx->ptag.reset(idx->slots() + 32);  // + the 32-B span the last probe group reads
       } catch (const Error& e) {           // no room for the tags: table probes only
@@ -1022,11 +1071,11 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
                                 idx->positions.p, idx->ptag.p, s));
         // once per index: later queries may run on other streams
         HIPC(hipStreamSynchronize(s));
-        idx->ps_ready = true;
+        idx->ps_ready.store(true, std::memory_order_release);
       }
     }
   }
-  diag = diag && idx->ps_ready;
+  diag = diag && idx->ps_ready.load(std::memory_order_acquire);
 
   if (!classic) {
     // one pass: probe + look-back + emit (k_query_fused); look-back words + ticket zeroed
@@ -1050,7 +1099,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   DBuf<uint64_t> tiles((size_t)nt + scan_u64_scratch(nt), s);
   uint64_t* tile_row0 = tiles.p;
   PinnedRec hrec = PinnedPool::get().take();
-  GiveBack give_back{hrec};
+  GiveBack give_back{hrec, s};
   uint64_t* total = &hrec.meta->n_kmers;
   LAUNCH("k_query_probe", s,
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qrec.p, qmulti.p, w0, w1, aligned,
@@ -1416,7 +1465,7 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   LAUNCH("k_scan_u32", s, launch_scan_u32(cnt.p, n_reads, status.p, cnt.p + n_reads, s));
   // one round trip for the staging span and the stream length (pinned: the GiveBack returns it)
   PinnedRec hr = PinnedPool::get().take();
-  GiveBack hr_back{hr};
+  GiveBack hr_back{hr, s};
   HIPC(hipMemcpyAsync(&hr.meta->n_pairs, d_span, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(&hr.meta->max_count, cnt.p + n_reads, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -1489,6 +1538,10 @@ struct ReadsHost {
   size_t n() const { return hasq.size(); }
 };
 
+// Largest base span of one device batch: every per-read window bound is <= its read length, so
+// their u32 sum cannot wrap below this.
+constexpr uint64_t SH_SPAN_MAX = (uint64_t)UINT32_MAX;
+
 void sh_count_reads_host(kmhg_index* idx, const ReadsHost& r, double min_ll, uint32_t source,
                          hipStream_t s) {
   const size_t n = r.n();
@@ -1501,8 +1554,17 @@ void sh_count_reads_host(kmhg_index* idx, const ReadsHost& r, double min_ll, uin
   HIPC(hipMemcpyAsync(dqual.p, r.qual.data(), nb, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(dhq.p, r.hasq.data(), n, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(doff.p, r.off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
-  sh_count_reads_device(idx, dseq.p, dqual.p, doff.p, dhq.p, (uint32_t)n, (double)nb / (double)n,
-                        min_ll, source, s);
+  // the device pass sizes its key stream by per-read window bounds summed in u32: batches of
+  // < SH_SPAN_MAX bases (offsets stay absolute, so a batch is a sub-range of the reads)
+  for (size_t i0 = 0; i0 < n;) {
+    size_t i1 = i0 + 1;
+    while (i1 < n && (uint64_t)(r.off[i1 + 1] - r.off[i0]) < SH_SPAN_MAX) ++i1;
+    const uint64_t span = (uint64_t)(r.off[i1] - r.off[i0]);
+    if (span >= SH_SPAN_MAX) fail(KMHG_EOVERFLOW, "a read of 2^32 or more bases");
+    sh_count_reads_device(idx, dseq.p, dqual.p, doff.p + i0, dhq.p + i0, (uint32_t)(i1 - i0),
+                          (double)span / (double)(i1 - i0), min_ll, source, s);
+    i0 = i1;
+  }
   HIPC(hipStreamSynchronize(s));                 // the host arrays are reused
 }
 
@@ -1781,6 +1843,189 @@ void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, 
   }
 }
 
+// ------------------------------------------------------------------ multi-device seq.kmer.pos
+// KMHG_DEVICES=d0,d1,... (SURVEY.md §5 "Config / flags"): the host-pointer seq.kmer.pos of the
+// R API (.Call("sequence_kmer_positions"), src/kmer_hash.c:1151-1172) is split over these
+// devices in one process, with the R signatures unchanged.  The index is replicated once per
+// device by peer copies over xGMI (the image: table + positions + code block), the query's
+// windows are cut into contiguous ranges (the multi-GPU shard unit of
+// kmhg_query_run_device_range), each device receives only its range's slice of the host
+// sequence (plus the neighbour chars the window rule reads) and queries it on its own host
+// thread, and the rows stay in each device's HBM until kmhg_query_fill copies every part
+// straight into the caller's buffer at its prefix offset.  Concatenation in range order is the
+// unsharded row order.
+void free_index(kmhg_index* idx);
+void free_query(kmhg_query* q);
+
+std::vector<int> query_devices() {
+  std::vector<int> out;
+  const char* e = std::getenv("KMHG_DEVICES");
+  if (!e || !*e) return out;
+  int n = 0;
+  HIPC(hipGetDeviceCount(&n));
+  const std::string str(e);
+  size_t a = 0;
+  while (a <= str.size()) {
+    size_t b = str.find(',', a);
+    if (b == std::string::npos) b = str.size();
+    const std::string tok = str.substr(a, b - a);
+    char* end = nullptr;
+    const long d = std::strtol(tok.c_str(), &end, 10);
+    if (tok.empty() || *end || d < 0 || d >= n)
+      fail(KMHG_EINVAL, "KMHG_DEVICES must list device ordinals (0.." + std::to_string(n - 1) +
+                            "), got \"" + str + "\"");
+    out.push_back((int)d);
+    a = b + 1;
+  }
+  return out;
+}
+
+// A copy of `home` on device `dev`, by peer copies (hipMemcpyPeerAsync: xGMI between MI355X
+// GPUs; a same-device copy when dev is home's own device).  Its diagonal-path bits and slot
+// tags are derived by its own first query, as for an imported image.
+kmhg_index* make_replica(kmhg_index* home, int dev) {
+  auto r = std::make_unique<kmhg_index>();
+  r->device = dev;
+  r->k = home->k; r->L = home->L; r->geom = home->geom;
+  r->U = home->U; r->N = home->N; r->P = home->P; r->max_n = home->max_n;
+  r->kmer_count = home->kmer_count;
+  r->row_order = home->row_order;
+  DeviceGuard g(dev);
+  hipStream_t s = lib_stream();
+  r->stream = s;
+  r->table.reset(home->slots());
+  HIPC(hipMemcpyPeerAsync(r->table.p, dev, home->table.p, home->device,
+                          home->slots() * sizeof(Slot), s));
+  if (home->N) {
+    r->positions.reset(home->N);
+    HIPC(hipMemcpyPeerAsync(r->positions.p, dev, home->positions.p, home->device, home->N * 4,
+                            s));
+  }
+  if (home->dcodes.p) {
+    const uint64_t w = diag_block_words(home->L - home->k + 1);
+    r->dcodes.reset(w);
+    HIPC(hipMemcpyPeerAsync(r->dcodes.p, dev, home->dcodes.p, home->device, w * 8, s));
+  }
+  HIPC(hipStreamSynchronize(s));
+  return r.release();
+}
+
+kmhg_index* replica_for(kmhg_index* home, int part, int dev) {
+  {
+    std::lock_guard<std::mutex> lk(home->rep_mu);
+    auto it = home->replicas.find(part);
+    if (it != home->replicas.end() && it->second->device == dev) return it->second;
+  }
+  kmhg_index* r = make_replica(home, dev);          // outside the lock: parts copy in parallel
+  kmhg_index* old = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(home->rep_mu);
+    auto& slot = home->replicas[part];
+    old = slot;                                     // a replica on another device (env changed)
+    slot = r;
+  }
+  if (old) free_index(old);
+  return r;
+}
+
+kmhg_query* query_multi_device(kmhg_index* idx, const char* seq, int64_t L, int k,
+                               const std::vector<int>& devs) {
+  {
+    DeviceGuard g(idx->device);
+    finish_build(idx);
+    if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
+  }
+  const int G = (int)devs.size();
+  const int64_t Nw = L - k + 1;
+  auto q = std::make_unique<kmhg_query>();
+  q->device = idx->device;
+  std::vector<kmhg_query*> parts(G, nullptr);
+  std::vector<Error> errs(G, Error{KMHG_OK, ""});
+  const bool poison = std::getenv("KMHG_SLICE_POISON") != nullptr;   // tests: garbage outside
+  auto run = [&](int i) {
+    try {
+      const int64_t w0 = Nw * i / G, w1 = Nw * (i + 1) / G;
+      kmhg_index* use = (i == 0 && devs[0] == idx->device) ? idx : replica_for(idx, i, devs[i]);
+      DeviceGuard g(devs[i]);
+      hipStream_t s = lib_stream();
+      // a full-length buffer holding only chars [a, b): the window rule of windows [w0, w1)
+      // reads chars [w0 - 1, w1 + k - 1); the tile stage's aligned loads and halo read a few
+      // more around them, which feed only windows outside the range
+      const int64_t a = std::max<int64_t>(0, (w0 & ~15ll) - 64);
+      const int64_t b = std::min<int64_t>(L, w1 + k + 64);
+      DBuf<uint8_t> d((size_t)L + 16, s);
+      if (poison) HIPC(hipMemsetAsync(d.p, 'A', (size_t)L + 16, s));
+      if (b > a) HIPC(hipMemcpyAsync(d.p + a, seq + a, (size_t)(b - a), hipMemcpyHostToDevice, s));
+      parts[i] = query_device(use, d.p, L, k, w0, w1, s);
+      HIPC(hipStreamSynchronize(s));
+    } catch (const Error& e) {
+      errs[i] = e;
+    } catch (const std::bad_alloc&) {
+      errs[i] = Error{KMHG_ENOMEM, "host allocation failed"};
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < G; ++i) th.emplace_back(run, i);
+  run(0);
+  for (auto& t : th) t.join();
+  q->parts = parts;                                  // freed with q, also on the error path
+  for (int i = 0; i < G; ++i)
+    if (errs[i].code != KMHG_OK) {
+      free_query(q.release());
+      fail(errs[i].code, errs[i].msg);
+    }
+  int64_t off = 0;
+  for (auto* p : parts) {
+    q->part_off.push_back(off);
+    off += p->H;
+  }
+  q->H = off;
+  return q.release();
+}
+
+// The rows of a multi-device query on its home device (peer copies, once), for the readers
+// that want one device buffer (kmhg_query_rows_device).
+void gather_parts(kmhg_query* q) {
+  if (q->parts.empty() || q->gathered) return;
+  DeviceGuard g(q->device);
+  hipStream_t s = lib_stream();
+  q->rows.reset((size_t)std::max<int64_t>(q->H, 1));
+  for (size_t i = 0; i < q->parts.size(); ++i)
+    if (q->parts[i]->H)
+      HIPC(hipMemcpyPeerAsync(q->rows.p + q->part_off[i], q->device, q->parts[i]->rows.p,
+                              q->parts[i]->device, (size_t)q->parts[i]->H * 8, s));
+  HIPC(hipStreamSynchronize(s));
+  q->stream = s;
+  q->gathered = true;
+}
+
+void free_query(kmhg_query* q) {
+  if (!q) return;
+  for (auto* p : q->parts) free_query(p);
+  DeviceGuard g(q->device);
+  // the caller keeps its stream alive until here (a multi-device query's own rows exist only
+  // once gathered, on the library stream)
+  if (q->parts.empty() || q->gathered) HIPC(hipStreamSynchronize(q->stream));
+  q->rows.ordered = false;                 // its stream is idle: straight back to the pool
+  delete q;
+}
+
+void free_index(kmhg_index* idx) {
+  if (!idx) return;
+  for (auto& kv : idx->replicas) free_index(kv.second);
+  idx->replicas.clear();
+  DeviceGuard g(idx->device);
+  if (idx->pending) {                  // never used: no need to wait, the record is recycled
+    PinnedPool::get().give(idx->rec, true);   // once the build's event has completed
+    idx->pending = false;
+  }
+  // stream-ordered release: the buffers return to the pool once work queued on the index's
+  // last stream has finished (queries on other streams are synchronised by their callers)
+  ReleaseGroup rg(idx->stream);
+  idx->bind_all(idx->stream);
+  delete idx;
+}
+
 }  // namespace
 
 // ============================================================================ C-ABI
@@ -1816,19 +2061,7 @@ int kmhg_build_device(const void* d_seq, size_t L, int k, int do_sort, void* str
 }
 
 int kmhg_free(kmhg_index* idx) {
-  return guarded([&] {
-    if (!idx) return;
-    DeviceGuard g(idx->device);
-    if (idx->pending) {                  // never used: no need to wait, the record is recycled
-      PinnedPool::get().give(idx->rec, true);   // once the build's event has completed
-      idx->pending = false;
-    }
-    // stream-ordered release: the buffers return to the pool once work queued on the index's
-    // last stream has finished (queries on other streams are synchronised by their callers)
-    ReleaseGroup rg(idx->stream);
-    idx->bind_all(idx->stream);
-    delete idx;
-  });
+  return guarded([&] { free_index(idx); });
 }
 
 // count.kmers: windows never span two sequences of the character vector, so a batch is the
@@ -2097,6 +2330,10 @@ int kmhg_sh_count_reads_device(kmhg_index** sh, const void* d_seq, const void* d
       HIPC(hipMemcpyAsync(&ends[1], d_offsets + n_reads, 8, hipMemcpyDeviceToHost, s));
       HIPC(hipStreamSynchronize(s));
       mean_len = (double)(ends[1] - ends[0]) / (double)n_reads;
+      // the key stream is sized by per-read window bounds (each <= the read's length) summed in
+      // u32: a batch spanning 2^32 or more bases could wrap that sum
+      if (ends[1] < ends[0] || (uint64_t)(ends[1] - ends[0]) >= SH_SPAN_MAX)
+        fail(KMHG_EINVAL, "a read batch must span fewer than 2^32 bases: split it");
     }
     sh_count_reads_device(c, (const uint8_t*)d_seq, (const uint8_t*)d_qual, d_offsets,
                           d_has_qual, (uint32_t)n_reads, mean_len, min_ll, source, s);
@@ -2342,6 +2579,12 @@ int kmhg_query_run(kmhg_index* idx, const char* seq, size_t L, int k, kmhg_query
     if (!idx || !seq || !q) fail(KMHG_EINVAL, "null argument");
     L = effective_len(seq, L);
     check_query_args(L, k);
+    const std::vector<int> devs = query_devices();
+    if (devs.size() > 1 && idx->sources == 0) {   // position index over several devices
+      *q = query_multi_device(idx, seq, (int64_t)L, k, devs);
+      if (n_rows) *n_rows = (*q)->H;
+      return;
+    }
     DeviceGuard g(idx->device);
     hipStream_t s = lib_stream();
     DBuf<uint8_t> d(L + 16, s);
@@ -2384,6 +2627,26 @@ int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
     if (!q) fail(KMHG_EINVAL, "null query");
     if (!q->H) return;
     if (!rows) fail(KMHG_EINVAL, "null output");
+    if (!q->parts.empty() && !q->gathered) {   // every part straight into its rows, in parallel
+      std::vector<Error> errs(q->parts.size(), Error{KMHG_OK, ""});
+      auto copy = [&](size_t i) {
+        try {
+          kmhg_query* p = q->parts[i];
+          if (!p->H) return;
+          DeviceGuard g(p->device);
+          d2h_host(rows + 2 * q->part_off[i], p->rows.p, (size_t)p->H * 8, lib_stream());
+        } catch (const Error& e) {
+          errs[i] = e;
+        }
+      };
+      std::vector<std::thread> th;
+      for (size_t i = 1; i < q->parts.size(); ++i) th.emplace_back(copy, i);
+      copy(0);
+      for (auto& t : th) t.join();
+      for (auto& e : errs)
+        if (e.code != KMHG_OK) fail(e.code, e.msg);
+      return;
+    }
     DeviceGuard g(q->device);
     hipStream_t s = lib_stream();
     d2h_host(rows, q->rows.p, (size_t)q->H * 8, s);
@@ -2393,6 +2656,7 @@ int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
 int kmhg_query_rows_device(kmhg_query* q, const int32_t** d_rows) {
   return guarded([&] {
     if (!q || !d_rows) fail(KMHG_EINVAL, "null argument");
+    gather_parts(q);
     *d_rows = reinterpret_cast<const int32_t*>(q->rows.p);
   });
 }
@@ -2404,6 +2668,14 @@ int kmhg_query_copy_device(kmhg_query* q, void* d_dst, void* stream) {
     if (!d_dst) fail(KMHG_EINVAL, "null output");
     DeviceGuard g(q->device);
     hipStream_t s = (hipStream_t)stream;
+    if (!q->parts.empty() && !q->gathered) {   // peer copies of the (finished) parts
+      for (size_t i = 0; i < q->parts.size(); ++i)
+        if (q->parts[i]->H)
+          HIPC(hipMemcpyPeerAsync(static_cast<int2*>(d_dst) + q->part_off[i], q->device,
+                                  q->parts[i]->rows.p, q->parts[i]->device,
+                                  (size_t)q->parts[i]->H * 8, s));
+      return;
+    }
     if (s != q->stream) {   // order after the emit kernel queued on q->stream
       hipEvent_t ev;
       HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -2416,13 +2688,7 @@ int kmhg_query_copy_device(kmhg_query* q, void* d_dst, void* stream) {
 }
 
 int kmhg_query_free(kmhg_query* q) {
-  return guarded([&] {
-    if (!q) return;
-    DeviceGuard g(q->device);
-    HIPC(hipStreamSynchronize(q->stream));   // the caller keeps its stream alive until here
-    q->rows.ordered = false;                 // its stream is idle: straight back to the pool
-    delete q;
-  });
+  return guarded([&] { free_query(q); });
 }
 
 int kmhg_image_sizes_get(const kmhg_index* cidx, kmhg_image_sizes* sz, int64_t header[8]) {

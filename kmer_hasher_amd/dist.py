@@ -78,14 +78,52 @@ def gather_rows(local: torch.Tensor, dst: int = 0, group=None) -> torch.Tensor |
     return None
 
 
-def sharded_query(engine, seq: torch.Tensor, k: int, dst: int = 0, group=None):
-    """seq.kmer.pos with the query windows split across ranks; rows gathered on `dst`."""
+def broadcast_sequence(seq: torch.Tensor | None, src: int, device: torch.device,
+                       group=None) -> torch.Tensor:
+    """C1: the root's uint8 sequence on every rank (its length first, then one
+    broadcast of the bytes; over RCCL the root fans out on its xGMI links)."""
+    rank = dist.get_rank(group)
+    n = torch.zeros(1, dtype=torch.int64, device=device)
+    if rank == src:
+        n[0] = seq.numel()
+    dist.broadcast(n, src, group=group)
+    out = seq if rank == src else torch.empty(int(n.item()), dtype=torch.uint8, device=device)
+    dist.broadcast(out, src, group=group)
+    return out
+
+
+def sharded_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, group=None,
+                  src: int | None = None, timings: dict | None = None):
+    """seq.kmer.pos with the query windows split across ranks; rows gathered on `dst`.
+
+    src=None: every rank already holds the whole query.  src=r: only rank r holds it (the R
+    session's query string arrives on one process) and it is broadcast first (C1).  `timings`
+    (optional) receives the seconds of each phase as seen by this rank: 'broadcast', 'query'
+    (the HIP range query) and 'gather'."""
+    import time
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+
+    def mark():
+        if timings is not None and seq is not None and seq.is_cuda:
+            torch.cuda.synchronize(seq.device)
+        return time.perf_counter()
+
+    t0 = mark()
+    if src is not None:
+        dev = seq.device if seq is not None else torch.device("cuda", torch.cuda.current_device())
+        seq = broadcast_sequence(seq, src, dev, group)
+    t1 = mark()
     n_windows = max(0, seq.numel() - k + 1)
     w0, w1 = shard_ranges(n_windows, world)[rank]
     local = engine.query_range(seq, k, w0, w1)
-    return gather_rows(local, dst, group)
+    t2 = mark()
+    rows = gather_rows(local, dst, group)
+    t3 = mark()
+    if timings is not None:
+        for name, dt in (("broadcast", t1 - t0), ("query", t2 - t1), ("gather", t3 - t2)):
+            timings[name] = timings.get(name, 0.0) + dt
+    return rows
 
 
 class HipQueryEngine:

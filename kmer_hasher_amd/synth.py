@@ -7,7 +7,8 @@ return ``numpy.uint8`` arrays of ASCII bases, and never touch the network or the
   add_n_runs(seq, frac, seed)        N-runs of length 1..100 covering ~frac of the bases
   add_lowercase(seq, frac, seed)     flips ~frac of the bases to lower case
   add_ambiguity(seq, frac, seed)     sprinkles IUPAC codes / '-' / '.' (encoded, not skipped)
-  repeat_rich(L, seed)               config 4: tandem arrays + interspersed families + N gaps
+  repeat_rich(L, seed)               tandem arrays + interspersed families + N gaps
+  config4(L, seed)                   config 4's sequence (repeat_rich tuned into the P band)
   derived(A, seed)                   config 5's B: SNVs, inversions, translocations, N-runs
 """
 from __future__ import annotations
@@ -114,6 +115,13 @@ def repeat_rich(L: int = 40_000_000, seed: int = 3, tandem_frac: float = 0.05,
     for g in range(n_gap_every, L - 100, n_gap_every):
         s[g:g + 100] = ord("N")
     return s
+
+
+def config4(L: int = 40_000_000, seed: int = 3) -> np.ndarray:
+    """BASELINE.json configs[3]: the repeat-rich sequence with the family share raised to 50 %,
+    which puts the 40 Mbp, k=31, seed-3 pair count at P = 685,613,382 (max n 14,097), inside
+    SURVEY.md §8(d)'s band P in [0.5e9, 1.5e9] (the 40 % default gives 4.75e8)."""
+    return repeat_rich(L, seed, family_frac=0.5)
 
 
 def derived(A: np.ndarray, seed: int = 5, snv: float = 0.01, n_rearr: int = 20,

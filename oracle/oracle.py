@@ -86,6 +86,10 @@ def _ref():
                                   C.c_int, C.POINTER(C.c_int)]
         lib.ref_kmer_count.restype = C.c_long
         lib.ref_kmer_count.argtypes = [C.c_void_p]
+        lib.ref_rows_chunk.restype = C.c_long
+        lib.ref_rows_chunk.argtypes = [C.c_void_p, C.c_uint, i64p, i32p, C.c_long]
+        lib.ref_totals.argtypes = [C.c_void_p, C.POINTER(C.c_long), C.POINTER(C.c_long),
+                                   C.POINTER(C.c_long)]
         _REF = lib
     return _REF
 
@@ -293,6 +297,45 @@ class RefIndex:
         if opt & 8:
             out["count"] = take(r.counts, r.n_counts, np.int32)
         return out
+
+    def time_positions(self, opt: int) -> tuple[float, int, int]:
+        """kmer_positions(opt) timed alone (the C bucket walk into flat arrays, as the R
+        matrices are filled); the arrays are freed without being copied.  Returns (seconds,
+        pos rows, pair rows)."""
+        import time
+        lib = _ref()
+        r = _RefPos()
+        t0 = time.perf_counter()
+        lib.ref_positions(self.h, opt, C.byref(r))
+        t = time.perf_counter() - t0
+        for p in (r.kmers, r.pos, r.pairs, r.counts):
+            if p:
+                lib.ref_free(p)
+        return t, int(r.n_pos), int(r.n_pairs)
+
+    def totals(self) -> tuple[int, int, int]:
+        """(N, P, max n) over the live buckets."""
+        n, p, m = C.c_long(0), C.c_long(0), C.c_long(0)
+        _ref().ref_totals(self.h, C.byref(n), C.byref(p), C.byref(m))
+        return int(n.value), int(p.value), int(m.value)
+
+    def rows_sha256(self, opt: int, chunk_rows: int = 1 << 24) -> tuple[str, int]:
+        """sha256 of kmer.pos's $pos (opt 2) or $pair.pos (opt 4) R-matrix data in the
+        reference's khash order, streamed from the bucket walk (ref_rows_chunk) so pair tables
+        of many GB are digested without being held.  Returns (hexdigest, rows)."""
+        import hashlib
+        width = 2 if opt == 2 else 3
+        st = np.zeros(5, np.int64)
+        buf = np.empty(width * chunk_rows, np.int32)
+        h = hashlib.sha256()
+        rows = 0
+        while True:
+            n = _ref().ref_rows_chunk(self.h, opt, st, buf, chunk_rows)
+            if n == 0:
+                break
+            h.update(memoryview(buf[:width * n]))
+            rows += n
+        return h.hexdigest(), rows
 
     @classmethod
     def counts(cls, seqs, k: int, source: int, source_n: int, into: "RefIndex | None" = None):

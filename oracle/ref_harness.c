@@ -108,6 +108,47 @@ int ref_positions(void *h, unsigned opt, ref_pos_result *r) {
   return 0;
 }
 
+/* The same bucket walk, streamed in chunks so a full-size pair.pos (config 4: ~7e8 rows, 8 GB)
+ * can be digested without materialising it.  opt = 2 (pos rows, 2 ints) or 4 (pair rows, 3
+ * ints).  st[0..4] = {bucket, label i of that bucket, j, m, entered}: zero it before the first
+ * call.  Writes at most cap rows into out and returns the number written (0 = walk finished). */
+long ref_rows_chunk(void *h, unsigned opt, long *st, int *out, long cap) {
+  khash_t(kmer_h) *hash = ((khash_ptr *)h)->hash;
+  long it = st[0], i = st[1], j = st[2], m = st[3], entered = st[4], b = 0;
+  while (it < (long)kh_end(hash) && b < cap) {
+    if (!kh_exist(hash, (khiter_t)it)) { ++it; continue; }
+    const kmer_pos_t *kv = &kh_val(hash, (khiter_t)it);
+    long n = (long)kv->v.n;
+    if (!entered) { ++i; j = 0; m = 1; entered = 1; }
+    if (opt == 2) {
+      for (; j < n && b < cap; ++j, ++b) { out[2 * b] = (int)i; out[2 * b + 1] = kv->v.a[j]; }
+      if (j >= n) { ++it; entered = 0; }
+    } else {
+      while (j < n && b < cap) {
+        for (; m < n && b < cap; ++m, ++b) {
+          out[3 * b] = (int)i; out[3 * b + 1] = kv->v.a[j]; out[3 * b + 2] = kv->v.a[m];
+        }
+        if (m >= n) { ++j; m = j + 1; }
+      }
+      if (j >= n) { ++it; entered = 0; }
+    }
+  }
+  st[0] = it; st[1] = i; st[2] = j; st[3] = m; st[4] = entered;
+  return b;
+}
+
+/* sum C(n,2), max n and N over the live buckets (sizes of the streamed walk) */
+void ref_totals(void *h, long *n_pos, long *n_pairs, long *max_n) {
+  khash_t(kmer_h) *hash = ((khash_ptr *)h)->hash;
+  long np = 0, pp = 0, mx = 0;
+  for (khiter_t it = kh_begin(hash); it != kh_end(hash); ++it) {
+    if (!kh_exist(hash, it)) continue;
+    long n = (long)kh_val(hash, it).v.n;
+    np += n; pp += n * (n - 1) / 2; if (n > mx) mx = n;
+  }
+  *n_pos = np; *n_pairs = pp; *max_n = mx;
+}
+
 /* seq.kmer.pos: returns 2 x n rows (i_end, j_start), column-major, as the R matrix data. */
 int ref_query(void *h, const char *seq, int k, long *n_rows, int **rows) {
   if ((long)strlen(seq) <= k || k > 31) return 3;

@@ -1,0 +1,52 @@
+"""Boundary option / error paths on the GPU: do.sort=TRUE through the
+C-ABI, and real results of more than 2^31-1 rows (R's int ncol, reference src/kmer_hash.c:1133,
+README.md:80-89) refused with the documented error instead of overflowing."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_do_sort_true_matches_oracle(gpu, testfa):
+    from kmer_hasher_amd import kmer_pos, make_kmer_hash, seq_kmer_pos, synth
+    rr = synth.add_n_runs(synth.repeat_rich(300_000, 12, n_gap_every=60_000), 0.001, 13)
+    for s, k in ((testfa, 15), (rr.tobytes().decode("latin-1"), 21)):
+        oi = O.OracleIndex(s, k)
+        for ds in (True, 1, False):
+            ptr = make_kmer_hash(s, k, do_sort=ds)
+            res = kmer_pos(ptr, 15)
+            assert np.array_equal(res["count"], oi.counts)
+            assert np.array_equal(res["pos"].reshape(-1), oi.pos_rows())
+            assert np.array_equal(res["pair.pos"].reshape(-1), oi.pair_rows())
+            assert np.array_equal(seq_kmer_pos(ptr, s, k).reshape(-1), oi.query(s, k))
+            ptr.free()
+
+
+def test_pair_rows_over_int_max_raise(gpu):
+    """One k-mer seen ~70,000 times: P = C(n, 2) ~ 2.45e9 > 2^31 - 1."""
+    from kmer_hasher_amd import kmer_pos, make_kmer_hash
+    from kmer_hasher_amd.api import KmerHashError
+    ptr = make_kmer_hash("A" * 70_001, 1)
+    inf = ptr.info()
+    n = inf.n_positions
+    assert inf.n_kmers == 1 and inf.n_pairs == n * (n - 1) // 2 > 2**31 - 1
+    with pytest.raises(KmerHashError, match="2\\^31-1 columns"):
+        kmer_pos(ptr, 4)
+    res = kmer_pos(ptr, 10)                     # pos + count alone are fine
+    assert res["count"].tolist() == [n]
+    ptr.free()
+
+
+def test_query_rows_over_int_max_raise(gpu):
+    """~46,343 windows of one k-mer against an index holding it ~46,342 times: H > 2^31 - 1
+    (the device holds the 17 GB of rows; the host copy is refused)."""
+    from kmer_hasher_amd import make_kmer_hash, seq_kmer_pos
+    from kmer_hasher_amd.api import KmerHashError
+    ptr = make_kmer_hash("A" * 46_342, 1)
+    n = ptr.info().n_positions
+    assert n * len(O.windows("A" * 46_343, 1)[0]) > 2**31 - 1
+    with pytest.raises(KmerHashError, match="2\\^31-1 columns"):
+        seq_kmer_pos(ptr, "A" * 46_343, 1)
+    ptr.free()
