@@ -51,17 +51,29 @@ CONFIGS = {
 }
 
 
-# HIP-event labels (kmhg_timing_*) -> kernel names as rocprofv3 reports them
-PMC_NAME = {"k_v2_scatter_seq": "k_v2_scatter<true, false, false>",
-            "k_v2_scatter": "k_v2_scatter<false, false, false>",
-            "k_v2_bucket_wg": "k_v2_bucket_wg<false>",
-            "k_query_probe": "k_query_probe<true>"}
+# HIP-event labels (kmhg_timing_*) -> the kernel names rocprofv3 reports (template instances in
+# full, and the variant a label launches: e.g. k_v2_hist0 runs k_v2_hist0p<true>)
+PMC_PREFIX = {"k_v2_scatter_seq": ("k_v2_scatter<true",),
+              "k_v2_scatter": ("k_v2_scatter<false",),
+              "k_v2_hist0": ("k_v2_hist0p<", "k_v2_hist0("),
+              "k_v2_hist": ("k_v2_hist<",),
+              "k_scan_u32": ("k_scan_lb_u32",),
+              "k_v2_bounds": ("k_v2_bounds_lo", "k_v2_bounds"),
+              "k_v2_bucket_wg": ("k_v2_bucket_wg<false",),
+              "k_query_probe": ("k_query_probe<",),
+              "k_read_pairs": ("k_read_pairs",), "k_read_pos": ("k_read_pos",),
+              "k_read_keys": ("k_read_keys",)}
 
 
 def pmc_traffic(pmc: dict, kernel: str):
-    """HBM bytes per launch of `kernel` from a profiles/pmc_*.json summary (rocprofv3 names
-    template instances in full)."""
-    return pmc.get(PMC_NAME.get(kernel, kernel), {}).get("hbm_bytes_per_launch")
+    """HBM bytes per launch of `kernel` from a profiles/pmc_*.json summary."""
+    if kernel in pmc and isinstance(pmc[kernel], dict):
+        return pmc[kernel].get("hbm_bytes_per_launch")
+    for pre in PMC_PREFIX.get(kernel, ()):
+        for name, v in pmc.items():
+            if isinstance(v, dict) and (name.startswith(pre) or name + "(" == pre):
+                return v.get("hbm_bytes_per_launch")
+    return None
 
 
 def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) -> int | None:

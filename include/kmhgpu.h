@@ -22,6 +22,11 @@
  *           (+ seq_kmer_positions, src/kmer_pos.c:110-136)
  *   kmhg_count / kmhg_count_device
  *        <- .Call("count_kmers", hash.ptr, params, seq)       src/kmer_hash.c:548-591
+ *   kmhg_build_device_part / kmhg_part_info / kmhg_part_export
+ *        <- the owner-computes partition of the reader pool  src/kmer_reader.c:28-39, 101-108
+ *           (multi-GPU make.kmer.hash; no single reference entry point)
+ *   KMHG_DEVICES=d0,d1,... (environment): kmhg_query_run splits seq.kmer.pos over those devices
+ *           (index peer-copied once per device, rows copied straight into the caller's buffer)
  *   registration of the three symbols with arities 3/2/3    src/kmer_hash.c:1205-1224
  *           is done by the R glue (kmer_hasher_amd/R/kmer_hash_glue.c) over this ABI.
  *
@@ -249,6 +254,25 @@ int kmhg_image_export(const kmhg_index *idx, void *d_table, void *d_positions, v
                       void *stream);
 int kmhg_image_import(const int64_t header[8], const void *d_table, const void *d_positions,
                       const void *d_codes, void *stream, kmhg_index **out);
+
+/* Owner-computes multi-GPU build (the reference's own partition pattern, every
+ * reader thread inserting only the k-mers it owns, src/kmer_reader.c:28-39): part `part` of
+ * `n_parts` walks every window of the (broadcast) sequence but keeps only the k-mers whose hash
+ * bucket lies in its contiguous range [b0, b0 + nb) of the whole table's buckets, so each k-mer
+ * is built on exactly one device, its positions ascending, with no all-to-all.  The parts,
+ * concatenated in bucket order (positions in part order, list ends rebased by each part's first
+ * position index), ARE the single-device index: the caller gathers them (RCCL) and imports the
+ * result with kmhg_image_import.  A part index refuses queries and readout.
+ *   info = {b0, nb, nb_total, slots per bucket, positions N, distinct k-mers U, pairs P, max n,
+ *           owns the side slot (key ~0 at k = 32) 0/1, code block bytes}
+ *   export: d_table <- its nb x capb slots with count >= 2 list ends + pos_base; d_side_slot <-
+ *   its side slot (16 B; meaningful when it owns it); d_positions <- its N int32 positions;
+ *   d_codes <- the sequence's code block (every part computes the same one).  Synchronous. */
+int kmhg_build_device_part(const void *d_seq, size_t L, int k, int part, int n_parts,
+                           void *stream, kmhg_index **out);
+int kmhg_part_info(kmhg_index *idx, int64_t info[10]);
+int kmhg_part_export(kmhg_index *idx, int64_t pos_base, void *d_table, void *d_side_slot,
+                     void *d_positions, void *d_codes, void *stream);
 
 /* Per-kernel HIP-event timing (KMHG_TIMING=1 also enables it).  The report is JSON:
  * {"kernel": [launches, total_ms], ...}; events are recorded on the kernels' own stream. */

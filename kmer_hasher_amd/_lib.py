@@ -86,6 +86,10 @@ _PROTOS = {
     "kmhg_image_sizes_get": (C.c_int, [vp, C.POINTER(ImageSizes), i64p]),
     "kmhg_image_export": (C.c_int, [vp, vp, vp, vp, vp]),
     "kmhg_image_import": (C.c_int, [i64p, vp, vp, vp, vp, C.POINTER(vp)]),
+    "kmhg_build_device_part": (C.c_int, [vp, C.c_size_t, C.c_int, C.c_int, C.c_int, vp,
+                                         C.POINTER(vp)]),
+    "kmhg_part_info": (C.c_int, [vp, i64p]),
+    "kmhg_part_export": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp]),
     "kmhg_timing_enable": (C.c_int, [C.c_int]),
     "kmhg_timing_select": (C.c_int, [C.c_char_p]),
     "kmhg_timing_reset": (C.c_int, []),

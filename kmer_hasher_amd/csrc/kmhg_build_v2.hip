@@ -71,12 +71,24 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ uint32_t div_magic(uint32_t x, uint64_t m) {
   return m ? (uint32_t)__umul64hi((uint64_t)x, m) : x;
 }
-__device__ __forceinline__ uint32_t digit_of_h(uint64_t h, uint32_t nb, const Digit& D) {
-  const uint32_t q = div_magic(bucket_of(h, nb), D.mdiv);
+// The bucket of hash h inside this build's part (Geom: whole table b0 = 0, nbh = nb); a key of
+// another part's range gives a value >= g.nb (unsigned wrap below b0).
+__device__ __forceinline__ uint32_t bucket_local(uint64_t h, const Geom& g) {
+  return bucket_of(h, g.nbh ? g.nbh : g.nb) - g.b0;
+}
+__device__ __forceinline__ bool in_part(uint64_t h, const Geom& g) {
+  return bucket_local(h, g) < g.nb;
+}
+// the side slot (key ~0 at k = 32) belongs to the bucket of mix64(~0) of the whole table
+__device__ __forceinline__ bool side_bucket(uint32_t b, const Geom& g) {
+  return b + g.b0 == bucket_of(mix64(EMPTY_KEY), g.nbh ? g.nbh : g.nb);
+}
+__device__ __forceinline__ uint32_t digit_of_h(uint64_t h, const Geom& g, const Digit& D) {
+  const uint32_t q = div_magic(bucket_local(h, g), D.mdiv);
   return q - div_magic(q, D.mR) * D.R;
 }
-__device__ __forceinline__ uint32_t digit_of(uint64_t key, uint32_t nb, const Digit& D) {
-  return digit_of_h(mix64(key), nb, D);
+__device__ __forceinline__ uint32_t digit_of(uint64_t key, const Geom& g, const Digit& D) {
+  return digit_of_h(mix64(key), g, D);
 }
 
 // Lanes of the wave holding the same `v` (nbits wide) among active lanes: one ballot per bit.
@@ -138,7 +150,10 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
       const int w = j * BLOCK + threadIdx.x;
       const int64_t s = tile0 + w;
       uint64_t key = 0;
-      if (s < Nw && window_key(st, HALO + w, s, L, k, key)) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
+      if (s < Nw && window_key(st, HALO + w, s, L, k, key)) {
+        const uint64_t h = mix64(key);
+        if (in_part(h, g)) atomicAdd(&lh[digit_of_h(h, g, D)], 1u);
+      }
     }
   }
   __syncthreads();
@@ -188,7 +203,10 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
       const int w = j * BLOCK + threadIdx.x;
       const int64_t s = tile0 + w;
       uint64_t key = 0;
-      if (s < Nw && window_key(st, HALO + w, s, L, k, key)) atomicAdd(&lh[digit_of(key, g.nb, D)], 1u);
+      if (s < Nw && window_key(st, HALO + w, s, L, k, key)) {
+        const uint64_t h = mix64(key);
+        if (in_part(h, g)) atomicAdd(&lh[digit_of_h(h, g, D)], 1u);
+      }
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) {
@@ -316,7 +334,7 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
       const uint64_t key = in[j] ? keys[e + j * BLOCK] : 0ull;
       if (skip_empty && key == EMPTY_KEY) in[j] = false;      // a padded read's unused slot
       const uint64_t h = in[j] ? mix64(key) : 1ull;
-      dg[j] = in[j] ? digit_of_h(h, g.nb, D) : 0u;
+      dg[j] = in[j] ? digit_of_h(h, g, D) : 0u;
       if (HLL && (h & ((1u << HLL_SAMPLE_BITS) - 1)) == 0)
         atomicMax(&hreg[(uint32_t)(h >> HLL_SAMPLE_BITS) & (HLL_REGS - 1)],
                   (uint32_t)__clzll(h | ((1ull << (HLL_SAMPLE_BITS + 8)) - 1)) + 1u);
@@ -572,7 +590,9 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       } else {
         act[c] = e < n && !(KEYS0 && skip_empty && key[c] == EMPTY_KEY);
       }
-      dg[c] = act[c] ? digit_of(key[c], g.nb, D) : 0;
+      const uint64_t h = mix64(key[c]);
+      if (FROM_SEQ) act[c] = act[c] && in_part(h, g);      // a part build keeps its buckets
+      dg[c] = act[c] ? digit_of_h(h, g, D) : 0;
     }
 #pragma unroll
     for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
@@ -666,10 +686,10 @@ k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_pt
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t i = c0 + (uint64_t)j * 64 + lane;
-      bk[j] = i < n ? bucket_of(mix64(keys[i]), g.nb) : g.nb;
+      bk[j] = i < n ? bucket_local(mix64(keys[i]), g) : g.nb;
     }
     int64_t before = -1;                       // bucket of element c0 - 1
-    if (c0) before = (int64_t)bucket_of(mix64(keys[c0 - 1]), g.nb);
+    if (c0) before = (int64_t)bucket_local(mix64(keys[c0 - 1]), g);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t i = c0 + (uint64_t)j * 64 + lane;
@@ -709,7 +729,7 @@ k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ 
   __syncthreads();
   const uint32_t tile = P / PTILE;
   for (uint32_t i = tile * PTILE + threadIdx.x; i < P; i += BLOCK)
-    atomicAdd(&cnt[digit_of(kprev[i], g.nb, Dlast)], 1u);
+    atomicAdd(&cnt[digit_of(kprev[i], g, Dlast)], 1u);
   __syncthreads();
   for (uint32_t hi = threadIdx.x; hi < R; hi += BLOCK) {
     const uint64_t b = (uint64_t)hi * div + lo;
@@ -889,7 +909,7 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
     const uint2 c = W.cc[j];
     *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
   }
-  if (lane == 0 && b == bucket_of(mix64(EMPTY_KEY), g.nb)) {
+  if (lane == 0 && side_bucket(b, g)) {
     const uint2 c = W.cc[V2_CAPB];
     *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
   }
@@ -1084,7 +1104,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     const uint2 c = W.cc[j];
     *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
   }
-  if (threadIdx.x == 0 && b == bucket_of(mix64(EMPTY_KEY), g.nb)) {
+  if (threadIdx.x == 0 && side_bucket(b, g)) {
     const uint2 c = W.cc[V2_CAPW];
     *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
   }
@@ -1359,7 +1379,7 @@ k_v2_bucket_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__
     st.max_count = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
     st.n_pairs = sh[4] + sh[5] + sh[6] + sh[7];
     bstats[b] = st;
-    if (b == bucket_of(mix64(EMPTY_KEY), g.nb))   // no window of this bucket is key ~0
+    if (side_bucket(b, g))   // no window of this bucket is key ~0
       *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
   }
   STAMP_WG(b, 6);

@@ -27,9 +27,14 @@ struct alignas(16) Slot {
 };
 
 // Table geometry: nb buckets x capb slots, plus one side slot at index nb*capb (kmhg_device.h).
+// A part build (owner-computes multi-GPU build) holds buckets [b0, b0 + nb) of a table of nbh
+// buckets: keys hash over nbh buckets, the part's arrays are indexed by bucket - b0.  A whole
+// table has b0 = 0 and nbh = 0 (= nb).
 struct Geom {
   uint32_t nb;
   uint32_t capb;
+  uint32_t b0 = 0;
+  uint32_t nbh = 0;
 };
 
 // Build-time tile geometry: one workgroup = 256 lanes x WPT windows, staged through LDS.

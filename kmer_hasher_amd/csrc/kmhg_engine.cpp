@@ -604,6 +604,9 @@ struct kmhg_index {
   DBuf<uint8_t> ptag;             // one tag byte per table slot (0 = empty)
   // ps_ready: published (release) after the preparing query's synchronize; read (acquire) by
   // later queries, possibly on other threads, before they use ptag / the uniq bits
+  // part of an owner-computes build (kmhg_build_device_part): holds buckets
+  // [geom.b0, geom.b0 + geom.nb) of a table of geom.nbh buckets; exported, never queried
+  bool is_part = false;
   std::atomic<bool> ps_ready{false};
   // copies of this index on other devices for multi-device queries (KMHG_DEVICES), keyed by
   // the query part they serve; made on first use by peer copies over xGMI, freed with the index
@@ -753,7 +756,7 @@ int co_spread_for(double distinct, uint64_t total) {
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
                             const uint64_t* d_keys = nullptr, int64_t n_keys = 0,
                             bool count_only = false, int co_spread = 1, bool skip_empty = false,
-                            bool codes = false) {
+                            bool codes = false, uint32_t part = 0, uint32_t n_parts = 1) {
   ReleaseGroup rg(s);             // the scratch buffers below: one release event
   const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
@@ -818,11 +821,30 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     if (std::string(e) == "wave") group = false;
   }
   if (count_only) { group = true; sorted = false; }   // the keys-only group bucket build
-  const uint32_t nb = group ? nb_g : nb_w;
-  const uint32_t passes = group ? passes_g : passes_w;
-  const uint32_t R = group ? R_g : R_w;
+  uint32_t nb = group ? nb_g : nb_w;
+  uint32_t passes = group ? passes_g : passes_w;
+  uint32_t R = group ? R_g : R_w;
+  // owner-computes part (the reference's reader-pool partition,
+  // src/kmer_reader.c:28-39): the whole build's geometry, of which this part keeps the buckets
+  // [b0, b1) -- every window is encoded and hashed, only the part's keys are partitioned
+  uint32_t b0 = 0, nbh = 0;
+  if (n_parts > 1) {
+    if (from_keys || count_only || sorted) fail(KMHG_EINVAL, "part builds index sequences only");
+    b0 = (uint32_t)((uint64_t)nb * part / n_parts);
+    const uint32_t b1 = (uint32_t)((uint64_t)nb * (part + 1) / n_parts);
+    nbh = nb;
+    idx->is_part = true;
+    if (b1 <= b0) {              // more parts than buckets: an empty part (nothing to build)
+      idx->geom = Geom{0u, group ? V2_CAPW : V2_CAPB, b0, nbh};
+      idx->table.reset(1);
+      idx->positions.reset(1);
+      return idx.release();
+    }
+    nb = b1 - b0;
+    passes = plan(nb, R);
+  }
   if (passes > 4) fail(KMHG_EOVERFLOW, "sequence too long for the partitioned build");
-  idx->geom = Geom{nb, group ? V2_CAPW : V2_CAPB};
+  idx->geom = Geom{nb, group ? V2_CAPW : V2_CAPB, b0, nbh};
   const Geom g = idx->geom;
   const uint64_t nhist = (uint64_t)R * ch.C;
   const uint32_t scan_tiles = tiles_for(nhist);
@@ -1003,6 +1025,7 @@ void finish_build(kmhg_index* idx) {
   const uint8_t* src = idx->src;
   idx->src = nullptr;
   if (hm.overflow) {
+    if (idx->is_part) fail(KMHG_EOVERFLOW, "a bucket of a part build overflowed its LDS table");
     std::unique_ptr<kmhg_index> v1(build_device_v1(src, idx->L, idx->k, idx->stream));
     idx->geom = v1->geom;
     idx->table.swap_with(v1->table);
@@ -1025,6 +1048,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
                          int64_t w1, hipStream_t s) {
   ReleaseGroup rg(s);
   if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
+  if (idx->is_part) fail(KMHG_EINVAL, "a part index must be assembled before it is queried");
   finish_build(idx);
   auto q = std::make_unique<kmhg_query>();
   q->device = idx->device;
@@ -1821,6 +1845,7 @@ void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, 
                       int32_t* counts, hipStream_t s) {
   ReleaseGroup rg(s);
   if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
+  if (idx->is_part) fail(KMHG_EINVAL, "a part index must be assembled before it is read");
   prepare_readout(idx, s);
   Canon& c = idx->canon;
   const uint32_t U = (uint32_t)idx->U;
@@ -1856,6 +1881,11 @@ void positions_device(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, 
 // unsharded row order.
 void free_index(kmhg_index* idx);
 void free_query(kmhg_query* q);
+
+// the bucket holding the side slot's key ~0 (bucket_of(mix64(~0), nb), kmhg_device.h) on the host
+uint32_t side_bucket_of(uint32_t nb) {
+  return (uint32_t)(((unsigned __int128)mix64(EMPTY_KEY) * nb) >> 64);
+}
 
 std::vector<int> query_devices() {
   std::vector<int> out;
@@ -2057,6 +2087,69 @@ int kmhg_build_device(const void* d_seq, size_t L, int k, int do_sort, void* str
     check_build_args(L, k);
     hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     *out = build_device((const uint8_t*)d_seq, (int64_t)L, k, s);
+  });
+}
+
+int kmhg_build_device_part(const void* d_seq, size_t L, int k, int part, int n_parts,
+                           void* stream, kmhg_index** out) {
+  return guarded([&] {
+    if (!d_seq || !out) fail(KMHG_EINVAL, "null argument");
+    check_build_args(L, k);
+    if (n_parts < 1 || part < 0 || part >= n_parts) fail(KMHG_EINVAL, "part out of range");
+    if (const char* e = std::getenv("KMHG_BUILD"))
+      if (std::string(e) == "v1") fail(KMHG_EINVAL, "part builds need the partitioned build");
+    hipStream_t s = (hipStream_t)stream;
+    *out = build_device_v2((const uint8_t*)d_seq, (int64_t)L, k, s, nullptr, 0, false, 1, false,
+                           true, (uint32_t)part, (uint32_t)n_parts);
+  });
+}
+
+int kmhg_part_info(kmhg_index* idx, int64_t info[10]) {
+  return guarded([&] {
+    if (!idx || !info) fail(KMHG_EINVAL, "null argument");
+    if (!idx->is_part) fail(KMHG_EINVAL, "not a part index");
+    DeviceGuard g(idx->device);
+    finish_build(idx);
+    const Geom& G = idx->geom;
+    const uint32_t side_b = side_bucket_of(G.nbh);
+    info[0] = G.b0;
+    info[1] = G.nb;
+    info[2] = G.nbh;
+    info[3] = G.capb;
+    info[4] = (int64_t)idx->N;
+    info[5] = (int64_t)idx->U;
+    info[6] = (int64_t)idx->P;
+    info[7] = idx->max_n;
+    info[8] = (G.nb && side_b >= G.b0 && side_b < G.b0 + G.nb) ? 1 : 0;
+    info[9] = idx->dcodes.p ? (int64_t)(diag_block_words(idx->L - idx->k + 1) * 8) : 0;
+  });
+}
+
+int kmhg_part_export(kmhg_index* idx, int64_t pos_base, void* d_table, void* d_side_slot,
+                     void* d_positions, void* d_codes, void* stream) {
+  return guarded([&] {
+    if (!idx) fail(KMHG_EINVAL, "null index");
+    if (!idx->is_part) fail(KMHG_EINVAL, "not a part index");
+    if (pos_base < 0 || pos_base + (int64_t)idx->N > (int64_t)UINT32_MAX)
+      fail(KMHG_EINVAL, "position base out of range");
+    DeviceGuard g(idx->device);
+    finish_build(idx);
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t n = (uint64_t)idx->geom.nb * idx->geom.capb;
+    if (d_table && n)
+      LAUNCH("k_part_rebase", s,
+             launch_part_rebase(idx->table.p, static_cast<Slot*>(d_table), n,
+                                (uint32_t)pos_base, s));
+    if (d_side_slot && idx->geom.nb)
+      LAUNCH("k_part_rebase", s,
+             launch_part_rebase(idx->table.p + n, static_cast<Slot*>(d_side_slot), 1,
+                                (uint32_t)pos_base, s));
+    if (d_positions && idx->N)
+      HIPC(hipMemcpyAsync(d_positions, idx->positions.p, idx->N * 4, hipMemcpyDeviceToDevice, s));
+    if (d_codes && idx->dcodes.p)
+      HIPC(hipMemcpyAsync(d_codes, idx->dcodes.p, diag_block_words(idx->L - idx->k + 1) * 8,
+                          hipMemcpyDeviceToDevice, s));
+    HIPC(hipStreamSynchronize(s));
   });
 }
 
@@ -2696,6 +2789,7 @@ int kmhg_image_sizes_get(const kmhg_index* cidx, kmhg_image_sizes* sz, int64_t h
     if (!cidx || !sz || !header) fail(KMHG_EINVAL, "null argument");
     kmhg_index* idx = const_cast<kmhg_index*>(cidx);   // completes a pending build
     if (idx->sources) fail(KMHG_EINVAL, "index images hold position indices only");
+    if (idx->is_part) fail(KMHG_EINVAL, "a part index is exported with kmhg_part_export");
     DeviceGuard g(idx->device);
     finish_build(idx);
     sz->table_bytes = (int64_t)(idx->slots() * sizeof(Slot));

@@ -37,6 +37,8 @@ struct ReadMeta {               // canonical-order readout preparation
 };
 
 void launch_table_init(Slot* T, uint64_t n, hipStream_t s);
+// dst[i] = src[i] with aux += base where count >= 2 (a part's list ends in the whole index)
+void launch_part_rebase(const Slot* src, Slot* dst, uint64_t n, uint32_t base, hipStream_t s);
 void launch_build_insert(const uint8_t* seq, int64_t L, int k, Slot* T, Geom g,
                          uint32_t* win_slot, int64_t Nw, bool aligned, hipStream_t s);
 void launch_build_compact(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket,

@@ -30,6 +30,21 @@ __global__ void __launch_bounds__(BLOCK) k_table_init(Slot* __restrict__ T, uint
   }
 }
 
+// Part export (owner-computes multi-GPU build): a part's slots with their list ends moved by the
+// part's first position index in the whole index (count >= 2: aux += base; a key seen once keeps
+// its position inline, an empty slot is copied as is).
+__global__ void __launch_bounds__(BLOCK) k_part_rebase(const Slot* __restrict__ src,
+                                                        Slot* __restrict__ dst, uint64_t n,
+                                                        uint32_t base) {
+  uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
+  for (; i < n; i += stride) {
+    uint4 v = *reinterpret_cast<const uint4*>(&src[i]);
+    if (v.z > 1u) v.w += base;
+    *reinterpret_cast<uint4*>(&dst[i]) = v;
+  }
+}
+
 // K_insert: encode + N-mask + find-or-insert + count.  One lane per window, TILE windows per
 // workgroup, lane-consecutive windows so the win_slot stores are coalesced.
 __global__ void __launch_bounds__(BLOCK)
@@ -1076,6 +1091,12 @@ static inline unsigned grid_for(uint64_t n, unsigned per) {
   return (unsigned)(g ? g : 1);
 }
 
+void launch_part_rebase(const Slot* src, Slot* dst, uint64_t n, uint32_t base, hipStream_t s) {
+  if (!n) return;
+  unsigned g = grid_for(n, BLOCK);
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(k_part_rebase, dim3(g), dim3(BLOCK), 0, s, src, dst, n, base);
+}
 void launch_table_init(Slot* T, uint64_t n, hipStream_t s) {
   unsigned g = grid_for(n, BLOCK);
   if (g > 8192) g = 8192;

@@ -39,6 +39,22 @@ class DeviceIndex:
         return cls(out.value)
 
     @classmethod
+    def build_part(cls, seq: torch.Tensor, k: int, part: int, n_parts: int,
+                   stream=None) -> "DevicePart":
+        """Part `part` of `n_parts` of an owner-computes build (kmhg_build_device_part): the
+        k-mers whose hash bucket lies in this part's range of the whole table, from every
+        window of `seq`."""
+        _check_seq(seq)
+        with torch.cuda.device(seq.device):
+            out = C.c_void_p()
+            _lib.check(_lib.lib().kmhg_build_device_part(C.c_void_p(seq.data_ptr()), seq.numel(),
+                                                         k, part, n_parts, _stream_ptr(stream),
+                                                         C.byref(out)))
+        p = DevicePart(out.value)
+        p.k, p.L, p.device = k, seq.numel(), seq.device
+        return p
+
+    @classmethod
     def count(cls, seq: torch.Tensor, k: int, source: int, source_n: int,
               into: "DeviceIndex | None" = None, stream=None) -> "DeviceIndex":
         """count.kmers of one HBM-resident sequence (kmhg_count_device): adds to `into`, or
@@ -183,6 +199,31 @@ class DeviceIndex:
             self.free()
         except Exception:
             pass
+
+
+PART_FIELDS = ("b0", "nb", "nb_total", "capb", "n_positions", "n_kmers", "n_pairs", "max_count",
+               "side_owner", "codes_bytes")
+SLOT_BYTES = 16
+
+
+class DevicePart(DeviceIndex):
+    """One part of an owner-computes build (DeviceIndex.build_part); dist.assemble_parts turns
+    the parts of all ranks into the whole index."""
+
+    def part_info(self) -> dict:
+        a = (C.c_int64 * 10)()
+        _lib.check(_lib.lib().kmhg_part_info(self._h, a))
+        return dict(zip(PART_FIELDS, list(a)))
+
+    def export_into(self, pos_base: int, table: torch.Tensor | None, side: torch.Tensor | None,
+                    positions: torch.Tensor | None, codes: torch.Tensor | None, stream=None):
+        """Write this part's rebased slots / side slot / positions / code block into the given
+        uint8 device views (None = skip)."""
+        def p(t):
+            return C.c_void_p(t.data_ptr()) if t is not None and t.numel() else None
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().kmhg_part_export(self._h, pos_base, p(table), p(side),
+                                                   p(positions), p(codes), _stream_ptr(stream)))
 
 
 class DeviceQuery:

@@ -126,6 +126,90 @@ def sharded_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, group=
     return rows
 
 
+# ------------------------------------------------------------------ owner-computes build (§8e)
+IMAGE_MAGIC = 0x6B6D6867          # 'kmhg', kmhg_image_import's header word 7
+
+
+def part_layout(infos: list[dict]) -> dict:
+    """Where each rank's part lands in the whole index: its first slot (bucket b0 x capb), its
+    first position index (the positions of the parts before it), and the totals."""
+    capb, nbt = infos[0]["capb"], infos[0]["nb_total"]
+    bases, acc = [], 0
+    for inf in infos:
+        bases.append(acc)
+        acc += inf["n_positions"]
+    owners = [r for r, inf in enumerate(infos) if inf["side_owner"]]
+    return {"capb": capb, "nb_total": nbt, "slots": nbt * capb + 1, "pos_base": bases,
+            "N": acc, "U": sum(i["n_kmers"] for i in infos),
+            "P": sum(i["n_pairs"] for i in infos),
+            "max_n": max(i["max_count"] for i in infos), "side_owner": owners[0] if owners else 0,
+            "codes_bytes": max(i["codes_bytes"] for i in infos)}
+
+
+def owner_build(seq: torch.Tensor | None, k: int, device: torch.device, src: int | None = 0,
+                group=None, stream=None):
+    """make.kmer.hash over G ranks, owner-computes (the reference's reader pool
+    gives each thread the k-mers it owns, src/kmer_reader.c:28-39): the sequence is broadcast
+    from `src` (C1; src=None: every rank holds it already), every rank walks all windows and
+    builds only the k-mers of its bucket range (kmhg_build_device_part).  Returns this rank's
+    DevicePart; assemble_parts() makes the whole index on every rank."""
+    from .device import DeviceIndex
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if src is not None:
+        seq = broadcast_sequence(seq, src, device, group)
+    return DeviceIndex.build_part(seq, k, rank, world, stream), seq
+
+
+def assemble_parts(part, device: torch.device, group=None, import_fn=None):
+    """All ranks' parts -> the whole index on every rank (all-gather of the rebased slot ranges
+    and of the positions, the side slot and code block from their owners), imported with
+    kmhg_image_import.  Bit-identical to the single-device build of the same sequence."""
+    from .device import PART_FIELDS, SLOT_BYTES, DeviceIndex
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    mine = part.part_info()
+    t = torch.tensor([mine[f] for f in PART_FIELDS], dtype=torch.int64, device=device)
+    got = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(got, t, group=group)
+    infos = [dict(zip(PART_FIELDS, g.tolist())) for g in got]
+    lay = part_layout(infos)
+    capb = lay["capb"]
+    slot_b = [inf["nb"] * capb * SLOT_BYTES for inf in infos]
+    pos_b = [inf["n_positions"] * 4 for inf in infos]
+    ms, mp = max(1, max(slot_b)), max(1, max(pos_b))
+    # padded all-gathers: every rank contributes max-sized buffers (one collective each)
+    send_t = torch.empty(ms, dtype=torch.uint8, device=device)
+    send_p = torch.empty(mp, dtype=torch.uint8, device=device)
+    side = torch.zeros(SLOT_BYTES, dtype=torch.uint8, device=device)
+    codes = torch.empty(max(1, lay["codes_bytes"]), dtype=torch.uint8, device=device)
+    code_src = next((r for r, inf in enumerate(infos) if inf["nb"] and inf["codes_bytes"]), 0)
+    part.export_into(lay["pos_base"][rank], send_t[:slot_b[rank]], side, send_p[:pos_b[rank]],
+                     codes if rank == code_src else None)
+    recv_t = torch.empty((world, ms), dtype=torch.uint8, device=device)
+    recv_p = torch.empty((world, mp), dtype=torch.uint8, device=device)
+    dist.all_gather(list(recv_t.unbind(0)), send_t, group=group)
+    dist.all_gather(list(recv_p.unbind(0)), send_p, group=group)
+    dist.broadcast(side, lay["side_owner"], group=group)
+    dist.broadcast(codes, code_src, group=group)
+    table = torch.empty(lay["slots"] * SLOT_BYTES, dtype=torch.uint8, device=device)
+    positions = torch.empty(max(1, lay["N"] * 4), dtype=torch.uint8, device=device)
+    for r, inf in enumerate(infos):
+        a = inf["b0"] * capb * SLOT_BYTES
+        table[a:a + slot_b[r]] = recv_t[r, :slot_b[r]]
+        b = lay["pos_base"][r] * 4
+        positions[b:b + pos_b[r]] = recv_p[r, :pos_b[r]]
+    table[-SLOT_BYTES:] = side
+    del recv_t, recv_p, send_t, send_p
+    header = [int(part.k), part.L, (lay["nb_total"] << 32) | capb, lay["U"], lay["N"], lay["P"],
+              lay["max_n"], IMAGE_MAGIC]
+    sizes = [table.numel(), lay["N"] * 4, lay["codes_bytes"]]
+    meta = torch.tensor(header + sizes, dtype=torch.int64)
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    return (import_fn or DeviceIndex.import_image)(meta, [table, positions, codes])
+
+
 class HipQueryEngine:
     """Adapter: a DeviceIndex (libkmhgpu) as a sharded-query engine."""
 

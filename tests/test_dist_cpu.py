@@ -85,3 +85,111 @@ def test_shard_ranges():
     r = kd.shard_ranges(1_000_003, 8)
     assert r[0][0] == 0 and r[-1][1] == 1_000_003
     assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+
+
+# ------------------------------------------------------------ owner-computes assembly (gloo)
+class FakePart:
+    """A part of a synthetic whole index (nb_total buckets x capb 16-B slots, N positions): owns
+    buckets [b0, b1) and the positions of its elements; list ends (count >= 2) are stored
+    part-local and rebased by export_into, as kmhg_part_export does."""
+
+    def __init__(self, rank, world, nb_total=11, capb=4, seed=5):
+        from kmer_hasher_amd.device import SLOT_BYTES
+        rng = np.random.default_rng(seed)
+        self.k, self.L = 21, 5000
+        slots = rng.integers(0, 2**31, size=(nb_total * capb + 1, 4), dtype=np.int64).astype(
+            np.uint32)
+        slots[:, 2] = rng.integers(0, 4, size=nb_total * capb + 1)          # counts 0..3
+        per_bucket = rng.integers(0, 9, size=nb_total)                       # positions / bucket
+        self.whole_pos = rng.integers(1, 10**6, size=int(per_bucket.sum()), dtype=np.int32)
+        self.b0 = nb_total * rank // world
+        self.b1 = nb_total * (rank + 1) // world
+        starts = np.concatenate([[0], np.cumsum(per_bucket)])
+        self.base = int(starts[self.b0])
+        self.n = int(starts[self.b1] - starts[self.b0])
+        self.whole_table = slots
+        local = slots.copy()
+        multi = local[:, 2] > 1
+        local[multi, 3] = (local[multi, 3] % 1000).astype(np.uint32)
+        self.whole_table[multi, 3] = local[multi, 3]           # keep aux + base in range
+        self.local = local
+        self.capb, self.nb_total, self.slot_bytes = capb, nb_total, SLOT_BYTES
+        side_b = 3
+        self.side_owner = int(self.b0 <= side_b < self.b1)
+        self.codes = np.arange(24, dtype=np.uint8)
+
+    def expected(self, world):
+        t = self.whole_table.copy()
+        # every part rebases its own slots by its own base
+        for r in range(world):
+            p = FakePart(r, world, self.nb_total, self.capb)
+            a, b = p.b0 * self.capb, p.b1 * self.capb
+            m = t[a:b, 2] > 1
+            t[a:b][m, 3] += np.uint32(p.base)
+        side_part = next(FakePart(r, world, self.nb_total, self.capb) for r in range(world)
+                         if FakePart(r, world, self.nb_total, self.capb).side_owner)
+        t[-1] = side_part.local[-1]
+        m = t[-1, 2] > 1
+        if m:
+            t[-1, 3] += np.uint32(side_part.base)
+        return t.view(np.uint8).reshape(-1), self.whole_pos.view(np.uint8)
+
+    def part_info(self):
+        return {"b0": self.b0, "nb": self.b1 - self.b0, "nb_total": self.nb_total,
+                "capb": self.capb, "n_positions": self.n, "n_kmers": 7 * (self.b1 - self.b0),
+                "n_pairs": self.n, "max_count": 3, "side_owner": self.side_owner,
+                "codes_bytes": 24}
+
+    def export_into(self, pos_base, table, side, positions, codes, stream=None):
+        assert pos_base == self.base
+        sl = self.local[self.b0 * self.capb:self.b1 * self.capb].copy()
+        m = sl[:, 2] > 1
+        sl[m, 3] += np.uint32(pos_base)
+        if table is not None and table.numel():
+            table.copy_(torch.from_numpy(sl.view(np.uint8).reshape(-1)))
+        if side is not None:
+            s = self.local[-1:].copy()
+            if s[0, 2] > 1:
+                s[0, 3] += np.uint32(pos_base)
+            side.copy_(torch.from_numpy(s.view(np.uint8).reshape(-1)))
+        if positions is not None and positions.numel():
+            positions.copy_(torch.from_numpy(
+                self.whole_pos[self.base:self.base + self.n].view(np.uint8).copy()))
+        if codes is not None:
+            codes.copy_(torch.from_numpy(self.codes))
+
+
+def _assemble_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        part = FakePart(rank, world)
+        meta, bufs = kd.assemble_parts(part, torch.device("cpu"),
+                                       import_fn=lambda m, b: (m, b))
+        want_t, want_p = part.expected(world)
+        ok = (np.array_equal(bufs[0].numpy(), want_t)
+              and np.array_equal(bufs[1].numpy()[:want_p.size], want_p)
+              and np.array_equal(bufs[2].numpy(), part.codes)
+              and meta.tolist()[:8] == [21, 5000, (11 << 32) | 4, 7 * 11, want_p.size // 4,
+                                        want_p.size // 4, 3, kd.IMAGE_MAGIC])
+        out_q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_assemble_parts_places_and_rebases(world):
+    """assemble_parts (the all-gather of owner-computes parts) puts every part's slots at its
+    bucket range, its positions at its base, rebased list ends, the side slot from its owner and
+    the code block -- on every rank.  world 5 over 11 buckets: uneven parts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_assemble_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert all(res[r] for r in range(world)), res

@@ -83,3 +83,66 @@ def test_two_ranks_one_gpu_sharded_query(gpu, world, k_index, kq):
                 p.kill()
     assert (nk, npos) == (oi.U, oi.N)
     assert got == want
+
+
+def _owner_worker(rank, world, port, seq_bytes, k, kq, out_q):
+    """Owner-computes build over `world` ranks sharing cuda:0 (gloo): the sequence and the query
+    live on rank 0 only and are broadcast (C1); each rank builds its bucket range
+    (kmhg_build_device_part); assemble_parts all-gathers the parts into the whole index on every
+    rank; then the sharded seq.kmer.pos with the query broadcast from rank 0."""
+    import torch
+    import torch.distributed as dist
+    from kmer_hasher_amd import dist as kd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()).to(dev) \
+            if rank == 0 else None
+        part, seq_all = kd.owner_build(seq, k, dev, src=0)
+        idx = kd.assemble_parts(part, dev)
+        info = idx.info()
+        part.free()
+        timings = {}
+        rows = kd.sharded_query(_HostRows(kd.HipQueryEngine(idx)), seq if rank == 0 else None,
+                                kq, dst=0, src=0, timings=timings)
+        torch.cuda.synchronize()
+        if rank == 0:
+            out_q.put(((info["n_kmers"], info["n_positions"], info["n_pairs"]),
+                       rows.numpy().reshape(-1).tolist(), sorted(timings)))
+        dist.barrier()
+        idx.free()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k,kq", [(2, 31, 31), (3, 21, 17)])
+def test_owner_computes_build_and_broadcast_query(gpu, world, k, kq):
+    import torch.multiprocessing as mp
+    from kmer_hasher_amd import synth
+    from oracle import oracle as O
+    s = synth.add_n_runs(synth.repeat_rich(150_000, 8, n_gap_every=11_003), 0.004, 6)
+    s[-k - 2] = ord("N")
+    seq_bytes = s.tobytes()
+    oi = O.OracleIndex(seq_bytes, k)
+    want = oi.query(seq_bytes, kq).tolist()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, seq_bytes, k, kq, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        (nk, npos, npair), got, phases = q.get(timeout=100)
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert (nk, npos, npair) == (oi.U, oi.N, oi.P)
+    assert got == want
+    assert phases == ["broadcast", "gather", "query"]

@@ -1,0 +1,88 @@
+"""Owner-computes build (reference partition pattern src/kmer_reader.c:28-39) on
+one GPU: the n parts of kmhg_build_device_part, placed by their part_info and exported with
+their list ends rebased (kmhg_part_export), must reassemble into exactly the single-device
+index -- the same table and positions bytes -- and answer kmer.pos / seq.kmer.pos as the oracle
+does.  Includes parts that own no bucket (more parts than buckets) and the k = 32 side slot."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _assemble_local(parts, torch):
+    from kmer_hasher_amd import dist as kd
+    from kmer_hasher_amd.device import SLOT_BYTES, DeviceIndex
+    infos = [p.part_info() for p in parts]
+    lay = kd.part_layout(infos)
+    dev = parts[0].device
+    table = torch.full((lay["slots"] * SLOT_BYTES,), 0xAB, dtype=torch.uint8, device=dev)
+    positions = torch.empty(max(1, lay["N"] * 4), dtype=torch.uint8, device=dev)
+    codes = torch.empty(max(1, lay["codes_bytes"]), dtype=torch.uint8, device=dev)
+    capb = lay["capb"]
+    code_src = next((r for r, inf in enumerate(infos) if inf["nb"] and inf["codes_bytes"]), 0)
+    for r, (p, inf) in enumerate(zip(parts, infos)):
+        a = inf["b0"] * capb * SLOT_BYTES
+        b = lay["pos_base"][r] * 4
+        side = table[-SLOT_BYTES:] if r == lay["side_owner"] else None
+        p.export_into(lay["pos_base"][r], table[a:a + inf["nb"] * capb * SLOT_BYTES], side,
+                      positions[b:b + inf["n_positions"] * 4], codes if r == code_src else None)
+    header = [parts[0].k, parts[0].L, (lay["nb_total"] << 32) | capb, lay["U"], lay["N"],
+              lay["P"], lay["max_n"], kd.IMAGE_MAGIC]
+    meta = torch.tensor(header + [table.numel(), lay["N"] * 4, lay["codes_bytes"]],
+                        dtype=torch.int64)
+    torch.cuda.synchronize()
+    return DeviceIndex.import_image(meta, [table, positions, codes]), table, positions
+
+
+@pytest.mark.parametrize("n_parts", [1, 2, 3, 5, 8])
+def test_parts_reassemble_to_the_single_build(gpu, n_parts):
+    torch = gpu
+    from kmer_hasher_amd import synth
+    from kmer_hasher_amd.device import DeviceIndex
+    rr = synth.add_n_runs(synth.repeat_rich(400_000, 31, n_gap_every=70_000), 0.001, 32)
+    cases = [(synth.iid(300_000, 33), 31), (rr, 21), (rr, 9),
+             (np.frombuffer(b"G" * 40 + b"ACGT" * 800 + b"G" * 35, np.uint8), 32),
+             (synth.iid(3_000, 34), 31)]                     # 3 buckets: some parts own none
+    for seq_np, k in cases:
+        seq = torch.from_numpy(seq_np.copy()).cuda()
+        whole = DeviceIndex.build(seq, k)
+        meta_w, bufs_w = whole.export_image()
+        parts = [DeviceIndex.build_part(seq, k, p, n_parts) for p in range(n_parts)]
+        idx, table, positions = _assemble_local(parts, torch)
+        inf_w, inf_a = whole.info(), idx.info()
+        for f in ("n_kmers", "n_positions", "n_pairs", "max_count", "table_slots"):
+            assert inf_w[f] == inf_a[f], (k, n_parts, f)
+        assert torch.equal(table, bufs_w[0][:table.numel()]), (k, n_parts)
+        assert torch.equal(positions[:inf_w["n_positions"] * 4],
+                           bufs_w[1][:inf_w["n_positions"] * 4]), (k, n_parts)
+        s = seq_np.tobytes()
+        oi = O.OracleIndex(s, k)
+        res = idx.positions(14)
+        assert np.array_equal(res["count"].cpu().numpy(), oi.counts)
+        assert np.array_equal(res["pos"].cpu().numpy().reshape(-1), oi.pos_rows())
+        assert np.array_equal(res["pair.pos"].cpu().numpy().reshape(-1), oi.pair_rows())
+        kq = min(k, 31)
+        q = idx.query(seq, kq)
+        assert np.array_equal(q.rows().cpu().numpy().reshape(-1), oi.query(s, kq)), (k, n_parts)
+        q.free()
+        for p in parts:
+            p.free()
+        idx.free()
+        whole.free()
+
+
+def test_part_index_refuses_queries(gpu):
+    torch = gpu
+    from kmer_hasher_amd import _lib, synth
+    from kmer_hasher_amd.device import DeviceIndex
+    seq = torch.from_numpy(synth.iid(50_000, 35)).cuda()
+    p = DeviceIndex.build_part(seq, 21, 0, 2)
+    with pytest.raises(_lib.KmhgError, match="assembled"):
+        p.query(seq, 21)
+    with pytest.raises(_lib.KmhgError, match="assembled"):
+        p.positions(8)
+    with pytest.raises(_lib.KmhgError, match="part out of range"):
+        DeviceIndex.build_part(seq, 21, 2, 2)
+    p.free()
