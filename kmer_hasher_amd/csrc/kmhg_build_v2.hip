@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
            uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
            uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
-           uint16_t* __restrict__ nbit) {
+           uint16_t* __restrict__ nbit, uint32_t* __restrict__ uniq0) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
   // zero the next scan's look-back words + ticket and the build meta (no memset launches)
@@ -145,6 +145,7 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
     stage_tile<true>(seq, L, tile0 - HALO, st, true);
     __syncthreads();
     if (code) diag_words_out(st, tile, ch.ntiles, code, nbit);
+    if (uniq0 && threadIdx.x < PTILE / 32) uniq0[(uint64_t)tile * (PTILE / 32) + threadIdx.x] = 0u;
 #pragma unroll 4
     for (int j = 0; j < PWPT; ++j) {
       const int w = j * BLOCK + threadIdx.x;
@@ -174,7 +175,7 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
             uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
             uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
-            uint16_t* __restrict__ nbit) {
+            uint16_t* __restrict__ nbit, uint32_t* __restrict__ uniq0) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
@@ -195,6 +196,10 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
     const int64_t tile0 = (int64_t)tile * PTILE;
     stage_pack(regs, st);                      // the previous tile's reads of st are done
     if (CODES) diag_words_out(st, tile, ch.ntiles, code, nbit);
+    // the repeated keys' window bits start clear: the bucket kernel sets them (uniq0 = the
+    // code block's uniq words, reused as "multi" bits until the first query)
+    if (CODES && uniq0 && threadIdx.x < PTILE / 32)
+      uniq0[(uint64_t)tile * (PTILE / 32) + threadIdx.x] = 0u;
     if (it + 1 < n_iter)
       stage_load<PSTAGE_W16, true>(regs, seq, L, (int64_t)tile_at(it + 1) * PTILE - HALO, true);
     __syncthreads();
@@ -963,7 +968,9 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
                                               Slot* __restrict__ T,
                                               int32_t* __restrict__ positions,
                                               BucketStats* __restrict__ bstats,
-                                              BuildMeta* __restrict__ meta, const uint32_t b) {
+                                              BuildMeta* __restrict__ meta, const uint32_t b,
+                                              uint8_t* __restrict__ TG = nullptr,
+                                              uint32_t* __restrict__ mbits = nullptr) {
   constexpr int PER = 2 * V2_BW_WG / BLOCK;           // elements per thread per batch (2x mean)
   constexpr uint32_t BATCH = BLOCK * PER;
   const int wave = threadIdx.x >> 6, lane = lane_id();
@@ -1088,7 +1095,11 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
             uint32_t cur = cc.y;
             if (multi && leader == lane) W.cc[slot[c]].y = cur + (uint32_t)__popcll(m);
             cur = __shfl(cur, leader);
-            if (multi) positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
+            if (multi) {
+              positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
+              // the diagonal query path's bits of repeated keys' windows (ps: 1-based start)
+              if (mbits) atomicOr(&mbits[(ps[c] - 1) >> 5], 1u << ((ps[c] - 1) & 31));
+            }
           }
         }
         __syncthreads();
@@ -1097,16 +1108,18 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   }
   __syncthreads();
   STAMP_WG(b, 4);
-  // the bucket's sub-table, coalesced 16-B slots
+  // the bucket's sub-table, coalesced 16-B slots (+ the query's slot tags, 1 B per slot)
   Slot* Tb = T + (uint64_t)b * V2_CAPW;
   for (uint32_t j = threadIdx.x; j < V2_CAPW; j += BLOCK) {
     const uint64_t kk = W.key[j];
     const uint2 c = W.cc[j];
     *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
+    if (TG) TG[(uint64_t)b * V2_CAPW + j] = kk == EMPTY_KEY ? (uint8_t)0 : slot_tag(mix64(kk));
   }
   if (threadIdx.x == 0 && side_bucket(b, g)) {
     const uint2 c = W.cc[V2_CAPW];
     *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
+    if (TG) TG[side_slot(g)] = 0;
   }
   STAMP_WG(b, 5);
 }
@@ -1116,12 +1129,13 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
                int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
-               BuildMeta* __restrict__ meta) {
+               BuildMeta* __restrict__ meta, uint8_t* __restrict__ TG,
+               uint32_t* __restrict__ mbits) {
   __shared__ GroupTable W;
   __shared__ uint64_t sh[8];
   __shared__ uint32_t red[3][4];
   bucket_wg_cas<COUNT_ONLY>(W, sh, red, keys, pos, start, g, T, positions, bstats, meta,
-                            blockIdx.x);
+                            blockIdx.x, TG, mbits);
 }
 
 // ---------------------------------------------------------------- V_bucket_sort (group per bucket)
@@ -1530,7 +1544,8 @@ static unsigned scatter8_grid(const Chunks& ch) {
 
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
-                     BuildMeta* meta, hipStream_t s, uint32_t* code, uint16_t* nbit) {
+                     BuildMeta* meta, hipStream_t s, uint32_t* code, uint16_t* nbit,
+                     uint32_t* uniq0) {
   static const int persist = [] {
     const char* e = std::getenv("KMHG_HIST0P");
     return (e && e[0] == '0') ? 0 : 1;
@@ -1541,15 +1556,15 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
     if (code && nbit)
       hipLaunchKernelGGL(k_v2_hist0p<true>, dim3(std::min<unsigned>(ch.ntiles, cap_c)), dim3(BLOCK),
                          0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status, n_status,
-                         meta, code, nbit);
+                         meta, code, nbit, uniq0);
     else
       hipLaunchKernelGGL(k_v2_hist0p<false>, dim3(std::min<unsigned>(ch.ntiles, cap_n)), dim3(BLOCK),
                          0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status, n_status,
-                         meta, nullptr, nullptr);
+                         meta, nullptr, nullptr, nullptr);
     return;
   }
   hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
-                     xcd_map(), scan_status, n_status, meta, code, nbit);
+                     xcd_map(), scan_status, n_status, meta, code, nbit, uniq0);
 }
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);
@@ -1636,13 +1651,13 @@ void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         bool count_only, hipStream_t s) {
+                         bool count_only, hipStream_t s, uint8_t* TG, uint32_t* mbits) {
   if (count_only)
     hipLaunchKernelGGL(k_v2_bucket_wg<true>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
-                       positions, bstats, meta);
+                       positions, bstats, meta, nullptr, nullptr);
   else
     hipLaunchKernelGGL(k_v2_bucket_wg<false>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g,
-                       T, positions, bstats, meta);
+                       T, positions, bstats, meta, TG, mbits);
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {

@@ -607,6 +607,9 @@ struct kmhg_index {
   // part of an owner-computes build (kmhg_build_device_part): holds buckets
   // [geom.b0, geom.b0 + geom.nb) of a table of geom.nbh buckets; exported, never queried
   bool is_part = false;
+  // the build wrote the slot tags (ptag) and the repeated keys' window bits (in the code
+  // block's uniq words): the first diagonal query only derives the window bits (V_diag_valid)
+  bool build_prepped = false;
   std::atomic<bool> ps_ready{false};
   // copies of this index on other devices for multi-device queries (KMHG_DEVICES), keyed by
   // the query part they serve; made on first use by peer copies over xGMI, freed with the index
@@ -756,7 +759,7 @@ int co_spread_for(double distinct, uint64_t total) {
 kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t s,
                             const uint64_t* d_keys = nullptr, int64_t n_keys = 0,
                             bool count_only = false, int co_spread = 1, bool skip_empty = false,
-                            bool codes = false, uint32_t part = 0, uint32_t n_parts = 1) {
+                            bool codes = false, uint32_t part = 0, uint32_t n_parts = 0) {
   ReleaseGroup rg(s);             // the scratch buffers below: one release event
   const uint8_t* d_src = d_seq;   // the caller's buffer (the v1 fallback re-reads it)
   auto idx = std::make_unique<kmhg_index>();
@@ -828,7 +831,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // src/kmer_reader.c:28-39): the whole build's geometry, of which this part keeps the buckets
   // [b0, b1) -- every window is encoded and hashed, only the part's keys are partitioned
   uint32_t b0 = 0, nbh = 0;
-  if (n_parts > 1) {
+  if (n_parts >= 1) {           // n_parts = 0: a whole build
     if (from_keys || count_only || sorted) fail(KMHG_EINVAL, "part builds index sequences only");
     b0 = (uint32_t)((uint64_t)nb * part / n_parts);
     const uint32_t b1 = (uint32_t)((uint64_t)nb * (part + 1) / n_parts);
@@ -882,20 +885,27 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = 1;
+  // the diagonal query path's slot tags and repeated-key bits written by the build itself
+  // (V_hist0 zeroes the bits, V_bucket_wg sets them and writes the tags with its sub-table), so
+  // an index's first query pays only V_diag_valid.  KMHG_BUILD_TAGS=0: the first query does it.
+  const char* bt = std::getenv("KMHG_BUILD_TAGS");
+  const bool prep = codes && !from_keys && group && !sorted && !count_only && n_parts == 0 &&
+                    !(bt && bt[0] == '0');
+  DiagBlock db{nullptr, nullptr, nullptr};
   if (from_keys) {   // pass 0 reads the caller's key stream in place (positions implicit)
     HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(n_valid), (int)Nw, 1, s));
     HIPC(hipMemsetAsync(meta, 0, sizeof(BuildMeta), s));
   } else {
     // a position index keeps its sequence's code words + window bits for the diagonal query
     // path (code words + N flags, 0.5 B per window with the first query's bits; V_hist0 writes them)
-    DiagBlock db{nullptr, nullptr, nullptr};
     if (codes) {
       idx->dcodes.reset(diag_block_words(Nw));
       db = idx->diag_block_of();
     }
+    if (prep) idx->ptag.reset(idx->slots() + 32);   // + the 32-B span the last probe group reads
     LAUNCH("k_v2_hist0", s,
            launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, status, n_status,
-                           meta, s, db.code, db.nbit));
+                           meta, s, db.code, db.nbit, prep ? db.uniq : nullptr));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     LAUNCH("k_v2_scatter_seq", s,
            launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, kA.p, pA.p,
@@ -970,11 +980,13 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   else if (group)
     LAUNCH("k_v2_bucket_wg", s,
            launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, bstats.p,
-                               meta, no_pos, s));
+                               meta, no_pos, s, prep ? idx->ptag.p : nullptr,
+                               prep ? db.uniq : nullptr));
   else
     LAUNCH("k_v2_bucket", s,
            launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
                             meta, s));
+  idx->build_prepped = prep;
   LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, gb.nb, n_valid, meta, idx->rec.meta, s));
   HIPC(hipEventRecord(idx->rec.ev, s));
 #ifdef KMHG_STAMPS
@@ -1026,6 +1038,7 @@ void finish_build(kmhg_index* idx) {
   idx->src = nullptr;
   if (hm.overflow) {
     if (idx->is_part) fail(KMHG_EOVERFLOW, "a bucket of a part build overflowed its LDS table");
+    idx->build_prepped = false;             // the table is rebuilt: tags and bits are redone
     std::unique_ptr<kmhg_index> v1(build_device_v1(src, idx->L, idx->k, idx->stream));
     idx->geom = v1->geom;
     idx->table.swap_with(v1->table);
@@ -1079,20 +1092,25 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   if (diag && !idx->ps_ready.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> lk(idx->ps_mu);
     if (!idx->ps_ready.load(std::memory_order_relaxed) && !idx->ps_failed) {
-      try {
-        idx->ptag.reset(idx->slots() + 32);  // + the 32-B span the last probe group reads
-      } catch (const Error& e) {           // no room for the tags: table probes only
-        if (e.code != KMHG_ENOMEM) throw;
-        idx->ps_failed = true;
-        (void)hipGetLastError();
+      if (!idx->build_prepped) {
+        try {
+          idx->ptag.reset(idx->slots() + 32);  // + the 32-B span the last probe group reads
+        } catch (const Error& e) {           // no room for the tags: table probes only
+          if (e.code != KMHG_ENOMEM) throw;
+          idx->ps_failed = true;
+          (void)hipGetLastError();
+        }
       }
       if (!idx->ps_failed) {
         idx->ptag.bind(s);
         idx->dcodes.bind(s);
         const DiagBlock db = idx->diag_block_of();
-        LAUNCH("k_diag_prep", s,
-               launch_diag_prep(db.nbit, idx->L, idx->k, db.uniq, idx->table.p, idx->slots(),
-                                idx->positions.p, idx->ptag.p, s));
+        if (idx->build_prepped)
+          LAUNCH("k_diag_valid", s, launch_diag_valid_multi(db.nbit, idx->L, idx->k, db.uniq, s));
+        else
+          LAUNCH("k_diag_prep", s,
+                 launch_diag_prep(db.nbit, idx->L, idx->k, db.uniq, idx->table.p, idx->slots(),
+                                  idx->positions.p, idx->ptag.p, s));
         // once per index: later queries may run on other streams
         HIPC(hipStreamSynchronize(s));
         idx->ps_ready.store(true, std::memory_order_release);

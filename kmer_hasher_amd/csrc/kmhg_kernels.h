@@ -94,6 +94,10 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
 // slots, and the `uniq` bits of every position of a key seen more than once cleared
 void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, const Slot* T,
                       uint64_t nslots, const int32_t* positions, uint8_t* TG, hipStream_t s);
+// An index whose build already wrote the slot tags and set the repeated keys' window bits in
+// the uniq words (V_bucket_wg): uniq = the indexed windows AND NOT those bits
+void launch_diag_valid_multi(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq,
+                             hipStream_t s);
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
 // exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
 // reduce-then-scan with `scratch` = scan_u64_scratch(n) u64
@@ -167,7 +171,7 @@ Chunks make_chunks(uint32_t ntiles);
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
                      BuildMeta* meta, hipStream_t s, uint32_t* code = nullptr,
-                     uint16_t* nbit = nullptr);
+                     uint16_t* nbit = nullptr, uint32_t* uniq0 = nullptr);
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
 // exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the histogram kernel
@@ -227,7 +231,8 @@ void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint
 // count_only: occurrence counts only (no positions written; slot aux unspecified)
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         bool count_only, hipStream_t s);
+                         bool count_only, hipStream_t s, uint8_t* TG = nullptr,
+                         uint32_t* mbits = nullptr);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);
 

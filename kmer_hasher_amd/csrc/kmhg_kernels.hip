@@ -291,7 +291,7 @@ k_inline_singles(Slot* __restrict__ T, uint64_t nslots, const int32_t* __restric
 // thread per word: u16 flag words 2a .. 2a + 3 hold chars [32a, 32a + 64), char 32a at bit 63.
 __global__ void __launch_bounds__(BLOCK)
 k_diag_valid(const uint16_t* __restrict__ nbit, int64_t L, int k, uint32_t* __restrict__ uniq,
-             uint64_t n_words) {
+             uint64_t n_words, int multi_in) {
   const uint64_t a = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (a >= n_words) return;
   const int64_t Nw = L - k + 1;
@@ -308,6 +308,7 @@ k_diag_valid(const uint16_t* __restrict__ nbit, int64_t L, int k, uint32_t* __re
     }
     u |= (v ? 1u : 0u) << i;
   }
+  if (multi_in) u &= ~uniq[a];                 // the build's repeated-key bits
   uniq[a] = u;
 }
 
@@ -349,11 +350,18 @@ void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, co
                       uint64_t nslots, const int32_t* positions, uint8_t* TG, hipStream_t s) {
   const uint64_t nw = diag_uniq_words(L - k + 1);
   hipLaunchKernelGGL(k_diag_valid, dim3((unsigned)((nw + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
-                     nbit, L, k, uniq, nw);
+                     nbit, L, k, uniq, nw, 0);
   uint64_t g = (nslots + BLOCK - 1) / BLOCK;
   if (g > 65536) g = 65536;
   hipLaunchKernelGGL(k_diag_prep, dim3((unsigned)(g ? g : 1)), dim3(BLOCK), 0, s, T, nslots,
                      positions, uniq, TG);
+}
+
+void launch_diag_valid_multi(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq,
+                             hipStream_t s) {
+  const uint64_t nw = diag_uniq_words(L - k + 1);
+  hipLaunchKernelGGL(k_diag_valid, dim3((unsigned)((nw + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                     nbit, L, k, uniq, nw, 1);
 }
 
 // A window's probe result as Q_emit reads it: qrec[s] = 0 (no hit), the 1-based index position

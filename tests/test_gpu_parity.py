@@ -285,8 +285,8 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
     ptr.free()
 
 
-@pytest.mark.parametrize("tags", ["1", "0"])
-def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags):
+@pytest.mark.parametrize("tags,btags", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags, btags):
     """The diagonal path of k_query_probe (anchors every 64th window; later windows follow the
     last anchor with a unique hit and take {count 1, aux = predicted position} only when the
     index window there is unique and its key, read from the index's own code words, equals
@@ -295,10 +295,13 @@ def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags):
     inversions, translocations, N-runs), its reverse complement, an unrelated one, repeat-rich
     input (multi-hit anchors predict nothing; keys with > 16 positions have their windows'
     unique bits cleared by a whole wave), shards of the window range that start inside a
-    diagonal, and a query k different from the index k (path off)."""
+    diagonal, and a query k different from the index k (path off).  btags: the slot tags and
+    repeated-key bits written by the build (V_bucket_wg, default) or by the first query
+    (KMHG_BUILD_TAGS=0, V_diag_prep)."""
     import torch
     from kmer_hasher_amd import device as D, synth
     monkeypatch.setenv("KMHG_QUERY_TAGS", tags)
+    monkeypatch.setenv("KMHG_BUILD_TAGS", btags)
     make, kpos, sqk = _api()
     A = synth.add_n_runs(synth.iid(300_000, 61), 0.0005, 62, max_run=40)
     B = synth.derived(A, 63)
@@ -348,6 +351,7 @@ def test_query_diagonal_edges_vs_oracle(gpu, monkeypatch, codes):
     in the index, and an index built without the code block (KMHG_DIAG_CODES=0: table probes)."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_DIAG_CODES", codes)
+    monkeypatch.setenv("KMHG_BUILD_TAGS", "1" if codes == "1" else "0")
     make, kpos, sqk = _api()
     rng = np.random.default_rng(91)
 
