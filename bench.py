@@ -209,11 +209,43 @@ def host_boundary(seq_bytes: bytes, k: int, calls: int = 10) -> dict:
     for _ in range(calls):
         rows = api.seq_kmer_pos(ptr, seq_bytes, k)
     t_q = (time.perf_counter() - t0) / calls
+    # the query's legs: kmhg_query_run (sequence H2D + the device query, synchronous), then
+    # kmhg_query_fill into a fresh array (R's allocMatrix: its pages are faulted in by the copy)
+    # and into an array already touched (the DMA + copy alone)
+    import ctypes as C
+    import numpy as np
+    from kmer_hasher_amd import _lib
+    L = _lib.lib()
+    t_run = t_fresh = t_warm = 0.0
+    warm = np.ones(2 * rows.shape[0], np.int32)
+    for _ in range(calls):
+        q, h = C.c_void_p(), C.c_int64()
+        t0 = time.perf_counter()
+        _lib.check(L.kmhg_query_run(ptr.handle, seq_bytes, len(seq_bytes), k, C.byref(q),
+                                    C.byref(h)))
+        t1 = time.perf_counter()
+        fresh = np.empty(2 * h.value, np.int32)
+        _lib.check(L.kmhg_query_fill(q, fresh.ctypes.data))
+        t2 = time.perf_counter()
+        _lib.check(L.kmhg_query_fill(q, warm.ctypes.data))
+        t3 = time.perf_counter()
+        L.kmhg_query_free(q)
+        t_run += t1 - t0
+        t_fresh += t2 - t1
+        t_warm += t3 - t2
+        del fresh
     ptr.free()
     mbp = len(seq_bytes) / 1e6
     return {"build": {"value": round(mbp / t_b, 2), "unit": "Mbp/s", "ms": round(t_b * 1e3, 3)},
             "query": {"value": round(mbp / t_q, 2), "unit": "Mbp/s", "ms": round(t_q * 1e3, 3),
-                      "rows": int(rows.shape[0])},
+                      "rows": int(rows.shape[0]),
+                      "legs_ms": {"h2d_and_device_query": round(t_run / calls * 1e3, 3),
+                                  "rows_to_fresh_array": round(t_fresh / calls * 1e3, 3),
+                                  "rows_to_touched_array": round(t_warm / calls * 1e3, 3),
+                                  "page_faults": round((t_fresh - t_warm) / calls * 1e3, 3),
+                                  "note": "fresh = a new array whose pages the copy faults in "
+                                          "(as R's allocMatrix); touched = the same copy into "
+                                          "resident pages (DMA + host copy only)"}},
             "calls": calls,
             "note": "PCIe-inclusive: host sequence in (pageable), host rows out, synchronous "
                     "per call (the R API); not `value`"}

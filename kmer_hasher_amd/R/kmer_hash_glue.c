@@ -121,6 +121,9 @@ SEXP kmer_positions(SEXP ptr_r, SEXP opt_flag_r) {
   return ret;
 }
 
+/* With KMHG_DEVICES=d0,d1,... in the environment, kmhg_query_run splits the query over those
+ * GPUs (index replicas peer-copied once, rows filled straight into the R matrix by
+ * kmhg_query_fill at each device's row offset): same signature, same result. */
 SEXP sequence_kmer_positions(SEXP ptr_r, SEXP seq_r, SEXP k_r) {
   kmhg_index *idx = gpu_index_of(ptr_r);
   if (TYPEOF(seq_r) != STRSXP || length(seq_r) != 1) error("seq_r should be a single sequence");

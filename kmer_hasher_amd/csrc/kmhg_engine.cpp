@@ -26,6 +26,7 @@
 #include "kmhg_common.h"
 #include "kmhg_kernels.h"
 #include "kmhg_fastx.h"
+#include "kmhg_khash.h"
 #include "kmhg_sh.h"
 #include "../../include/kmhgpu.h"
 
@@ -461,6 +462,8 @@ hipStream_t lib_stream() {
 // the host copy of chunk i, which d2h_threads() threads split (they also take the destination's
 // first-touch page faults in parallel).  Synchronous: returns once dst holds the bytes.
 constexpr size_t D2H_CHUNK = 16u << 20;
+constexpr size_t H2D_CHUNK = 4u << 20;
+constexpr size_t H2D_STAGE_MIN = 2u << 20;
 constexpr size_t D2H_STAGE_MIN = 4u << 20;
 static int d2h_threads() {                           // KMHG_D2H_THREADS (A/B), default 4
   static const int n = [] {
@@ -482,6 +485,19 @@ static void host_copy_par(char* dst, const char* src, size_t n) {
   for (auto& x : th) x.join();
 }
 
+struct PinStage {
+  std::mutex mu;
+  char* pin[2] = {nullptr, nullptr};
+};
+static PinStage& pin_stage() {           // the device's two pinned D2H_CHUNK buffers
+  static std::mutex map_mu;
+  static std::map<int, PinStage> stages;
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(map_mu);
+  return stages[dev];
+}
+
 void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (!bytes) return;
   static const bool staged = [] {
@@ -494,21 +510,9 @@ void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
     return;
   }
   // two pinned chunks per device, so the parts of a multi-device query copy out concurrently
-  struct Stage {
-    std::mutex mu;
-    char* pin[2] = {nullptr, nullptr};
-  };
-  static std::mutex map_mu;
-  static std::map<int, Stage> stages;
-  int dev = 0;
-  HIPC(hipGetDevice(&dev));
-  Stage* st;
-  {
-    std::lock_guard<std::mutex> g(map_mu);
-    st = &stages[dev];
-  }
-  std::lock_guard<std::mutex> g(st->mu);
-  char** pin = st->pin;
+  PinStage& st = pin_stage();
+  std::lock_guard<std::mutex> g(st.mu);
+  char** pin = st.pin;
   if (!pin[0])
     for (int i = 0; i < 2; ++i)
       HIPC(hipHostMalloc(reinterpret_cast<void**>(&pin[i]), D2H_CHUNK, hipHostMallocPortable));
@@ -541,6 +545,54 @@ void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
     if (i + 2 < nch) issue(i + 2);
   }
 }
+
+
+void h2d_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (!bytes) return;
+  static const bool staged = [] {
+    const char* e = std::getenv("KMHG_H2D");
+    return !(e && std::string(e) == "direct");
+  }();
+  if (!staged || bytes < H2D_STAGE_MIN) {
+    HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+    return;                                      // pageable: the runtime stages it
+  }
+  PinStage& st = pin_stage();
+  std::lock_guard<std::mutex> g(st.mu);
+  char** pin = st.pin;
+  if (!pin[0])
+    for (int i = 0; i < 2; ++i)
+      HIPC(hipHostMalloc(reinterpret_cast<void**>(&pin[i]), D2H_CHUNK, hipHostMallocPortable));
+  struct Ev2 {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    ~Ev2() {   // every exit: the DMAs out of the pinned chunks have finished, events destroyed
+      for (int i = 0; i < 2; ++i)
+        if (e[i]) {
+          if (used[i]) (void)hipEventSynchronize(e[i]);
+          (void)hipEventDestroy(e[i]);
+        }
+    }
+  } ev;
+  for (int i = 0; i < 2; ++i) HIPC(hipEventCreateWithFlags(&ev.e[i], hipEventDisableTiming));
+  const size_t nch = (bytes + H2D_CHUNK - 1) / H2D_CHUNK;
+  for (size_t i = 0; i < nch; ++i) {
+    const int b = (int)(i & 1);
+    if (ev.used[b]) HIPC(hipEventSynchronize(ev.e[b]));     // its previous DMA is done
+    const size_t off = i * H2D_CHUNK, n = std::min(H2D_CHUNK, bytes - off);
+    host_copy_par(pin[b], static_cast<const char*>(src) + off, n);
+    HIPC(hipMemcpyAsync(static_cast<char*>(dst) + off, pin[b], n, hipMemcpyHostToDevice, s));
+    HIPC(hipEventRecord(ev.e[b], s));
+    ev.used[b] = true;
+  }
+}
+
+// Pageable host -> device copy for the host-pointer entry points (the R string of make.kmer.hash
+// / seq.kmer.pos): inputs above H2D_STAGE_MIN go through the device's two pinned chunks,
+// d2h_threads() threads filling chunk i + 1 while the DMA of chunk i runs.  Returns once the
+// DMAs have completed (the pinned chunks are reused by the next caller).  KMHG_H2D=direct: one
+// pageable hipMemcpyAsync (A/B).
+void h2d_host(void* dst, const void* src, size_t bytes, hipStream_t s);
 
 // The hash table is sized from the number of windows (an upper bound on distinct k-mers) for a
 // load factor <= 0.7; capacity is not a power of two (slot = mulhi(hash, cap)).
@@ -1726,69 +1778,6 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
   c.ready = true;
 }
 
-// khash 0.2.8 bucket-order replay (the reference's row order, src/kmer_hash.c:1096-1124).
-// The reference only ever calls kh_get (read-only) and kh_put on NEW keys, so its final table
-// depends only on the distinct keys in first-insertion order = our first-occurrence order.  This
-// replays kh_put's sizing (4 buckets minimum; when occupancy reaches (int)(0.77 nb + 0.5) the
-// table is resized to the next power of two above nb, src/khash.h:307-317), its probe sequence
-// (i + ++step) & mask from hash (u32)(key>>33 ^ key ^ key<<11) (src/khash.h:385), and kh_resize's
-// in-place rehash, which moves elements by kick-out in old-bucket order (src/khash.h:244-306).
-// Returns order[r] = first-occurrence id of the r-th live bucket.
-std::vector<uint32_t> khash_bucket_order(const std::vector<uint64_t>& keys) {
-  enum : uint8_t { LIVE = 0, MOVED = 1, EMPTY = 2 };
-  auto hash = [](uint64_t k) { return (uint32_t)((k >> 33) ^ k ^ (k << 11)); };
-  uint32_t nb = 0, size = 0, upper = 0;
-  std::vector<uint8_t> st;
-  std::vector<uint64_t> key;
-  std::vector<uint32_t> val;
-  auto resize = [&](uint32_t want) {
-    uint32_t nnb = 4;
-    while (nnb < want) nnb <<= 1;
-    if (size >= (uint32_t)(nnb * 0.77 + 0.5)) return;   // too small: unchanged
-    std::vector<uint8_t> nst(nnb, EMPTY);
-    if (nnb > nb) { key.resize(nnb); val.resize(nnb); }
-    const uint32_t nmask = nnb - 1;
-    for (uint32_t j = 0; j < nb; ++j) {
-      if (st[j] != LIVE) continue;
-      uint64_t k = key[j];
-      uint32_t v = val[j];
-      st[j] = MOVED;
-      for (;;) {                            // kick-out: displace a not-yet-moved element
-        uint32_t i = hash(k) & nmask, step = 0;
-        while (nst[i] != EMPTY) i = (i + (++step)) & nmask;
-        nst[i] = LIVE;
-        if (i < nb && st[i] == LIVE) {
-          std::swap(k, key[i]);
-          std::swap(v, val[i]);
-          st[i] = MOVED;
-        } else {
-          key[i] = k;
-          val[i] = v;
-          break;
-        }
-      }
-    }
-    st.swap(nst);
-    nb = nnb;
-    upper = (uint32_t)(nb * 0.77 + 0.5);
-  };
-  for (uint32_t u = 0; u < (uint32_t)keys.size(); ++u) {
-    if (size >= upper) resize(nb + 1);      // no deletions: n_occupied == size
-    const uint32_t mask = nb - 1;
-    uint32_t i = hash(keys[u]) & mask, step = 0;
-    while (st[i] != EMPTY) i = (i + (++step)) & mask;   // distinct keys: never a match
-    key[i] = keys[u];
-    val[i] = u;
-    st[i] = LIVE;
-    ++size;
-  }
-  std::vector<uint32_t> order;
-  order.reserve(size);
-  for (uint32_t j = 0; j < nb; ++j)
-    if (st[j] == LIVE) order.push_back(val[j]);
-  return order;
-}
-
 // Readout arrays for idx->row_order.  The first-occurrence arrays are built on the GPU
 // (prepare_canon); the khash order relabels them: the keys go to the host once, the bucket
 // order is replayed there (inherently sequential, ~0.1 us per key), and the permuted arrays
@@ -2003,7 +1992,7 @@ kmhg_query* query_multi_device(kmhg_index* idx, const char* seq, int64_t L, int 
       const int64_t b = std::min<int64_t>(L, w1 + k + 64);
       DBuf<uint8_t> d((size_t)L + 16, s);
       if (poison) HIPC(hipMemsetAsync(d.p, 'A', (size_t)L + 16, s));
-      if (b > a) HIPC(hipMemcpyAsync(d.p + a, seq + a, (size_t)(b - a), hipMemcpyHostToDevice, s));
+      if (b > a) h2d_host(d.p + a, seq + a, (size_t)(b - a), s);
       parts[i] = query_device(use, d.p, L, k, w0, w1, s);
       HIPC(hipStreamSynchronize(s));
     } catch (const Error& e) {
@@ -2090,7 +2079,7 @@ int kmhg_build(const char* seq, size_t L, int k, int do_sort, kmhg_index** out) 
     check_build_args(L, k);
     hipStream_t s = lib_stream();
     DBuf<uint8_t> d(L + 16, s);
-    HIPC(hipMemcpyAsync(d.p, seq, L, hipMemcpyHostToDevice, s));
+    h2d_host(d.p, seq, L, s);
     std::unique_ptr<kmhg_index> idx(build_device(d.p, (int64_t)L, k, s));
     finish_build(idx.get());   // synchronous, like make_kmer_h_index (and d dies here)
     *out = idx.release();
@@ -2699,7 +2688,7 @@ int kmhg_query_run(kmhg_index* idx, const char* seq, size_t L, int k, kmhg_query
     DeviceGuard g(idx->device);
     hipStream_t s = lib_stream();
     DBuf<uint8_t> d(L + 16, s);
-    HIPC(hipMemcpyAsync(d.p, seq, L, hipMemcpyHostToDevice, s));
+    h2d_host(d.p, seq, L, s);
     *q = query_device(idx, d.p, (int64_t)L, k, 0, (int64_t)L - k + 1, s);
     HIPC(hipStreamSynchronize(s));
     if (n_rows) *n_rows = (*q)->H;
