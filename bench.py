@@ -424,6 +424,11 @@ def main():
                     help="skip the read-counting / depth legs (count.kmers.fq.sh.rp)")
     ap.add_argument("--profile", action="store_true",
                     help="short run for rocprofv3 (no CPU leg, no JSON extras)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 process group (nccl = RCCL; gloo only to rehearse the N > 1 "
+                         "code on one GPU)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="N > 1 rehearsal on a one-GPU box: every rank on cuda:0 (with gloo)")
     args = ap.parse_args()
     # the side legs (query, counts, reads, depth) run for at least 50 timed calls: 20 calls of a
     # 0.1-0.5 ms leg are a few ms of wall time, where one host hiccup shows as a 2x swing
@@ -437,8 +442,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.rehearse:
+            local = 0
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -507,6 +517,13 @@ def main():
     ktimes = D.timing_report()
     D.timing_enable(False)
     D.timing_select(None)
+
+    # ---------------- N > 1: the owner-computes build of ONE genome of N x L bases:
+    # rank 0 holds it and broadcasts it, every rank builds the k-mers of its bucket range
+    # (kmhg_build_device_part); assembling the whole index on every rank is timed once, apart
+    sharded = None
+    if world > 1 and not args.profile:
+        sharded = bench_sharded_build(args, k, L, dev, world, rank, seed)
 
     # ---------------- query: self seq.kmer.pos against one resident index.  The first query of an
     # index also derives the diagonal path's unique-window bits and slot tags (k_diag_valid /
@@ -772,6 +789,8 @@ def main():
             if "k_depth_probe" in dper:
                 out["depth"]["roofline"] = _leg_roofline(
                     dper, "k_depth_probe", depth_algorithmic_bytes("k_depth_probe", L, 2))
+        if sharded:
+            out["sharded_build"] = sharded
         if not args.profile:
             out["host_boundary"] = host_boundary(host_seq.tobytes(), k)
         if not args.no_cpu and not args.profile:
@@ -792,6 +811,59 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def bench_sharded_build(args, k, L, dev, world, rank, seed):
+    """Owner-computes make.kmer.hash of one (world x L)-base sequence over the ranks: a step is
+    every rank's part build (kmhg_build_device_part), max over ranks.  Returns rank 0's record."""
+    import torch
+    import torch.distributed as dist
+    from kmer_hasher_amd import device as D
+    from kmer_hasher_amd import dist as kd
+    from kmer_hasher_amd import synth
+    big = torch.from_numpy(synth.iid(L * world, 1000 + seed)).to(dev) if rank == 0 else None
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    seq_all = kd.broadcast_sequence(big, 0, dev)
+    torch.cuda.synchronize()
+    t_bc = time.perf_counter() - t0
+    for _ in range(max(1, args.warmup)):
+        D.DeviceIndex.build_part(seq_all, k, rank, world).wait().free()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        D.DeviceIndex.build_part(seq_all, k, rank, world).free()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t_part = time.perf_counter() - t0
+    part = D.DeviceIndex.build_part(seq_all, k, rank, world).wait()
+    inf = part.part_info()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    idx = kd.assemble_parts(part, dev)
+    torch.cuda.synchronize()
+    t_asm = time.perf_counter() - t0
+    U = idx.info()["n_kmers"]
+    idx.free()
+    part.free()
+    tt = torch.tensor([t_part, t_bc, t_asm], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t_part, t_bc, t_asm = tt.tolist()
+    if rank != 0:
+        return None
+    Ltot = L * world
+    return {"value": round(Ltot / 1e6 * args.steps / t_part, 2), "unit": "Mbp/s",
+            "ms_per_step": round(t_part / args.steps * 1e3, 4), "seq_len": Ltot, "k": k,
+            "distinct_kmers": U, "rank0_part_kmers": inf["n_kmers"],
+            "sequence_broadcast_ms": round(t_bc * 1e3, 3),
+            "assemble_ms": round(t_asm * 1e3, 3),
+            "note": "owner-computes build of ONE sequence of n_gpus x seq_len bases: each rank "
+                    "walks every window and builds the k-mers of its bucket range "
+                    "(kmhg_build_device_part); the parts together are the whole index, "
+                    "assembling it on every rank (all-gather) is timed once as assemble_ms"}
 
 
 def _emit(out):

@@ -960,8 +960,8 @@ __device__ __forceinline__ int lds_find_g(const GroupTable& W, uint64_t key) {
 // for buckets it does not take).  W, sh, red are the caller's LDS.
 // COUNT_ONLY (occurrence counts of a key stream, kmhg_sh.hip's read counting): pass B -- the
 // positions -- is skipped; slots get {key, count, unspecified aux}.
-template <bool COUNT_ONLY = false>
-__device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint32_t (*red)[4],
+template <bool COUNT_ONLY = false, int TB = BLOCK>
+__device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint32_t (*red)[TB / 64],
                                               const uint64_t* __restrict__ keys,
                                               const uint32_t* __restrict__ pos,
                                               const uint32_t* __restrict__ start, Geom g,
@@ -971,16 +971,17 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
                                               BuildMeta* __restrict__ meta, const uint32_t b,
                                               uint8_t* __restrict__ TG = nullptr,
                                               uint32_t* __restrict__ mbits = nullptr) {
-  constexpr int PER = 2 * V2_BW_WG / BLOCK;           // elements per thread per batch (2x mean)
-  constexpr uint32_t BATCH = BLOCK * PER;
+  constexpr int NW = TB / 64;                         // waves of the workgroup
+  constexpr int PER = 2 * V2_BW_WG / TB;              // elements per thread per batch (2x mean)
+  constexpr uint32_t BATCH = TB * PER;
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const uint32_t s0 = start[b], s1 = start[b + 1];
   const bool one_batch = s1 - s0 <= BATCH;
   uint64_t key[PER];
   uint32_t ps[PER];
   int slot[PER];
-  // element c of thread t in a batch: i0 + c * BLOCK + t, so position order = (c, wave, lane)
-  auto elem = [&](uint32_t i0, int c) { return i0 + (uint32_t)c * BLOCK + threadIdx.x; };
+  // element c of thread t in a batch: i0 + c * TB + t, so position order = (c, wave, lane)
+  auto elem = [&](uint32_t i0, int c) { return i0 + (uint32_t)c * TB + threadIdx.x; };
   auto load = [&](uint32_t i0) {
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
@@ -991,7 +992,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   };
   STAMP_WG(b, 0);
   load(s0);                                           // in flight while the table is cleared
-  for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += BLOCK) {
+  for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += TB) {
     W.key[j] = EMPTY_KEY;
     W.cc[j] = make_uint2(0u, 0u);
   }
@@ -1018,15 +1019,15 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     return;
   }
   STAMP_WG(b, 2);
-  // counts: thread t owns slots t, t + BLOCK, ... (lane-contiguous: conflict-free LDS; thread-
+  // counts: thread t owns slots t, t + TB, ... (lane-contiguous: conflict-free LDS; thread-
   // contiguous runs of 6 slots ran 0.104 ms against 0.096 for the kernel)
-  constexpr uint32_t SPT = (V2_CAPW + 1 + BLOCK - 1) / BLOCK;
+  constexpr uint32_t SPT = (V2_CAPW + 1 + TB - 1) / TB;
   uint32_t cnt[SPT];
   uint32_t cs = 0, occ = 0, mx = 0;
   uint64_t pairs = 0;
 #pragma unroll
   for (uint32_t q = 0; q < SPT; ++q) {
-    const uint32_t j = q * BLOCK + threadIdx.x;
+    const uint32_t j = q * TB + threadIdx.x;
     const uint32_t c = j <= V2_CAPW ? W.cc[j].x : 0u;
     cnt[q] = c;
     cs += c;
@@ -1042,17 +1043,17 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   if (lane == 0) {
     red[0][wave] = occ;
     red[1][wave] = mx;
-    sh[4 + wave] = pairs;                  // sh[4..7]: the block scan below uses sh[0..3]
+    sh[NW + wave] = pairs;                 // sh[NW..2NW): the block scan below uses sh[0..NW)
   }
   const bool has_multi = __syncthreads_or(mx > 1);
   // list offsets (only repeated keys have lists): any slot order gives each key a contiguous
-  // range of [s0, s1), here slot q * BLOCK + t in (t, q) order
+  // range of [s0, s1), here slot q * TB + t in (t, q) order
   if (!COUNT_ONLY && has_multi) {
     uint64_t tot;
-    uint32_t off_run = s0 + (uint32_t)block_excl_scan(cs, sh, tot);
+    uint32_t off_run = s0 + (uint32_t)block_excl_scan_n<NW>(cs, sh, tot);
 #pragma unroll
     for (uint32_t q = 0; q < SPT; ++q) {
-      const uint32_t j = q * BLOCK + threadIdx.x;
+      const uint32_t j = q * TB + threadIdx.x;
       if (j <= V2_CAPW) W.cc[j].y = off_run;
       off_run += cnt[q];
     }
@@ -1061,9 +1062,15 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   STAMP_WG(b, 3);
   if (threadIdx.x == 0) {
     BucketStats st;
-    st.n_kmers = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    st.max_count = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
-    st.n_pairs = sh[4] + sh[5] + sh[6] + sh[7];
+    st.n_kmers = 0;
+    st.max_count = 0;
+    st.n_pairs = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      st.n_kmers += red[0][w];
+      st.max_count = max(st.max_count, red[1][w]);
+      st.n_pairs += sh[NW + w];
+    }
     bstats[b] = st;
   }
   // pass B: keys seen once keep their position inline (cc.y); repeated keys are ranked in
@@ -1083,7 +1090,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     for (int c = 0; c < PER; ++c) {
       const bool act = elem(i0, c) < s1;
       // waves take turns on this c: wave w ranks after waves < w have advanced the cursors
-      for (int turn = 0; turn < 4; ++turn) {
+      for (int turn = 0; turn < NW; ++turn) {
         if (wave == turn) {
           uint2 cc = make_uint2(0u, 0u);
           if (act) cc = W.cc[slot[c]];
@@ -1110,7 +1117,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   STAMP_WG(b, 4);
   // the bucket's sub-table, coalesced 16-B slots (+ the query's slot tags, 1 B per slot)
   Slot* Tb = T + (uint64_t)b * V2_CAPW;
-  for (uint32_t j = threadIdx.x; j < V2_CAPW; j += BLOCK) {
+  for (uint32_t j = threadIdx.x; j < V2_CAPW; j += TB) {
     const uint64_t kk = W.key[j];
     const uint2 c = W.cc[j];
     *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
@@ -1124,18 +1131,20 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   STAMP_WG(b, 5);
 }
 
-template <bool COUNT_ONLY>
-__global__ void __launch_bounds__(BLOCK)
+// TB threads per workgroup: 256 (4 waves) or 512 (8 waves: the LDS table allows 6 workgroups
+// per CU, so 8-wave groups fill the CU's 32 wave slots where 4-wave groups stop at 24).
+template <bool COUNT_ONLY, int TB = BLOCK>
+__global__ void __launch_bounds__(TB)
 k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
                int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
                BuildMeta* __restrict__ meta, uint8_t* __restrict__ TG,
                uint32_t* __restrict__ mbits) {
   __shared__ GroupTable W;
-  __shared__ uint64_t sh[8];
-  __shared__ uint32_t red[3][4];
-  bucket_wg_cas<COUNT_ONLY>(W, sh, red, keys, pos, start, g, T, positions, bstats, meta,
-                            blockIdx.x, TG, mbits);
+  __shared__ uint64_t sh[2 * (TB / 64)];
+  __shared__ uint32_t red[3][TB / 64];
+  bucket_wg_cas<COUNT_ONLY, TB>(W, sh, red, keys, pos, start, g, T, positions, bstats, meta,
+                                blockIdx.x, TG, mbits);
 }
 
 // ---------------------------------------------------------------- V_bucket_sort (group per bucket)
@@ -1649,12 +1658,20 @@ void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint
   hipLaunchKernelGGL(k_v2_bucket_sort, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
                      positions, bstats, meta);
 }
+// KMHG_BUCKET_TB=512|256: threads of the position-build group bucket kernel (A/B)
+static int bucket_tb() {
+  const char* e = std::getenv("KMHG_BUCKET_TB");     // read per launch: the tests switch it
+  return (e && std::string(e) == "512") ? 512 : 256;
+}
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, uint8_t* TG, uint32_t* mbits) {
   if (count_only)
     hipLaunchKernelGGL(k_v2_bucket_wg<true>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
                        positions, bstats, meta, nullptr, nullptr);
+  else if (bucket_tb() == 512)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, 512>), dim3(g.nb), dim3(512), 0, s, keys, pos, start,
+                       g, T, positions, bstats, meta, TG, mbits);
   else
     hipLaunchKernelGGL(k_v2_bucket_wg<false>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g,
                        T, positions, bstats, meta, TG, mbits);

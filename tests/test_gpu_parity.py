@@ -195,12 +195,15 @@ def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
         ptr.free()
 
 
-@pytest.mark.parametrize("bucket", ["wave", "group", "sort"])
+@pytest.mark.parametrize("bucket", ["wave", "group", "group512", "sort"])
 def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     """Both bucket kernels on every size class: one wave per 256-window bucket, and one
     workgroup per 1024-window bucket (chosen automatically when it saves a radix pass, e.g. at
     100 Mbp): repeated keys spanning waves, buckets beyond one batch (tandem repeats), N-runs."""
     from kmer_hasher_amd import synth
+    if bucket == "group512":                # the 8-wave group bucket kernel (KMHG_BUCKET_TB)
+        monkeypatch.setenv("KMHG_BUCKET_TB", "512")
+        bucket = "group"
     monkeypatch.setenv("KMHG_BUCKET", bucket)
     rng = np.random.default_rng(21)
     for k in (3, 12, 31, 32):

@@ -34,5 +34,8 @@ for line in open(sys.argv[1]):
               "counts", d.get("counts", {}).get("value"),
               "depth", d.get("depth", {}).get("value"),
               "dprobe", d.get("depth", {}).get("kernels_ms_per_step", {}).get("k_depth_probe"),
+              "hb_build_ms", d.get("host_boundary", {}).get("build", {}).get("ms"),
+              "hb_query_ms", d.get("host_boundary", {}).get("query", {}).get("ms"),
+              "q_first_new", d.get("query", {}).get("first_query_new_index_ms"),
               " ".join(f"{k}={v:.4f}" for k, v in sorted(km.items())))
 PY

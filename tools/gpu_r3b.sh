@@ -15,3 +15,9 @@ for c in 3 4 5; do
     2> "$OUT/config$c.err" || { echo "config $c failed"; tail -20 "$OUT/config$c.err"; exit 1; }
   cat "$OUT/config$c.json"
 done
+# N > 1 bench code rehearsed on one GPU: two ranks on cuda:0 over gloo (config 2 + sharded build)
+timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 \
+  --backend gloo --rehearse --no-cpu --no-reads > "$OUT/rehearse2.json" 2> "$OUT/rehearse2.err" \
+  || { echo "rehearsal failed"; tail -30 "$OUT/rehearse2.err"; exit 1; }
+cat "$OUT/rehearse2.json"
