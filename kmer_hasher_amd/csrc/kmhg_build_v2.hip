@@ -946,6 +946,39 @@ __device__ __forceinline__ int lds_insert_g(GroupTable& W, uint64_t key) {
   return -1;
 }
 
+// One-atomic insert (KMHG_BUCKET_FP=1): during pass A the {count, cur} word of a slot holds
+// {count, 32-bit fingerprint} and ONE 64-bit CAS claims a free slot with count 1 (the claimer then
+// stores the full key); an occurrence that meets its fingerprint adds 1 to the count; another
+// fingerprint moves on.  A key seen once -- almost every key of an i.i.d. sequence -- costs one
+// LDS atomic instead of a CAS and an add.  Two keys of one bucket with equal fingerprints would
+// share a count: the caller checks every element against its slot's full key afterwards and
+// redoes the bucket with lds_insert_g if any differs.
+__device__ __forceinline__ uint64_t fp_of(uint64_t key) {
+  return ((key * 0x9E3779B97F4A7C15ull) >> 32) << 32;     // independent of the bucket/home bits
+}
+__device__ __forceinline__ int lds_insert_fp(GroupTable& W, uint64_t key) {
+  unsigned long long* word = reinterpret_cast<unsigned long long*>(W.cc);
+  if (key == EMPTY_KEY) {
+    atomicAdd(&word[V2_CAPW], 1ull);
+    return (int)V2_CAPW;
+  }
+  const uint64_t fp = fp_of(key);
+  uint32_t j = local_home(mix64(key), V2_CAPW);
+  for (uint32_t n = 0; n < V2_CAPW; ++n) {
+    const uint64_t prev = atomicCAS(&word[j], 0ull, (unsigned long long)(fp | 1ull));
+    if (prev == 0) {
+      W.key[j] = key;
+      return (int)j;
+    }
+    if ((prev & 0xFFFFFFFF00000000ull) == fp) {
+      atomicAdd(&word[j], 1ull);
+      return (int)j;
+    }
+    if (++j == V2_CAPW) j = 0;
+  }
+  return -1;
+}
+
 __device__ __forceinline__ int lds_find_g(const GroupTable& W, uint64_t key) {
   if (key == EMPTY_KEY) return (int)V2_CAPW;
   uint32_t j = local_home(mix64(key), V2_CAPW);
@@ -970,7 +1003,8 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
                                               BucketStats* __restrict__ bstats,
                                               BuildMeta* __restrict__ meta, const uint32_t b,
                                               uint8_t* __restrict__ TG = nullptr,
-                                              uint32_t* __restrict__ mbits = nullptr) {
+                                              uint32_t* __restrict__ mbits = nullptr,
+                                              int fp_insert = 0) {
   constexpr int NW = TB / 64;                         // waves of the workgroup
   constexpr int PER = 2 * V2_BW_WG / TB;              // elements per thread per batch (2x mean)
   constexpr uint32_t BATCH = TB * PER;
@@ -1002,7 +1036,35 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   // pass A: distinct keys + counts (CAS on a table shared by the four waves).  (Measured:
   // skipping the count atomic for a key's claiming occurrence ran 35 % slower, 141 vs 105 us.)
   bool ovf = false;
-  for (uint32_t i0 = s0; i0 < s1; i0 += BATCH) {
+  bool done = false;
+  if (fp_insert && one_batch) {              // one atomic per key seen once (lds_insert_fp)
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      slot[c] = -1;
+      if (elem(s0, c) < s1) {
+        slot[c] = lds_insert_fp(W, key[c]);
+        if (slot[c] < 0) ovf = true;
+      }
+    }
+    __syncthreads();                         // the claimers' key stores
+    bool bad = ovf || fp_insert == 2;        // 2: tests force the collision path
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (slot[c] >= 0 && slot[c] < (int)V2_CAPW && W.key[slot[c]] != key[c]) bad = true;
+    if (!__syncthreads_or(bad)) {
+#pragma unroll
+      for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += TB) W.cc[j].y = 0u;   // fingerprints out
+      done = true;
+    } else {                                 // a fingerprint collision: redo with the CAS build
+      for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += TB) {
+        W.key[j] = EMPTY_KEY;
+        W.cc[j] = make_uint2(0u, 0u);
+      }
+      ovf = false;
+    }
+    __syncthreads();
+  }
+  for (uint32_t i0 = s0; !done && i0 < s1; i0 += BATCH) {
     if (i0 != s0) load(i0);
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
@@ -1139,12 +1201,12 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
                int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
                BuildMeta* __restrict__ meta, uint8_t* __restrict__ TG,
-               uint32_t* __restrict__ mbits) {
+               uint32_t* __restrict__ mbits, int fp_insert) {
   __shared__ GroupTable W;
   __shared__ uint64_t sh[2 * (TB / 64)];
   __shared__ uint32_t red[3][TB / 64];
   bucket_wg_cas<COUNT_ONLY, TB>(W, sh, red, keys, pos, start, g, T, positions, bstats, meta,
-                                blockIdx.x, TG, mbits);
+                                blockIdx.x, TG, mbits, fp_insert);
 }
 
 // ---------------------------------------------------------------- V_bucket_sort (group per bucket)
@@ -1663,18 +1725,24 @@ static int bucket_tb() {
   const char* e = std::getenv("KMHG_BUCKET_TB");     // read per launch: the tests switch it
   return (e && std::string(e) == "512") ? 512 : 256;
 }
+// KMHG_BUCKET_FP=1: the one-atomic fingerprint insert of pass A (A/B)
+static int bucket_fp() {
+  const char* e = std::getenv("KMHG_BUCKET_FP");
+  return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+}
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, uint8_t* TG, uint32_t* mbits) {
+  const int fp = bucket_fp();
   if (count_only)
     hipLaunchKernelGGL(k_v2_bucket_wg<true>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
-                       positions, bstats, meta, nullptr, nullptr);
+                       positions, bstats, meta, nullptr, nullptr, fp);
   else if (bucket_tb() == 512)
     hipLaunchKernelGGL((k_v2_bucket_wg<false, 512>), dim3(g.nb), dim3(512), 0, s, keys, pos, start,
-                       g, T, positions, bstats, meta, TG, mbits);
+                       g, T, positions, bstats, meta, TG, mbits, fp);
   else
     hipLaunchKernelGGL(k_v2_bucket_wg<false>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g,
-                       T, positions, bstats, meta, TG, mbits);
+                       T, positions, bstats, meta, TG, mbits, fp);
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {

@@ -195,14 +195,19 @@ def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
         ptr.free()
 
 
-@pytest.mark.parametrize("bucket", ["wave", "group", "group512", "sort"])
+@pytest.mark.parametrize("bucket", ["wave", "group", "group512", "groupfp", "group512fp",
+                                    "groupfpforce", "sort"])
 def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     """Both bucket kernels on every size class: one wave per 256-window bucket, and one
     workgroup per 1024-window bucket (chosen automatically when it saves a radix pass, e.g. at
     100 Mbp): repeated keys spanning waves, buckets beyond one batch (tandem repeats), N-runs."""
     from kmer_hasher_amd import synth
-    if bucket == "group512":                # the 8-wave group bucket kernel (KMHG_BUCKET_TB)
-        monkeypatch.setenv("KMHG_BUCKET_TB", "512")
+    if bucket.startswith("group"):
+        # the 8-wave group bucket kernel (KMHG_BUCKET_TB), the one-atomic fingerprint insert
+        monkeypatch.setenv("KMHG_BUCKET_TB", "512" if "512" in bucket else "256")
+        # KMHG_BUCKET_FP=2 takes every bucket through the fingerprint-collision fallback
+        monkeypatch.setenv("KMHG_BUCKET_FP", "2" if bucket.endswith("force") else
+                           "1" if bucket.endswith("fp") else "0")
         bucket = "group"
     monkeypatch.setenv("KMHG_BUCKET", bucket)
     rng = np.random.default_rng(21)

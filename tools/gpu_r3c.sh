@@ -13,6 +13,7 @@ timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/
 timeout -k 10 300 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
   || { echo "bench failed"; tail -30 "$OUT/bench.err"; exit 1; }
 cat "$OUT/bench.json"
-timeout -k 10 600 bash tools/ab.sh "KMHG_BUCKET_TB=256" "KMHG_BUCKET_TB=512" "KMHG_BUILD_TAGS=0" \
-  "KMHG_H2D=direct" -- --no-cpu --no-reads || { echo "ab failed"; exit 1; }
+timeout -k 10 700 bash tools/ab.sh "KMHG_BUCKET_TB=256" "KMHG_BUCKET_TB=512" "KMHG_BUCKET_FP=1" \
+  "KMHG_BUCKET_TB=512 KMHG_BUCKET_FP=1" "KMHG_BUILD_TAGS=0" "KMHG_H2D=direct" \
+  -- --no-cpu --no-reads || { echo "ab failed"; exit 1; }
 cp gpurun_out/ab.log "$OUT/ab.log"
