@@ -1183,7 +1183,19 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     const uint64_t kk = W.key[j];
     const uint2 c = W.cc[j];
     *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
-    if (TG) TG[(uint64_t)b * V2_CAPW + j] = kk == EMPTY_KEY ? (uint8_t)0 : slot_tag(mix64(kk));
+  }
+  if (TG) {                    // 4 tags per lane, one 4-B store (byte stores cost 4x the issue)
+    static_assert(V2_CAPW % 4 == 0, "tag words");
+    uint32_t* tw = reinterpret_cast<uint32_t*>(TG + (uint64_t)b * V2_CAPW);
+    for (uint32_t w = threadIdx.x; w < V2_CAPW / 4; w += TB) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t kk = W.key[4 * w + q];
+        v |= (uint32_t)(kk == EMPTY_KEY ? 0u : slot_tag(mix64(kk))) << (8 * q);
+      }
+      tw[w] = v;
+    }
   }
   if (threadIdx.x == 0 && side_bucket(b, g)) {
     const uint2 c = W.cc[V2_CAPW];

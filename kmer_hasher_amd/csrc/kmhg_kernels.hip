@@ -949,9 +949,30 @@ template <class Off>
 __global__ void __launch_bounds__(BLOCK)
 k_row_tiles(const Off* __restrict__ off, uint32_t nkeys, uint64_t nrows, uint32_t tile,
             uint32_t* __restrict__ tile_key, uint32_t ntiles) {
-  for (uint32_t m = blockIdx.x * BLOCK + threadIdx.x; m < nkeys; m += gridDim.x * BLOCK) {
-    const uint64_t lo = off[m], hi = m + 1 < nkeys ? (uint64_t)off[m + 1] : nrows;
-    for (uint64_t t = (lo + tile - 1) / tile; t * tile < hi; ++t) tile_key[t] = m;
+  // one lane per key writes the tiles whose first row the key holds; a key spanning more than
+  // RT_LANE tiles (a heavy key's pairs: C(14,097, 2) rows = 48 K tiles at config 4) is handed
+  // to the whole wave, which strides over its tiles, instead of one lane storing them in turn
+  constexpr uint64_t RT_LANE = 8;
+  const int lane = lane_id();
+  const uint32_t stride = gridDim.x * BLOCK;
+  for (uint32_t m0 = blockIdx.x * BLOCK + (threadIdx.x & ~63u); m0 < nkeys; m0 += stride) {
+    const uint32_t m = m0 + lane;                // wave-uniform trip count: m0 is per wave
+    uint64_t t0 = 0, t1 = 0;
+    if (m < nkeys) {
+      const uint64_t lo = off[m], hi = m + 1 < nkeys ? (uint64_t)off[m + 1] : nrows;
+      t0 = (lo + tile - 1) / tile;
+      t1 = (hi + tile - 1) / tile;               // tiles t with t * tile in [lo, hi)
+      if (t1 > t0 && t1 - t0 <= RT_LANE)
+        for (uint64_t t = t0; t < t1; ++t) tile_key[t] = m;
+    }
+    uint64_t heavy = __ballot(t1 > t0 + RT_LANE);
+    while (heavy) {
+      const int src = __ffsll((unsigned long long)heavy) - 1;
+      heavy &= heavy - 1;
+      const uint64_t a = __shfl(t0, src), b = __shfl(t1, src);
+      const uint32_t key = m0 + (uint32_t)src;
+      for (uint64_t t = a + (uint64_t)lane; t < b; t += 64) tile_key[t] = key;
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) tile_key[ntiles] = nkeys - 1;
 }
