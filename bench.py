@@ -41,7 +41,8 @@ CONFIGS = {
             L=10_000_000, k=31),
     3: dict(workload="configs[2]: synthetic 100 Mbp iid ACGT (splitmix64 seed 2+rank), k=21, "
                      "index build + seq.kmer.pos self-query", L=100_000_000, k=21),
-    4: dict(workload="configs[3]: synthetic 40 Mbp repeat-rich (synth.repeat_rich seed 3), k=31, "
+    4: dict(workload="configs[3]: synthetic 40 Mbp repeat-rich (synth.config4 seed 3: "
+                     "repeat_rich with 50 % families, P = 6.86e8 in SURVEY §8(d)'s band), k=31, "
                      "kmer.pos(opt.flag=14: pos + pair.pos + count) readout into HBM",
             L=40_000_000, k=31),
     5: dict(workload="configs[4]: two synthetic 500 Mbp sequences (A iid seed 4; B = A + 1% SNV "

@@ -359,7 +359,7 @@ def test_query_diagonal_edges_vs_oracle(gpu, monkeypatch, codes):
     in the index, and an index built without the code block (KMHG_DIAG_CODES=0: table probes)."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_DIAG_CODES", codes)
-    monkeypatch.setenv("KMHG_BUILD_TAGS", "1" if codes == "1" else "0")
+    monkeypatch.setenv("KMHG_BUILD_TAGS", "1" if codes == "1" else "0")   # (tags need codes)
     make, kpos, sqk = _api()
     rng = np.random.default_rng(91)
 
