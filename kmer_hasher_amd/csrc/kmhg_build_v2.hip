@@ -1574,8 +1574,21 @@ static inline unsigned grid_of(uint64_t n, unsigned per) {
   return (unsigned)(g ? g : 1);
 }
 
+// KMHG_SCATTER_WPC=n (A/B): at most n scatter workgroups per CU.  Fewer tiles in flight per XCD
+// means fewer partially written digit-run lines held dirty in its L2 (beyond the Infinity
+// Cache, config 3 writes 1.4-1.7x the algorithmic bytes), at the cost of latency hiding.
 static unsigned scatter_cap() {
-  static unsigned cap = resident_blocks((const void*)k_v2_scatter<true, false, false, 4>);
+  static unsigned cap = [] {
+    unsigned c = resident_blocks((const void*)k_v2_scatter<true, false, false, 4>);
+    if (const char* e = std::getenv("KMHG_SCATTER_WPC")) {
+      int dev = 0, cus = 256;
+      if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      const unsigned want = (unsigned)std::max(1, std::atoi(e)) * (unsigned)std::max(cus, 1);
+      c = std::min(c, want);
+    }
+    return c;
+  }();
   return cap;
 }
 
