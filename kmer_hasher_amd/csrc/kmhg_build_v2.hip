@@ -1065,7 +1065,9 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     __syncthreads();
   }
   // (Measured round 3, A/B in one run: letting the claiming occurrence skip the count add --
-  // counts pass adds 1 per occupied slot -- made the kernel 100 -> 142 us, as in round 2.)
+  // counts pass adds 1 per occupied slot -- made the kernel 100 -> 142 us, as in round 2; and
+  // issuing the first CAS of all 8 elements of a lane back to back before resolving any,
+  // 98 -> 112 us.)
   for (uint32_t i0 = s0; !done && i0 < s1; i0 += BATCH) {
     if (i0 != s0) load(i0);
 #pragma unroll
