@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 #include "kmhg_common.h"
 #include "kmhg_device.h"
 #include "kmhg_kernels.h"
@@ -83,9 +84,13 @@ __device__ __forceinline__ bool in_part(uint64_t h, const Geom& g) {
 __device__ __forceinline__ bool side_bucket(uint32_t b, const Geom& g) {
   return b + g.b0 == bucket_of(mix64(EMPTY_KEY), g.nbh ? g.nbh : g.nb);
 }
-__device__ __forceinline__ uint32_t digit_of_h(uint64_t h, const Geom& g, const Digit& D) {
-  const uint32_t q = div_magic(bucket_local(h, g), D.mdiv);
+// radix digit of a bucket id (bucket-id streams carry it instead of the key)
+__device__ __forceinline__ uint32_t digit_of_b(uint32_t b, const Digit& D) {
+  const uint32_t q = div_magic(b, D.mdiv);
   return q - div_magic(q, D.mR) * D.R;
+}
+__device__ __forceinline__ uint32_t digit_of_h(uint64_t h, const Geom& g, const Digit& D) {
+  return digit_of_b(bucket_local(h, g), D);
 }
 __device__ __forceinline__ uint32_t digit_of(uint64_t key, const Geom& g, const Digit& D) {
   return digit_of_h(mix64(key), g, D);
@@ -170,12 +175,16 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
 // issued, so the wait for those loads never waits on these stores.  (A/B, config 2: validity
 // ballots kept in the window loop and stored per tile cost 24 -> 30-41 us; a kernel of its own
 // 18 us; these stores ~1 us.)
-template <bool CODES>
+// BIDS (bucket-id builds): every window's bucket id (~0 for a window that is not indexed or
+// outside this part) is stored in window order, one coalesced 4-B store per window, so the first
+// scatter pass reads the ids instead of encoding and hashing every window a second time.
+template <bool CODES, bool BIDS = false>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
             uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
             uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
-            uint16_t* __restrict__ nbit, uint32_t* __restrict__ uniq0) {
+            uint16_t* __restrict__ nbit, uint32_t* __restrict__ uniq0,
+            uint32_t* __restrict__ bids) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
@@ -208,10 +217,15 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
       const int w = j * BLOCK + threadIdx.x;
       const int64_t s = tile0 + w;
       uint64_t key = 0;
+      uint32_t bl = ~0u;
       if (s < Nw && window_key(st, HALO + w, s, L, k, key)) {
-        const uint64_t h = mix64(key);
-        if (in_part(h, g)) atomicAdd(&lh[digit_of_h(h, g, D)], 1u);
+        const uint32_t b = bucket_local(mix64(key), g);
+        if (b < g.nb) {
+          atomicAdd(&lh[digit_of_b(b, D)], 1u);
+          bl = b;
+        }
       }
+      if (BIDS && s < Nw) bids[s] = bl;
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) {
@@ -306,7 +320,8 @@ constexpr uint32_t HLL_SAMPLE_BITS = 6;
 constexpr uint32_t HLL_PART_ROWS = 256;        // V_hll workgroups (partial rows) at most
 static_assert(HLL_PART_WORDS == HLL_PART_ROWS * 64 + 1, "V_hll partial rows + ticket");
 
-template <bool HLL>
+// BID: the stream holds u32 bucket ids (BM scatter passes), digits without hashing.
+template <bool HLL, bool BID = false>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
           Digit D, uint32_t* __restrict__ hist, Chunks ch, int remap,
@@ -330,11 +345,20 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
   const uint32_t R = D.R;
   for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
   __syncthreads();
-  for (uint64_t e = e0 + threadIdx.x; e < e1; e += 4 * BLOCK) {
-    uint32_t dg[4];
-    bool in[4];
+  constexpr int NL = BID ? 8 : 4;                 // loads in flight per lane
+  const uint32_t* __restrict__ bids = reinterpret_cast<const uint32_t*>(keys);
+  for (uint64_t e = e0 + threadIdx.x; e < e1; e += NL * BLOCK) {
+    uint32_t dg[NL];
+    bool in[NL];
+    if (BID) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {                // 4 loads in flight per lane
+      for (int j = 0; j < NL; ++j) {
+        in[j] = e + j * BLOCK < e1;
+        dg[j] = in[j] ? digit_of_b(bids[e + j * BLOCK], D) : 0u;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NL && !BID; ++j) {
       in[j] = e + j * BLOCK < e1;
       const uint64_t key = in[j] ? keys[e + j * BLOCK] : 0ull;
       if (skip_empty && key == EMPTY_KEY) in[j] = false;      // a padded read's unused slot
@@ -345,7 +369,7 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
                   (uint32_t)__clzll(h | ((1ull << (HLL_SAMPLE_BITS + 8)) - 1)) + 1u);
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NL; ++j)
       if (in[j]) atomicAdd(&lh[dg[j]], 1u);
   }
   __syncthreads();
@@ -451,13 +475,13 @@ k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __res
 // (84-96 VGPRs, 24 waves / CU instead of 12).  More waves did not make the pass faster (config 2
 // neutral, config 3 +10 %): it is bound by the digit-run write pattern, not by latency hiding.
 // (Also measured: 320-digit arrays alone, or forcing 4 waves of the 4-wave kernel with spills.)
-template <int NWV>
+template <int NWV, class KT, bool IL_ONLY>
 struct ScatterLDS {
-  static constexpr uint32_t MAXR = NWV == 4 ? V2_MAXR : V2_MAXR_IL;
+  static constexpr uint32_t MAXR = (NWV == 4 && !IL_ONLY) ? V2_MAXR : V2_MAXR_IL;
   uint32_t wc[NWV][MAXR];      // per-wave digit counts -> per-wave tile-local cursors
   uint32_t tstart[MAXR];       // tile-local start of each digit
   uint32_t gbase[MAXR];        // global start of each digit for this tile (scanned histogram)
-  uint64_t skey[PTILE];
+  KT skey[PTILE];
   uint32_t spos[PTILE];
   uint32_t sdst[PTILE];
   PStage st;
@@ -486,7 +510,12 @@ __device__ __forceinline__ uint64_t block_excl_scan_n(uint64_t v, uint64_t* lds,
 // exactly n keys (loads clamped, no pad) and positions are implicit (e + 1), so the stream is
 // neither copied nor paired with an iota array first.  NOPOS: keys only (count-only builds:
 // nobody reads the positions), 8 B per element in and out instead of 12.
-template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false, int NWV = 4>
+// BM (bucket-id streams, position builds that keep code words): 0 = (key u64, pos) elements;
+// 1 = (bucket id u32, pos) in and out -- the digit needs no hash, and the key is cut from the
+// code words by the bucket kernel; 2 = the last pass: (bucket id, pos) in, positions only out.
+// kin / kout then point at u32 arrays.  8 B per element instead of 12 through the middle passes,
+// 4 B out of the last.
+template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false, int NWV = 4, int BM = 0>
 __global__ void __launch_bounds__(NWV * 64)
 k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned,
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
@@ -494,7 +523,12 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
              const uint32_t* __restrict__ hist, Chunks ch,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad, int remap,
              int skip_empty) {
-  using SL = ScatterLDS<NWV>;
+  using KT = typename std::conditional<BM != 0, uint32_t, uint64_t>::type;
+  using SL = ScatterLDS<NWV, KT, BM != 0>;    // bucket-id builds: interleaved schedule only
+  static_assert(BM == 0 || !NOPOS, "bucket-id streams carry positions");
+  // KEYS0 with BM: the first pass over V_hist0's per-window bucket ids (~0: not indexed)
+  const KT* __restrict__ kinT = reinterpret_cast<const KT*>(kin);
+  KT* __restrict__ koutT = reinterpret_cast<KT*>(kout);
   constexpr int TB = NWV * 64;                  // threads per workgroup
   constexpr int PER = PTILE / NWV / 64;         // elements per lane
   constexpr int DPT = (int)((SL::MAXR + TB - 1) / TB);   // digits owned per thread
@@ -532,7 +566,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
     }
   };
   // the next tile's inputs are in flight while this one is processed
-  uint64_t nkey[PER];
+  KT nkey[PER];
   uint32_t npos[PER];
   StageRegs<PSTAGE_W16> nchars;
   auto prefetch = [&](uint32_t tv) {
@@ -545,10 +579,9 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       for (int cc = 0; cc < PER; ++cc) {   // e < ntiles * PTILE <= n_max + pad: in bounds
         const uint64_t e = t0 + wbase + (uint32_t)cc * 64 + lane;
         if (KEYS0) {
-          nkey[cc] = kin[e < n ? e : n - 1];
-          npos[cc] = (uint32_t)(e + 1);
+          nkey[cc] = kinT[e < n ? e : n - 1];    // positions implicit: e + 1 (below)
         } else {
-          nkey[cc] = kin[e];
+          nkey[cc] = kinT[e];
           npos[cc] = NOPOS ? 0u : pin[e];
         }
       }
@@ -562,13 +595,13 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
   for (int q = 0; q < DPT; ++q) cursor[q] = ngb[q];
 #pragma unroll
   for (int j = 0; j < PTILE / TB; ++j) {
-    kout[pad + threadIdx.x] = 0;
+    if (BM != 2) koutT[pad + threadIdx.x] = 0;
     if (!NOPOS) pout[pad + threadIdx.x] = 0;
   }
   for (uint32_t it = 0; it < n_iter; ++it) {
     const uint32_t tile = tile_at(it);
     const uint64_t tile0 = (uint64_t)tile * PTILE;
-    uint64_t key[PER];
+    KT key[PER];
     uint32_t ps[PER], dg[PER];
     bool act[PER];
     if (ch.interleaved) {
@@ -579,7 +612,10 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       stage_pack(nchars, S.st);
     } else {
 #pragma unroll
-      for (int cc = 0; cc < PER; ++cc) { key[cc] = nkey[cc]; ps[cc] = npos[cc]; }
+      for (int cc = 0; cc < PER; ++cc) {
+        key[cc] = nkey[cc];
+        ps[cc] = KEYS0 ? (uint32_t)(tile0 + wbase + (uint32_t)cc * 64 + lane + 1) : npos[cc];
+      }
     }
     prefetch(tile_at(min(it + 1, n_iter - 1)));   // unconditional: static vmcnt
     for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
@@ -589,15 +625,21 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       const uint32_t w = wbase + (uint32_t)c * 64 + lane;     // element index inside the tile
       const uint64_t e = tile0 + w;
       if (FROM_SEQ) {
-        key[c] = 0;
-        act[c] = e < n && window_key(S.st, HALO + (int)w, (int64_t)e, L, k, key[c]);
+        uint64_t kk = 0;
+        act[c] = e < n && window_key(S.st, HALO + (int)w, (int64_t)e, L, k, kk);
         ps[c] = (uint32_t)(e + 1);
+        const uint64_t h = mix64(kk);
+        const uint32_t bl = bucket_local(h, g);
+        act[c] = act[c] && bl < g.nb;                        // a part build keeps its buckets
+        key[c] = BM ? (KT)bl : (KT)kk;
+        dg[c] = act[c] ? digit_of_b(bl, D) : 0;
+      } else if (BM) {
+        act[c] = e < n && !(KEYS0 && (uint32_t)key[c] == ~0u);
+        dg[c] = act[c] ? digit_of_b((uint32_t)key[c], D) : 0;
       } else {
         act[c] = e < n && !(KEYS0 && skip_empty && key[c] == EMPTY_KEY);
+        dg[c] = act[c] ? digit_of_h(mix64((uint64_t)key[c]), g, D) : 0;
       }
-      const uint64_t h = mix64(key[c]);
-      if (FROM_SEQ) act[c] = act[c] && in_part(h, g);      // a part build keeps its buckets
-      dg[c] = act[c] ? digit_of_h(h, g, D) : 0;
     }
 #pragma unroll
     for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
@@ -664,7 +706,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       const uint32_t i = (uint32_t)(j * TB) + threadIdx.x;
       // lanes past the tile's end store into the PTILE-element pad behind the outputs
       const uint32_t dst = i < (uint32_t)tile_n ? S.sdst[i] : pad + threadIdx.x;
-      kout[dst] = S.skey[i];
+      if (BM != 2) koutT[dst] = S.skey[i];
       if (!NOPOS) pout[dst] = S.spos[i];
     }
   }
@@ -676,7 +718,11 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
 // below by a shuffle (one extra load per chunk), so every key is read and hashed once.
 __global__ void __launch_bounds__(BLOCK)
 k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
-            uint32_t* __restrict__ start) {
+            uint32_t* __restrict__ start, int bid) {
+  const uint32_t* __restrict__ bids = reinterpret_cast<const uint32_t*>(keys);
+  auto bucket_at = [&](uint64_t i) -> uint32_t {
+    return bid ? bids[i] : bucket_local(mix64(keys[i]), g);
+  };
   const uint64_t n = *n_ptr;
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   if (n == 0) {
@@ -691,10 +737,10 @@ k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_pt
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t i = c0 + (uint64_t)j * 64 + lane;
-      bk[j] = i < n ? bucket_local(mix64(keys[i]), g) : g.nb;
+      bk[j] = i < n ? bucket_at(i) : g.nb;
     }
     int64_t before = -1;                       // bucket of element c0 - 1
-    if (c0) before = (int64_t)bucket_local(mix64(keys[c0 - 1]), g);
+    if (c0) before = (int64_t)bucket_at(c0 - 1);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t i = c0 + (uint64_t)j * 64 + lane;
@@ -724,7 +770,7 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ n_ptr, Geom g,
                Digit Dlast, uint32_t div, const uint32_t* __restrict__ hist, uint32_t C,
                const uint32_t* __restrict__ lo_start, uint32_t spread,
-               uint32_t* __restrict__ start) {
+               uint32_t* __restrict__ start, int bid) {
   __shared__ uint32_t cnt[V2_MAXR];
   const uint32_t lo = blockIdx.x;
   const uint32_t R = Dlast.R;
@@ -734,7 +780,8 @@ k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ 
   __syncthreads();
   const uint32_t tile = P / PTILE;
   for (uint32_t i = tile * PTILE + threadIdx.x; i < P; i += BLOCK)
-    atomicAdd(&cnt[digit_of(kprev[i], g, Dlast)], 1u);
+    atomicAdd(&cnt[bid ? digit_of_b(reinterpret_cast<const uint32_t*>(kprev)[i], Dlast)
+                       : digit_of(kprev[i], g, Dlast)], 1u);
   __syncthreads();
   for (uint32_t hi = threadIdx.x; hi < R; hi += BLOCK) {
     const uint64_t b = (uint64_t)hi * div + lo;
@@ -993,7 +1040,13 @@ __device__ __forceinline__ int lds_find_g(const GroupTable& W, uint64_t key) {
 // for buckets it does not take).  W, sh, red are the caller's LDS.
 // COUNT_ONLY (occurrence counts of a key stream, kmhg_sh.hip's read counting): pass B -- the
 // positions -- is skipped; slots get {key, count, unspecified aux}.
-template <bool COUNT_ONLY = false, int TB = BLOCK>
+// CK (bucket-id streams): the stream holds positions only; each window's key is cut from the
+// sequence's code words (`code`, 16 chars per u32) at its position -- three loads per window
+// from a 0.25 B/window array, against 8 B of key per window carried through every radix pass.
+struct Words3 {                                // three consecutive code words, 4-B aligned
+  uint32_t a, b, c;
+};
+template <bool COUNT_ONLY = false, int TB = BLOCK, bool CK = false>
 __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint32_t (*red)[TB / 64],
                                               const uint64_t* __restrict__ keys,
                                               const uint32_t* __restrict__ pos,
@@ -1004,7 +1057,10 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
                                               BuildMeta* __restrict__ meta, const uint32_t b,
                                               uint8_t* __restrict__ TG = nullptr,
                                               uint32_t* __restrict__ mbits = nullptr,
-                                              int fp_insert = 0) {
+                                              int fp_insert = 0,
+                                              const uint32_t* __restrict__ code = nullptr,
+                                              int k = 0) {
+  static_assert(!(CK && COUNT_ONLY), "code-word keys belong to position builds");
   constexpr int NW = TB / 64;                         // waves of the workgroup
   constexpr int PER = 2 * V2_BW_WG / TB;              // elements per thread per batch (2x mean)
   constexpr uint32_t BATCH = TB * PER;
@@ -1017,6 +1073,25 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   // element c of thread t in a batch: i0 + c * TB + t, so position order = (c, wave, lane)
   auto elem = [&](uint32_t i0, int c) { return i0 + (uint32_t)c * TB + threadIdx.x; };
   auto load = [&](uint32_t i0) {
+    if (CK) {                    // positions first, then all the code words in flight at once
+      uint32_t wa[PER], wb[PER], wc[PER];
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        const uint32_t i = elem(i0, c);
+        ps[c] = i < s1 ? pos[i] : 1u;               // 1-based window start
+      }
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {       // one 12-B load per window (global_load_dwordx3)
+        const Words3 w3 = *reinterpret_cast<const Words3*>(code + ((ps[c] - 1u) >> 4));
+        wa[c] = w3.a;
+        wb[c] = w3.b;
+        wc[c] = w3.c;
+      }
+#pragma unroll
+      for (int c = 0; c < PER; ++c)
+        key[c] = elem(i0, c) < s1 ? code_key(wa[c], wb[c], wc[c], (int64_t)ps[c] - 1, k) : 0;
+      return;
+    }
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       const uint32_t i = elem(i0, c);
@@ -1211,18 +1286,19 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
 
 // TB threads per workgroup: 256 (4 waves) or 512 (8 waves: the LDS table allows 6 workgroups
 // per CU, so 8-wave groups fill the CU's 32 wave slots where 4-wave groups stop at 24).
-template <bool COUNT_ONLY, int TB = BLOCK>
+template <bool COUNT_ONLY, int TB = BLOCK, bool CK = false>
 __global__ void __launch_bounds__(TB)
 k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
                int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
                BuildMeta* __restrict__ meta, uint8_t* __restrict__ TG,
-               uint32_t* __restrict__ mbits, int fp_insert) {
+               uint32_t* __restrict__ mbits, int fp_insert, const uint32_t* __restrict__ code,
+               int k) {
   __shared__ GroupTable W;
   __shared__ uint64_t sh[2 * (TB / 64)];
   __shared__ uint32_t red[3][TB / 64];
-  bucket_wg_cas<COUNT_ONLY, TB>(W, sh, red, keys, pos, start, g, T, positions, bstats, meta,
-                                blockIdx.x, TG, mbits, fp_insert);
+  bucket_wg_cas<COUNT_ONLY, TB, CK>(W, sh, red, keys, pos, start, g, T, positions, bstats, meta,
+                                    blockIdx.x, TG, mbits, fp_insert, code, k);
 }
 
 // ---------------------------------------------------------------- V_bucket_sort (group per bucket)
@@ -1581,18 +1657,19 @@ static inline unsigned grid_of(uint64_t n, unsigned per) {
 // KMHG_SCATTER_WPC=n (A/B): at most n scatter workgroups per CU.  Fewer tiles in flight per XCD
 // means fewer partially written digit-run lines held dirty in its L2 (beyond the Infinity
 // Cache, config 3 writes 1.4-1.7x the algorithmic bytes), at the cost of latency hiding.
+static unsigned scatter_cap_of(const void* kernel) {
+  unsigned c = resident_blocks(kernel);
+  if (const char* e = std::getenv("KMHG_SCATTER_WPC")) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const unsigned want = (unsigned)std::max(1, std::atoi(e)) * (unsigned)std::max(cus, 1);
+    c = std::min(c, want);
+  }
+  return c;
+}
 static unsigned scatter_cap() {
-  static unsigned cap = [] {
-    unsigned c = resident_blocks((const void*)k_v2_scatter<true, false, false, 4>);
-    if (const char* e = std::getenv("KMHG_SCATTER_WPC")) {
-      int dev = 0, cus = 256;
-      if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      const unsigned want = (unsigned)std::max(1, std::atoi(e)) * (unsigned)std::max(cus, 1);
-      c = std::min(c, want);
-    }
-    return c;
-  }();
+  static unsigned cap = scatter_cap_of((const void*)k_v2_scatter<true, false, false, 4>);
   return cap;
 }
 
@@ -1617,8 +1694,9 @@ Chunks make_chunks(uint32_t ntiles) {
   ch.C = (ntiles + ch.tpc - 1) / ch.tpc;   // every chunk holds >= 1 tile
   return ch;
 }
-static unsigned scatter_grid(const Chunks& ch) {
-  return ch.interleaved ? std::min<unsigned>(ch.ntiles, scatter_cap()) : ch.C;
+// `cap`: the launched variant's resident workgroups (its own VGPR / LDS occupancy)
+static unsigned scatter_grid(const Chunks& ch, unsigned cap) {
+  return ch.interleaved ? std::min<unsigned>(ch.ntiles, cap) : ch.C;
 }
 
 // 8-wave scatter workgroups only with KMHG_SC8=1 (interleaved schedule, R <= V2_MAXR_IL):
@@ -1632,35 +1710,45 @@ static unsigned scatter8_grid(const Chunks& ch) {
   static const unsigned cap = resident_blocks((const void*)k_v2_scatter<true, false, false, 8>, 512);
   return std::min<unsigned>(ch.ntiles, cap);
 }
-#define KMHG_SCATTER(FS, K0, NP, ...)                                                       \
+#define KMHG_SCATTER_BM(FS, K0, NP, BM, ...)                                                 \
   do {                                                                                      \
     if (scatter8(ch, D))                                                                    \
-      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, 8>), dim3(scatter8_grid(ch)), dim3(512), \
-                         0, s, __VA_ARGS__);                                                \
-    else                                                                                    \
-      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, 4>), dim3(scatter_grid(ch)), dim3(BLOCK),\
-                         0, s, __VA_ARGS__);                                                \
+      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, 8, BM>), dim3(scatter8_grid(ch)),        \
+                         dim3(512), 0, s, __VA_ARGS__);                                     \
+    else {                                                                                  \
+      static const unsigned cap_ = scatter_cap_of((const void*)k_v2_scatter<FS, K0, NP, 4, BM>); \
+      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, 4, BM>), dim3(scatter_grid(ch, cap_)),   \
+                         dim3(BLOCK), 0, s, __VA_ARGS__);                                   \
+    }                                                                                       \
   } while (0)
+#define KMHG_SCATTER(FS, K0, NP, ...) KMHG_SCATTER_BM(FS, K0, NP, 0, __VA_ARGS__)
 
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
                      BuildMeta* meta, hipStream_t s, uint32_t* code, uint16_t* nbit,
-                     uint32_t* uniq0) {
+                     uint32_t* uniq0, uint32_t* bids) {
   static const int persist = [] {
     const char* e = std::getenv("KMHG_HIST0P");
     return (e && e[0] == '0') ? 0 : 1;
   }();
+  if (bids) {                  // bucket-id builds: the persistent kernel (interleaved schedule)
+    static const unsigned cap_b = resident_blocks((const void*)k_v2_hist0p<true, true>);
+    hipLaunchKernelGGL((k_v2_hist0p<true, true>), dim3(std::min<unsigned>(ch.ntiles, cap_b)),
+                       dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status,
+                       n_status, meta, code, nbit, uniq0, bids);
+    return;
+  }
   if (ch.interleaved && persist) {
     static const unsigned cap_c = resident_blocks((const void*)k_v2_hist0p<true>);
     static const unsigned cap_n = resident_blocks((const void*)k_v2_hist0p<false>);
     if (code && nbit)
       hipLaunchKernelGGL(k_v2_hist0p<true>, dim3(std::min<unsigned>(ch.ntiles, cap_c)), dim3(BLOCK),
                          0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status, n_status,
-                         meta, code, nbit, uniq0);
+                         meta, code, nbit, uniq0, nullptr);
     else
       hipLaunchKernelGGL(k_v2_hist0p<false>, dim3(std::min<unsigned>(ch.ntiles, cap_n)), dim3(BLOCK),
                          0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status, n_status,
-                         meta, nullptr, nullptr, nullptr);
+                         meta, nullptr, nullptr, nullptr, nullptr);
     return;
   }
   hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
@@ -1677,6 +1765,13 @@ void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total,
                        (const uint64_t*)status, total);
   }
 }
+void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
+                        uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
+                        hipStream_t s, uint32_t* save_col0) {
+  hipLaunchKernelGGL((k_v2_hist<false, true>), dim3(ch.C), dim3(BLOCK), 0, s,
+                     reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ch, xcd_map(),
+                     scan_status, n_status, nullptr, nullptr, save_col0, 0);
+}
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0, bool skip_empty) {
@@ -1691,9 +1786,10 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 }
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
-                         uint32_t spread, uint32_t* start, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_bounds_lo, dim3(div), dim3(BLOCK), 0, s, kprev, n_ptr, g, Dlast, div,
-                     hist, C, lo_start, spread, start);
+                         uint32_t spread, uint32_t* start, hipStream_t s, const uint32_t* bprev) {
+  hipLaunchKernelGGL(k_v2_bounds_lo, dim3(div), dim3(BLOCK), 0, s,
+                     bprev ? reinterpret_cast<const uint64_t*>(bprev) : kprev, n_ptr, g, Dlast,
+                     div, hist, C, lo_start, spread, start, bprev ? 1 : 0);
 }
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s) {
@@ -1707,6 +1803,30 @@ void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geo
                            uint32_t pad, hipStream_t s) {
   KMHG_SCATTER(true, false, false, seq, L, k, Nw, 1, nullptr, nullptr, nullptr, g, D, hist, ch,
                kout, pout, pad, xcd_map(), 0);
+}
+void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
+                            const uint32_t* hist, Chunks ch, uint32_t* bout, uint32_t* pout,
+                            uint32_t pad, hipStream_t s) {
+  const uint64_t* ki = reinterpret_cast<const uint64_t*>(bids);
+  uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
+  if (bout)
+    KMHG_SCATTER_BM(false, true, false, 1, nullptr, (int64_t)0, 0, Nw, 0, ki, nullptr, nullptr, g,
+                    D, hist, ch, ko, pout, pad, xcd_map(), 0);
+  else
+    KMHG_SCATTER_BM(false, true, false, 2, nullptr, (int64_t)0, 0, Nw, 0, ki, nullptr, nullptr, g,
+                    D, hist, ch, ko, pout, pad, xcd_map(), 0);
+}
+void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
+                           Geom g, Digit D, const uint32_t* hist, Chunks ch, uint32_t* bout,
+                           uint32_t* pout, uint32_t pad, hipStream_t s) {
+  const uint64_t* ki = reinterpret_cast<const uint64_t*>(bin);
+  uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
+  if (bout)
+    KMHG_SCATTER_BM(false, false, false, 1, nullptr, (int64_t)0, 0, (int64_t)0, 0, ki, pin,
+                    n_ptr, g, D, hist, ch, ko, pout, pad, xcd_map(), 0);
+  else
+    KMHG_SCATTER_BM(false, false, false, 2, nullptr, (int64_t)0, 0, (int64_t)0, 0, ki, pin,
+                    n_ptr, g, D, hist, ch, ko, pout, pad, xcd_map(), 0);
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
@@ -1732,10 +1852,12 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
                hist, ch, kout, nullptr, pad, xcd_map(), 0);
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
-                      uint64_t n_max, hipStream_t s) {
+                      uint64_t n_max, hipStream_t s, const uint32_t* bids) {
   unsigned gr = grid_of(n_max > g.nb ? n_max : g.nb, BLOCK);
   if (gr > 16384) gr = 16384;
-  hipLaunchKernelGGL(k_v2_bounds, dim3(gr), dim3(BLOCK), 0, s, keys, n_ptr, g, start);
+  hipLaunchKernelGGL(k_v2_bounds, dim3(gr), dim3(BLOCK), 0, s,
+                     bids ? reinterpret_cast<const uint64_t*>(bids) : keys, n_ptr, g, start,
+                     bids ? 1 : 0);
 }
 void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                       Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
@@ -1762,17 +1884,24 @@ static int bucket_fp() {
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         bool count_only, hipStream_t s, uint8_t* TG, uint32_t* mbits) {
+                         bool count_only, hipStream_t s, uint8_t* TG, uint32_t* mbits,
+                         const uint32_t* code, int k) {
   const int fp = bucket_fp();
   if (count_only)
     hipLaunchKernelGGL(k_v2_bucket_wg<true>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
-                       positions, bstats, meta, nullptr, nullptr, fp);
+                       positions, bstats, meta, nullptr, nullptr, fp, nullptr, 0);
+  else if (bucket_tb() == 512 && code)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, 512, true>), dim3(g.nb), dim3(512), 0, s, keys, pos,
+                       start, g, T, positions, bstats, meta, TG, mbits, fp, code, k);
   else if (bucket_tb() == 512)
     hipLaunchKernelGGL((k_v2_bucket_wg<false, 512>), dim3(g.nb), dim3(512), 0, s, keys, pos, start,
-                       g, T, positions, bstats, meta, TG, mbits, fp);
+                       g, T, positions, bstats, meta, TG, mbits, fp, nullptr, 0);
+  else if (code)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, BLOCK, true>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
+                       pos, start, g, T, positions, bstats, meta, TG, mbits, fp, code, k);
   else
     hipLaunchKernelGGL(k_v2_bucket_wg<false>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g,
-                       T, positions, bstats, meta, TG, mbits, fp);
+                       T, positions, bstats, meta, TG, mbits, fp, nullptr, 0);
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {

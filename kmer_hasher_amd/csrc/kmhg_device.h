@@ -244,6 +244,16 @@ __device__ __forceinline__ bool window_key(const ST& st, int o, int64_t s, int64
   return true;
 }
 
+// The key of window j (0-based) from a sequence's global code words (the stage's format, 16
+// chars per u32 MSB-first; a, b, c = words j / 16 .. j / 16 + 2): window_key's extraction.
+__device__ __forceinline__ uint64_t code_key(uint32_t a, uint32_t b, uint32_t c, int64_t j, int k) {
+  const int sh = (int)(j & 15) * 2;
+  const uint64_t x = ((uint64_t)a << 32) | b;
+  const uint64_t y = c;
+  const uint64_t t = (x << sh) | ((y << sh) >> 32);
+  return t >> (64 - 2 * k);
+}
+
 // ------------------------------------------------------------------ hash table primitives
 // Table geometry: nb buckets of capb slots (+ one side slot at nb*capb).  A key's bucket is
 // mulhi(h, nb) (high hash bits), its home inside the bucket mulhi32(lo32(h), capb), and linear

@@ -906,7 +906,27 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const Geom g = idx->geom;
   const uint64_t nhist = (uint64_t)R * ch.C;
   const uint32_t scan_tiles = tiles_for(nhist);
-  DBuf<uint64_t> kA(Nw + PTILE, s), kB(Nw + PTILE, s);   // + pad (launch_v2_scatter)
+  // bucket-id streams (position builds that keep the code words): the radix passes carry
+  // (bucket id, pos) -- 8 B per window instead of 12 -- the last pass positions only, and the
+  // bucket kernel cuts each key from the code words.  The cut is a random 12-B read per window:
+  // cheap while the code words (Nw / 4 bytes) stay in an XCD's 4 MB L2, a 128-B Infinity-Cache
+  // line per window beyond.  Measured (A/B in one run): config 2 (10 M windows, 2.5 MB of code)
+  // 30.1 -> 31.1 Gbp/s; config 3 (100 M, 25 MB) 28.5 -> 24.0 (bucket kernel 0.84 -> 2.0 ms).
+  // So on up to BID_MAX_WINDOWS; KMHG_BUILD_BID=0 / 1 forces key / bucket-id streams.
+  constexpr int64_t BID_MAX_WINDOWS = 12 << 20;
+  const char* bide = std::getenv("KMHG_BUILD_BID");
+  const bool bid_on = bide ? bide[0] == '1' : Nw <= BID_MAX_WINDOWS;
+  const bool bid = codes && !from_keys && group && !sorted && !count_only && ch.interleaved &&
+                   bid_on;
+  DBuf<uint64_t> kA(bid ? 1 : Nw + PTILE, s), kB(bid ? 1 : Nw + PTILE, s);   // + pad
+  // bucket ids: pass p writes bA / bB alternately; the last pass writes none (the bucket bounds
+  // pass V_bounds of 3+ passes reads the last one's, so it is written there)
+  const bool bounds_from_hist = ch.interleaved && passes <= 2 &&
+                                !(std::getenv("KMHG_BOUNDS") &&
+                                  std::string(std::getenv("KMHG_BOUNDS")) == "scan");
+  // (bB first holds V_hist0's per-window ids, the first pass's input)
+  DBuf<uint32_t> bA(bid && (passes > 1 || !bounds_from_hist) ? Nw + PTILE : 1, s);
+  DBuf<uint32_t> bB(bid ? Nw + PTILE : 1, s);
   const bool no_pos = count_only && group && !sorted;   // keys only through the passes
   DBuf<uint32_t> pA(no_pos ? 1 : Nw + PTILE, s), pB(no_pos ? 1 : Nw + PTILE, s);
   const uint32_t pad = (uint32_t)Nw;
@@ -933,9 +953,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 
   // bucket starts straight from the histograms (V_bounds_lo) for one or two passes;
   // KMHG_BOUNDS=scan (tests) forces the pass over the sorted keys (V_bounds)
-  const char* be = std::getenv("KMHG_BOUNDS");
-  const bool bounds_scan = be && std::string(be) == "scan";
-  const bool bounds_lo = ch.interleaved && passes <= 2 && !bounds_scan;
+  const bool bounds_lo = bounds_from_hist;
   DBuf<uint32_t> lo_start(bounds_lo && passes == 2 ? R : 1, s);
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
@@ -962,14 +980,35 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     if (prep) idx->ptag.reset(idx->slots() + 32);   // + the 32-B span the last probe group reads
     LAUNCH("k_v2_hist0", s,
            launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, status, n_status,
-                           meta, s, db.code, db.nbit, prep ? db.uniq : nullptr));
+                           meta, s, db.code, db.nbit, prep ? db.uniq : nullptr,
+                           bid ? bB.p : nullptr));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
-    LAUNCH("k_v2_scatter_seq", s,
-           launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, kA.p, pA.p,
-                                 pad, s));
+    if (bid)
+      LAUNCH("k_v2_scatter_seq", s,
+             launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ch,
+                                    passes == 1 && bounds_lo ? nullptr : bA.p, pA.p, pad, s));
+    else
+      LAUNCH("k_v2_scatter_seq", s,
+             launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, kA.p, pA.p,
+                                   pad, s));
     div = R;
   }
-  for (uint32_t p = from_keys ? 0 : 1; p < passes; ++p) {
+  uint32_t *bin = bA.p, *bout = bB.p;
+  for (uint32_t p = 1; bid && p < passes; ++p) {
+    const Digit Dp = make_digit(div, R);
+    const bool last = p + 1 == passes;
+    LAUNCH("k_v2_hist", s,
+           launch_v2_hist_bid(bin, n_valid, g, Dp, hist.p, ch, status, n_status, s,
+                              bounds_lo && passes == 2 ? lo_start.p : nullptr));
+    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
+    LAUNCH("k_v2_scatter", s,
+           launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hist.p, ch,
+                                 last && bounds_lo ? nullptr : bout, pout, pad, s));
+    std::swap(bin, bout);
+    std::swap(pin, pout);
+    div *= R;
+  }
+  for (uint32_t p = from_keys ? 0 : 1; !bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
     const bool keys0 = from_keys && p == 0;
     const uint64_t* src = keys0 ? d_keys : kin;
@@ -1020,9 +1059,11 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     LAUNCH("k_v2_bounds", s,
            launch_v2_bounds_lo(passes == 2 ? kout : nullptr, n_valid, g, make_digit(div_last, R),
                                div_last, hist.p, ch.C, passes == 2 ? lo_start.p : nullptr,
-                               g.nb / gb.nb, start.p, s));
+                               g.nb / gb.nb, start.p, s,
+                               bid && passes == 2 ? bout : nullptr));
   } else {
-    LAUNCH("k_v2_bounds", s, launch_v2_bounds(kin, n_valid, gb, start.p, (uint64_t)Nw, s));
+    LAUNCH("k_v2_bounds", s, launch_v2_bounds(kin, n_valid, gb, start.p, (uint64_t)Nw, s,
+                                              bid ? bin : nullptr));
   }
 #ifdef KMHG_STAMPS
   static uint64_t* stamps = nullptr;
@@ -1038,7 +1079,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     LAUNCH("k_v2_bucket_wg", s,
            launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, bstats.p,
                                meta, no_pos, s, prep ? idx->ptag.p : nullptr,
-                               prep ? db.uniq : nullptr));
+                               prep ? db.uniq : nullptr, bid ? db.code : nullptr, k));
   else
     LAUNCH("k_v2_bucket", s,
            launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,

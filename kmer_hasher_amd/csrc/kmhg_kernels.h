@@ -171,7 +171,8 @@ Chunks make_chunks(uint32_t ntiles);
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
                      BuildMeta* meta, hipStream_t s, uint32_t* code = nullptr,
-                     uint16_t* nbit = nullptr, uint32_t* uniq0 = nullptr);
+                     uint16_t* nbit = nullptr, uint32_t* uniq0 = nullptr,
+                     uint32_t* bids = nullptr);
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
 // exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the histogram kernel
@@ -193,9 +194,11 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 // value (div of them); kprev = the last pass's input keys, lo_start = the previous pass's digit
 // starts (saved by launch_v2_hist's save_col0; nullptr for one pass); start[b / spread] for
 // buckets b that are multiples of spread, start[nb / spread] = n
+// bprev (bucket-id streams): the last pass's input bucket ids instead of kprev
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
-                         uint32_t spread, uint32_t* start, hipStream_t s);
+                         uint32_t spread, uint32_t* start, hipStream_t s,
+                         const uint32_t* bprev = nullptr);
 // also copies *n_valid (launch it after the pass's scan) to *host_n
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s);
@@ -216,8 +219,22 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s);
+// Bucket-id streams (position builds that keep the sequence's code words): V_hist0 stores
+// every window's bucket id (`bids`, Nw u32, ~0 = not indexed), the radix passes carry (bucket
+// id u32, pos u32) and the last pass writes positions only (bout = nullptr); the bucket kernel
+// cuts the keys from the code words.  Histograms without hashing.
+void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
+                            const uint32_t* hist, Chunks ch, uint32_t* bout, uint32_t* pout,
+                            uint32_t pad, hipStream_t s);
+void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
+                           Geom g, Digit D, const uint32_t* hist, Chunks ch, uint32_t* bout,
+                           uint32_t* pout, uint32_t pad, hipStream_t s);
+void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
+                        uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
+                        hipStream_t s, uint32_t* save_col0 = nullptr);
+// bids (bucket-id streams): the sorted bucket ids instead of keys
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
-                      uint64_t n_max, hipStream_t s);
+                      uint64_t n_max, hipStream_t s, const uint32_t* bids = nullptr);
 struct BucketStats {           // per-bucket partials of the build statistics
   uint32_t n_kmers, max_count;
   uint64_t n_pairs;
@@ -229,10 +246,11 @@ void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint
                            Geom g, Slot* T, int32_t* positions, BucketStats* bstats,
                            BuildMeta* meta, hipStream_t s);
 // count_only: occurrence counts only (no positions written; slot aux unspecified)
+// code (bucket-id streams): keys unused, each window's key cut from the code words at its pos
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, uint8_t* TG = nullptr,
-                         uint32_t* mbits = nullptr);
+                         uint32_t* mbits = nullptr, const uint32_t* code = nullptr, int k = 0);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);
 

@@ -439,16 +439,6 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
   __syncthreads();
 }
 
-// The key of index window j (0-based) from the index's code words: the stage's window_key
-// extraction on global words (qw = j / 16, three consecutive words).
-__device__ __forceinline__ uint64_t code_key(uint32_t a, uint32_t b, uint32_t c, int64_t j, int k) {
-  const int sh = (int)(j & 15) * 2;
-  const uint64_t x = ((uint64_t)a << 32) | b;
-  const uint64_t y = c;
-  const uint64_t t = (x << sh) | ((y << sh) >> 32);
-  return t >> (64 - 2 * k);
-}
-
 // The diagonal path of a staged tile, every lane's WPT windows: the verification words of every
 // prediction are loaded first, all in flight at once (a window without a prediction loads word
 // 0, so every lane issues a static number of loads), then resolved; windows whose prediction

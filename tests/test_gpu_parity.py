@@ -222,16 +222,20 @@ def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     _check_against_oracle("G" * 40, 32, qks=[31])
 
 
+@pytest.mark.parametrize("stream", ["bid", "keys"])
 @pytest.mark.parametrize("bounds", ["lo", "scan", "sc8"])
 @pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
-def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds):
+def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds, stream):
     """More radix passes than the input needs (KMHG_MAXR caps the radix): 1-4 passes with N-runs
     and repeat-rich input.  Bucket starts come from the radix histograms for one or two passes
     (k_v2_bounds_lo: the partial-tile count at each low digit's first element; a zero-width
     tile at a tile boundary) and from a pass over the sorted keys otherwise or with
-    KMHG_BOUNDS=scan; both against the oracle."""
+    KMHG_BOUNDS=scan; both against the oracle.  Position builds carry bucket ids through the
+    passes and cut the keys from the code words (default); KMHG_BUILD_BID=0 carries the keys."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_MAXR", maxr)
+    monkeypatch.setenv("KMHG_BUCKET", "group")     # bucket-id streams need group buckets
+    monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
     if bounds == "sc8":                    # the 8-wave radix scatter (KMHG_SC8=1)
         monkeypatch.setenv("KMHG_SC8", "1")
     else:
