@@ -54,8 +54,8 @@ CONFIGS = {
 
 # HIP-event labels (kmhg_timing_*) -> the kernel names rocprofv3 reports (template instances in
 # full, and the variant a label launches: e.g. k_v2_hist0 runs k_v2_hist0p<true>)
-PMC_PREFIX = {"k_v2_scatter_seq": ("k_v2_scatter<true",),
-              "k_v2_scatter": ("k_v2_scatter<false",),
+PMC_PREFIX = {"k_v2_scatter_seq": ("k_v2_scatter<true", "k_v2_scatter<false, true"),
+              "k_v2_scatter": ("k_v2_scatter<false, false",),
               "k_v2_hist0": ("k_v2_hist0p<", "k_v2_hist0("),
               "k_v2_hist": ("k_v2_hist<",),
               "k_scan_u32": ("k_scan_lb_u32",),
@@ -77,14 +77,31 @@ def pmc_traffic(pmc: dict, kernel: str):
     return None
 
 
+BID_MAX_WINDOWS = 12 << 20   # kmhg_engine.cpp build_device_v2: bucket-id streams up to here
+
+
+def bid_streams(Nw: int) -> bool:
+    """Whether a position build of Nw windows runs bucket-id radix streams (the engine's rule,
+    KMHG_BUILD_BID=0/1 forcing it)."""
+    e = os.environ.get("KMHG_BUILD_BID")
+    return e.startswith("1") if e else Nw <= BID_MAX_WINDOWS
+
+
 def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) -> int | None:
-    """Minimal bytes each kernel must move (DESIGN.md "Roofline accounting")."""
+    """Minimal bytes each kernel must move (DESIGN.md "Roofline accounting").  Bucket-id builds
+    (bid_streams): V_hist0 writes a 4-B id per window, the first pass reads the ids and writes
+    (id, pos), the last pass reads them and writes positions, the bucket kernel reads positions
+    and cuts the keys from the code words (0.25 B per window once)."""
+    bid = bid_streams(Nw)
+    if kernel == "k_v2_hist0" and bid:
+        return L + 4 * Nw
     if kernel == "k_v2_scatter_seq":    # read L chars; write (key 8 B, pos 4 B) per valid window
-        return L + 12 * N
+        return 4 * Nw + 8 * N if bid else L + 12 * N
     if kernel == "k_v2_scatter":        # one radix pass: read + write 12 B per window
-        return 24 * N
+        return 12 * N if bid else 24 * N
     if kernel in ("k_v2_bucket", "k_v2_bucket_wg", "k_v2_bucket_sort"):   # read 12 B/window; one 16-B slot per distinct key; 4 B per
-        return 12 * N + 16 * U + 4 * (N - U)   # position of a repeated key (>= N - U of them)
+        rd = 4 * N + Nw // 4 if bid else 12 * N
+        return rd + 16 * U + 4 * (N - U)   # position of a repeated key (>= N - U of them)
     if kernel == "k_build_insert":      # read L chars; key+count per distinct key; slot id/window
         return L + 12 * U + 4 * Nw
     if kernel == "k_build_compact":     # key+count read, key+count+offset written per key

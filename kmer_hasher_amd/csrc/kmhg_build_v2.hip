@@ -1072,9 +1072,11 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   int slot[PER];
   // element c of thread t in a batch: i0 + c * TB + t, so position order = (c, wave, lane)
   auto elem = [&](uint32_t i0, int c) { return i0 + (uint32_t)c * TB + threadIdx.x; };
+  uint32_t wa[PER], wb[PER], wc[PER];                 // CK: each window's three code words
+  // CK: load() issues the positions, then the code words, all in flight at once; cut() turns
+  // them into keys -- after the table clear for the first batch, so the clear hides the loads
   auto load = [&](uint32_t i0) {
-    if (CK) {                    // positions first, then all the code words in flight at once
-      uint32_t wa[PER], wb[PER], wc[PER];
+    if (CK) {
 #pragma unroll
       for (int c = 0; c < PER; ++c) {
         const uint32_t i = elem(i0, c);
@@ -1087,9 +1089,6 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
         wb[c] = w3.b;
         wc[c] = w3.c;
       }
-#pragma unroll
-      for (int c = 0; c < PER; ++c)
-        key[c] = elem(i0, c) < s1 ? code_key(wa[c], wb[c], wc[c], (int64_t)ps[c] - 1, k) : 0;
       return;
     }
 #pragma unroll
@@ -1099,6 +1098,13 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
       ps[c] = (!COUNT_ONLY && i < s1) ? pos[i] : 0;
     }
   };
+  auto cut = [&](uint32_t i0) {
+    if (CK) {
+#pragma unroll
+      for (int c = 0; c < PER; ++c)
+        key[c] = elem(i0, c) < s1 ? code_key(wa[c], wb[c], wc[c], (int64_t)ps[c] - 1, k) : 0;
+    }
+  };
   STAMP_WG(b, 0);
   load(s0);                                           // in flight while the table is cleared
   for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += TB) {
@@ -1106,6 +1112,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     W.cc[j] = make_uint2(0u, 0u);
   }
   __syncthreads();
+  cut(s0);
   STAMP_WG(b, 1);
   STAMP_WG_DRAIN(b, 6);
   // pass A: distinct keys + counts (CAS on a table shared by the four waves).  (Measured:
@@ -1144,7 +1151,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   // issuing the first CAS of all 8 elements of a lane back to back before resolving any,
   // 98 -> 112 us.)
   for (uint32_t i0 = s0; !done && i0 < s1; i0 += BATCH) {
-    if (i0 != s0) load(i0);
+    if (i0 != s0) { load(i0); cut(i0); }
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       slot[c] = -1;
@@ -1219,6 +1226,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   for (uint32_t i0 = s0; i0 < (COUNT_ONLY ? s0 : s1); i0 += BATCH) {
     if (!one_batch) {
       load(i0);
+      cut(i0);
 #pragma unroll
       for (int c = 0; c < PER; ++c) slot[c] = elem(i0, c) < s1 ? lds_find_g(W, key[c]) : -1;
     }
