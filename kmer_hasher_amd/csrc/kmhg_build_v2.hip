@@ -239,6 +239,9 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
 // Single pass: tiles in ticket order, decoupled look-back (kmhg_device.h) for the tile base.
 // `status` holds one look-back word per tile and the ticket at status[ntiles]; the preceding
 // histogram kernel zeroed them.  *total <- sum (the number of valid windows).
+// J entries per thread (TILE = BLOCK * J per workgroup): J = 32 for long arrays (a 4x shorter
+// look-back chain, 16-B loads).
+template <int J>
 __global__ void __launch_bounds__(BLOCK)
 k_scan_lb_u32(uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ status,
               uint32_t ntiles, uint32_t* __restrict__ total) {
@@ -246,14 +249,21 @@ k_scan_lb_u32(uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ statu
   __shared__ uint32_t tk;
   __shared__ uint64_t base_sh;
   const uint32_t tile = take_ticket(reinterpret_cast<uint32_t*>(status + ntiles), &tk);
-  const uint64_t base = (uint64_t)tile * TILE + (uint64_t)threadIdx.x * WPT;
-  uint32_t v[WPT];
+  const uint64_t base = (uint64_t)tile * (BLOCK * J) + (uint64_t)threadIdx.x * J;
+  uint32_t v[J];
   uint64_t sum = 0;
+  if (J % 4 == 0 && base + J <= n) {          // whole: 16-B loads (a is 16-B aligned, J % 4 == 0)
 #pragma unroll
-  for (int j = 0; j < WPT; ++j) {
-    v[j] = (base + j < n) ? a[base + j] : 0u;
-    sum += v[j];
+    for (int j = 0; j < J; j += 4) {
+      const uint4 x = *reinterpret_cast<const uint4*>(a + base + j);
+      v[j] = x.x; v[j + 1] = x.y; v[j + 2] = x.z; v[j + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = (base + j < n) ? a[base + j] : 0u;
   }
+#pragma unroll
+  for (int j = 0; j < J; ++j) sum += v[j];
   uint64_t tot;
   const uint64_t ex = block_excl_scan(sum, sh, tot);
   if (threadIdx.x < 64) {
@@ -266,9 +276,19 @@ k_scan_lb_u32(uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ statu
   __syncthreads();
   uint64_t run = ex + base_sh;
 #pragma unroll
-  for (int j = 0; j < WPT; ++j) {
-    if (base + j < n) a[base + j] = (uint32_t)run;
-    run += v[j];
+  for (int j = 0; j < J; ++j) {
+    const uint32_t x = v[j];
+    v[j] = (uint32_t)run;
+    run += x;
+  }
+  if (J % 4 == 0 && base + J <= n) {
+#pragma unroll
+    for (int j = 0; j < J; j += 4)
+      *reinterpret_cast<uint4*>(a + base + j) = make_uint4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (base + j < n) a[base + j] = v[j];
   }
 }
 
@@ -1762,10 +1782,21 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
   hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
                      xcd_map(), scan_status, n_status, meta, code, nbit, uniq0);
 }
+// Beyond 64 tiles of 2048 entries: the 32-per-thread look-back scan at any length.  Measured
+// (A/B in one run, `profiles/rd3n_ab_scan_*`): config 3's 15 M-entry histograms 89 -> 60 us per
+// scan (three launches of reduce-then-scan before), config 2's 0.5 M 7.7 -> 7.0 us.
+// KMHG_SCAN=8 (A/B): 8 entries per thread up to LB_SCAN_MAX_TILES tiles, reduce-then-scan beyond.
+static int scan_mode() {
+  const char* e = std::getenv("KMHG_SCAN");     // read per launch: A/B
+  return (e && e[0] == '8') ? 8 : 32;
+}
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);
-  if (nt <= LB_SCAN_MAX_TILES) {
-    hipLaunchKernelGGL(k_scan_lb_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, status, nt, total);
+  const uint32_t nt32 = grid_of(n, BLOCK * 32);
+  if (scan_mode() == 32 && nt > 64) {
+    hipLaunchKernelGGL(k_scan_lb_u32<32>, dim3(nt32), dim3(BLOCK), 0, s, a, n, status, nt32, total);
+  } else if (nt <= LB_SCAN_MAX_TILES) {
+    hipLaunchKernelGGL(k_scan_lb_u32<WPT>, dim3(nt), dim3(BLOCK), 0, s, a, n, status, nt, total);
   } else {   // long arrays: three launches beat a look-back chain of many tiles
     hipLaunchKernelGGL(k_tile_sum_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, status);
     launch_scan_tiles_u64(status, nt, status + nt, s);

@@ -1177,7 +1177,8 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   // default: probe / scan / emit.  KMHG_QUERY=fused: one pass with a decoupled look-back
   // (k_query_fused) -- measured slower (config 2: 0.403 ms against 0.365 ms for the three
   // kernels; a tile that has probed waits for its predecessors' totals while holding its CU
-  // slot, and the probe is occupancy/latency bound), kept for A/B and covered by the tests
+  // slot, and the probe is occupancy/latency bound; re-measured round 3 with the diagonal path,
+  // A/B in one run: self query 94 -> 53 Gbp/s), kept for A/B and covered by the tests
   const char* qe = std::getenv("KMHG_QUERY");
   const bool classic = !(qe && std::string(qe) == "fused");
   uint64_t H = 0;

@@ -176,9 +176,9 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
 // exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the histogram kernel
-// launched before it; total <- sum.  Single-pass look-back up to LB_SCAN_MAX_TILES tiles,
-// reduce-then-scan (status = tile sums) beyond.
-constexpr uint32_t LB_SCAN_MAX_TILES = 256;
+// launched before it; total <- sum.  Single-pass look-back (8192-entry tiles beyond 64 2048-entry
+// tiles).
+constexpr uint32_t LB_SCAN_MAX_TILES = 256;   // (KMHG_SCAN=8; 8192-entry tiles beyond 64 tiles)
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s);
 // hll_rows (count-only builds, first pass): the histogram workgroups also sketch the distinct
 // keys (HyperLogLog, HLL_REGS registers, 1/64 key-space sample) into one 256-B row each (ch.C
