@@ -22,7 +22,9 @@ GOLD = os.path.join(HERE, "golden")
 
 @pytest.fixture(scope="module")
 def exe():
-    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools", "asan")],
+    # flock: pytest-xdist workers each run this fixture; one make at a time
+    r = subprocess.run(["flock", os.path.join(ROOT, "tools", "asan", ".build.lock"),
+                        "make", "-s", "-C", os.path.join(ROOT, "tools", "asan")],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     return EXE
