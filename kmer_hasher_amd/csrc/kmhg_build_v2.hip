@@ -997,11 +997,24 @@ struct GroupTable {
   uint64_t key[V2_CAPW + 1];
   uint2 cc[V2_CAPW + 1];
 };
+// Compact form (default for position and count-only builds, 12 B per slot: 18.4 KB instead of
+// 24.6 KB, so 8 workgroups fit a CU's LDS instead of 6).  `val` is the count during pass A; the
+// counts pass moves every slot's count into the registers of the thread that owns the slot for
+// the write-out (slot q * TB + t), and `val` becomes the inline position of a key seen once or
+// the list cursor of a repeated key, tagged VAL_MULTI so that pass B can tell them apart.
+struct GroupTableC {
+  uint64_t key[V2_CAPW + 1];
+  uint32_t val[V2_CAPW + 1];
+};
+constexpr uint32_t VAL_MULTI = 0x80000000u;    // positions and list offsets are < 2^31
+__device__ __forceinline__ uint32_t* gt_count(GroupTable& W, int j) { return &W.cc[j].x; }
+__device__ __forceinline__ uint32_t* gt_count(GroupTableC& W, int j) { return &W.val[j]; }
 
 // Find-or-insert by CAS only.  (Measured, 10 Mbp: a plain read before the CAS 0.098 -> 0.186 ms;
 // the claiming occurrence skipping its count atomic 0.098 -> 0.136 ms; a per-lane state machine
 // over a lane's elements, one CAS per trip, 0.098 -> 0.204 ms.)
-__device__ __forceinline__ int lds_insert_g(GroupTable& W, uint64_t key) {
+template <class GT>
+__device__ __forceinline__ int lds_insert_g(GT& W, uint64_t key) {
   if (key == EMPTY_KEY) return (int)V2_CAPW;
   uint32_t j = local_home(mix64(key), V2_CAPW);
   for (uint32_t n = 0; n < V2_CAPW; ++n) {
@@ -1046,7 +1059,8 @@ __device__ __forceinline__ int lds_insert_fp(GroupTable& W, uint64_t key) {
   return -1;
 }
 
-__device__ __forceinline__ int lds_find_g(const GroupTable& W, uint64_t key) {
+template <class GT>
+__device__ __forceinline__ int lds_find_g(const GT& W, uint64_t key) {
   if (key == EMPTY_KEY) return (int)V2_CAPW;
   uint32_t j = local_home(mix64(key), V2_CAPW);
   for (uint32_t n = 0; n < V2_CAPW; ++n) {
@@ -1066,8 +1080,8 @@ __device__ __forceinline__ int lds_find_g(const GroupTable& W, uint64_t key) {
 struct Words3 {                                // three consecutive code words, 4-B aligned
   uint32_t a, b, c;
 };
-template <bool COUNT_ONLY = false, int TB = BLOCK, bool CK = false>
-__device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint32_t (*red)[TB / 64],
+template <bool COUNT_ONLY = false, int TB = BLOCK, bool CK = false, class GT = GroupTable>
+__device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*red)[TB / 64],
                                               const uint64_t* __restrict__ keys,
                                               const uint32_t* __restrict__ pos,
                                               const uint32_t* __restrict__ start, Geom g,
@@ -1081,8 +1095,12 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
                                               const uint32_t* __restrict__ code = nullptr,
                                               int k = 0) {
   static_assert(!(CK && COUNT_ONLY), "code-word keys belong to position builds");
+  constexpr bool C12 = std::is_same<GT, GroupTableC>::value;
+  static_assert(V2_CAPW % TB == 0, "the side slot V2_CAPW is slot q = V2_CAPW / TB of thread 0");
   constexpr int NW = TB / 64;                         // waves of the workgroup
-  constexpr int PER = 2 * V2_BW_WG / TB;              // elements per thread per batch (2x mean)
+  // elements per thread per batch: 2x the mean (C12 + code words: 1.5x, for the VGPR budget of
+  // 8 waves / SIMD; a larger bucket takes more batches)
+  constexpr int PER = (C12 && CK ? 3 : 4) * V2_BW_WG / 2 / TB;
   constexpr uint32_t BATCH = TB * PER;
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const uint32_t s0 = start[b], s1 = start[b + 1];
@@ -1129,7 +1147,8 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   load(s0);                                           // in flight while the table is cleared
   for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += TB) {
     W.key[j] = EMPTY_KEY;
-    W.cc[j] = make_uint2(0u, 0u);
+    if constexpr (C12) W.val[j] = 0u;
+    else W.cc[j] = make_uint2(0u, 0u);
   }
   __syncthreads();
   cut(s0);
@@ -1139,7 +1158,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   // skipping the count atomic for a key's claiming occurrence ran 35 % slower, 141 vs 105 us.)
   bool ovf = false;
   bool done = false;
-  if (fp_insert && one_batch) {              // one atomic per key seen once (lds_insert_fp)
+  if constexpr (!C12) if (fp_insert && one_batch) {   // one atomic per key seen once (lds_insert_fp)
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       slot[c] = -1;
@@ -1178,7 +1197,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
       if (elem(i0, c) < s1) {
         slot[c] = lds_insert_g(W, key[c]);
         if (slot[c] < 0) ovf = true;
-        else atomicAdd(&W.cc[slot[c]].x, 1u);
+        else atomicAdd(gt_count(W, slot[c]), 1u);
       }
     }
   }
@@ -1196,7 +1215,7 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
 #pragma unroll
   for (uint32_t q = 0; q < SPT; ++q) {
     const uint32_t j = q * TB + threadIdx.x;
-    const uint32_t c = j <= V2_CAPW ? W.cc[j].x : 0u;
+    const uint32_t c = j <= V2_CAPW ? *gt_count(W, j) : 0u;
     cnt[q] = c;
     cs += c;
     occ += c ? 1u : 0u;
@@ -1222,7 +1241,11 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
 #pragma unroll
     for (uint32_t q = 0; q < SPT; ++q) {
       const uint32_t j = q * TB + threadIdx.x;
-      if (j <= V2_CAPW) W.cc[j].y = off_run;
+      if constexpr (C12) {
+        if (j <= V2_CAPW) W.val[j] = cnt[q] > 1 ? (VAL_MULTI | off_run) : off_run;
+      } else {
+        if (j <= V2_CAPW) W.cc[j].y = off_run;
+      }
       off_run += cnt[q];
     }
     __syncthreads();
@@ -1252,8 +1275,13 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     }
     if (!has_multi) {                    // every key seen once: positions go inline
 #pragma unroll
-      for (int c = 0; c < PER; ++c)
-        if (elem(i0, c) < s1) W.cc[slot[c]].y = ps[c];
+      for (int c = 0; c < PER; ++c) {
+        if constexpr (C12) {
+          if (elem(i0, c) < s1) W.val[slot[c]] = ps[c];
+        } else {
+          if (elem(i0, c) < s1) W.cc[slot[c]].y = ps[c];
+        }
+      }
       continue;
     }
     for (int c = 0; c < PER; ++c) {
@@ -1261,16 +1289,29 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
       // waves take turns on this c: wave w ranks after waves < w have advanced the cursors
       for (int turn = 0; turn < NW; ++turn) {
         if (wave == turn) {
-          uint2 cc = make_uint2(0u, 0u);
-          if (act) cc = W.cc[slot[c]];
-          const bool multi = act && cc.x > 1;
-          if (act && !multi) W.cc[slot[c]].y = ps[c];
+          bool multi;
+          uint32_t cur;                  // a repeated key's list cursor (VAL_MULTI kept in C12)
+          if constexpr (C12) {
+            const uint32_t v = act ? W.val[slot[c]] : 0u;
+            multi = act && (v & VAL_MULTI);
+            if (act && !multi) W.val[slot[c]] = ps[c];
+            cur = v;
+          } else {
+            uint2 cc = make_uint2(0u, 0u);
+            if (act) cc = W.cc[slot[c]];
+            multi = act && cc.x > 1;
+            if (act && !multi) W.cc[slot[c]].y = ps[c];
+            cur = cc.y;
+          }
           if (__ballot(multi)) {
             const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS_WG, multi);
             const int leader = multi ? __ffsll((unsigned long long)m) - 1 : lane;
-            uint32_t cur = cc.y;
-            if (multi && leader == lane) W.cc[slot[c]].y = cur + (uint32_t)__popcll(m);
+            if (multi && leader == lane) {
+              if constexpr (C12) W.val[slot[c]] = cur + (uint32_t)__popcll(m);
+              else W.cc[slot[c]].y = cur + (uint32_t)__popcll(m);
+            }
             cur = __shfl(cur, leader);
+            if constexpr (C12) cur &= ~VAL_MULTI;
             if (multi) {
               positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
               // the diagonal query path's bits of repeated keys' windows (ps: 1-based start)
@@ -1286,10 +1327,23 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
   STAMP_WG(b, 4);
   // the bucket's sub-table, coalesced 16-B slots (+ the query's slot tags, 1 B per slot)
   Slot* Tb = T + (uint64_t)b * V2_CAPW;
-  for (uint32_t j = threadIdx.x; j < V2_CAPW; j += TB) {
-    const uint64_t kk = W.key[j];
-    const uint2 c = W.cc[j];
-    *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
+  if constexpr (C12) {         // counts from the registers of the slot's owner (counts pass)
+#pragma unroll
+    for (uint32_t q = 0; q < SPT; ++q) {
+      const uint32_t j = q * TB + threadIdx.x;
+      if (j < V2_CAPW) {
+        const uint64_t kk = W.key[j];
+        const uint32_t aux = COUNT_ONLY ? 0u : (W.val[j] & ~VAL_MULTI);
+        *reinterpret_cast<uint4*>(&Tb[j]) =
+            make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), cnt[q], aux);
+      }
+    }
+  } else {
+    for (uint32_t j = threadIdx.x; j < V2_CAPW; j += TB) {
+      const uint64_t kk = W.key[j];
+      const uint2 c = W.cc[j];
+      *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
+    }
   }
   if (TG) {                    // 4 tags per lane, one 4-B store (byte stores cost 4x the issue)
     static_assert(V2_CAPW % 4 == 0, "tag words");
@@ -1305,7 +1359,11 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
     }
   }
   if (threadIdx.x == 0 && side_bucket(b, g)) {
-    const uint2 c = W.cc[V2_CAPW];
+    uint2 c;
+    if constexpr (C12)
+      c = make_uint2(cnt[V2_CAPW / TB], COUNT_ONLY ? 0u : (W.val[V2_CAPW] & ~VAL_MULTI));
+    else
+      c = W.cc[V2_CAPW];
     *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
     if (TG) TG[side_slot(g)] = 0;
   }
@@ -1314,19 +1372,21 @@ __device__ __forceinline__ void bucket_wg_cas(GroupTable& W, uint64_t* sh, uint3
 
 // TB threads per workgroup: 256 (4 waves) or 512 (8 waves: the LDS table allows 6 workgroups
 // per CU, so 8-wave groups fill the CU's 32 wave slots where 4-wave groups stop at 24).
-template <bool COUNT_ONLY, int TB = BLOCK, bool CK = false>
-__global__ void __launch_bounds__(TB)
+// C12: the compact 12-B-per-slot LDS table (GroupTableC; not with the fingerprint insert).
+template <bool COUNT_ONLY, int TB = BLOCK, bool CK = false, bool C12 = false>
+__global__ void __launch_bounds__(TB, C12 ? 2048 / TB : 1)    // C12: 8 workgroups per CU (LDS)
 k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
                int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
                BuildMeta* __restrict__ meta, uint8_t* __restrict__ TG,
                uint32_t* __restrict__ mbits, int fp_insert, const uint32_t* __restrict__ code,
                int k) {
-  __shared__ GroupTable W;
+  using GT = typename std::conditional<C12, GroupTableC, GroupTable>::type;
+  __shared__ GT W;
   __shared__ uint64_t sh[2 * (TB / 64)];
   __shared__ uint32_t red[3][TB / 64];
-  bucket_wg_cas<COUNT_ONLY, TB, CK>(W, sh, red, keys, pos, start, g, T, positions, bstats, meta,
-                                    blockIdx.x, TG, mbits, fp_insert, code, k);
+  bucket_wg_cas<COUNT_ONLY, TB, CK, GT>(W, sh, red, keys, pos, start, g, T, positions, bstats,
+                                        meta, blockIdx.x, TG, mbits, fp_insert, code, k);
 }
 
 // ---------------------------------------------------------------- V_bucket_sort (group per bucket)
@@ -1921,14 +1981,30 @@ static int bucket_fp() {
   const char* e = std::getenv("KMHG_BUCKET_FP");
   return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
 }
+// KMHG_BUCKET_C12=0: the 16-B-per-slot LDS table (GroupTable) instead of the compact one (A/B)
+static bool bucket_c12() {
+  const char* e = std::getenv("KMHG_BUCKET_C12");    // read per launch: the tests switch it
+  return !(e && e[0] == '0');
+}
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, uint8_t* TG, uint32_t* mbits,
                          const uint32_t* code, int k) {
   const int fp = bucket_fp();
-  if (count_only)
+  const bool c12 = !fp && bucket_c12();
+  if (count_only && c12)
+    hipLaunchKernelGGL((k_v2_bucket_wg<true, BLOCK, false, true>), dim3(g.nb), dim3(BLOCK), 0, s,
+                       keys, pos, start, g, T, positions, bstats, meta, nullptr, nullptr, 0,
+                       nullptr, 0);
+  else if (count_only)
     hipLaunchKernelGGL(k_v2_bucket_wg<true>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
                        positions, bstats, meta, nullptr, nullptr, fp, nullptr, 0);
+  else if (c12 && bucket_tb() == 256 && code)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, BLOCK, true, true>), dim3(g.nb), dim3(BLOCK), 0, s,
+                       keys, pos, start, g, T, positions, bstats, meta, TG, mbits, 0, code, k);
+  else if (c12 && bucket_tb() == 256)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, BLOCK, false, true>), dim3(g.nb), dim3(BLOCK), 0, s,
+                       keys, pos, start, g, T, positions, bstats, meta, TG, mbits, 0, nullptr, 0);
   else if (bucket_tb() == 512 && code)
     hipLaunchKernelGGL((k_v2_bucket_wg<false, 512, true>), dim3(g.nb), dim3(512), 0, s, keys, pos,
                        start, g, T, positions, bstats, meta, TG, mbits, fp, code, k);

@@ -195,8 +195,8 @@ def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
         ptr.free()
 
 
-@pytest.mark.parametrize("bucket", ["wave", "group", "group512", "groupfp", "group512fp",
-                                    "groupfpforce", "sort"])
+@pytest.mark.parametrize("bucket", ["wave", "group", "group16", "group512", "groupfp",
+                                    "group512fp", "groupfpforce", "sort"])
 def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     """Both bucket kernels on every size class: one wave per 256-window bucket, and one
     workgroup per 1024-window bucket (chosen automatically when it saves a radix pass, e.g. at
@@ -208,6 +208,8 @@ def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
         # KMHG_BUCKET_FP=2 takes every bucket through the fingerprint-collision fallback
         monkeypatch.setenv("KMHG_BUCKET_FP", "2" if bucket.endswith("force") else
                            "1" if bucket.endswith("fp") else "0")
+        # group16: the 16-B-per-slot LDS table instead of the compact 12-B one (KMHG_BUCKET_C12)
+        monkeypatch.setenv("KMHG_BUCKET_C12", "0" if bucket == "group16" else "1")
         bucket = "group"
     monkeypatch.setenv("KMHG_BUCKET", bucket)
     rng = np.random.default_rng(21)
