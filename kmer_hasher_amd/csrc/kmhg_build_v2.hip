@@ -712,7 +712,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       wave_sync();
       if (act[c]) {
         const uint32_t ld = cur + (uint32_t)__popcll(grp & lanemask_lt());
-        S.skey[ld] = key[c];
+        if (BM != 2) S.skey[ld] = key[c];      // the last bucket-id pass writes positions only
         S.spos[ld] = ps[c];
         S.sdst[ld] = S.gbase[dg[c]] + (ld - S.tstart[dg[c]]);
       }

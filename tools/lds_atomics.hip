@@ -84,6 +84,8 @@ template <int VARIANT>
 __global__ void __launch_bounds__(256) kpa(uint64_t* out, uint32_t seed, int reps) {
   __shared__ uint64_t key[CAP + 1];
   __shared__ uint2 cc[CAP + 1];
+  __shared__ uint64_t qk[(VARIANT == 4 || VARIANT == 5) ? 4 : 1][256];   // per-wave failure queue
+  __shared__ uint16_t qj[(VARIANT == 4 || VARIANT == 5) ? 4 : 1][256];
   uint64_t acc = 0;
   for (int rep = 0; rep < reps; ++rep) {
     for (int j = threadIdx.x; j <= CAP; j += 256) { key[j] = ~0ull; cc[j] = make_uint2(0, 0); }
@@ -146,6 +148,74 @@ __global__ void __launch_bounds__(256) kpa(uint64_t* out, uint32_t seed, int rep
           const uint64_t prev = atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kv[q]);
           if (prev == ~0ull || prev == kv[q]) { pend[q] = false; slot[q] = j; atomicAdd(&cc[j].x, 1u); }
         }
+      }
+    } else if (VARIANT == 4 || VARIANT == 5) {
+      // home round for every element (one CAS each); the failures of each wave are compacted
+      // into a per-wave LDS queue and probed on 64 at a time, so a long probe chain holds up
+      // only the queue's lanes, not every element round.  The resolved slot goes back to the
+      // owner through the queue (VARIANT 5: no write-back, owners re-find in pass B instead).
+      const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+      int qi[4];
+      uint32_t nq = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t h = homek(mixk(kv[q]));
+        const uint64_t prev = atomicCAS((unsigned long long*)&key[h], ~0ull, (unsigned long long)kv[q]);
+        const bool ok = prev == ~0ull || prev == kv[q];
+        if (ok) { slot[q] = h; atomicAdd(&cc[h].x, 1u); }
+        const uint64_t fm = __ballot(!ok);
+        qi[q] = -1;
+        if (!ok) {
+          const uint32_t r = nq + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+          qk[w][r] = kv[q];
+          qj[w][r] = h + 1 == CAP ? 0 : h + 1;
+          qi[q] = (int)r;
+        }
+        nq += (uint32_t)__popcll(fm);
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t b0 = 0; b0 < nq; b0 += 64) {
+        const uint32_t i = b0 + lane;
+        if (i < nq) {
+          const uint64_t kk = qk[w][i];
+          uint32_t j = qj[w][i];
+          for (;;) {
+            const uint64_t prev = atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kk);
+            if (prev == ~0ull || prev == kk) break;
+            if (++j == CAP) j = 0;
+          }
+          atomicAdd(&cc[j].x, 1u);
+          if (VARIANT == 4) qj[w][i] = (uint16_t)j;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (qi[q] >= 0) slot[q] = VARIANT == 4 ? (int)qj[w][qi[q]] : -1;
+    } else if (VARIANT == 7 || VARIANT == 8) {   // calibration: no CAS (7: count adds at home)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t j = homek(mixk(kv[c]));
+        slot[c] = j;
+        if (VARIANT == 7) atomicAdd(&cc[j].x, 1u);
+      }
+    } else if (VARIANT == 9) {         // one CAS per element at its home, no probing
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t j = homek(mixk(kv[c]));
+        acc += atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kv[c]);
+        slot[c] = j;
+      }
+    } else if (VARIANT == 6) {         // element by element without the count adds
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t j = homek(mixk(kv[c]));
+        for (;;) {
+          const uint64_t prev = atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kv[c]);
+          if (prev == ~0ull || prev == kv[c]) break;
+          if (++j == CAP) j = 0;
+        }
+        slot[c] = j;
       }
     } else {
       int c = 0;
@@ -228,6 +298,13 @@ int main() {
   run_pa<1>("pass A, per-lane state machine");
   run_pa<2>("pass A, state machine, homes first");
   run_pa<3>("pass A, home round then failures");
+  run_pa<4>("pass A, home round + per-wave queue");
+  run_pa<5>("pass A, home round + queue, no slot back");
+  run_pa<6>("pass A, element by element, no adds");
+  run_pa<0>("pass A, element by element (again)");
+  run_pa<7>("calib: keys + clear + adds, no CAS");
+  run_pa<8>("calib: keys + clear only");
+  run_pa<9>("calib: one CAS per element, no probing");
   run<6>("CAS64 rtn fails, 8 lanes", 6);
   run<7>("CAS64 rtn fails, 1 lane", 6);
   run<8>("CAS64 rtn fails, 32 lanes", 6);
