@@ -206,6 +206,66 @@ __global__ void __launch_bounds__(256) kpa(uint64_t* out, uint32_t seed, int rep
         acc += atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kv[c]);
         slot[c] = j;
       }
+    } else if (VARIANT == 10 || VARIANT == 11) {
+      // CAS at home; a collision scans on G slots per round trip with plain reads (ds_read2),
+      // CAS-ing the first empty slot it sees (a lost race rescans from there)
+      constexpr int G = VARIANT == 10 ? 4 : 8;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint64_t kk = kv[c];
+        uint32_t j = homek(mixk(kk));
+        uint64_t prev = atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kk);
+        if (!(prev == ~0ull || prev == kk)) {
+          if (++j == CAP) j = 0;
+          for (;;) {
+            uint64_t g[G];
+#pragma unroll
+            for (int q = 0; q < G; ++q) {
+              uint32_t jj = j + q;
+              if (jj >= CAP) jj -= CAP;
+              g[q] = key[jj];
+            }
+            int hit = -1;
+#pragma unroll
+            for (int q = G - 1; q >= 0; --q)
+              if (g[q] == ~0ull || g[q] == kk) hit = q;
+            if (hit < 0) { j += G; if (j >= CAP) j -= CAP; continue; }
+            j += hit;
+            if (j >= CAP) j -= CAP;
+            if (g[hit] == kk) break;
+            prev = atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kk);
+            if (prev == ~0ull || prev == kk) break;
+            if (++j == CAP) j = 0;
+          }
+        }
+        slot[c] = j;
+        atomicAdd(&cc[j].x, 1u);
+      }
+    } else if (VARIANT == 12) {
+      // per-lane state machine over the lane's elements, ONE LDS instruction per trip (the CAS);
+      // the count adds run after the loop, one full-wave instruction per element index
+      uint32_t hm[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) hm[q] = homek(mixk(kv[q]));
+      int c = 0;
+      uint64_t kk = kv[0];
+      uint32_t j = hm[0];
+      bool live = true;
+      while (__any(live)) {
+        if (live) {
+          const uint64_t prev = atomicCAS((unsigned long long*)&key[j], ~0ull, (unsigned long long)kk);
+          if (prev == ~0ull || prev == kk) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) if (q == c) slot[q] = j;
+            ++c;
+            if (c == 4) live = false;
+#pragma unroll
+            for (int q = 1; q < 4; ++q) if (q == c) { kk = kv[q]; j = hm[q]; }
+          } else if (++j == CAP) j = 0;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) atomicAdd(&cc[slot[q]].x, 1u);
     } else if (VARIANT == 6) {         // element by element without the count adds
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -305,6 +365,10 @@ int main() {
   run_pa<7>("calib: keys + clear + adds, no CAS");
   run_pa<8>("calib: keys + clear only");
   run_pa<9>("calib: one CAS per element, no probing");
+  run_pa<10>("pass A, home CAS, then 4-slot read scans");
+  run_pa<11>("pass A, home CAS, then 8-slot read scans");
+  run_pa<0>("pass A, element by element (3rd)");
+  run_pa<12>("pass A, state machine, one LDS op per trip");
   run<6>("CAS64 rtn fails, 8 lanes", 6);
   run<7>("CAS64 rtn fails, 1 lane", 6);
   run<8>("CAS64 rtn fails, 32 lanes", 6);
