@@ -6,9 +6,10 @@
 //   V_encode    LDS-staged 2-bit encode + N mask of every window (as K_insert) -> (key, pos)
 //               per window, plus a per-tile histogram of the first radix digit of its bucket
 //   V_scan      exclusive scan of the digit histograms (decoupled look-back)
-//   V_scatter   stable radix pass: every wave ranks its 512 elements by digit with ballots
-//               (no atomics), elements land at histogram offsets -- LSD over 1-3 digits sorts
-//               the windows by bucket while keeping position order inside a bucket
+//   V_scatter   stable radix pass: every wave ranks its 512 elements by digit with the
+//               returned values of its LDS count atomics (lane-ordered), elements land at
+//               histogram offsets -- LSD over 1-3 digits sorts the windows by bucket while
+//               keeping position order inside a bucket
 //   V_hist      digit histogram for the next radix pass
 //   V_bounds    bucket start offsets in the bucket-sorted stream
 //   V_bucket    ONE WAVE PER BUCKET: the bucket's keys go into a wave-private LDS hash table
@@ -133,7 +134,8 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
            uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
            uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
-           uint16_t* __restrict__ nbit, uint32_t* __restrict__ uniq0) {
+           uint16_t* __restrict__ nbit, uint32_t* __restrict__ uniq0,
+           uint32_t* __restrict__ bids = nullptr) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
   // zero the next scan's look-back words + ticket and the build meta (no memset launches)
@@ -156,10 +158,15 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
       const int w = j * BLOCK + threadIdx.x;
       const int64_t s = tile0 + w;
       uint64_t key = 0;
+      uint32_t bl = ~0u;
       if (s < Nw && window_key(st, HALO + w, s, L, k, key)) {
-        const uint64_t h = mix64(key);
-        if (in_part(h, g)) atomicAdd(&lh[digit_of_h(h, g, D)], 1u);
+        const uint32_t b = bucket_local(mix64(key), g);
+        if (b < g.nb) {
+          atomicAdd(&lh[digit_of_b(b, D)], 1u);
+          bl = b;
+        }
       }
+      if (bids && s < Nw) bids[s] = bl;
     }
   }
   __syncthreads();
@@ -661,9 +668,21 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
         dg[c] = act[c] ? digit_of_h(mix64((uint64_t)key[c]), g, D) : 0;
       }
     }
+#ifndef KMHG_BALLOT_RANK
+    // Stable ranks from the count atomics themselves: the lanes of one LDS instruction that hit
+    // the same counter are served in lane order (CDNA4; tools/lds_order.hip checks it, and the
+    // bucket kernels check every bucket's stream order), and a wave's instructions run in
+    // program order, so the returned running count is the element's rank among the wave's
+    // elements of its digit in (c, lane) = input order.
+    // (the rank rides in the digit's register, bits 16+: digit < 2^16, rank < PTILE)
+#pragma unroll
+    for (int c = 0; c < PER; ++c)
+      if (act[c]) dg[c] |= atomicAdd(&S.wc[wave][dg[c]], 1u) << 16;
+#else
 #pragma unroll
     for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
       if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
+#endif
     __syncthreads();
     // tile-local digit starts: thread t owns digits [DPT t, DPT t + DPT)
     uint32_t dsum[DPT];
@@ -699,6 +718,18 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       }
     }
     __syncthreads();
+#ifndef KMHG_BALLOT_RANK
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      if (act[c]) {
+        const uint32_t d = dg[c] & 0xFFFFu;
+        const uint32_t ld = S.wc[wave][d] + (dg[c] >> 16);
+        if (BM != 2) S.skey[ld] = key[c];      // the last bucket-id pass writes positions only
+        S.spos[ld] = ps[c];
+        S.sdst[ld] = S.gbase[d] + (ld - S.tstart[d]);
+      }
+    }
+#else
 #pragma unroll
     for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
       const uint64_t grp = match_bits(dg[c], D.nbits, act[c]);
@@ -717,6 +748,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
         S.sdst[ld] = S.gbase[dg[c]] + (ld - S.tstart[dg[c]]);
       }
     }
+#endif
     __syncthreads();
     // a static count of store instructions per lane (masked, fully unrolled), so the wait for
     // the next tile's prefetched loads at the loop top is vmcnt(#stores), not vmcnt(0): the
@@ -814,6 +846,19 @@ k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ 
   if (lo == 0 && threadIdx.x == 0) start[g.nb / spread] = n;
 }
 
+// The radix passes are stable by the lane order of the LDS count atomics (V_scatter), so a
+// bucket's stream lists its windows in ascending position -- the order the position lists keep.
+// The bucket kernels check it with one neighbour load per element and report a violation like
+// an LDS table overflow, which rebuilds the index with the global-atomic build (finish_build).
+__device__ __forceinline__ bool stream_out_of_order(const uint32_t* __restrict__ pos, uint32_t i,
+                                                    uint32_t s0, uint32_t s1, uint32_t p) {
+#ifdef KMHG_NO_ORDER_CHECK                   // A/B variant builds only: the check's cost
+  return false;
+#else
+  return i > s0 && i < s1 && pos[i - 1] >= p;
+#endif
+}
+
 // ---------------------------------------------------------------- V_bucket (wave per bucket)
 // One LDS round trip per probe: the CAS itself says whether the slot was free (inserted), held
 // this key (found) or another key (move on).
@@ -860,12 +905,14 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   int slot[PER];
   bool in[PER];
   // the first batch's loads are in flight while the sub-table is initialised
+  bool ovf = false;
 #pragma unroll
   for (int c = 0; c < PER; ++c) {
     const uint32_t i = s0 + 64 * c + lane;
     in[c] = i < s1;
     key[c] = in[c] ? keys[i] : 0;
     ps[c] = in[c] ? pos[i] : 0;
+    ovf |= stream_out_of_order(pos, i, s0, s1, ps[c]);
   }
   for (uint32_t j = lane; j <= V2_CAPB; j += 64) {
     W.key[j] = EMPTY_KEY;
@@ -874,7 +921,6 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
   wave_sync();
   STAMP(b, 1);
   // pass A: distinct keys + counts
-  bool ovf = false;
   for (uint32_t i0 = s0; i0 < s1; i0 += 64 * PER) {
     if (i0 != s0) {
 #pragma unroll
@@ -883,6 +929,7 @@ k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
         in[c] = i < s1;
         key[c] = in[c] ? keys[i] : 0;
         ps[c] = in[c] ? pos[i] : 0;
+        ovf |= stream_out_of_order(pos, i, s0, s1, ps[c]);
       }
     }
     STAMP(b, 2);
@@ -1093,7 +1140,7 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
                                               uint32_t* __restrict__ mbits = nullptr,
                                               int fp_insert = 0,
                                               const uint32_t* __restrict__ code = nullptr,
-                                              int k = 0) {
+                                              int k = 0, uint32_t* edge = nullptr) {
   static_assert(!(CK && COUNT_ONLY), "code-word keys belong to position builds");
   constexpr bool C12 = std::is_same<GT, GroupTableC>::value;
   static_assert(V2_CAPW % TB == 0, "the side slot V2_CAPW is slot q = V2_CAPW / TB of thread 0");
@@ -1111,6 +1158,8 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
   // element c of thread t in a batch: i0 + c * TB + t, so position order = (c, wave, lane)
   auto elem = [&](uint32_t i0, int c) { return i0 + (uint32_t)c * TB + threadIdx.x; };
   uint32_t wa[PER], wb[PER], wc[PER];                 // CK: each window's three code words
+  bool ovf = false;                                   // LDS table full
+  bool disorder = false;                              // the bucket's stream out of position order
   // CK: load() issues the positions, then the code words, all in flight at once; cut() turns
   // them into keys -- after the table clear for the first batch, so the clear hides the loads
   auto load = [&](uint32_t i0) {
@@ -1119,6 +1168,7 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
       for (int c = 0; c < PER; ++c) {
         const uint32_t i = elem(i0, c);
         ps[c] = i < s1 ? pos[i] : 1u;               // 1-based window start
+        if (!one_batch || !edge) disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
       }
 #pragma unroll
       for (int c = 0; c < PER; ++c) {       // one 12-B load per window (global_load_dwordx3)
@@ -1134,6 +1184,8 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
       const uint32_t i = elem(i0, c);
       key[c] = i < s1 ? keys[i] : 0;
       ps[c] = (!COUNT_ONLY && i < s1) ? pos[i] : 0;
+      if (!COUNT_ONLY && (!one_batch || !edge))
+        disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
     }
   };
   auto cut = [&](uint32_t i0) {
@@ -1156,7 +1208,6 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
   STAMP_WG_DRAIN(b, 6);
   // pass A: distinct keys + counts (CAS on a table shared by the four waves).  (Measured:
   // skipping the count atomic for a key's claiming occurrence ran 35 % slower, 141 vs 105 us.)
-  bool ovf = false;
   bool done = false;
   if constexpr (!C12) if (fp_insert && one_batch) {   // one atomic per key seen once (lds_insert_fp)
 #pragma unroll
@@ -1201,9 +1252,56 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
       }
     }
   }
-  if (__syncthreads_or(ovf)) {
+  // Stream order of a one-batch bucket (multi-batch buckets and callers without `edge` check it
+  // with a neighbour load per element in load()): element (c, wave, lane) follows (c, wave,
+  // lane - 1) -- a shuffle -- and lane 0 follows lane 63 of the wave before (of row c - 1 for
+  // wave 0), exchanged through `edge` and read after the barrier below.  Here, after pass A,
+  // the positions have long arrived, so the check makes no load wait earlier than it did.
+#ifdef KMHG_NO_ORDER_CHECK
+  const bool chk = false;
+#else
+  const bool chk = !COUNT_ONLY && one_batch && edge;
+#endif
+  // (edge: row `wave` holds that wave's lane-63 positions, 8 per row, written and read as
+  // pairs -- a handful of LDS instructions per wave: single-lane LDS instructions cost nearly a
+  // full one each in this LDS-bound kernel)
+  if (chk) {
+    if (threadIdx.x == 0) edge[8 * NW] = 0u;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      // lane - 1's position by a DPP wave shift (a VALU move; __shfl_up is an LDS permute)
+      const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ps[c], 0x138 /* wave_shr:1 */,
+                                                                0xF, 0xF, false);
+      if (lane > 0 && elem(s0, c) < s1 && up >= ps[c]) disorder = true;
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int q = 0; q < PER; q += 2)
+        *reinterpret_cast<uint2*>(&edge[8 * wave + q]) = make_uint2(ps[q], q + 1 < PER ? ps[q + 1] : 0u);
+    }
+  }
+  if (__syncthreads_or(ovf || disorder)) {
     if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
     return;
+  }
+  if (chk && lane == 0) {
+    // lane 0 of wave w follows lane 63 of wave w - 1 (same row); wave 0 follows wave NW - 1
+    const uint32_t* row = edge + 8 * (wave ? wave - 1 : NW - 1);
+    uint32_t pv[PER + 1];
+#pragma unroll
+    for (int q = 0; q < PER; q += 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(&row[q]);
+      pv[q] = v.x;
+      pv[q + 1] = v.y;
+    }
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t e = elem(s0, c);
+      const uint32_t prev = wave ? pv[c] : (c ? pv[c - 1] : 0u);   // wave 0: row c - 1
+      bad |= e > s0 && e < s1 && prev >= ps[c];
+    }
+    if (bad) edge[8 * NW] = 1u;              // read after the counts pass's barrier
   }
   STAMP_WG(b, 2);
   // counts: thread t owns slots t, t + TB, ... (lane-contiguous: conflict-free LDS; thread-
@@ -1233,6 +1331,10 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
     sh[NW + wave] = pairs;                 // sh[NW..2NW): the block scan below uses sh[0..NW)
   }
   const bool has_multi = __syncthreads_or(mx > 1);
+  if (chk && edge[8 * NW]) {                 // stream out of order at a wave / row boundary
+    if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
+    return;
+  }
   // list offsets (only repeated keys have lists): any slot order gives each key a contiguous
   // range of [s0, s1), here slot q * TB + t in (t, q) order
   if (!COUNT_ONLY && has_multi) {
@@ -1385,8 +1487,9 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   __shared__ GT W;
   __shared__ uint64_t sh[2 * (TB / 64)];
   __shared__ uint32_t red[3][TB / 64];
+  __shared__ __attribute__((aligned(16))) uint32_t edge[8 * (TB / 64) + 1];   // stream-order check
   bucket_wg_cas<COUNT_ONLY, TB, CK, GT>(W, sh, red, keys, pos, start, g, T, positions, bstats,
-                                        meta, blockIdx.x, TG, mbits, fp_insert, code, k);
+                                        meta, blockIdx.x, TG, mbits, fp_insert, code, k, edge);
 }
 
 // ---------------------------------------------------------------- V_bucket_sort (group per bucket)
@@ -1457,6 +1560,8 @@ k_v2_bucket_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__
       skr[c] = (uint32_t)mix64(k) >> 16;
       S.esk[e] = (uint16_t)skr[c];
       bad |= k == EMPTY_KEY;
+      // out of order: the CAS build below reports it (overflow -> global-atomic rebuild)
+      bad |= stream_out_of_order(pos, s0 + e, s0, s1, S.epos[e]);
     }
   }
   for (uint32_t j = threadIdx.x; j < V2_CAPW / 4; j += BLOCK)
@@ -1815,10 +1920,13 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
                      uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
                      BuildMeta* meta, hipStream_t s, uint32_t* code, uint16_t* nbit,
                      uint32_t* uniq0, uint32_t* bids) {
-  static const int persist = [] {
-    const char* e = std::getenv("KMHG_HIST0P");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
+  const char* hp = std::getenv("KMHG_HIST0P");   // read per launch: the tests switch it
+  const int persist = (hp && hp[0] == '0') ? 0 : 1;
+  if (bids && !persist) {      // bucket-id builds, one workgroup per tile (KMHG_HIST0P=0, A/B)
+    hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
+                       xcd_map(), scan_status, n_status, meta, code, nbit, uniq0, bids);
+    return;
+  }
   if (bids) {                  // bucket-id builds: the persistent kernel (interleaved schedule)
     static const unsigned cap_b = resident_blocks((const void*)k_v2_hist0p<true, true>);
     hipLaunchKernelGGL((k_v2_hist0p<true, true>), dim3(std::min<unsigned>(ch.ntiles, cap_b)),
@@ -2017,6 +2125,21 @@ void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32
   else
     hipLaunchKernelGGL(k_v2_bucket_wg<false>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g,
                        T, positions, bstats, meta, TG, mbits, fp, nullptr, 0);
+}
+// Test knob (KMHG_TEST_DISORDER=1, tests only): swaps the first two positions of bucket 0's
+// stream, so the bucket kernel's order check must report it and the build fall back.
+__global__ void k_v2_test_disorder(uint32_t* __restrict__ pos, const uint32_t* __restrict__ start) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const uint32_t a = start[0], b = start[1];
+    if (b - a >= 2) {
+      const uint32_t t = pos[a];
+      pos[a] = pos[a + 1];
+      pos[a + 1] = t;
+    }
+  }
+}
+void launch_v2_test_disorder(uint32_t* pos, const uint32_t* start, hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_test_disorder, dim3(1), dim3(64), 0, s, pos, start);
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {

@@ -1071,6 +1071,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   HIPC(hipMemsetAsync(stamps, 0, sizeof(uint64_t) * 8 * nb, s));
   kmhg::set_stamp_buffer(stamps);
 #endif
+  // tests only: bucket 0's stream out of order -> the bucket kernel's check -> v1 rebuild
+  if (!no_pos && std::getenv("KMHG_TEST_DISORDER") && std::getenv("KMHG_TEST_DISORDER")[0] == '1')
+    launch_v2_test_disorder(pin, start.p, s);
   if (sorted)
     LAUNCH("k_v2_bucket_sort", s,
            launch_v2_bucket_sort(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,

@@ -225,7 +225,31 @@ def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
 
 
 @pytest.mark.parametrize("stream", ["bid", "keys"])
-@pytest.mark.parametrize("bounds", ["lo", "scan", "sc8"])
+def test_stream_disorder_falls_back(gpu, monkeypatch, stream):
+    """The radix passes are stable because same-address LDS count atomics of one instruction
+    are served in lane order (tools/lds_order.hip); the bucket kernels check that every
+    bucket's stream is in ascending position order.  KMHG_TEST_DISORDER swaps two positions of
+    bucket 0's stream: the check must report it, and the index is rebuilt by the global-atomic
+    build (image header: one bucket) with results equal to the oracle."""
+    import torch
+    from kmer_hasher_amd import synth
+    from kmer_hasher_amd.device import DeviceIndex
+    monkeypatch.setenv("KMHG_BUCKET", "group")
+    monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
+    s = synth.add_n_runs(synth.iid(300_000, 51), 0.002, 9).tobytes().decode("latin-1")
+    seq = torch.frombuffer(bytearray(s.encode("latin-1")), dtype=torch.uint8).cuda()
+    for disorder, one_bucket in (("0", False), ("1", True)):
+        monkeypatch.setenv("KMHG_TEST_DISORDER", disorder)
+        idx = DeviceIndex.build(seq, 31).wait()
+        meta, _ = idx.export_image()
+        nb = int(meta[2].item()) >> 32
+        assert (nb == 1) == one_bucket, (disorder, nb)
+        idx.free()
+        _check_against_oracle(s, 31, pairs=False)
+
+
+@pytest.mark.parametrize("stream", ["bid", "keys"])
+@pytest.mark.parametrize("bounds", ["lo", "scan", "sc8", "h0tile"])
 @pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
 def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds, stream):
     """More radix passes than the input needs (KMHG_MAXR caps the radix): 1-4 passes with N-runs
@@ -240,6 +264,8 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds, stream):
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
     if bounds == "sc8":                    # the 8-wave radix scatter (KMHG_SC8=1)
         monkeypatch.setenv("KMHG_SC8", "1")
+    elif bounds == "h0tile":               # the first histogram one workgroup per tile
+        monkeypatch.setenv("KMHG_HIST0P", "0")
     else:
         monkeypatch.setenv("KMHG_BOUNDS", bounds)
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
