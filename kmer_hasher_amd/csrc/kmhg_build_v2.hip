@@ -1392,6 +1392,7 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
       for (int turn = 0; turn < NW; ++turn) {
         if (wave == turn) {
           bool multi;
+          bool continue_turn = false;    // C12: ranked by the cursor atomic below
           uint32_t cur;                  // a repeated key's list cursor (VAL_MULTI kept in C12)
           if constexpr (C12) {
             const uint32_t v = act ? W.val[slot[c]] : 0u;
@@ -1405,7 +1406,18 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
             if (act && !multi) W.cc[slot[c]].y = ps[c];
             cur = cc.y;
           }
-          if (__ballot(multi)) {
+          if constexpr (C12) {
+#ifndef KMHG_BALLOT_RANK
+            // the cursor atomic's lane-ordered returns rank the wave's windows of one key
+            if (multi) {
+              const uint32_t at = atomicAdd(&W.val[slot[c]], 1u) & ~VAL_MULTI;
+              positions[at] = (int32_t)ps[c];
+              if (mbits) atomicOr(&mbits[(ps[c] - 1) >> 5], 1u << ((ps[c] - 1) & 31));
+            }
+            continue_turn = true;
+#endif
+          }
+          if (!continue_turn && __ballot(multi)) {
             const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS_WG, multi);
             const int leader = multi ? __ffsll((unsigned long long)m) - 1 : lane;
             if (multi && leader == lane) {
@@ -1585,6 +1597,10 @@ k_v2_bucket_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__
       el[c] = pass == 0 ? q : (act[c] ? S.sidx[0][q] : 0u);
       const uint32_t sk = pass == 0 ? skr[c] : (act[c] ? (uint32_t)S.esk[el[c]] : 0u);
       dg[c] = pass == 0 ? (sk & 255u) : (sk >> 8);
+#ifndef KMHG_BALLOT_RANK
+      // stable rank from the lane-ordered count atomic (as V_scatter)
+      rk[c] = act[c] ? atomicAdd(&S.cntw[wave][dg[c]], 1u) : 0u;
+#else
       const uint64_t grp = match_bits(dg[c], 8, act[c]);
       const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
       uint32_t cur = 0;
@@ -1595,6 +1611,7 @@ k_v2_bucket_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__
       cur = __shfl(cur, leader);
       wave_sync();
       rk[c] = cur + (uint32_t)__popcll(grp & lanemask_lt());
+#endif
     }
     __syncthreads();
     {   // digit bases: thread t owns digit t over the 4 waves
