@@ -185,8 +185,11 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
 // BIDS (bucket-id builds): every window's bucket id (~0 for a window that is not indexed or
 // outside this part) is stored in window order, one coalesced 4-B store per window, so the first
 // scatter pass reads the ids instead of encoding and hashing every window a second time.
+#ifndef KMHG_HIST0_WAVES
+#define KMHG_HIST0_WAVES 6   // Win8: 80 VGPRs without spills (7 spills 44 B / lane)
+#endif
 template <bool CODES, bool BIDS = false>
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK, KMHG_HIST0_WAVES)
 k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
             uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
             uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
@@ -219,6 +222,35 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
     if (it + 1 < n_iter)
       stage_load<PSTAGE_W16, true>(regs, seq, L, (int64_t)tile_at(it + 1) * PTILE - HALO, true);
     __syncthreads();
+#ifndef KMHG_HIST0_STRIDED
+    // thread t takes the 8 consecutive windows [8 t, 8 t + 8) of the tile: their code and N
+    // flags come from 8 LDS reads (Win8) instead of 6 per window -- this pass was bound
+    // by those reads -- and their bucket ids leave as two 16-B stores
+    static_assert(PWPT == 8, "Win8 covers 8 windows per thread");
+    {
+      const int w0 = PWPT * threadIdx.x;
+      const int64_t s0 = tile0 + w0;
+      const Win8 win(st, HALO + w0, s0, L, k);
+      uint32_t bl[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bl[j] = ~0u;
+        if (s0 + j < Nw && win.valid(j)) {
+          const uint32_t b = bucket_local(mix64(win.key(j)), g);
+          if (b < g.nb) {
+            atomicAdd(&lh[digit_of_b(b, D)], 1u);
+            bl[j] = b;
+          }
+        }
+      }
+      // the id array holds Nw + PTILE entries: a tile's last 16-B stores stay inside it
+      if (BIDS && s0 < Nw) {
+        uint4* o = reinterpret_cast<uint4*>(bids + s0);
+        o[0] = make_uint4(bl[0], bl[1], bl[2], bl[3]);
+        o[1] = make_uint4(bl[4], bl[5], bl[6], bl[7]);
+      }
+    }
+#else
 #pragma unroll 4
     for (int j = 0; j < PWPT; ++j) {
       const int w = j * BLOCK + threadIdx.x;
@@ -234,6 +266,7 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
       }
       if (BIDS && s < Nw) bids[s] = bl;
     }
+#endif
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) {
       hist[(size_t)d * ch.C + tile] = lh[d];

@@ -244,6 +244,37 @@ __device__ __forceinline__ bool window_key(const ST& st, int o, int64_t s, int64
   return true;
 }
 
+// Eight consecutive windows at stage offsets o0 .. o0 + 7 (global starts s0 .. s0 + 7), the same
+// rule as window_key, from 4 code words and 4 N-flag words read once: 8 LDS reads for 8 windows
+// instead of 48.  o0 % 8 == 0 and o0 >= 8 (the stage has HALO chars in front).  key(j) and
+// valid(j) take static j; only the six words stay live across the windows.
+struct Win8 {
+  uint64_t hi, lo, nx;                       // code bits of chars 16 q .., N flags of 16 qn ..
+  int b, c0, k;
+  int64_t s0, L;
+  template <class ST>
+  __device__ __forceinline__ Win8(const ST& st, int o0, int64_t s0_, int64_t L_, int k_)
+      : k(k_), s0(s0_), L(L_) {
+    const int q = o0 >> 4, qn = (o0 - 1) >> 4;
+    b = o0 & 15;
+    c0 = (o0 - 1) & 15;
+    hi = ((uint64_t)st.code[q] << 32) | st.code[q + 1];
+    lo = ((uint64_t)st.code[q + 2] << 32) | st.code[q + 3];
+    nx = ((uint64_t)st.nbit[qn] << 48) | ((uint64_t)st.nbit[qn + 1] << 32) |
+         ((uint64_t)st.nbit[qn + 2] << 16) | (uint64_t)st.nbit[qn + 3];
+  }
+  __device__ __forceinline__ uint64_t key(int j) const {
+    const int sh = 2 * (b + j);              // <= 30: the window's chars start here
+    const uint64_t top = sh ? (hi << sh) | (lo >> (64 - sh)) : hi;
+    return top >> (64 - 2 * k);
+  }
+  __device__ __forceinline__ bool valid(int j) const {
+    const int64_t s = s0 + j;
+    const uint64_t m = (nx << (c0 + j)) >> (63 - k);   // N flags of chars [o - 1, o + k)
+    return s + k <= L && !(m & ((2ull << (k - 1)) - 1ull)) && !(s + k == L && ((m >> k) & 1ull));
+  }
+};
+
 // The key of window j (0-based) from a sequence's global code words (the stage's format, 16
 // chars per u32 MSB-first; a, b, c = words j / 16 .. j / 16 + 2): window_key's extraction.
 __device__ __forceinline__ uint64_t code_key(uint32_t a, uint32_t b, uint32_t c, int64_t j, int k) {
