@@ -246,7 +246,8 @@ __device__ __forceinline__ bool window_key(const ST& st, int o, int64_t s, int64
 
 // Eight consecutive windows at stage offsets o0 .. o0 + 7 (global starts s0 .. s0 + 7), the same
 // rule as window_key, from 4 code words and 4 N-flag words read once: 8 LDS reads for 8 windows
-// instead of 48.  o0 % 8 == 0 and o0 >= 8 (the stage has HALO chars in front).  key(j) and
+// instead of 48.  o0 >= 1 (the stage has HALO chars in front); chars [o0 - 1, o0 + 7 + k) lie
+// in the 64 chars from 16 * ((o0 - 1) / 16) for any o0 % 16 and k <= 32.  key(j) and
 // valid(j) take static j; only the six words stay live across the windows.
 struct Win8 {
   uint64_t hi, lo, nx;                       // code bits of chars 16 q .., N flags of 16 qn ..
@@ -255,16 +256,18 @@ struct Win8 {
   template <class ST>
   __device__ __forceinline__ Win8(const ST& st, int o0, int64_t s0_, int64_t L_, int k_)
       : k(k_), s0(s0_), L(L_) {
+    // (words past the stage's end are clamped: the windows of the stage never reach them)
+    constexpr int W = ST::kWords - 1;
     const int q = o0 >> 4, qn = (o0 - 1) >> 4;
     b = o0 & 15;
     c0 = (o0 - 1) & 15;
     hi = ((uint64_t)st.code[q] << 32) | st.code[q + 1];
-    lo = ((uint64_t)st.code[q + 2] << 32) | st.code[q + 3];
+    lo = ((uint64_t)st.code[min(q + 2, W)] << 32) | st.code[min(q + 3, W)];
     nx = ((uint64_t)st.nbit[qn] << 48) | ((uint64_t)st.nbit[qn + 1] << 32) |
-         ((uint64_t)st.nbit[qn + 2] << 16) | (uint64_t)st.nbit[qn + 3];
+         ((uint64_t)st.nbit[min(qn + 2, W)] << 16) | (uint64_t)st.nbit[min(qn + 3, W)];
   }
   __device__ __forceinline__ uint64_t key(int j) const {
-    const int sh = 2 * (b + j);              // <= 30: the window's chars start here
+    const int sh = 2 * (b + j);              // <= 44: the window's chars start here
     const uint64_t top = sh ? (hi << sh) | (lo >> (64 - sh)) : hi;
     return top >> (64 - 2 * k);
   }

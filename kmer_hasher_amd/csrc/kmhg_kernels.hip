@@ -498,6 +498,100 @@ __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_sta
   }
 }
 
+// The same in two phases.  Phase 1, per lane over 8 CONSECUTIVE windows w0 .. w0 + 7 of the tile
+// (w0 = 8 t): they share one anchor (64 | 8), so their predictions are consecutive index windows
+// p0 .. p0 + 7 and their verification needs 4 code words and 2 uniq words for the lot, read once
+// (6 loads, not 32); their own keys come from Win8 (8 LDS reads, not 48); their records leave as
+// two 16-B stores.  Phase 2 probes the windows phase 1 did not resolve, with the strided window
+// -> lane map (window j * BLOCK + t): a miss run (the k windows over an SNV) would otherwise be
+// one lane's serial chain of random reads (config 5: probe 5.1 -> 6.4 ms with phase 1's map).
+// Writes qrec / qmulti itself; returns the lane's row count.
+struct DiagProbeLDS {
+  uint64_t key[TILE];            // unresolved windows' keys
+  uint8_t todo[TILE];            // 1: window w needs a table probe
+};
+template <class ST>
+__device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t t_start,
+                                                  int64_t w0r, int64_t w1, int64_t L, int kq,
+                                                  const Slot* __restrict__ T, Geom g, DiagIdx X,
+                                                  const uint8_t* __restrict__ TG,
+                                                  const DiagAnchors& A, uint32_t* __restrict__ qrec,
+                                                  uint2* __restrict__ qmulti, DiagProbeLDS& P) {
+  static_assert(DG_STRIDE % 8 == 0 && WPT == 8, "a lane's 8 windows share one anchor");
+  const int w0 = 8 * (int)threadIdx.x;
+  const int64_t s0 = t_start + w0;
+  const Win8 win(st, o0 + w0, s0, L, kq);
+  const int la = A.last[w0 / DG_STRIDE];
+  const int64_t pbase = la >= 0 ? (int64_t)A.anc[la] + (w0 - la * DG_STRIDE) : 0;
+  const bool pred = la >= 0 && pbase <= X.nA;             // anc > 0, so pbase >= 1
+  const uint64_t p0 = pred ? (uint64_t)(pbase - 1) : 0ull;  // 0-based index window of j = 0
+  const uint64_t cq = p0 >> 4, uq = p0 >> 5;
+  const uint64_t ulast = X.nA > 0 ? (uint64_t)(X.nA - 1) >> 5 : 0ull;
+  const uint64_t ih = ((uint64_t)X.code[cq] << 32) | X.code[cq + 1];
+  const uint64_t il = ((uint64_t)X.code[cq + 2] << 32) | X.code[cq + 3];
+  const uint64_t ub = ((uint64_t)X.uniq[min(uq + 1, ulast)] << 32) | X.uniq[uq];
+  const int ro = (int)(p0 & 15), rb = (int)(p0 & 31);
+  uint32_t rec[8];
+  uint64_t rows = 0;
+  uint32_t todo = 0;                                       // byte j: window j left to phase 2
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t s = s0 + j;
+    uint32_t count = 0, aux = 0;
+    if (s < w1 && win.valid(j)) {
+      const uint64_t key = win.key(j);
+      bool hit;
+      if (j == 0 && w0 % DG_STRIDE == 0) {               // an anchor: probed already
+        const uint2 ai = A.info[w0 / DG_STRIDE];
+        count = ai.x; aux = ai.y;
+        hit = true;
+      } else {
+        const int sh = 2 * (ro + j);                       // <= 44
+        const uint64_t top = sh ? (ih << sh) | (il >> (64 - sh)) : ih;
+        const uint64_t ikey = top >> (64 - 2 * kq);
+        hit = pred && (int64_t)(p0 + j) < X.nA && ((ub >> (rb + j)) & 1ull) && ikey == key;
+        count = 1; aux = (uint32_t)(p0 + 1 + j);
+      }
+      if (!hit) {
+        count = 0; aux = 0;
+        P.key[w0 + j] = key;
+        todo |= 1u << (8 * (j & 3));
+      }
+    }
+    if (j == 3) {
+      *reinterpret_cast<uint32_t*>(&P.todo[w0]) = todo;
+      todo = 0;
+    }
+    rec[j] = count == 0 ? 0u : (count == 1 ? aux : QREC_MULTI);
+    if (count > 1 && s < w1) qmulti[s - w0r] = make_uint2(count, aux - count);
+    rows += count;
+  }
+  *reinterpret_cast<uint32_t*>(&P.todo[w0 + 4]) = todo;
+  if (s0 + 7 < w1) {                                       // 32-B aligned: s0 - w0r = 8 (. . .)
+    uint4* o = reinterpret_cast<uint4*>(qrec + (s0 - w0r));
+    o[0] = make_uint4(rec[0], rec[1], rec[2], rec[3]);
+    o[1] = make_uint4(rec[4], rec[5], rec[6], rec[7]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (s0 + j < w1) qrec[s0 + j - w0r] = rec[j];
+  }
+  __syncthreads();             // phase 1's keys, flags and records (vmcnt drained) are in place
+#pragma unroll 2
+  for (int j = 0; j < 8; ++j) {
+    const int w = j * BLOCK + (int)threadIdx.x;
+    if (P.todo[w]) {
+      const int64_t s = t_start + w;
+      uint32_t count = 0, aux = 0;
+      if (TG) table_find_tag(T, TG, g, P.key[w], count, aux);
+      else table_find4(T, g, P.key[w], count, aux);
+      put_qrec(qrec, qmulti, s - w0r, count, aux);
+      rows += count;
+    }
+  }
+  return rows;
+}
+
 // At least 6 waves per SIMD: the diagonal probe needs 81 VGPRs unconstrained (5 waves / SIMD);
 // capped it fits 72 with no spill (7 waves).  A/B in one run, config 2: self query 87.0 / 90.0 ->
 // 90.9 / 95.4 Gbp/s, unrelated 41.4 -> 44.3; 8 waves (64 VGPRs) spills 44 B / lane and is slower.
@@ -518,6 +612,9 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
   __shared__ DiagAnchors A;
+#ifndef KMHG_PROBE_STRIDED
+  __shared__ DiagProbeLDS PL;
+#endif
   const uint32_t tile = blockIdx.x;
   // windows [w0, w1) of the FULL sequence: halo chars come from the real neighbours, so the
   // N / end-of-sequence rules at a shard boundary are those of the unsharded walk
@@ -532,6 +629,13 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
 #define KMHG_PROBE_UNROLL 2
 #endif
   if (DIAG) {
+#ifndef KMHG_PROBE_STRIDED
+    rows = diag_resolve8(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A, qrec, qmulti, PL);
+    uint64_t tot8;
+    block_excl_scan(rows, sh, tot8);
+    if (threadIdx.x == 0) tile_rows[tile] = tot8;
+    return;
+#endif
     diag_resolve(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
                  [&](int w, int64_t s, uint32_t count, uint32_t aux) {
                    if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
