@@ -441,6 +441,73 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
   }
 }
 
+// Persistent form for the interleaved schedule (position builds' later passes): workgroup w walks
+// virtual tiles w, w + G, ... (XCD-contiguous like the scatter), thread t taking the 8
+// consecutive elements [8 t, 8 t + 8) of a tile with 16-B loads, the next tile's loads in flight
+// while this one is counted -- the one-tile-per-workgroup form exposed every workgroup's load
+// latency (config 2: 14.5 us for 40 MB).  `in` holds n + PTILE elements (the passes' padded
+// streams), so whole-tile loads stay inside it.
+template <bool BID>
+__global__ void __launch_bounds__(BLOCK)
+k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
+           uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
+           uint32_t n_status, uint32_t* __restrict__ save_col0) {
+  __shared__ uint32_t lh[V2_MAXR];
+  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
+    scan_status[i] = 0;
+  const uint64_t n = *n_ptr;
+  const uint32_t G = gridDim.x, R = D.R;
+  const uint32_t n_iter = (ch.ntiles - blockIdx.x + G - 1) / G;
+  auto tile_at = [&](uint32_t i) -> uint32_t {
+    const uint32_t v = blockIdx.x + i * G;
+    return remap ? xcd_remap(v, ch.ntiles) : v;
+  };
+  // the previous pass's scanned column 0, saved by the workgroup that writes column 0 (tile 0)
+  // before it does
+  if (save_col0 && tile_at(0) == 0)
+    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) save_col0[d] = hist[(size_t)d * ch.C];
+  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
+  constexpr int NV = BID ? 2 : 4;                      // 16-B loads per thread per tile
+  uint4 nx[NV];
+  auto prefetch = [&](uint32_t tile) {
+    const uint4* src = reinterpret_cast<const uint4*>(in) +
+                       ((uint64_t)tile * PTILE + 8u * threadIdx.x) / (BID ? 4 : 2);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) nx[v] = src[v];
+  };
+  prefetch(tile_at(0));
+  for (uint32_t it = 0; it < n_iter; ++it) {
+    const uint32_t tile = tile_at(it);
+    uint4 cur[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) cur[v] = nx[v];
+    if (it + 1 < n_iter) prefetch(tile_at(it + 1));
+    __syncthreads();                                   // lh zeroed (previous tile written out)
+    const uint64_t e0 = (uint64_t)tile * PTILE + 8u * threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (e0 + j < n) {
+        uint32_t dg;
+        if (BID) {
+          const uint4 w = cur[j >> 2];
+          const uint32_t id = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
+          dg = digit_of_b(id, D);
+        } else {
+          const uint4 w = cur[j >> 1];
+          const uint64_t key = (j & 1) ? (((uint64_t)w.w << 32) | w.z) : (((uint64_t)w.y << 32) | w.x);
+          dg = digit_of_h(mix64(key), g, D);
+        }
+        atomicAdd(&lh[dg], 1u);
+      }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
+      hist[(size_t)d * ch.C + tile] = lh[d];
+      lh[d] = 0;
+    }
+  }
+}
+
 // V_hll: register-wise max of the histogram workgroups' HLL rows.  V_hll_part: workgroup g
 // reduces rows [g * rpw, (g + 1) * rpw) into partial row g (thread t takes packed word t mod 64
 // of every 16th row: each row one coalesced 256-B read, eight rows in flight per thread);
@@ -2022,16 +2089,36 @@ void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total,
                        (const uint64_t*)status, total);
   }
 }
+// KMHG_HISTP=0: the one-tile-per-workgroup histogram kernel (A/B)
+static bool hist_persistent(const Chunks& ch) {
+  const char* e = std::getenv("KMHG_HISTP");          // read per launch: the tests switch it
+  return ch.interleaved && !(e && e[0] == '0');
+}
 void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
                         uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
                         hipStream_t s, uint32_t* save_col0) {
+  if (hist_persistent(ch)) {
+    static const unsigned cap = resident_blocks((const void*)k_v2_histp<true>);
+    hipLaunchKernelGGL(k_v2_histp<true>, dim3(std::min<unsigned>(ch.ntiles, cap)), dim3(BLOCK), 0,
+                       s, reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ch,
+                       xcd_map(), scan_status, n_status, save_col0);
+    return;
+  }
   hipLaunchKernelGGL((k_v2_hist<false, true>), dim3(ch.C), dim3(BLOCK), 0, s,
                      reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ch, xcd_map(),
                      scan_status, n_status, nullptr, nullptr, save_col0, 0);
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
-                    uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0, bool skip_empty) {
+                    uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0, bool skip_empty,
+                    bool padded) {
+  if (padded && !hll_rows && !skip_empty && hist_persistent(ch)) {
+    static const unsigned cap = resident_blocks((const void*)k_v2_histp<false>);
+    hipLaunchKernelGGL(k_v2_histp<false>, dim3(std::min<unsigned>(ch.ntiles, cap)), dim3(BLOCK),
+                       0, s, keys, n_ptr, g, D, hist, ch, xcd_map(), scan_status, n_status,
+                       save_col0);
+    return;
+  }
   if (hll_rows)
     hipLaunchKernelGGL(k_v2_hist<true>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
                        ch, xcd_map(), scan_status, n_status, hll_rows, hll_regs, save_col0,

@@ -1017,7 +1017,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     LAUNCH("k_v2_hist", s,
            launch_v2_hist(src, n_valid, g, Dp, hist.p, ch, status, n_status, s,
                           hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
-                          save ? lo_start.p : nullptr, keys0 && skip_empty));
+                          save ? lo_start.p : nullptr, keys0 && skip_empty,
+                          /*padded=*/!keys0));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     if (hll) {   // after the scan: the estimate travels with the valid key count
       LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ch.C, hll_regs.p,

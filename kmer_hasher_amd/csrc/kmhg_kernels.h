@@ -189,7 +189,8 @@ constexpr uint32_t HLL_PART_WORDS = 256 * 64 + 1;
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr,
-                    uint32_t* save_col0 = nullptr, bool skip_empty = false);
+                    uint32_t* save_col0 = nullptr, bool skip_empty = false,
+                    bool padded = false);
 // bucket starts from the histograms (passes <= 2, interleaved schedule): one workgroup per lo
 // value (div of them); kprev = the last pass's input keys, lo_start = the previous pass's digit
 // starts (saved by launch_v2_hist's save_col0; nullptr for one pass); start[b / spread] for

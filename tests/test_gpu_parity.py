@@ -249,7 +249,7 @@ def test_stream_disorder_falls_back(gpu, monkeypatch, stream):
 
 
 @pytest.mark.parametrize("stream", ["bid", "keys"])
-@pytest.mark.parametrize("bounds", ["lo", "scan", "sc8", "h0tile"])
+@pytest.mark.parametrize("bounds", ["lo", "scan", "sc8", "h0tile", "histtile"])
 @pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
 def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds, stream):
     """More radix passes than the input needs (KMHG_MAXR caps the radix): 1-4 passes with N-runs
@@ -266,6 +266,8 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds, stream):
         monkeypatch.setenv("KMHG_SC8", "1")
     elif bounds == "h0tile":               # the first histogram one workgroup per tile
         monkeypatch.setenv("KMHG_HIST0P", "0")
+    elif bounds == "histtile":             # the later histograms one workgroup per tile
+        monkeypatch.setenv("KMHG_HISTP", "0")
     else:
         monkeypatch.setenv("KMHG_BOUNDS", bounds)
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
