@@ -274,6 +274,12 @@ int kmhg_part_info(kmhg_index *idx, int64_t info[10]);
 int kmhg_part_export(kmhg_index *idx, int64_t pos_base, void *d_table, void *d_side_slot,
                      void *d_positions, void *d_codes, void *stream);
 
+/* Device self-check of the property the radix passes' stable ranks rest on: the lanes of one
+ * returning LDS add that hit the same address receive old values in increasing lane order
+ * (kmhg_build_v2.hip V_scatter; the bucket kernels also verify every bucket's stream order and
+ * fall back).  Writes the same-digit lane pairs found out of order and the pairs checked. */
+int kmhg_check_lds_lane_order(uint64_t *out_of_order, uint64_t *checked);
+
 /* Per-kernel HIP-event timing (KMHG_TIMING=1 also enables it).  The report is JSON:
  * {"kernel": [launches, total_ms], ...}; events are recorded on the kernels' own stream. */
 int kmhg_timing_enable(int on);

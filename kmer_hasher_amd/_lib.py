@@ -90,6 +90,7 @@ _PROTOS = {
                                          C.POINTER(vp)]),
     "kmhg_part_info": (C.c_int, [vp, i64p]),
     "kmhg_part_export": (C.c_int, [vp, C.c_int64, vp, vp, vp, vp, vp]),
+    "kmhg_check_lds_lane_order": (C.c_int, [C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "kmhg_timing_enable": (C.c_int, [C.c_int]),
     "kmhg_timing_select": (C.c_int, [C.c_char_p]),
     "kmhg_timing_reset": (C.c_int, []),

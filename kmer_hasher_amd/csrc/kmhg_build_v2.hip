@@ -2263,6 +2263,43 @@ void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32
     hipLaunchKernelGGL(k_v2_bucket_wg<false>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g,
                        T, positions, bstats, meta, TG, mbits, fp, nullptr, 0);
 }
+// The hardware property the radix passes' ranks rest on, checked on the device itself
+// (kmhg_check_lds_lane_order; tools/lds_order.hip is the stand-alone probe): the lanes of one
+// returning LDS add that hit the same address get old values in increasing lane order.  Every
+// wave draws skewed random digits, adds, and compares each lane with every lower lane of the
+// same digit.
+__global__ void __launch_bounds__(BLOCK)
+k_lane_order_check(unsigned long long* __restrict__ res, uint32_t seed, int iters) {
+  __shared__ uint32_t cnt[BLOCK / 64][128];
+  __shared__ uint32_t got[BLOCK / 64][64], dig[BLOCK / 64][64];
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  uint32_t r = (seed ^ (blockIdx.x * BLOCK + threadIdx.x) * 2654435761u) | 1u;
+  unsigned long long bad = 0, chk = 0;
+  for (int it = 0; it < iters; ++it) {
+    for (int d = lane; d < 128; d += 64) cnt[w][d] = 0;
+    wave_sync();
+    r ^= r << 13; r ^= r >> 17; r ^= r << 5;
+    const uint32_t d = (r & 1) ? (r >> 8) % 4 : (r >> 8) % 99;
+    const bool act = ((r >> 20) & 7) != 0;
+    const uint32_t v = act ? atomicAdd(&cnt[w][d], 1u) : 0u;
+    got[w][lane] = act ? v : 0xFFFFFFFFu;
+    dig[w][lane] = d;
+    wave_sync();
+    if (act)
+      for (int m = 0; m < lane; ++m)
+        if (got[w][m] != 0xFFFFFFFFu && dig[w][m] == d) {
+          ++chk;
+          bad += got[w][m] > v ? 1u : 0u;
+        }
+    wave_sync();
+  }
+  atomicAdd(&res[0], bad);
+  atomicAdd(&res[1], chk);
+}
+void launch_lane_order_check(unsigned long long* res, hipStream_t s) {
+  hipLaunchKernelGGL(k_lane_order_check, dim3(1024), dim3(BLOCK), 0, s, res, 12345u, 64);
+}
+
 // Test knob (KMHG_TEST_DISORDER=1, tests only): swaps the first two positions of bucket 0's
 // stream, so the bucket kernel's order check must report it and the build fall back.
 __global__ void k_v2_test_disorder(uint32_t* __restrict__ pos, const uint32_t* __restrict__ start) {

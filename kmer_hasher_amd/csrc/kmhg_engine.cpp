@@ -2908,6 +2908,19 @@ int kmhg_image_import(const int64_t header[8], const void* d_table, const void* 
   });
 }
 
+int kmhg_check_lds_lane_order(uint64_t* out_of_order, uint64_t* checked) {
+  return guarded([&] {
+    if (!out_of_order || !checked) fail(KMHG_EINVAL, "null result pointer");
+    DBuf<unsigned long long> res(2, nullptr);
+    HIPC(hipMemsetAsync(res.p, 0, 2 * sizeof(unsigned long long), nullptr));
+    launch_lane_order_check(res.p, nullptr);
+    unsigned long long h[2] = {0, 0};
+    HIPC(hipMemcpy(h, res.p, sizeof(h), hipMemcpyDeviceToHost));
+    *out_of_order = h[0];
+    *checked = h[1];
+  });
+}
+
 int kmhg_timing_enable(int on) {
   Timing::get().on = on != 0;
   return KMHG_OK;

@@ -252,6 +252,7 @@ void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, uint8_t* TG = nullptr,
                          uint32_t* mbits = nullptr, const uint32_t* code = nullptr, int k = 0);
+void launch_lane_order_check(unsigned long long* res, hipStream_t s);
 void launch_v2_test_disorder(uint32_t* pos, const uint32_t* start, hipStream_t s);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);

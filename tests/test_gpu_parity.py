@@ -224,6 +224,18 @@ def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
     _check_against_oracle("G" * 40, 32, qks=[31])
 
 
+def test_lds_atomic_lane_order(gpu):
+    """The radix passes rank equal digits by the values their LDS count atomics return; that is
+    stable only if the lanes of one instruction hitting one address are served in lane order.
+    Checked on this device through the C-ABI (kmhg_check_lds_lane_order)."""
+    import ctypes as C
+    from kmer_hasher_amd import _lib
+    bad, chk = C.c_uint64(0), C.c_uint64(0)
+    _lib.check(_lib.lib().kmhg_check_lds_lane_order(C.byref(bad), C.byref(chk)))
+    assert chk.value > 1_000_000, chk.value
+    assert bad.value == 0, (bad.value, chk.value)
+
+
 @pytest.mark.parametrize("stream", ["bid", "keys"])
 def test_stream_disorder_falls_back(gpu, monkeypatch, stream):
     """The radix passes are stable because same-address LDS count atomics of one instruction
