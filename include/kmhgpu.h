@@ -84,7 +84,16 @@ typedef struct {
   int32_t sources;       /* counts index (count.kmers): source_n; 0 for a position index */
   int32_t kind;          /* 0 position index, 1 counts index, 2 suffix hash (canonical counts) */
   int64_t kmer_count;    /* khash_ptr.kmer_count: distinct k-mers added (both kinds) */
+  int32_t build;         /* KMHG_BUILD_*: how the table was built (0 = imported / assembled) */
+  int32_t fallback;      /* 1: a partitioned build was rebuilt with the global-atomic build (a
+                            bucket's LDS table overflowed or its stream failed the order check) */
 } kmhg_info;
+
+/* kmhg_info.build */
+#define KMHG_BUILD_GLOBAL 1              /* global-atomic insert (KMHG_BUILD=v1, or the fallback) */
+#define KMHG_BUILD_PARTITIONED 2         /* radix partition + per-bucket LDS tables (default) */
+#define KMHG_BUILD_PARTITIONED_BALLOT 3  /* the same with ballot ranks: the device failed the
+                                            LDS lane-order self-check */
 
 const char *kmhg_last_error(void);
 int kmhg_version(void);

@@ -17,6 +17,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "kmhgpu.h")
 
 KMHG_OK, KMHG_EINVAL, KMHG_ENOMEM, KMHG_EDEVICE, KMHG_EOVERFLOW = 0, 1, 2, 3, 4
 KMHG_ORDER_FIRST, KMHG_ORDER_KHASH = 0, 1
+KMHG_BUILD_GLOBAL, KMHG_BUILD_PARTITIONED, KMHG_BUILD_PARTITIONED_BALLOT = 1, 2, 3
 
 
 class KmhgError(RuntimeError):
@@ -29,7 +30,8 @@ class Info(C.Structure):
     _fields_ = [("k", C.c_int32), ("device", C.c_int32), ("seq_len", C.c_int64),
                 ("n_kmers", C.c_int64), ("n_positions", C.c_int64), ("n_pairs", C.c_int64),
                 ("max_count", C.c_int64), ("table_slots", C.c_int64), ("device_bytes", C.c_int64),
-                ("sources", C.c_int32), ("kind", C.c_int32), ("kmer_count", C.c_int64)]
+                ("sources", C.c_int32), ("kind", C.c_int32), ("kmer_count", C.c_int64),
+                ("build", C.c_int32), ("fallback", C.c_int32)]
 
 
 class ImageSizes(C.Structure):

@@ -3,21 +3,24 @@
 // Replaces the same reference loops as K_insert/K_scatter/K_sort (src/kmer_pos.c:36-50, 66-98,
 // 21-33; kvec growth src/kvec.h:74-80) with an HBM-streaming design for CDNA4:
 //
-//   V_encode    LDS-staged 2-bit encode + N mask of every window (as K_insert) -> (key, pos)
-//               per window, plus a per-tile histogram of the first radix digit of its bucket
-//   V_scan      exclusive scan of the digit histograms (decoupled look-back)
+//   V_hist0     LDS-staged 2-bit encode + N mask of every window (as K_insert) and a per-tile
+//               histogram of the first radix digit of each window's bucket; keeps the sequence's
+//               code words (the diagonal query path) and, for small inputs, every window's
+//               bucket id
+//   V_scan      exclusive scan of the [digit][tile] histograms (decoupled look-back)
 //   V_scatter   stable radix pass: every wave ranks its 512 elements by digit with the
-//               returned values of its LDS count atomics (lane-ordered), elements land at
-//               histogram offsets -- LSD over 1-3 digits sorts the windows by bucket while
-//               keeping position order inside a bucket
+//               returned values of its LDS count atomics (lane-ordered; a device self-check picks
+//               ballot ranks where that does not hold), elements land at histogram offsets --
+//               LSD over 1-3 digits sorts the windows by bucket while keeping position order
+//               inside a bucket
 //   V_hist      digit histogram for the next radix pass
-//   V_bounds    bucket start offsets in the bucket-sorted stream
-//   V_bucket    ONE WAVE PER BUCKET: the bucket's keys go into a wave-private LDS hash table
-//               (LDS CAS + LDS atomics), counts are scanned in LDS, and a second in-order pass
-//               ranks equal keys with ballots, so positions are written ascending per key by
-//               construction (no sort).  The LDS table is written out as the bucket's
-//               sub-table of the global table; CSR arrays get dense ids from a look-back over
-//               buckets.
+//   V_bounds    bucket start offsets in the bucket-sorted stream (from the histograms for <= 2
+//               passes)
+//   V_bucket_wg ONE WORKGROUP PER BUCKET of ~1,024 windows: the bucket's keys go into a shared
+//               LDS hash table (LDS CAS + count atomics), the counts are scanned, repeated keys'
+//               windows are ranked in position order, so positions are written ascending per key
+//               by construction (no sort).  The LDS table is written out as the bucket's
+//               sub-table of the global table.
 //
 // A bucket's windows are exactly its keys' positions, so the CSR slice of bucket b is
 // [start[b], start[b+1]) of `positions` with no global coordination.
@@ -52,14 +55,6 @@ __device__ uint64_t* g_stamps;
 #define STAMP_WG(b, i) do {} while (0)
 #define STAMP_WG_DRAIN(b, i) do {} while (0)
 #endif
-
-// LDS sub-table of one bucket, private to one wave (slot V2_CAPB = side slot of key ~0).
-// SoA: 8-B keys (64-bit CAS on an 8-B stride touches 32 bank pairs, not 16) and {cnt, cur}
-// pairs (cnt = occurrences; cur = CSR offset, then the running cursor of pass B).
-struct WaveTable {
-  uint64_t key[V2_CAPB + 1];
-  uint2 cc[V2_CAPB + 1];
-};
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -126,53 +121,6 @@ __device__ __forceinline__ void diag_words_out(const PStage& st, uint32_t tile, 
   }
 }
 
-// ---------------------------------------------------------------- V_hist0 (from the sequence)
-// LDS-staged 2-bit encode + N mask of every window of the tile (as K_insert) and the tile's
-// histogram of the first radix digit of the windows' buckets.  Nothing else is written: the
-// first scatter pass re-reads the chars (1 B/window) instead of a 12 B/window key stream.
-__global__ void __launch_bounds__(BLOCK)
-k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
-           uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
-           uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
-           uint16_t* __restrict__ nbit, uint32_t* __restrict__ uniq0,
-           uint32_t* __restrict__ bids = nullptr) {
-  __shared__ PStage st;
-  __shared__ uint32_t lh[V2_MAXR];
-  // zero the next scan's look-back words + ticket and the build meta (no memset launches)
-  for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
-    scan_status[i] = 0;
-  if (blockIdx.x == 0 && threadIdx.x < sizeof(BuildMeta) / 4)
-    reinterpret_cast<uint32_t*>(meta)[threadIdx.x] = 0u;
-  const uint32_t c = remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x;
-  const uint32_t t_begin = c * ch.tpc, t_end = min(t_begin + ch.tpc, ch.ntiles);
-  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) lh[d] = 0;
-  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
-    const int64_t tile0 = (int64_t)tile * PTILE;
-    __syncthreads();                           // previous tile's stage reads done
-    stage_tile<true>(seq, L, tile0 - HALO, st, true);
-    __syncthreads();
-    if (code) diag_words_out(st, tile, ch.ntiles, code, nbit);
-    if (uniq0 && threadIdx.x < PTILE / 32) uniq0[(uint64_t)tile * (PTILE / 32) + threadIdx.x] = 0u;
-#pragma unroll 4
-    for (int j = 0; j < PWPT; ++j) {
-      const int w = j * BLOCK + threadIdx.x;
-      const int64_t s = tile0 + w;
-      uint64_t key = 0;
-      uint32_t bl = ~0u;
-      if (s < Nw && window_key(st, HALO + w, s, L, k, key)) {
-        const uint32_t b = bucket_local(mix64(key), g);
-        if (b < g.nb) {
-          atomicAdd(&lh[digit_of_b(b, D)], 1u);
-          bl = b;
-        }
-      }
-      if (bids && s < Nw) bids[s] = bl;
-    }
-  }
-  __syncthreads();
-  for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) hist[(size_t)d * ch.C + c] = lh[d];
-}
-
 // Persistent form for the interleaved schedule (one histogram column per tile): workgroup w
 // walks virtual tiles w, w + G, ... (XCD-contiguous like the scatter) and loads the next tile's
 // chars into registers while it encodes the current one, so the load latency of all but the
@@ -191,10 +139,9 @@ k_v2_hist0(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g
 template <bool CODES, bool BIDS = false>
 __global__ void __launch_bounds__(BLOCK, KMHG_HIST0_WAVES)
 k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
-            uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
+            uint32_t* __restrict__ hist, uint32_t ntiles, uint64_t* __restrict__ scan_status,
             uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
-            uint16_t* __restrict__ nbit, uint32_t* __restrict__ uniq0,
-            uint32_t* __restrict__ bids) {
+            uint16_t* __restrict__ nbit, uint32_t* __restrict__ bids) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
@@ -202,11 +149,8 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
   if (blockIdx.x == 0 && threadIdx.x < sizeof(BuildMeta) / 4)
     reinterpret_cast<uint32_t*>(meta)[threadIdx.x] = 0u;
   const uint32_t G = gridDim.x;
-  const uint32_t n_iter = (ch.ntiles - blockIdx.x + G - 1) / G;
-  auto tile_at = [&](uint32_t i) -> uint32_t {
-    const uint32_t v = blockIdx.x + i * G;
-    return remap ? xcd_remap(v, ch.ntiles) : v;
-  };
+  const uint32_t n_iter = (ntiles - blockIdx.x + G - 1) / G;
+  auto tile_at = [&](uint32_t i) -> uint32_t { return xcd_remap(blockIdx.x + i * G, ntiles); };
   for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) lh[d] = 0;
   StageRegs<PSTAGE_W16> regs;
   stage_load<PSTAGE_W16, true>(regs, seq, L, (int64_t)tile_at(0) * PTILE - HALO, true);
@@ -214,15 +158,10 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
     const uint32_t tile = tile_at(it);
     const int64_t tile0 = (int64_t)tile * PTILE;
     stage_pack(regs, st);                      // the previous tile's reads of st are done
-    if (CODES) diag_words_out(st, tile, ch.ntiles, code, nbit);
-    // the repeated keys' window bits start clear: the bucket kernel sets them (uniq0 = the
-    // code block's uniq words, reused as "multi" bits until the first query)
-    if (CODES && uniq0 && threadIdx.x < PTILE / 32)
-      uniq0[(uint64_t)tile * (PTILE / 32) + threadIdx.x] = 0u;
+    if (CODES) diag_words_out(st, tile, ntiles, code, nbit);
     if (it + 1 < n_iter)
       stage_load<PSTAGE_W16, true>(regs, seq, L, (int64_t)tile_at(it + 1) * PTILE - HALO, true);
     __syncthreads();
-#ifndef KMHG_HIST0_STRIDED
     // thread t takes the 8 consecutive windows [8 t, 8 t + 8) of the tile: their code and N
     // flags come from 8 LDS reads (Win8) instead of 6 per window -- this pass was bound
     // by those reads -- and their bucket ids leave as two 16-B stores
@@ -250,26 +189,9 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
         o[1] = make_uint4(bl[4], bl[5], bl[6], bl[7]);
       }
     }
-#else
-#pragma unroll 4
-    for (int j = 0; j < PWPT; ++j) {
-      const int w = j * BLOCK + threadIdx.x;
-      const int64_t s = tile0 + w;
-      uint64_t key = 0;
-      uint32_t bl = ~0u;
-      if (s < Nw && window_key(st, HALO + w, s, L, k, key)) {
-        const uint32_t b = bucket_local(mix64(key), g);
-        if (b < g.nb) {
-          atomicAdd(&lh[digit_of_b(b, D)], 1u);
-          bl = b;
-        }
-      }
-      if (BIDS && s < Nw) bids[s] = bl;
-    }
-#endif
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) {
-      hist[(size_t)d * ch.C + tile] = lh[d];
+      hist[(size_t)d * ntiles + tile] = lh[d];
       lh[d] = 0;                               // next tile's atomics follow a barrier
     }
   }
@@ -332,45 +254,6 @@ k_scan_lb_u32(uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ statu
   }
 }
 
-// Reduce-then-scan (no tickets, no spinning) for long arrays: per-tile sums -> one-workgroup
-// scan of the tile sums (k_scan_tiles_u64) -> per-tile exclusive scan seeded with its base.
-__global__ void __launch_bounds__(BLOCK)
-k_tile_sum_u32(const uint32_t* __restrict__ a, uint64_t n, uint64_t* __restrict__ tsum) {
-  __shared__ uint64_t sh[8];
-  const uint64_t base = (uint64_t)blockIdx.x * TILE;
-  uint64_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < WPT; ++j) {
-    const uint64_t i = base + (uint64_t)j * BLOCK + threadIdx.x;
-    if (i < n) sum += a[i];
-  }
-  uint64_t tot;
-  block_excl_scan(sum, sh, tot);
-  if (threadIdx.x == 0) tsum[blockIdx.x] = tot;
-}
-
-__global__ void __launch_bounds__(BLOCK)
-k_tile_scan_u32(uint32_t* __restrict__ a, uint64_t n, const uint64_t* __restrict__ tbase,
-                uint32_t* __restrict__ total) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *total = (uint32_t)tbase[gridDim.x];
-  __shared__ uint64_t sh[8];
-  const uint64_t base = (uint64_t)blockIdx.x * TILE + (uint64_t)threadIdx.x * WPT;
-  uint32_t v[WPT];
-  uint64_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < WPT; ++j) {
-    v[j] = (base + j < n) ? a[base + j] : 0u;
-    sum += v[j];
-  }
-  uint64_t tot;
-  uint64_t run = block_excl_scan(sum, sh, tot) + tbase[blockIdx.x];
-#pragma unroll
-  for (int j = 0; j < WPT; ++j) {
-    if (base + j < n) a[base + j] = (uint32_t)run;
-    run += v[j];
-  }
-}
-
 // ---------------------------------------------------------------- V_hist (passes >= 1)
 // HLL (count-only builds, first pass): a HyperLogLog sketch of the distinct keys rides on the
 // histogram pass, which hashes every key anyway.  A 1/HLL_SAMPLE key-space sample (h mod 64 == 0)
@@ -384,7 +267,7 @@ static_assert(HLL_PART_WORDS == HLL_PART_ROWS * 64 + 1, "V_hll partial rows + ti
 template <bool HLL, bool BID = false>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
-          Digit D, uint32_t* __restrict__ hist, Chunks ch, int remap,
+          Digit D, uint32_t* __restrict__ hist, uint32_t ntiles,
           uint64_t* __restrict__ scan_status, uint32_t n_status, uint32_t* __restrict__ hll_rows,
           uint32_t* __restrict__ hll_regs, uint32_t* __restrict__ save_col0, int skip_empty) {
   __shared__ uint32_t lh[V2_MAXR];
@@ -393,15 +276,15 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
     scan_status[i] = 0;
   // the previous pass's scanned column 0 (digit starts), kept for V_bounds_lo before this
   // workgroup -- the only writer of column 0 -- overwrites it
-  if (save_col0 && (remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x) == 0)
-    for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) save_col0[d] = hist[(size_t)d * ch.C];
+  const uint32_t c = xcd_remap(blockIdx.x, ntiles);      // one workgroup per tile
+  if (save_col0 && c == 0)
+    for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) save_col0[d] = hist[(size_t)d * ntiles];
   if (HLL) {
     for (uint32_t i = threadIdx.x; i < HLL_REGS; i += BLOCK) hreg[i] = 0;
   }
   const uint64_t n = *n_ptr;
-  const uint32_t c = remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x;
-  const uint64_t e0 = (uint64_t)c * ch.tpc * PTILE;
-  const uint64_t e1 = min(n, e0 + (uint64_t)ch.tpc * PTILE);
+  const uint64_t e0 = (uint64_t)c * PTILE;
+  const uint64_t e1 = min(n, e0 + (uint64_t)PTILE);
   const uint32_t R = D.R;
   for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
   __syncthreads();
@@ -433,7 +316,7 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
       if (in[j]) atomicAdd(&lh[dg[j]], 1u);
   }
   __syncthreads();
-  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[(size_t)d * ch.C + c] = lh[d];
+  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) hist[(size_t)d * ntiles + c] = lh[d];
   if (HLL && threadIdx.x < HLL_REGS / 4) {
     const uint32_t* h4 = hreg + 4 * threadIdx.x;
     hll_rows[(size_t)blockIdx.x * (HLL_REGS / 4) + threadIdx.x] =
@@ -450,22 +333,19 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
 template <bool BID>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
-           uint32_t* __restrict__ hist, Chunks ch, int remap, uint64_t* __restrict__ scan_status,
+           uint32_t* __restrict__ hist, uint32_t ntiles, uint64_t* __restrict__ scan_status,
            uint32_t n_status, uint32_t* __restrict__ save_col0) {
   __shared__ uint32_t lh[V2_MAXR];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
     scan_status[i] = 0;
   const uint64_t n = *n_ptr;
   const uint32_t G = gridDim.x, R = D.R;
-  const uint32_t n_iter = (ch.ntiles - blockIdx.x + G - 1) / G;
-  auto tile_at = [&](uint32_t i) -> uint32_t {
-    const uint32_t v = blockIdx.x + i * G;
-    return remap ? xcd_remap(v, ch.ntiles) : v;
-  };
+  const uint32_t n_iter = (ntiles - blockIdx.x + G - 1) / G;
+  auto tile_at = [&](uint32_t i) -> uint32_t { return xcd_remap(blockIdx.x + i * G, ntiles); };
   // the previous pass's scanned column 0, saved by the workgroup that writes column 0 (tile 0)
   // before it does
   if (save_col0 && tile_at(0) == 0)
-    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) save_col0[d] = hist[(size_t)d * ch.C];
+    for (uint32_t d = threadIdx.x; d < R; d += BLOCK) save_col0[d] = hist[(size_t)d * ntiles];
   for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
   constexpr int NV = BID ? 2 : 4;                      // 16-B loads per thread per tile
   uint4 nx[NV];
@@ -502,7 +382,7 @@ k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, 
     }
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
-      hist[(size_t)d * ch.C + tile] = lh[d];
+      hist[(size_t)d * ntiles + tile] = lh[d];
       lh[d] = 0;
     }
   }
@@ -598,14 +478,18 @@ k_v2_hll_final(const uint32_t* __restrict__ part, uint32_t n_part, double* __res
 // drops invalid ones; later passes read the (key, pos) stream.  The tile is re-ordered by digit
 // in LDS first and written out run by run, so each wave store covers a few contiguous runs
 // instead of 64 scattered addresses.
-// NWV = 8 (512 threads, KMHG_SC8=1, up to V2_MAXR_IL digits): 4 elements per lane instead of 8
-// (84-96 VGPRs, 24 waves / CU instead of 12).  More waves did not make the pass faster (config 2
-// neutral, config 3 +10 %): it is bound by the digit-run write pattern, not by latency hiding.
-// (Also measured: 320-digit arrays alone, or forcing 4 waves of the 4-wave kernel with spills.)
-template <int NWV, class KT, bool IL_ONLY>
+// Persistent workgroup b walks virtual tiles b, b + G, ...: every XCD owns one contiguous tile
+// range (xcd_remap), so the tiles running at the same time on an XCD are neighbours and their
+// partial output lines merge in that XCD's L2.  Histograms are per tile; each tile's digit bases
+// are prefetched with its inputs.
+// (Removed in round 4 after measurement: 8-wave workgroups, +10 % at config 3, and a chunked
+// schedule with per-chunk histograms, -10 %: each workgroup's open digit-run heads overflow the
+// L2.)
+constexpr int SC_NWV = 4;                       // waves per scatter workgroup
+template <class KT>
 struct ScatterLDS {
-  static constexpr uint32_t MAXR = (NWV == 4 && !IL_ONLY) ? V2_MAXR : V2_MAXR_IL;
-  uint32_t wc[NWV][MAXR];      // per-wave digit counts -> per-wave tile-local cursors
+  static constexpr uint32_t MAXR = V2_MAXR_IL;
+  uint32_t wc[SC_NWV][MAXR];   // per-wave digit counts -> per-wave tile-local cursors
   uint32_t tstart[MAXR];       // tile-local start of each digit
   uint32_t gbase[MAXR];        // global start of each digit for this tile (scanned histogram)
   KT skey[PTILE];
@@ -642,20 +526,23 @@ __device__ __forceinline__ uint64_t block_excl_scan_n(uint64_t v, uint64_t* lds,
 // code words by the bucket kernel; 2 = the last pass: (bucket id, pos) in, positions only out.
 // kin / kout then point at u32 arrays.  8 B per element instead of 12 through the middle passes,
 // 4 B out of the last.
-template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false, int NWV = 4, int BM = 0>
-__global__ void __launch_bounds__(NWV * 64)
-k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int aligned,
+// BALLOT: stable ranks from one ballot per digit bit instead of the count atomics' lane-ordered
+// returns -- chosen at run time where the device self-check finds that order violated.
+template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false, int BM = 0, bool BALLOT = false>
+__global__ void __launch_bounds__(SC_NWV * 64)
+k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
-             const uint32_t* __restrict__ hist, Chunks ch,
-             uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad, int remap,
+             const uint32_t* __restrict__ hist, uint32_t ntiles,
+             uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad,
              int skip_empty) {
   using KT = typename std::conditional<BM != 0, uint32_t, uint64_t>::type;
-  using SL = ScatterLDS<NWV, KT, BM != 0>;    // bucket-id builds: interleaved schedule only
+  using SL = ScatterLDS<KT>;
   static_assert(BM == 0 || !NOPOS, "bucket-id streams carry positions");
   // KEYS0 with BM: the first pass over V_hist0's per-window bucket ids (~0: not indexed)
   const KT* __restrict__ kinT = reinterpret_cast<const KT*>(kin);
   KT* __restrict__ koutT = reinterpret_cast<KT*>(kout);
+  constexpr int NWV = SC_NWV;
   constexpr int TB = NWV * 64;                  // threads per workgroup
   constexpr int PER = PTILE / NWV / 64;         // elements per lane
   constexpr int DPT = (int)((SL::MAXR + TB - 1) / TB);   // digits owned per thread
@@ -667,29 +554,16 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
   // elements to read: every window (FROM_SEQ) or the caller's whole key stream (KEYS0, passed
   // as Nw: with skip_empty it is longer than the valid count the scan left in *n_ptr)
   const uint64_t n = (FROM_SEQ || KEYS0) ? (uint64_t)Nw : (uint64_t)*n_ptr;
-  // Two tile schedules (Chunks, kmhg_kernels.h); thread t owns digits [DPT t, DPT t + DPT).
-  //  interleaved (ch.interleaved): persistent workgroup b walks virtual tiles b, b + G, ...;
-  //    with `remap` every XCD owns one contiguous tile range, so the tiles running at the same
-  //    time on an XCD are neighbours and their partial output lines merge in that XCD's L2.
-  //    Histograms are per tile; each tile's digit bases are prefetched with its inputs.
-  //  chunked: one workgroup per chunk of consecutive tiles, histograms per chunk; the digit
-  //    cursors advance in registers from tile to tile.
+  // thread t owns digits [DPT t, DPT t + DPT)
   const uint32_t G = gridDim.x;
-  const uint32_t chunk = ch.interleaved ? 0u : (remap ? xcd_remap(blockIdx.x, ch.C) : blockIdx.x);
-  const uint32_t n_iter = ch.interleaved
-                              ? (ch.ntiles - blockIdx.x + G - 1) / G
-                              : min(chunk * ch.tpc + ch.tpc, ch.ntiles) - chunk * ch.tpc;
-  auto tile_at = [&](uint32_t i) -> uint32_t {
-    if (!ch.interleaved) return chunk * ch.tpc + i;
-    const uint32_t v = blockIdx.x + i * G;
-    return remap ? xcd_remap(v, ch.ntiles) : v;
-  };
-  uint32_t cursor[DPT], ngb[DPT];
+  const uint32_t n_iter = (ntiles - blockIdx.x + G - 1) / G;
+  auto tile_at = [&](uint32_t i) -> uint32_t { return xcd_remap(blockIdx.x + i * G, ntiles); };
+  uint32_t ngb[DPT];
   auto load_bases = [&](uint32_t tv) {     // unconditional (clamped) loads: static count
 #pragma unroll
     for (int q = 0; q < DPT; ++q) {
       const uint32_t d = min(threadIdx.x * DPT + q, R - 1);
-      ngb[q] = hist[(size_t)d * ch.C + (ch.interleaved ? tv : chunk)];
+      ngb[q] = hist[(size_t)d * ntiles + tv];
     }
   };
   // the next tile's inputs are in flight while this one is processed
@@ -719,8 +593,6 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
   // previous tile's write-out on the first iteration.
   prefetch(tile_at(0));
 #pragma unroll
-  for (int q = 0; q < DPT; ++q) cursor[q] = ngb[q];
-#pragma unroll
   for (int j = 0; j < PTILE / TB; ++j) {
     if (BM != 2) koutT[pad + threadIdx.x] = 0;
     if (!NOPOS) pout[pad + threadIdx.x] = 0;
@@ -731,10 +603,9 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
     KT key[PER];
     uint32_t ps[PER], dg[PER];
     bool act[PER];
-    if (ch.interleaved) {
+    uint32_t cursor[DPT];
 #pragma unroll
-      for (int q = 0; q < DPT; ++q) cursor[q] = ngb[q];
-    }
+    for (int q = 0; q < DPT; ++q) cursor[q] = ngb[q];
     if (FROM_SEQ) {
       stage_pack(nchars, S.st);
     } else {
@@ -768,21 +639,21 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
         dg[c] = act[c] ? digit_of_h(mix64((uint64_t)key[c]), g, D) : 0;
       }
     }
-#ifndef KMHG_BALLOT_RANK
-    // Stable ranks from the count atomics themselves: the lanes of one LDS instruction that hit
-    // the same counter are served in lane order (CDNA4; tools/lds_order.hip checks it, and the
-    // bucket kernels check every bucket's stream order), and a wave's instructions run in
-    // program order, so the returned running count is the element's rank among the wave's
-    // elements of its digit in (c, lane) = input order.
-    // (the rank rides in the digit's register, bits 16+: digit < 2^16, rank < PTILE)
+    if (!BALLOT) {
+      // Stable ranks from the count atomics themselves: the lanes of one LDS instruction that
+      // hit the same counter are served in lane order (CDNA4; kmhg_check_lds_lane_order checks
+      // it on the device before the first build), and a wave's instructions run in program
+      // order, so the returned running count is the element's rank among the wave's elements
+      // of its digit in (c, lane) = input order.
+      // (the rank rides in the digit's register, bits 16+: digit < 2^16, rank < PTILE)
 #pragma unroll
-    for (int c = 0; c < PER; ++c)
-      if (act[c]) dg[c] |= atomicAdd(&S.wc[wave][dg[c]], 1u) << 16;
-#else
+      for (int c = 0; c < PER; ++c)
+        if (act[c]) dg[c] |= atomicAdd(&S.wc[wave][dg[c]], 1u) << 16;
+    } else {
 #pragma unroll
-    for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
-      if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
-#endif
+      for (int c = 0; c < PER; ++c)          // counts only: order-free LDS atomics
+        if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
+    }
     __syncthreads();
     // tile-local digit starts: thread t owns digits [DPT t, DPT t + DPT)
     uint32_t dsum[DPT];
@@ -806,7 +677,6 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       if (d < R) {
         S.tstart[d] = run;
         S.gbase[d] = cursor[q];
-        cursor[q] += dsum[q];
         uint32_t cur = run;
 #pragma unroll
         for (int w = 0; w < NWV; ++w) {
@@ -818,37 +688,37 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       }
     }
     __syncthreads();
-#ifndef KMHG_BALLOT_RANK
+    if (!BALLOT) {
 #pragma unroll
-    for (int c = 0; c < PER; ++c) {
-      if (act[c]) {
-        const uint32_t d = dg[c] & 0xFFFFu;
-        const uint32_t ld = S.wc[wave][d] + (dg[c] >> 16);
-        if (BM != 2) S.skey[ld] = key[c];      // the last bucket-id pass writes positions only
-        S.spos[ld] = ps[c];
-        S.sdst[ld] = S.gbase[d] + (ld - S.tstart[d]);
+      for (int c = 0; c < PER; ++c) {
+        if (act[c]) {
+          const uint32_t d = dg[c] & 0xFFFFu;
+          const uint32_t ld = S.wc[wave][d] + (dg[c] >> 16);
+          if (BM != 2) S.skey[ld] = key[c];      // the last bucket-id pass writes positions only
+          S.spos[ld] = ps[c];
+          S.sdst[ld] = S.gbase[d] + (ld - S.tstart[d]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
+        const uint64_t grp = match_bits(dg[c], D.nbits, act[c]);
+        const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
+        uint32_t cur = 0;
+        if (act[c] && leader == lane) {
+          cur = S.wc[wave][dg[c]];
+          S.wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
+        }
+        cur = __shfl(cur, leader);
+        wave_sync();
+        if (act[c]) {
+          const uint32_t ld = cur + (uint32_t)__popcll(grp & lanemask_lt());
+          if (BM != 2) S.skey[ld] = key[c];
+          S.spos[ld] = ps[c];
+          S.sdst[ld] = S.gbase[dg[c]] + (ld - S.tstart[dg[c]]);
+        }
       }
     }
-#else
-#pragma unroll
-    for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
-      const uint64_t grp = match_bits(dg[c], D.nbits, act[c]);
-      const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
-      uint32_t cur = 0;
-      if (act[c] && leader == lane) {
-        cur = S.wc[wave][dg[c]];
-        S.wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
-      }
-      cur = __shfl(cur, leader);
-      wave_sync();
-      if (act[c]) {
-        const uint32_t ld = cur + (uint32_t)__popcll(grp & lanemask_lt());
-        if (BM != 2) S.skey[ld] = key[c];      // the last bucket-id pass writes positions only
-        S.spos[ld] = ps[c];
-        S.sdst[ld] = S.gbase[dg[c]] + (ld - S.tstart[dg[c]]);
-      }
-    }
-#endif
     __syncthreads();
     // a static count of store instructions per lane (masked, fully unrolled), so the wait for
     // the next tile's prefetched loads at the loop top is vmcnt(#stores), not vmcnt(0): the
@@ -861,6 +731,224 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, int 
       if (BM != 2) koutT[dst] = S.skey[i];
       if (!NOPOS) pout[dst] = S.spos[i];
     }
+  }
+}
+
+// ---------------------------------------------------------------- V_scatter_wc (write-combined)
+// The same stable pass for key streams beyond the caches, with every output line written whole.
+// Measured (tools/scatter_pattern.hip, profiles/rd4a_scatter_pattern.txt): moving 100 M 12-B
+// elements in the radix-313 digit runs of a 2048-element tile (6.5 elements per run) takes
+// 1.15 ms; the same bytes in whole 128-B lines 0.46 ms -- the scatter passes at config 3 (1.0 and
+// 0.92 ms) were bound by their write pattern, not by their work.  Runs aligned to 64 B still
+// cost 1.3x (keys) / 1.25x (positions) of whole lines.
+// So each workgroup owns a contiguous CHUNK of tiles (one workgroup per CU: the output range of
+// a digit over the chunk is contiguous, its start from the scanned [digit][tile] histogram at
+// the chunk's first tile), and the tail of every digit's output that does not fill a 128-B line
+// (< 16 keys, < 32 positions) waits in LDS (PK / PP) until a later tile completes the line.  The
+// digit's owner thread (thread d owns digit d; its cursor and pending starts live in its
+// registers) writes the waiting elements of a line that completes, the tile's write-out the
+// rest, in the same tile: the line is whole in L2 before it is written back.  Only the first and
+// last line of a digit's range in a chunk are ever partial.
+constexpr int WC_NW = 8;                        // waves per workgroup (512 threads)
+constexpr int WC_TB = WC_NW * 64;
+constexpr uint32_t WC_KL = 16;                  // keys per 128-B line
+constexpr uint32_t WC_PL = 32;                  // positions per 128-B line
+struct WcLDS {
+  static constexpr uint32_t MAXR = V2_MAXR_IL;
+  uint32_t wc[WC_NW][MAXR];    // per-wave digit counts -> per-wave tile-local cursors
+  uint32_t tstart[MAXR];       // tile-local start of each digit
+  uint32_t ocur[MAXR];         // global index of the digit's first element of this tile
+  uint32_t nk0[MAXR];          // keys at global index >= nk0 wait in PK after this tile
+  uint32_t np0[MAXR];          // ... positions >= np0 in PP
+  uint64_t skey[PTILE];
+  uint32_t spos[PTILE];
+  uint16_t sdig[PTILE];
+  __attribute__((aligned(16))) uint64_t PK[MAXR][WC_KL];
+  __attribute__((aligned(16))) uint32_t PP[MAXR][WC_PL];
+  PStage st;
+};
+static_assert(V2_MAXR_IL <= WC_TB, "one digit per thread");
+
+// elements [0, n) of a pending row to out[g0 ..): 16-B stores where g0 allows
+template <class T>
+__device__ __forceinline__ void wc_flush(T* __restrict__ out, uint64_t g0, const T* row, uint32_t n) {
+  constexpr uint32_t V = 16 / sizeof(T);        // elements per 16-B store
+  uint32_t j = 0;
+  if (g0 % V == 0) {
+    for (; j + V <= n; j += V)
+      *reinterpret_cast<uint4*>(out + g0 + j) = *reinterpret_cast<const uint4*>(row + j);
+  }
+  for (; j < n; ++j) out[g0 + j] = row[j];
+}
+
+template <bool FROM_SEQ, bool BALLOT>
+__global__ void __launch_bounds__(WC_TB)
+k_v2_scatter_wc(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
+                const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
+                const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
+                const uint32_t* __restrict__ hist, uint32_t ntiles,
+                uint64_t* __restrict__ kout, uint32_t* __restrict__ pout) {
+  constexpr int PER = PTILE / WC_TB;            // elements per lane
+  __shared__ WcLDS S;
+  __shared__ uint64_t sh[WC_NW];
+  const uint32_t R = D.R;
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const uint32_t wbase = (uint32_t)wave * (PTILE / WC_NW);
+  const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
+  // chunk of consecutive tiles; neighbouring chunks on one XCD
+  const uint32_t G = gridDim.x;
+  const uint32_t chunk = xcd_remap(blockIdx.x, G);
+  const uint32_t m = (ntiles + G - 1) / G;
+  const uint32_t t_begin = min(chunk * m, ntiles), t_end = min(t_begin + m, ntiles);
+  if (t_begin >= t_end) return;
+  const uint32_t n_iter = t_end - t_begin;
+  // the owner thread's digit state (registers)
+  const uint32_t d_own = threadIdx.x;
+  uint32_t gcur = 0, pk0 = 0, pp0 = 0;
+  if (d_own < R) gcur = pk0 = pp0 = hist[(size_t)d_own * ntiles + t_begin];
+  uint64_t nkey[PER];
+  uint32_t npos[PER];
+  StageRegs<PSTAGE_W16> nchars;
+  auto prefetch = [&](uint32_t tv) {
+    const uint64_t t0 = (uint64_t)tv * PTILE;
+    if (FROM_SEQ) {
+      if (threadIdx.x < BLOCK) stage_load<PSTAGE_W16, true>(nchars, seq, L, (int64_t)t0 - HALO, true);
+    } else {
+#pragma unroll
+      for (int cc = 0; cc < PER; ++cc) {       // e < ntiles * PTILE <= n_max + pad: in bounds
+        const uint64_t e = t0 + wbase + (uint32_t)cc * 64 + lane;
+        nkey[cc] = kin[e];
+        npos[cc] = pin[e];
+      }
+    }
+  };
+  prefetch(t_begin);
+  for (uint32_t it = 0; it < n_iter; ++it) {
+    const uint32_t tile = t_begin + it;
+    const uint64_t tile0 = (uint64_t)tile * PTILE;
+    uint64_t key[PER];
+    uint32_t ps[PER], dg[PER];
+    bool act[PER];
+    if (FROM_SEQ) {
+      if (threadIdx.x < BLOCK) stage_pack(nchars, S.st);
+    } else {
+#pragma unroll
+      for (int cc = 0; cc < PER; ++cc) {
+        key[cc] = nkey[cc];
+        ps[cc] = npos[cc];
+      }
+    }
+    if (it + 1 < n_iter) prefetch(tile + 1);
+    for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
+    __syncthreads();                       // stage packed; previous tile's write-out done
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const uint32_t w = wbase + (uint32_t)c * 64 + lane;     // element index inside the tile
+      const uint64_t e = tile0 + w;
+      if (FROM_SEQ) {
+        uint64_t kk = 0;
+        act[c] = e < n && window_key(S.st, HALO + (int)w, (int64_t)e, L, k, kk);
+        ps[c] = (uint32_t)(e + 1);
+        const uint32_t bl = bucket_local(mix64(kk), g);
+        act[c] = act[c] && bl < g.nb;                        // a part build keeps its buckets
+        key[c] = kk;
+        dg[c] = act[c] ? digit_of_b(bl, D) : 0;
+      } else {
+        act[c] = e < n;
+        dg[c] = act[c] ? digit_of_h(mix64(key[c]), g, D) : 0;
+      }
+    }
+    if (!BALLOT) {     // stable ranks from the count atomics' lane-ordered returns (V_scatter)
+#pragma unroll
+      for (int c = 0; c < PER; ++c)
+        if (act[c]) dg[c] |= atomicAdd(&S.wc[wave][dg[c]], 1u) << 16;
+    } else {
+#pragma unroll
+      for (int c = 0; c < PER; ++c)
+        if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
+    }
+    __syncthreads();
+    // digit phase: thread d owns digit d
+    uint32_t nd = 0;
+    if (d_own < R) {
+#pragma unroll
+      for (int w = 0; w < WC_NW; ++w) nd += S.wc[w][d_own];
+    }
+    uint64_t tile_n;
+    const uint32_t ts = (uint32_t)block_excl_scan_n<WC_NW>(nd, sh, tile_n);
+    if (d_own < R) {
+      S.tstart[d_own] = ts;
+      uint32_t cur = ts;
+#pragma unroll
+      for (int w = 0; w < WC_NW; ++w) {
+        const uint32_t t = S.wc[w][d_own];
+        S.wc[w][d_own] = cur;
+        cur += t;
+      }
+      const uint32_t end = gcur + nd;
+      const uint32_t nk = max(end & ~(WC_KL - 1), pk0), np = max(end & ~(WC_PL - 1), pp0);
+      // a line completes: its waiting elements go out now, the new ones in the write-out
+      if (nk > pk0) wc_flush(kout, pk0, S.PK[d_own], gcur - pk0);
+      if (np > pp0) wc_flush(pout, pp0, S.PP[d_own], gcur - pp0);
+      S.ocur[d_own] = gcur;
+      S.nk0[d_own] = nk;
+      S.np0[d_own] = np;
+      gcur = end;
+      pk0 = nk;
+      pp0 = np;
+    }
+    __syncthreads();                       // bases ready; old waiting elements read
+    if (!BALLOT) {
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        if (act[c]) {
+          const uint32_t d = dg[c] & 0xFFFFu;
+          const uint32_t ld = S.wc[wave][d] + (dg[c] >> 16);
+          S.skey[ld] = key[c];
+          S.spos[ld] = ps[c];
+          S.sdig[ld] = (uint16_t)d;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
+        const uint64_t grp = match_bits(dg[c], D.nbits, act[c]);
+        const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
+        uint32_t cur = 0;
+        if (act[c] && leader == lane) {
+          cur = S.wc[wave][dg[c]];
+          S.wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
+        }
+        cur = __shfl(cur, leader);
+        wave_sync();
+        if (act[c]) {
+          const uint32_t ld = cur + (uint32_t)__popcll(grp & lanemask_lt());
+          S.skey[ld] = key[c];
+          S.spos[ld] = ps[c];
+          S.sdig[ld] = (uint16_t)dg[c];
+        }
+      }
+    }
+    __syncthreads();
+    // write-out, run by run: elements below the digit's waiting start go to HBM, the rest wait
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t i = (uint32_t)(j * WC_TB) + threadIdx.x;
+      if (i < (uint32_t)tile_n) {
+        const uint32_t d = S.sdig[i];
+        const uint32_t gi = S.ocur[d] + (i - S.tstart[d]);
+        const uint32_t nk = S.nk0[d], np = S.np0[d];
+        if (gi < nk) kout[gi] = S.skey[i];
+        else S.PK[d][gi - nk] = S.skey[i];
+        if (gi < np) pout[gi] = S.spos[i];
+        else S.PP[d][gi - np] = S.spos[i];
+      }
+    }
+  }
+  __syncthreads();                         // the last tile's waiting elements are in LDS
+  if (d_own < R) {                         // the chunk's last, partial lines
+    wc_flush(kout, pk0, S.PK[d_own], gcur - pk0);
+    wc_flush(pout, pp0, S.PP[d_own], gcur - pp0);
   }
 }
 
@@ -952,218 +1040,31 @@ k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ 
 // an LDS table overflow, which rebuilds the index with the global-atomic build (finish_build).
 __device__ __forceinline__ bool stream_out_of_order(const uint32_t* __restrict__ pos, uint32_t i,
                                                     uint32_t s0, uint32_t s1, uint32_t p) {
-#ifdef KMHG_NO_ORDER_CHECK                   // A/B variant builds only: the check's cost
-  return false;
-#else
   return i > s0 && i < s1 && pos[i - 1] >= p;
-#endif
-}
-
-// ---------------------------------------------------------------- V_bucket (wave per bucket)
-// One LDS round trip per probe: the CAS itself says whether the slot was free (inserted), held
-// this key (found) or another key (move on).
-__device__ __forceinline__ int lds_insert(WaveTable& W, uint64_t key) {
-  if (key == EMPTY_KEY) return (int)V2_CAPB;
-  uint32_t j = local_home(mix64(key), V2_CAPB);
-  for (uint32_t n = 0; n < V2_CAPB; ++n) {
-    const uint64_t prev = atomicCAS((unsigned long long*)&W.key[j],
-                                    (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-    if (prev == EMPTY_KEY || prev == key) return (int)j;
-    if (++j == V2_CAPB) j = 0;
-  }
-  return -1;   // sub-table full: the host falls back to the global-atomic build
-}
-
-__device__ __forceinline__ int lds_find(const WaveTable& W, uint64_t key) {
-  if (key == EMPTY_KEY) return (int)V2_CAPB;
-  uint32_t j = local_home(mix64(key), V2_CAPB);
-  for (uint32_t n = 0; n < V2_CAPB; ++n) {
-    if (W.key[j] == key) return (int)j;
-    if (++j == V2_CAPB) j = 0;
-  }
-  return -1;
-}
-
-__global__ void __launch_bounds__(BLOCK)
-k_v2_bucket(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
-            const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
-            int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
-            BuildMeta* __restrict__ meta, int remap) {
-  __shared__ WaveTable wt[4];
-  constexpr int PER = 2 * V2_BW / 64;             // elements per lane per batch (2x mean)
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  WaveTable& W = wt[wave];
-  // buckets are independent: no ordering, no ticket (one shared counter would serialise
-  // ~88 grabs/us chip-wide -- MI355X_MICROARCH.md "dequeue")
-  const uint32_t b = (remap ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x) * 4 + wave;
-  if (b >= g.nb) return;
-  STAMP(b, 0);
-  const uint32_t s0 = start[b], s1 = start[b + 1];
-  const bool one_batch = s1 - s0 <= 64 * PER;     // typical bucket: everything stays in VGPRs
-  uint64_t key[PER];
-  uint32_t ps[PER];
-  int slot[PER];
-  bool in[PER];
-  // the first batch's loads are in flight while the sub-table is initialised
-  bool ovf = false;
-#pragma unroll
-  for (int c = 0; c < PER; ++c) {
-    const uint32_t i = s0 + 64 * c + lane;
-    in[c] = i < s1;
-    key[c] = in[c] ? keys[i] : 0;
-    ps[c] = in[c] ? pos[i] : 0;
-    ovf |= stream_out_of_order(pos, i, s0, s1, ps[c]);
-  }
-  for (uint32_t j = lane; j <= V2_CAPB; j += 64) {
-    W.key[j] = EMPTY_KEY;
-    W.cc[j] = make_uint2(0u, 0u);
-  }
-  wave_sync();
-  STAMP(b, 1);
-  // pass A: distinct keys + counts
-  for (uint32_t i0 = s0; i0 < s1; i0 += 64 * PER) {
-    if (i0 != s0) {
-#pragma unroll
-      for (int c = 0; c < PER; ++c) {
-        const uint32_t i = i0 + 64 * c + lane;
-        in[c] = i < s1;
-        key[c] = in[c] ? keys[i] : 0;
-        ps[c] = in[c] ? pos[i] : 0;
-        ovf |= stream_out_of_order(pos, i, s0, s1, ps[c]);
-      }
-    }
-    STAMP(b, 2);
-#pragma unroll
-    for (int c = 0; c < PER; ++c) {
-      slot[c] = -1;
-      if (in[c]) {
-        slot[c] = lds_insert(W, key[c]);
-        if (slot[c] < 0) ovf = true;
-        else atomicAdd(&W.cc[slot[c]].x, 1u);
-      }
-    }
-  }
-  wave_sync();
-  STAMP(b, 3);
-  if (__ballot(ovf)) {
-    if (lane == 0) atomicOr(&meta->overflow, 1u);
-    return;
-  }
-  // exclusive scan of the counts over the bucket's slots; lane owns SPL contiguous slots
-  constexpr uint32_t SPL = (V2_CAPB + 1 + 63) / 64;
-  const uint32_t j0 = lane * SPL;
-  const uint32_t j1 = min(j0 + SPL, V2_CAPB + 1);
-  uint32_t cs = 0, occ = 0, mx = 0;
-  uint64_t pairs = 0;
-  for (uint32_t j = j0; j < j1; ++j) {
-    const uint32_t c = W.cc[j].x;
-    cs += c;
-    occ += c ? 1u : 0u;
-    mx = max(mx, c);
-    pairs += (uint64_t)c * (c - (c ? 1u : 0u)) / 2;
-  }
-  const uint64_t incl = wave_incl_scan(cs);
-  uint32_t off_run = s0 + (uint32_t)(incl - cs);
-  for (uint32_t j = j0; j < j1; ++j) {
-    W.cc[j].y = off_run;
-    off_run += W.cc[j].x;
-  }
-  for (int d = 32; d >= 1; d >>= 1) {
-    pairs += __shfl_xor(pairs, d);
-    occ += __shfl_xor(occ, d);
-    mx = max(mx, (uint32_t)__shfl_xor(mx, d));
-  }
-  if (lane == 0) {
-    BucketStats st;
-    st.n_kmers = occ;
-    st.max_count = mx;
-    st.n_pairs = pairs;
-    bstats[b] = st;
-  }
-  wave_sync();
-  STAMP(b, 4);
-  // pass B: positions in stream (= position) order.  Repeated keys are ranked by ballots in
-  // lane (= position) order; afterwards cc.y = end for them and = the position for keys seen
-  // once, which is exactly the slot's aux word.
-  for (uint32_t i0 = s0; i0 < s1; i0 += 64 * PER) {
-    if (!one_batch) {
-#pragma unroll
-      for (int c = 0; c < PER; ++c) {
-        const uint32_t i = i0 + 64 * c + lane;
-        key[c] = i < s1 ? keys[i] : 0;
-        ps[c] = i < s1 ? pos[i] : 0;
-      }
-#pragma unroll
-      for (int c = 0; c < PER; ++c) {
-        const uint32_t i = i0 + 64 * c + lane;
-        slot[c] = i < s1 ? lds_find(W, key[c]) : -1;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < PER; ++c) {
-      const uint32_t i = i0 + 64 * c + lane;
-      const bool act = i < s1;
-      uint2 cc = make_uint2(0u, 0u);                // {cnt, cur}
-      if (act) cc = W.cc[slot[c]];
-      const bool multi = act && cc.x > 1;
-      // a key seen once keeps its position inline in its slot (Slot::aux); nothing is written
-      if (act && !multi) W.cc[slot[c]].y = ps[c];
-      if (__ballot(multi)) {
-        const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS, multi);
-        const int leader = multi ? __ffsll((unsigned long long)m) - 1 : lane;
-        uint32_t cur = cc.y;
-        if (multi && leader == lane) W.cc[slot[c]].y = cur + (uint32_t)__popcll(m);
-        cur = __shfl(cur, leader);
-        wave_sync();
-        if (multi) positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
-      }
-    }
-  }
-  wave_sync();
-  STAMP(b, 5);
-  // the bucket's sub-table, coalesced 16-B slots (empty ones included: no table init needed)
-  Slot* Tb = T + (uint64_t)b * V2_CAPB;
-  for (uint32_t j = lane; j < V2_CAPB; j += 64) {
-    const uint64_t kk = W.key[j];
-    const uint2 c = W.cc[j];
-    *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
-  }
-  if (lane == 0 && side_bucket(b, g)) {
-    const uint2 c = W.cc[V2_CAPB];
-    *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
-  }
-  STAMP(b, 6);
 }
 
 // ---------------------------------------------------------------- V_bucket_wg (group per bucket)
-// Large buckets (V2_BW_WG windows on average): ONE WORKGROUP per bucket with one shared LDS
-// sub-table of V2_CAPW slots.  Four times fewer buckets means one radix pass less from ~16 Mbp
-// (65K wave buckets) up to ~100 Mbp (102K group buckets at radix 320).  Keys seen once need no
-// ranking; buckets holding repeated keys rank them c by c, the waves taking turns.
-struct GroupTable {
-  uint64_t key[V2_CAPW + 1];
-  uint2 cc[V2_CAPW + 1];
-};
-// Compact form (default for position and count-only builds, 12 B per slot: 18.4 KB instead of
-// 24.6 KB, so 8 workgroups fit a CU's LDS instead of 6).  `val` is the count during pass A; the
-// counts pass moves every slot's count into the registers of the thread that owns the slot for
-// the write-out (slot q * TB + t), and `val` becomes the inline position of a key seen once or
-// the list cursor of a repeated key, tagged VAL_MULTI so that pass B can tell them apart.
+// ONE WORKGROUP per bucket (V2_BW_WG windows on average) with one shared LDS sub-table of
+// V2_CAPW slots, 12 B per slot (8-B key + one u32 `val`: 18.4 KB, so 8 workgroups fit a CU's
+// LDS).  `val` is the count during pass A; the counts pass moves every slot's count into the
+// registers of the thread that owns the slot for the write-out (slot q * TB + t), and `val`
+// becomes the inline position of a key seen once or the list cursor of a repeated key, tagged
+// VAL_MULTI so that pass B can tell them apart.
+// (Removed in round 4 after measurement, see DESIGN.md §5: one wave per 256-window bucket, a
+// 16-B-per-slot table, 8-wave workgroups, a one-atomic fingerprint insert, a sort-based bucket
+// build, and slot tags written by the build.)
 struct GroupTableC {
   uint64_t key[V2_CAPW + 1];
   uint32_t val[V2_CAPW + 1];
 };
 constexpr uint32_t VAL_MULTI = 0x80000000u;    // positions and list offsets are < 2^31
-__device__ __forceinline__ uint32_t* gt_count(GroupTable& W, int j) { return &W.cc[j].x; }
-__device__ __forceinline__ uint32_t* gt_count(GroupTableC& W, int j) { return &W.val[j]; }
 
 // Find-or-insert by CAS only.  (Measured, 10 Mbp: a plain read before the CAS 0.098 -> 0.186 ms;
 // the claiming occurrence skipping its count atomic 0.098 -> 0.136 ms; a per-lane state machine
 // over a lane's elements, one CAS per trip, 0.098 -> 0.204 ms.)
-template <class GT>
-__device__ __forceinline__ int lds_insert_g(GT& W, uint64_t key) {
+__device__ __forceinline__ int lds_insert_g(GroupTableC& W, uint64_t key, uint64_t h) {
   if (key == EMPTY_KEY) return (int)V2_CAPW;
-  uint32_t j = local_home(mix64(key), V2_CAPW);
+  uint32_t j = local_home(h, V2_CAPW);
   for (uint32_t n = 0; n < V2_CAPW; ++n) {
     const uint64_t prev = atomicCAS((unsigned long long*)&W.key[j],
                                     (unsigned long long)EMPTY_KEY, (unsigned long long)key);
@@ -1173,41 +1074,7 @@ __device__ __forceinline__ int lds_insert_g(GT& W, uint64_t key) {
   return -1;
 }
 
-// One-atomic insert (KMHG_BUCKET_FP=1): during pass A the {count, cur} word of a slot holds
-// {count, 32-bit fingerprint} and ONE 64-bit CAS claims a free slot with count 1 (the claimer then
-// stores the full key); an occurrence that meets its fingerprint adds 1 to the count; another
-// fingerprint moves on.  A key seen once -- almost every key of an i.i.d. sequence -- costs one
-// LDS atomic instead of a CAS and an add.  Two keys of one bucket with equal fingerprints would
-// share a count: the caller checks every element against its slot's full key afterwards and
-// redoes the bucket with lds_insert_g if any differs.
-__device__ __forceinline__ uint64_t fp_of(uint64_t key) {
-  return ((key * 0x9E3779B97F4A7C15ull) >> 32) << 32;     // independent of the bucket/home bits
-}
-__device__ __forceinline__ int lds_insert_fp(GroupTable& W, uint64_t key) {
-  unsigned long long* word = reinterpret_cast<unsigned long long*>(W.cc);
-  if (key == EMPTY_KEY) {
-    atomicAdd(&word[V2_CAPW], 1ull);
-    return (int)V2_CAPW;
-  }
-  const uint64_t fp = fp_of(key);
-  uint32_t j = local_home(mix64(key), V2_CAPW);
-  for (uint32_t n = 0; n < V2_CAPW; ++n) {
-    const uint64_t prev = atomicCAS(&word[j], 0ull, (unsigned long long)(fp | 1ull));
-    if (prev == 0) {
-      W.key[j] = key;
-      return (int)j;
-    }
-    if ((prev & 0xFFFFFFFF00000000ull) == fp) {
-      atomicAdd(&word[j], 1ull);
-      return (int)j;
-    }
-    if (++j == V2_CAPW) j = 0;
-  }
-  return -1;
-}
-
-template <class GT>
-__device__ __forceinline__ int lds_find_g(const GT& W, uint64_t key) {
+__device__ __forceinline__ int lds_find_g(const GroupTableC& W, uint64_t key) {
   if (key == EMPTY_KEY) return (int)V2_CAPW;
   uint32_t j = local_home(mix64(key), V2_CAPW);
   for (uint32_t n = 0; n < V2_CAPW; ++n) {
@@ -1217,37 +1084,35 @@ __device__ __forceinline__ int lds_find_g(const GT& W, uint64_t key) {
   return -1;
 }
 
-// The CAS build of one group bucket (the body of V_bucket_wg; also the fallback of V_bucket_sort
-// for buckets it does not take).  W, sh, red are the caller's LDS.
 // COUNT_ONLY (occurrence counts of a key stream, kmhg_sh.hip's read counting): pass B -- the
 // positions -- is skipped; slots get {key, count, unspecified aux}.
 // CK (bucket-id streams): the stream holds positions only; each window's key is cut from the
 // sequence's code words (`code`, 16 chars per u32) at its position -- three loads per window
 // from a 0.25 B/window array, against 8 B of key per window carried through every radix pass.
+// BALLOT: repeated keys' windows ranked by ballots instead of the cursor atomic's lane order.
+// Every key must hash to this bucket: a stream entry that does not (an unstable pass moving
+// another bucket's window in) is reported like an LDS overflow.
 struct Words3 {                                // three consecutive code words, 4-B aligned
   uint32_t a, b, c;
 };
-template <bool COUNT_ONLY = false, int TB = BLOCK, bool CK = false, class GT = GroupTable>
-__device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*red)[TB / 64],
-                                              const uint64_t* __restrict__ keys,
-                                              const uint32_t* __restrict__ pos,
-                                              const uint32_t* __restrict__ start, Geom g,
-                                              Slot* __restrict__ T,
-                                              int32_t* __restrict__ positions,
-                                              BucketStats* __restrict__ bstats,
-                                              BuildMeta* __restrict__ meta, const uint32_t b,
-                                              uint8_t* __restrict__ TG = nullptr,
-                                              uint32_t* __restrict__ mbits = nullptr,
-                                              int fp_insert = 0,
-                                              const uint32_t* __restrict__ code = nullptr,
-                                              int k = 0, uint32_t* edge = nullptr) {
+template <bool COUNT_ONLY, bool CK, bool BALLOT>
+__global__ void __launch_bounds__(BLOCK, BALLOT ? 6 : 2048 / BLOCK)   // 8 workgroups per CU (LDS)
+k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
+               const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
+               int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
+               BuildMeta* __restrict__ meta, const uint32_t* __restrict__ code, int k) {
   static_assert(!(CK && COUNT_ONLY), "code-word keys belong to position builds");
-  constexpr bool C12 = std::is_same<GT, GroupTableC>::value;
-  static_assert(V2_CAPW % TB == 0, "the side slot V2_CAPW is slot q = V2_CAPW / TB of thread 0");
+  static_assert(V2_CAPW % BLOCK == 0, "the side slot V2_CAPW is slot q = V2_CAPW / TB of thread 0");
+  constexpr int TB = BLOCK;
   constexpr int NW = TB / 64;                         // waves of the workgroup
-  // elements per thread per batch: 2x the mean (C12 + code words: 1.5x, for the VGPR budget of
-  // 8 waves / SIMD; a larger bucket takes more batches)
-  constexpr int PER = (C12 && CK ? 3 : 4) * V2_BW_WG / 2 / TB;
+  __shared__ GroupTableC W;
+  __shared__ uint64_t sh[2 * NW];
+  __shared__ uint32_t red[2][NW];
+  __shared__ __attribute__((aligned(16))) uint32_t edge[8 * NW + 1];   // stream-order check
+  const uint32_t b = blockIdx.x;
+  // elements per thread per batch: 2x the mean (code words: 1.5x, for the VGPR budget of
+  // 8 waves / SIMD); a larger bucket takes more batches
+  constexpr int PER = (CK ? 3 : 4) * V2_BW_WG / 2 / TB;
   constexpr uint32_t BATCH = TB * PER;
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const uint32_t s0 = start[b], s1 = start[b + 1];
@@ -1268,7 +1133,7 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
       for (int c = 0; c < PER; ++c) {
         const uint32_t i = elem(i0, c);
         ps[c] = i < s1 ? pos[i] : 1u;               // 1-based window start
-        if (!one_batch || !edge) disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
+        if (!one_batch) disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
       }
 #pragma unroll
       for (int c = 0; c < PER; ++c) {       // one 12-B load per window (global_load_dwordx3)
@@ -1284,8 +1149,7 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
       const uint32_t i = elem(i0, c);
       key[c] = i < s1 ? keys[i] : 0;
       ps[c] = (!COUNT_ONLY && i < s1) ? pos[i] : 0;
-      if (!COUNT_ONLY && (!one_batch || !edge))
-        disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
+      if (!COUNT_ONLY && !one_batch) disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
     }
   };
   auto cut = [&](uint32_t i0) {
@@ -1299,69 +1163,38 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
   load(s0);                                           // in flight while the table is cleared
   for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += TB) {
     W.key[j] = EMPTY_KEY;
-    if constexpr (C12) W.val[j] = 0u;
-    else W.cc[j] = make_uint2(0u, 0u);
+    W.val[j] = 0u;
   }
   __syncthreads();
   cut(s0);
   STAMP_WG(b, 1);
   STAMP_WG_DRAIN(b, 6);
-  // pass A: distinct keys + counts (CAS on a table shared by the four waves).  (Measured:
-  // skipping the count atomic for a key's claiming occurrence ran 35 % slower, 141 vs 105 us.)
-  bool done = false;
-  if constexpr (!C12) if (fp_insert && one_batch) {   // one atomic per key seen once (lds_insert_fp)
-#pragma unroll
-    for (int c = 0; c < PER; ++c) {
-      slot[c] = -1;
-      if (elem(s0, c) < s1) {
-        slot[c] = lds_insert_fp(W, key[c]);
-        if (slot[c] < 0) ovf = true;
-      }
-    }
-    __syncthreads();                         // the claimers' key stores
-    bool bad = ovf || fp_insert == 2;        // 2: tests force the collision path
-#pragma unroll
-    for (int c = 0; c < PER; ++c)
-      if (slot[c] >= 0 && slot[c] < (int)V2_CAPW && W.key[slot[c]] != key[c]) bad = true;
-    if (!__syncthreads_or(bad)) {
-#pragma unroll
-      for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += TB) W.cc[j].y = 0u;   // fingerprints out
-      done = true;
-    } else {                                 // a fingerprint collision: redo with the CAS build
-      for (uint32_t j = threadIdx.x; j <= V2_CAPW; j += TB) {
-        W.key[j] = EMPTY_KEY;
-        W.cc[j] = make_uint2(0u, 0u);
-      }
-      ovf = false;
-    }
-    __syncthreads();
-  }
-  // (Measured round 3, A/B in one run: letting the claiming occurrence skip the count add --
-  // counts pass adds 1 per occupied slot -- made the kernel 100 -> 142 us, as in round 2; and
-  // issuing the first CAS of all 8 elements of a lane back to back before resolving any,
-  // 98 -> 112 us.)
-  for (uint32_t i0 = s0; !done && i0 < s1; i0 += BATCH) {
+  // pass A: distinct keys + counts (CAS on a table shared by the four waves).  (Measured round
+  // 3, A/B in one run: letting the claiming occurrence skip the count add -- counts pass adds 1
+  // per occupied slot -- made the kernel 100 -> 142 us, as in round 2; and issuing the first
+  // CAS of all 8 elements of a lane back to back before resolving any, 98 -> 112 us.)
+  for (uint32_t i0 = s0; i0 < s1; i0 += BATCH) {
     if (i0 != s0) { load(i0); cut(i0); }
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       slot[c] = -1;
       if (elem(i0, c) < s1) {
-        slot[c] = lds_insert_g(W, key[c]);
+        // bucket membership (one multiply-high: CK keys are cut from the code words at the
+        // stream's positions, so this checks the positions too)
+        const uint64_t h = mix64(key[c]);
+        if (bucket_local(h, g) != b) disorder = true;
+        slot[c] = lds_insert_g(W, key[c], h);
         if (slot[c] < 0) ovf = true;
-        else atomicAdd(gt_count(W, slot[c]), 1u);
+        else atomicAdd(&W.val[slot[c]], 1u);
       }
     }
   }
-  // Stream order of a one-batch bucket (multi-batch buckets and callers without `edge` check it
-  // with a neighbour load per element in load()): element (c, wave, lane) follows (c, wave,
-  // lane - 1) -- a shuffle -- and lane 0 follows lane 63 of the wave before (of row c - 1 for
-  // wave 0), exchanged through `edge` and read after the barrier below.  Here, after pass A,
-  // the positions have long arrived, so the check makes no load wait earlier than it did.
-#ifdef KMHG_NO_ORDER_CHECK
-  const bool chk = false;
-#else
-  const bool chk = !COUNT_ONLY && one_batch && edge;
-#endif
+  // Stream order of a one-batch bucket (multi-batch buckets check it with a neighbour load per
+  // element in load()): element (c, wave, lane) follows (c, wave, lane - 1) -- a DPP shift --
+  // and lane 0 follows lane 63 of the wave before (of row c - 1 for wave 0), exchanged through
+  // `edge` and read after the barrier below.  Here, after pass A, the positions have long
+  // arrived, so the check makes no load wait earlier than it did.
+  const bool chk = !COUNT_ONLY && one_batch;
   // (edge: row `wave` holds that wave's lane-63 positions, 8 per row, written and read as
   // pairs -- a handful of LDS instructions per wave: single-lane LDS instructions cost nearly a
   // full one each in this LDS-bound kernel)
@@ -1413,7 +1246,7 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
 #pragma unroll
   for (uint32_t q = 0; q < SPT; ++q) {
     const uint32_t j = q * TB + threadIdx.x;
-    const uint32_t c = j <= V2_CAPW ? *gt_count(W, j) : 0u;
+    const uint32_t c = j <= V2_CAPW ? W.val[j] : 0u;
     cnt[q] = c;
     cs += c;
     occ += c ? 1u : 0u;
@@ -1443,11 +1276,7 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
 #pragma unroll
     for (uint32_t q = 0; q < SPT; ++q) {
       const uint32_t j = q * TB + threadIdx.x;
-      if constexpr (C12) {
-        if (j <= V2_CAPW) W.val[j] = cnt[q] > 1 ? (VAL_MULTI | off_run) : off_run;
-      } else {
-        if (j <= V2_CAPW) W.cc[j].y = off_run;
-      }
+      if (j <= V2_CAPW) W.val[j] = cnt[q] > 1 ? (VAL_MULTI | off_run) : off_run;
       off_run += cnt[q];
     }
     __syncthreads();
@@ -1466,7 +1295,7 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
     }
     bstats[b] = st;
   }
-  // pass B: keys seen once keep their position inline (cc.y); repeated keys are ranked in
+  // pass B: keys seen once keep their position inline (val); repeated keys are ranked in
   // position order, the waves taking turns so that wave w follows waves < w
   for (uint32_t i0 = s0; i0 < (COUNT_ONLY ? s0 : s1); i0 += BATCH) {
     if (!one_batch) {
@@ -1477,13 +1306,8 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
     }
     if (!has_multi) {                    // every key seen once: positions go inline
 #pragma unroll
-      for (int c = 0; c < PER; ++c) {
-        if constexpr (C12) {
-          if (elem(i0, c) < s1) W.val[slot[c]] = ps[c];
-        } else {
-          if (elem(i0, c) < s1) W.cc[slot[c]].y = ps[c];
-        }
-      }
+      for (int c = 0; c < PER; ++c)
+        if (elem(i0, c) < s1) W.val[slot[c]] = ps[c];
       continue;
     }
     for (int c = 0; c < PER; ++c) {
@@ -1491,46 +1315,21 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
       // waves take turns on this c: wave w ranks after waves < w have advanced the cursors
       for (int turn = 0; turn < NW; ++turn) {
         if (wave == turn) {
-          bool multi;
-          bool continue_turn = false;    // C12: ranked by the cursor atomic below
-          uint32_t cur;                  // a repeated key's list cursor (VAL_MULTI kept in C12)
-          if constexpr (C12) {
-            const uint32_t v = act ? W.val[slot[c]] : 0u;
-            multi = act && (v & VAL_MULTI);
-            if (act && !multi) W.val[slot[c]] = ps[c];
-            cur = v;
-          } else {
-            uint2 cc = make_uint2(0u, 0u);
-            if (act) cc = W.cc[slot[c]];
-            multi = act && cc.x > 1;
-            if (act && !multi) W.cc[slot[c]].y = ps[c];
-            cur = cc.y;
-          }
-          if constexpr (C12) {
-#ifndef KMHG_BALLOT_RANK
+          const uint32_t v = act ? W.val[slot[c]] : 0u;
+          const bool multi = act && (v & VAL_MULTI);
+          if (act && !multi) W.val[slot[c]] = ps[c];
+          if (!BALLOT) {
             // the cursor atomic's lane-ordered returns rank the wave's windows of one key
             if (multi) {
               const uint32_t at = atomicAdd(&W.val[slot[c]], 1u) & ~VAL_MULTI;
               positions[at] = (int32_t)ps[c];
-              if (mbits) atomicOr(&mbits[(ps[c] - 1) >> 5], 1u << ((ps[c] - 1) & 31));
             }
-            continue_turn = true;
-#endif
-          }
-          if (!continue_turn && __ballot(multi)) {
+          } else if (__ballot(multi)) {
             const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS_WG, multi);
             const int leader = multi ? __ffsll((unsigned long long)m) - 1 : lane;
-            if (multi && leader == lane) {
-              if constexpr (C12) W.val[slot[c]] = cur + (uint32_t)__popcll(m);
-              else W.cc[slot[c]].y = cur + (uint32_t)__popcll(m);
-            }
-            cur = __shfl(cur, leader);
-            if constexpr (C12) cur &= ~VAL_MULTI;
-            if (multi) {
-              positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
-              // the diagonal query path's bits of repeated keys' windows (ps: 1-based start)
-              if (mbits) atomicOr(&mbits[(ps[c] - 1) >> 5], 1u << ((ps[c] - 1) & 31));
-            }
+            if (multi && leader == lane) W.val[slot[c]] = v + (uint32_t)__popcll(m);
+            const uint32_t cur = (uint32_t)__shfl((int)v, leader) & ~VAL_MULTI;
+            if (multi) positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
           }
         }
         __syncthreads();
@@ -1539,337 +1338,22 @@ __device__ __forceinline__ void bucket_wg_cas(GT& W, uint64_t* sh, uint32_t (*re
   }
   __syncthreads();
   STAMP_WG(b, 4);
-  // the bucket's sub-table, coalesced 16-B slots (+ the query's slot tags, 1 B per slot)
+  // the bucket's sub-table, coalesced 16-B slots, counts from the registers of the slot's owner
   Slot* Tb = T + (uint64_t)b * V2_CAPW;
-  if constexpr (C12) {         // counts from the registers of the slot's owner (counts pass)
 #pragma unroll
-    for (uint32_t q = 0; q < SPT; ++q) {
-      const uint32_t j = q * TB + threadIdx.x;
-      if (j < V2_CAPW) {
-        const uint64_t kk = W.key[j];
-        const uint32_t aux = COUNT_ONLY ? 0u : (W.val[j] & ~VAL_MULTI);
-        *reinterpret_cast<uint4*>(&Tb[j]) =
-            make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), cnt[q], aux);
-      }
-    }
-  } else {
-    for (uint32_t j = threadIdx.x; j < V2_CAPW; j += TB) {
+  for (uint32_t q = 0; q < SPT; ++q) {
+    const uint32_t j = q * TB + threadIdx.x;
+    if (j < V2_CAPW) {
       const uint64_t kk = W.key[j];
-      const uint2 c = W.cc[j];
-      *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), c.x, c.y);
-    }
-  }
-  if (TG) {                    // 4 tags per lane, one 4-B store (byte stores cost 4x the issue)
-    static_assert(V2_CAPW % 4 == 0, "tag words");
-    uint32_t* tw = reinterpret_cast<uint32_t*>(TG + (uint64_t)b * V2_CAPW);
-    for (uint32_t w = threadIdx.x; w < V2_CAPW / 4; w += TB) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint64_t kk = W.key[4 * w + q];
-        v |= (uint32_t)(kk == EMPTY_KEY ? 0u : slot_tag(mix64(kk))) << (8 * q);
-      }
-      tw[w] = v;
+      const uint32_t aux = COUNT_ONLY ? 0u : (W.val[j] & ~VAL_MULTI);
+      *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), cnt[q], aux);
     }
   }
   if (threadIdx.x == 0 && side_bucket(b, g)) {
-    uint2 c;
-    if constexpr (C12)
-      c = make_uint2(cnt[V2_CAPW / TB], COUNT_ONLY ? 0u : (W.val[V2_CAPW] & ~VAL_MULTI));
-    else
-      c = W.cc[V2_CAPW];
+    const uint2 c = make_uint2(cnt[V2_CAPW / TB], COUNT_ONLY ? 0u : (W.val[V2_CAPW] & ~VAL_MULTI));
     *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
-    if (TG) TG[side_slot(g)] = 0;
   }
   STAMP_WG(b, 5);
-}
-
-// TB threads per workgroup: 256 (4 waves) or 512 (8 waves: the LDS table allows 6 workgroups
-// per CU, so 8-wave groups fill the CU's 32 wave slots where 4-wave groups stop at 24).
-// C12: the compact 12-B-per-slot LDS table (GroupTableC; not with the fingerprint insert).
-template <bool COUNT_ONLY, int TB = BLOCK, bool CK = false, bool C12 = false>
-__global__ void __launch_bounds__(TB, C12 ? 2048 / TB : 1)    // C12: 8 workgroups per CU (LDS)
-k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
-               const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
-               int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
-               BuildMeta* __restrict__ meta, uint8_t* __restrict__ TG,
-               uint32_t* __restrict__ mbits, int fp_insert, const uint32_t* __restrict__ code,
-               int k) {
-  using GT = typename std::conditional<C12, GroupTableC, GroupTable>::type;
-  __shared__ GT W;
-  __shared__ uint64_t sh[2 * (TB / 64)];
-  __shared__ uint32_t red[3][TB / 64];
-  __shared__ __attribute__((aligned(16))) uint32_t edge[8 * (TB / 64) + 1];   // stream-order check
-  bucket_wg_cas<COUNT_ONLY, TB, CK, GT>(W, sh, red, keys, pos, start, g, T, positions, bstats,
-                                        meta, blockIdx.x, TG, mbits, fp_insert, code, k, edge);
-}
-
-// ---------------------------------------------------------------- V_bucket_sort (group per bucket)
-// The same group bucket built without LDS atomics (the CAS build is bound by the LDS atomic
-// unit: one 64-bit CAS + one add per window).  The bucket's windows (<= V2_CAPW of them, in
-// position order) are stably sorted by sk = the top 16 bits of lo32(mix64(key)) with two 8-bit
-// passes of ballot ranks (the scatter passes' multi-split, per-wave digit counters), so:
-//   * equal keys become contiguous runs (a run = one distinct k-mer, its length = its count, its
-//     windows already in position order -> positions[s0 + sorted index] directly),
-//   * runs come in home order (home = (sk * capb) >> 16, non-decreasing in sk), and the linear-
-//     probing table is laid out directly: run q goes to p_q = max(home_q, p_{q-1} + 1), i.e.
-//     p_q = q + max(over, max_{q' <= q}(home_q' - q')) -- one block max-scan -- where `over`
-//     (the runs pushed past the end, which wrap into slots [0, over)) is max(0, D - capb + M).
-// Different keys with equal sk that interleave (needs an sk collision AND a repeated key, both
-// rare), the k = 32 key ~0, and buckets larger than V2_CAPW take the CAS build instead.
-constexpr uint32_t NS = V2_CAPW;            // windows a sorted bucket may hold
-constexpr int PS = NS / BLOCK;              // ... per thread
-struct SortLDS {
-  uint64_t ekey[NS];                        // windows in position order
-  uint32_t epos[NS];
-  uint16_t esk[NS];
-  uint16_t sidx[2][NS];                     // sort passes: window indices in sorted order
-  uint32_t cntw[4][256];                    // per-wave digit counters -> bases
-  uint16_t rs[NS + 1];                      // run starts (sorted index), rs[D] = n
-  uint8_t occ[V2_CAPW];                     // table slots taken by a run
-};
-union BucketLDS {
-  GroupTable W;
-  SortLDS S;
-};
-
-__device__ __forceinline__ int wave_max_i32(int v) {
-  for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d));
-  return v;
-}
-
-__global__ void __launch_bounds__(BLOCK)
-k_v2_bucket_sort(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
-                 const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
-                 int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
-                 BuildMeta* __restrict__ meta) {
-  __shared__ BucketLDS U;
-  __shared__ uint64_t sh[8];
-  __shared__ uint32_t red[3][4];
-  __shared__ int wmax[4];
-  const uint32_t b = blockIdx.x;
-  const uint32_t s0 = start[b], s1 = start[b + 1];
-  const uint32_t n = s1 - s0;
-  if (n > NS) {
-    bucket_wg_cas(U.W, sh, red, keys, pos, start, g, T, positions, bstats, meta, b);
-    return;
-  }
-  SortLDS& S = U.S;
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  STAMP_WG(b, 0);
-  constexpr uint32_t WSPAN = NS / 4;        // windows per wave, contiguous: e = wave*WSPAN + c*64 + lane
-  // ---- load (coalesced per wave), sort keys in registers and LDS
-  uint32_t skr[PS];
-  bool bad = false;
-#pragma unroll
-  for (int c = 0; c < PS; ++c) {
-    const uint32_t e = wave * WSPAN + (uint32_t)c * 64 + lane;
-    skr[c] = 0;
-    if (e < n) {
-      const uint64_t k = keys[s0 + e];
-      S.ekey[e] = k;
-      S.epos[e] = pos[s0 + e];
-      skr[c] = (uint32_t)mix64(k) >> 16;
-      S.esk[e] = (uint16_t)skr[c];
-      bad |= k == EMPTY_KEY;
-      // out of order: the CAS build below reports it (overflow -> global-atomic rebuild)
-      bad |= stream_out_of_order(pos, s0 + e, s0, s1, S.epos[e]);
-    }
-  }
-  for (uint32_t j = threadIdx.x; j < V2_CAPW / 4; j += BLOCK)
-    reinterpret_cast<uint32_t*>(S.occ)[j] = 0u;
-  if (__syncthreads_or(bad)) {
-    bucket_wg_cas(U.W, sh, red, keys, pos, start, g, T, positions, bstats, meta, b);
-    return;
-  }
-  STAMP_WG(b, 1);
-  // ---- two stable 8-bit passes; element order inside a pass = (wave, c, lane)
-#pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    for (uint32_t d = lane; d < 256; d += 64) S.cntw[wave][d] = 0u;
-    wave_sync();
-    uint32_t dg[PS], rk[PS], el[PS];
-    bool act[PS];
-#pragma unroll
-    for (int c = 0; c < PS; ++c) {
-      const uint32_t q = wave * WSPAN + (uint32_t)c * 64 + lane;
-      act[c] = q < n;
-      el[c] = pass == 0 ? q : (act[c] ? S.sidx[0][q] : 0u);
-      const uint32_t sk = pass == 0 ? skr[c] : (act[c] ? (uint32_t)S.esk[el[c]] : 0u);
-      dg[c] = pass == 0 ? (sk & 255u) : (sk >> 8);
-#ifndef KMHG_BALLOT_RANK
-      // stable rank from the lane-ordered count atomic (as V_scatter)
-      rk[c] = act[c] ? atomicAdd(&S.cntw[wave][dg[c]], 1u) : 0u;
-#else
-      const uint64_t grp = match_bits(dg[c], 8, act[c]);
-      const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
-      uint32_t cur = 0;
-      if (act[c] && leader == lane) {
-        cur = S.cntw[wave][dg[c]];
-        S.cntw[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
-      }
-      cur = __shfl(cur, leader);
-      wave_sync();
-      rk[c] = cur + (uint32_t)__popcll(grp & lanemask_lt());
-#endif
-    }
-    __syncthreads();
-    {   // digit bases: thread t owns digit t over the 4 waves
-      const uint32_t t = threadIdx.x;
-      const uint32_t c0 = S.cntw[0][t], c1 = S.cntw[1][t], c2 = S.cntw[2][t], c3 = S.cntw[3][t];
-      uint64_t tot;
-      const uint32_t base = (uint32_t)block_excl_scan(c0 + c1 + c2 + c3, sh, tot);
-      S.cntw[0][t] = base;
-      S.cntw[1][t] = base + c0;
-      S.cntw[2][t] = base + c0 + c1;
-      S.cntw[3][t] = base + c0 + c1 + c2;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < PS; ++c)
-      if (act[c]) S.sidx[pass][S.cntw[wave][dg[c]] + rk[c]] = (uint16_t)el[c];
-    __syncthreads();
-    STAMP_WG(b, 2 + pass);
-  }
-  // ---- runs: thread t takes sorted indices [t*PS, t*PS + PS)
-  const uint16_t* srt = S.sidx[1];
-  const uint32_t i0 = threadIdx.x * PS;
-  uint64_t kk[PS];
-  uint32_t pp[PS], sk[PS];
-  bool rst[PS];
-  uint64_t prevk = 0;
-  uint32_t prevsk = 0x10000u;
-  if (i0 > 0 && i0 < n) {
-    const uint32_t e = srt[i0 - 1];
-    prevk = S.ekey[e];
-    prevsk = S.esk[e];
-  }
-  bool il = false;                          // interleaved keys of equal sk
-  uint32_t nrun = 0;
-#pragma unroll
-  for (int j = 0; j < PS; ++j) {
-    const uint32_t i = i0 + j;
-    rst[j] = false;
-    if (i >= n) continue;
-    const uint32_t e = srt[i];
-    kk[j] = S.ekey[e];
-    pp[j] = S.epos[e];
-    sk[j] = S.esk[e];
-    rst[j] = i == 0 || kk[j] != prevk;
-    if (rst[j] && i > 0 && sk[j] == prevsk) {  // sk collision: is this key already a run?
-      for (int m = (int)i - 2; m >= 0; --m) {
-        const uint32_t em = srt[m];
-        if (S.esk[em] != sk[j]) break;
-        if (S.ekey[em] == kk[j]) { il = true; break; }
-      }
-    }
-    nrun += rst[j] ? 1u : 0u;
-    prevk = kk[j];
-    prevsk = sk[j];
-  }
-  if (__syncthreads_or(il)) {
-    bucket_wg_cas(U.W, sh, red, keys, pos, start, g, T, positions, bstats, meta, b);
-    return;
-  }
-  STAMP_WG(b, 4);
-  uint64_t D64;
-  uint32_t q = (uint32_t)block_excl_scan(nrun, sh, D64);   // run index of this thread's first run
-  const uint32_t D = (uint32_t)D64;
-  {
-    uint32_t qq = q;
-#pragma unroll
-    for (int j = 0; j < PS; ++j)
-      if (rst[j]) S.rs[qq++] = (uint16_t)(i0 + j);
-    if (threadIdx.x == 0) S.rs[D] = (uint16_t)n;
-  }
-  // prefix max of (home - q) over runs: thread-local running max, then across threads
-  int lmax = INT_MIN;
-  {
-    uint32_t qq = q;
-#pragma unroll
-    for (int j = 0; j < PS; ++j)
-      if (rst[j]) {
-        const int home = (int)((sk[j] * V2_CAPW) >> 16);
-        lmax = max(lmax, home - (int)qq);
-        ++qq;
-      }
-  }
-  // exclusive max over threads < t: wave inclusive max-scan + per-wave maxima in LDS
-  int incl = lmax;
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(incl, d);
-    if (lane >= d) incl = max(incl, y);
-  }
-  if (lane == 63) wmax[wave] = incl;
-  int excl = __shfl_up(incl, 1);
-  if (lane == 0) excl = INT_MIN;
-  __syncthreads();                          // also publishes S.rs
-  for (int w = 0; w < wave; ++w) excl = max(excl, wmax[w]);
-  const int M = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-  const int over = max(0, (int)D - (int)V2_CAPW + M);
-  const bool full = D >= V2_CAPW;           // no empty slot left: the host rebuilds with v1
-  // ---- table slots of this thread's runs, positions of repeated k-mers
-  Slot* Tb = T + (uint64_t)b * V2_CAPW;
-  uint32_t mx = 0;
-  uint64_t pairs = 0;
-  {
-    uint32_t qq = q;
-    int run_max = excl;
-    uint32_t cur_q = q - 1;                 // run of the element before this thread's first run start
-#pragma unroll
-    for (int j = 0; j < PS; ++j) {
-      const uint32_t i = i0 + j;
-      if (i >= n) continue;
-      if (rst[j]) {
-        cur_q = qq++;
-        const int home = (int)((sk[j] * V2_CAPW) >> 16);
-        run_max = max(run_max, home - (int)cur_q);
-        const uint32_t cnt = (uint32_t)S.rs[cur_q + 1] - i;
-        mx = max(mx, cnt);
-        pairs += (uint64_t)cnt * (cnt - 1) / 2;
-        if (!full) {
-          const int p = (int)cur_q + max(over, run_max);
-          const uint32_t slot = p < (int)V2_CAPW ? (uint32_t)p : (uint32_t)p - V2_CAPW;
-          S.occ[slot] = 1;
-          *reinterpret_cast<uint4*>(&Tb[slot]) =
-              make_uint4((uint32_t)kk[j], (uint32_t)(kk[j] >> 32), cnt,
-                         cnt == 1 ? pp[j] : s0 + i + cnt);
-        }
-      }
-      // repeated k-mer: every window writes its position at its sorted index
-      const uint32_t rq = rst[j] ? cur_q : (cur_q == 0xFFFFFFFFu ? 0u : cur_q);
-      const uint32_t cnt_here = (uint32_t)S.rs[rq + 1] - (uint32_t)S.rs[rq];
-      if (cnt_here > 1 && !full) positions[s0 + i] = (int32_t)pp[j];
-    }
-  }
-  // stats
-  for (int d = 32; d >= 1; d >>= 1) {
-    pairs += __shfl_xor(pairs, d);
-    mx = max(mx, (uint32_t)__shfl_xor(mx, d));
-  }
-  if (lane == 0) {
-    red[1][wave] = mx;
-    sh[4 + wave] = pairs;
-  }
-  __syncthreads();                          // S.occ complete
-  STAMP_WG(b, 5);
-  if (full) {
-    if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
-    return;
-  }
-  for (uint32_t j = threadIdx.x; j < V2_CAPW; j += BLOCK)
-    if (!S.occ[j])
-      *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-  if (threadIdx.x == 0) {
-    BucketStats st;
-    st.n_kmers = D;
-    st.max_count = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
-    st.n_pairs = sh[4] + sh[5] + sh[6] + sh[7];
-    bstats[b] = st;
-    if (side_bucket(b, g))   // no window of this bucket is key ~0
-      *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
-  }
-  STAMP_WG(b, 6);
 }
 
 // V_stats: reduce the per-bucket partials (grid-stride, one atomic per workgroup; meta was
@@ -1940,192 +1424,90 @@ static unsigned resident_blocks(const void* kernel, int threads = BLOCK) {
   return (unsigned)(cus > 0 ? cus : 256) * (unsigned)per;
 }
 
-
-// XCD-contiguous tile mapping (xcd_remap), on unless KMHG_XCD=0 (A/B switch for profiling)
-static int xcd_map() {
-  static int on = [] {
-    const char* e = std::getenv("KMHG_XCD");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on;
-}
-
-// the bucket kernel's writes are whole sub-tables: remapped only with KMHG_XCD_BUCKET=1
-static int xcd_map_bucket() {
-  static int on = [] {
-    const char* e = std::getenv("KMHG_XCD_BUCKET");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return on;
-}
-
 static inline unsigned grid_of(uint64_t n, unsigned per) {
   uint64_t g = (n + per - 1) / per;
   return (unsigned)(g ? g : 1);
 }
 
-// KMHG_SCATTER_WPC=n (A/B): at most n scatter workgroups per CU.  Fewer tiles in flight per XCD
-// means fewer partially written digit-run lines held dirty in its L2 (beyond the Infinity
-// Cache, config 3 writes 1.4-1.7x the algorithmic bytes), at the cost of latency hiding.
-static unsigned scatter_cap_of(const void* kernel) {
-  unsigned c = resident_blocks(kernel);
-  if (const char* e = std::getenv("KMHG_SCATTER_WPC")) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const unsigned want = (unsigned)std::max(1, std::atoi(e)) * (unsigned)std::max(cus, 1);
-    c = std::min(c, want);
-  }
-  return c;
-}
-static unsigned scatter_cap() {
-  static unsigned cap = scatter_cap_of((const void*)k_v2_scatter<true, false, false, 4>);
-  return cap;
-}
+// The lane order of same-address LDS atomics, checked once per device (kmhg_check_lds_lane_order
+// runs the same kernel for the tests): where it does not hold, every build takes the ballot-rank
+// kernels.  KMHG_TEST_BALLOT=1 (tests) forces them.
+bool ballot_ranks();
 
-// Tile schedule of the radix passes: interleaved (default) or chunked (KMHG_RADIX=chunked, kept
-// for A/B: measured slower, each workgroup's R open run heads per digit overflow the L2).
-Chunks make_chunks(uint32_t ntiles) {
-  static int chunked = [] {
-    const char* e = std::getenv("KMHG_RADIX");
-    return (e && std::string(e) == "chunked") ? 1 : 0;
-  }();
-  Chunks ch;
-  ch.ntiles = ntiles;
-  if (!chunked) {
-    ch.interleaved = 1;
-    ch.C = ntiles;
-    ch.tpc = 1;
-    return ch;
-  }
-  ch.interleaved = 0;
-  const uint32_t C0 = std::max(1u, std::min<uint32_t>(ntiles, scatter_cap()));
-  ch.tpc = (ntiles + C0 - 1) / C0;
-  ch.C = (ntiles + ch.tpc - 1) / ch.tpc;   // every chunk holds >= 1 tile
-  return ch;
-}
-// `cap`: the launched variant's resident workgroups (its own VGPR / LDS occupancy)
-static unsigned scatter_grid(const Chunks& ch, unsigned cap) {
-  return ch.interleaved ? std::min<unsigned>(ch.ntiles, cap) : ch.C;
-}
-
-// 8-wave scatter workgroups only with KMHG_SC8=1 (interleaved schedule, R <= V2_MAXR_IL):
-// measured neutral at config 2 (R = 99), -3 % on the read-counting passes, +10 % slower at
-// config 3 (R = 313), so the 4-wave kernel stays the default
-static bool scatter8(const Chunks& ch, const Digit& D) {
-  const char* e = std::getenv("KMHG_SC8");       // read per launch: the tests switch it
-  return e && e[0] == '1' && ch.interleaved && D.R <= V2_MAXR_IL;
-}
-static unsigned scatter8_grid(const Chunks& ch) {
-  static const unsigned cap = resident_blocks((const void*)k_v2_scatter<true, false, false, 8>, 512);
-  return std::min<unsigned>(ch.ntiles, cap);
-}
-#define KMHG_SCATTER_BM(FS, K0, NP, BM, ...)                                                 \
-  do {                                                                                      \
-    if (scatter8(ch, D))                                                                    \
-      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, 8, BM>), dim3(scatter8_grid(ch)),        \
-                         dim3(512), 0, s, __VA_ARGS__);                                     \
-    else {                                                                                  \
-      static const unsigned cap_ = scatter_cap_of((const void*)k_v2_scatter<FS, K0, NP, 4, BM>); \
-      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, 4, BM>), dim3(scatter_grid(ch, cap_)),   \
-                         dim3(BLOCK), 0, s, __VA_ARGS__);                                   \
-    }                                                                                       \
+#define KMHG_SCATTER_BM(FS, K0, NP, BM, ...)                                                  \
+  do {                                                                                       \
+    if (ballot_ranks()) {                                                                    \
+      static const unsigned cap_ = resident_blocks((const void*)k_v2_scatter<FS, K0, NP, BM, true>, \
+                                                   SC_NWV * 64);                             \
+      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, BM, true>), dim3(std::min(ntiles, cap_)),  \
+                         dim3(SC_NWV * 64), 0, s, __VA_ARGS__);                              \
+    } else {                                                                                 \
+      static const unsigned cap_ = resident_blocks((const void*)k_v2_scatter<FS, K0, NP, BM, false>, \
+                                                   SC_NWV * 64);                             \
+      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, BM, false>), dim3(std::min(ntiles, cap_)), \
+                         dim3(SC_NWV * 64), 0, s, __VA_ARGS__);                              \
+    }                                                                                        \
   } while (0)
 #define KMHG_SCATTER(FS, K0, NP, ...) KMHG_SCATTER_BM(FS, K0, NP, 0, __VA_ARGS__)
 
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
-                     uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
+                     uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                      BuildMeta* meta, hipStream_t s, uint32_t* code, uint16_t* nbit,
-                     uint32_t* uniq0, uint32_t* bids) {
-  const char* hp = std::getenv("KMHG_HIST0P");   // read per launch: the tests switch it
-  const int persist = (hp && hp[0] == '0') ? 0 : 1;
-  if (bids && !persist) {      // bucket-id builds, one workgroup per tile (KMHG_HIST0P=0, A/B)
-    hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
-                       xcd_map(), scan_status, n_status, meta, code, nbit, uniq0, bids);
-    return;
-  }
-  if (bids) {                  // bucket-id builds: the persistent kernel (interleaved schedule)
+                     uint32_t* bids) {
+  if (bids) {                  // bucket-id builds (keep the code words)
     static const unsigned cap_b = resident_blocks((const void*)k_v2_hist0p<true, true>);
-    hipLaunchKernelGGL((k_v2_hist0p<true, true>), dim3(std::min<unsigned>(ch.ntiles, cap_b)),
-                       dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status,
-                       n_status, meta, code, nbit, uniq0, bids);
-    return;
+    hipLaunchKernelGGL((k_v2_hist0p<true, true>), dim3(std::min<unsigned>(ntiles, cap_b)),
+                       dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ntiles, scan_status,
+                       n_status, meta, code, nbit, bids);
+  } else if (code && nbit) {
+    static const unsigned cap_c = resident_blocks((const void*)k_v2_hist0p<true, false>);
+    hipLaunchKernelGGL((k_v2_hist0p<true, false>), dim3(std::min<unsigned>(ntiles, cap_c)),
+                       dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ntiles, scan_status,
+                       n_status, meta, code, nbit, nullptr);
+  } else {
+    static const unsigned cap_n = resident_blocks((const void*)k_v2_hist0p<false, false>);
+    hipLaunchKernelGGL((k_v2_hist0p<false, false>), dim3(std::min<unsigned>(ntiles, cap_n)),
+                       dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ntiles, scan_status,
+                       n_status, meta, nullptr, nullptr, nullptr);
   }
-  if (ch.interleaved && persist) {
-    static const unsigned cap_c = resident_blocks((const void*)k_v2_hist0p<true>);
-    static const unsigned cap_n = resident_blocks((const void*)k_v2_hist0p<false>);
-    if (code && nbit)
-      hipLaunchKernelGGL(k_v2_hist0p<true>, dim3(std::min<unsigned>(ch.ntiles, cap_c)), dim3(BLOCK),
-                         0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status, n_status,
-                         meta, code, nbit, uniq0, nullptr);
-    else
-      hipLaunchKernelGGL(k_v2_hist0p<false>, dim3(std::min<unsigned>(ch.ntiles, cap_n)), dim3(BLOCK),
-                         0, s, seq, L, k, Nw, g, D, hist, ch, xcd_map(), scan_status, n_status,
-                         meta, nullptr, nullptr, nullptr, nullptr);
-    return;
-  }
-  hipLaunchKernelGGL(k_v2_hist0, dim3(ch.C), dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ch,
-                     xcd_map(), scan_status, n_status, meta, code, nbit, uniq0);
 }
 // Beyond 64 tiles of 2048 entries: the 32-per-thread look-back scan at any length.  Measured
 // (A/B in one run, `profiles/rd3n_ab_scan_*`): config 3's 15 M-entry histograms 89 -> 60 us per
 // scan (three launches of reduce-then-scan before), config 2's 0.5 M 7.7 -> 7.0 us.
-// KMHG_SCAN=8 (A/B): 8 entries per thread up to LB_SCAN_MAX_TILES tiles, reduce-then-scan beyond.
-static int scan_mode() {
-  const char* e = std::getenv("KMHG_SCAN");     // read per launch: A/B
-  return (e && e[0] == '8') ? 8 : 32;
-}
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);
-  const uint32_t nt32 = grid_of(n, BLOCK * 32);
-  if (scan_mode() == 32 && nt > 64) {
+  if (nt > 64) {
+    const uint32_t nt32 = grid_of(n, BLOCK * 32);
     hipLaunchKernelGGL(k_scan_lb_u32<32>, dim3(nt32), dim3(BLOCK), 0, s, a, n, status, nt32, total);
-  } else if (nt <= LB_SCAN_MAX_TILES) {
+  } else {
     hipLaunchKernelGGL(k_scan_lb_u32<WPT>, dim3(nt), dim3(BLOCK), 0, s, a, n, status, nt, total);
-  } else {   // long arrays: three launches beat a look-back chain of many tiles
-    hipLaunchKernelGGL(k_tile_sum_u32, dim3(nt), dim3(BLOCK), 0, s, a, n, status);
-    launch_scan_tiles_u64(status, nt, status + nt, s);
-    hipLaunchKernelGGL(k_tile_scan_u32, dim3(nt), dim3(BLOCK), 0, s, a, n,
-                       (const uint64_t*)status, total);
   }
-}
-// KMHG_HISTP=0: the one-tile-per-workgroup histogram kernel (A/B)
-static bool hist_persistent(const Chunks& ch) {
-  const char* e = std::getenv("KMHG_HISTP");          // read per launch: the tests switch it
-  return ch.interleaved && !(e && e[0] == '0');
 }
 void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
-                        uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
+                        uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                         hipStream_t s, uint32_t* save_col0) {
-  if (hist_persistent(ch)) {
-    static const unsigned cap = resident_blocks((const void*)k_v2_histp<true>);
-    hipLaunchKernelGGL(k_v2_histp<true>, dim3(std::min<unsigned>(ch.ntiles, cap)), dim3(BLOCK), 0,
-                       s, reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ch,
-                       xcd_map(), scan_status, n_status, save_col0);
-    return;
-  }
-  hipLaunchKernelGGL((k_v2_hist<false, true>), dim3(ch.C), dim3(BLOCK), 0, s,
-                     reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ch, xcd_map(),
-                     scan_status, n_status, nullptr, nullptr, save_col0, 0);
+  static const unsigned cap = resident_blocks((const void*)k_v2_histp<true>);
+  hipLaunchKernelGGL(k_v2_histp<true>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0, s,
+                     reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ntiles,
+                     scan_status, n_status, save_col0);
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
-                    Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
+                    uint32_t ntiles, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0, bool skip_empty,
                     bool padded) {
-  if (padded && !hll_rows && !skip_empty && hist_persistent(ch)) {
+  if (padded && !hll_rows && !skip_empty) {
     static const unsigned cap = resident_blocks((const void*)k_v2_histp<false>);
-    hipLaunchKernelGGL(k_v2_histp<false>, dim3(std::min<unsigned>(ch.ntiles, cap)), dim3(BLOCK),
-                       0, s, keys, n_ptr, g, D, hist, ch, xcd_map(), scan_status, n_status,
-                       save_col0);
+    hipLaunchKernelGGL(k_v2_histp<false>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0,
+                       s, keys, n_ptr, g, D, hist, ntiles, scan_status, n_status, save_col0);
     return;
   }
   if (hll_rows)
-    hipLaunchKernelGGL(k_v2_hist<true>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
-                       ch, xcd_map(), scan_status, n_status, hll_rows, hll_regs, save_col0,
+    hipLaunchKernelGGL(k_v2_hist<true>, dim3(ntiles), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
+                       ntiles, scan_status, n_status, hll_rows, hll_regs, save_col0,
                        skip_empty ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_v2_hist<false>, dim3(ch.C), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
-                       ch, xcd_map(), scan_status, n_status, nullptr, nullptr, save_col0,
+    hipLaunchKernelGGL(k_v2_hist<false>, dim3(ntiles), dim3(BLOCK), 0, s, keys, n_ptr, g, D, hist,
+                       ntiles, scan_status, n_status, nullptr, nullptr, save_col0,
                        skip_empty ? 1 : 0);
 }
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
@@ -2143,57 +1525,81 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
                      host_n);
 }
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
-                           const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                           const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s) {
-  KMHG_SCATTER(true, false, false, seq, L, k, Nw, 1, nullptr, nullptr, nullptr, g, D, hist, ch,
-               kout, pout, pad, xcd_map(), 0);
+  KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
+               kout, pout, pad, 0);
+}
+// write-combined passes (k_v2_scatter_wc): one workgroup per CU, each over a chunk of tiles
+#define KMHG_SCATTER_WC(FS, ...)                                                              \
+  do {                                                                                       \
+    if (ballot_ranks()) {                                                                    \
+      static const unsigned cap_ = resident_blocks((const void*)k_v2_scatter_wc<FS, true>, WC_TB); \
+      hipLaunchKernelGGL((k_v2_scatter_wc<FS, true>), dim3(std::min(ntiles, cap_)), dim3(WC_TB), \
+                         0, s, __VA_ARGS__);                                                 \
+    } else {                                                                                 \
+      static const unsigned cap_ = resident_blocks((const void*)k_v2_scatter_wc<FS, false>, WC_TB); \
+      hipLaunchKernelGGL((k_v2_scatter_wc<FS, false>), dim3(std::min(ntiles, cap_)), dim3(WC_TB), \
+                         0, s, __VA_ARGS__);                                                 \
+    }                                                                                        \
+  } while (0)
+void launch_v2_scatter_seq_wc(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
+                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                              uint32_t* pout, hipStream_t s) {
+  KMHG_SCATTER_WC(true, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles, kout, pout);
+}
+void launch_v2_scatter_wc(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
+                          Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                          uint32_t* pout, hipStream_t s) {
+  KMHG_SCATTER_WC(false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D, hist, ntiles,
+                  kout, pout);
 }
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
-                            const uint32_t* hist, Chunks ch, uint32_t* bout, uint32_t* pout,
+                            const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
                             uint32_t pad, hipStream_t s) {
   const uint64_t* ki = reinterpret_cast<const uint64_t*>(bids);
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
   if (bout)
-    KMHG_SCATTER_BM(false, true, false, 1, nullptr, (int64_t)0, 0, Nw, 0, ki, nullptr, nullptr, g,
-                    D, hist, ch, ko, pout, pad, xcd_map(), 0);
+    KMHG_SCATTER_BM(false, true, false, 1, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
+                    D, hist, ntiles, ko, pout, pad, 0);
   else
-    KMHG_SCATTER_BM(false, true, false, 2, nullptr, (int64_t)0, 0, Nw, 0, ki, nullptr, nullptr, g,
-                    D, hist, ch, ko, pout, pad, xcd_map(), 0);
+    KMHG_SCATTER_BM(false, true, false, 2, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
+                    D, hist, ntiles, ko, pout, pad, 0);
 }
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
-                           Geom g, Digit D, const uint32_t* hist, Chunks ch, uint32_t* bout,
+                           Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
                            uint32_t* pout, uint32_t pad, hipStream_t s) {
   const uint64_t* ki = reinterpret_cast<const uint64_t*>(bin);
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
   if (bout)
-    KMHG_SCATTER_BM(false, false, false, 1, nullptr, (int64_t)0, 0, (int64_t)0, 0, ki, pin,
-                    n_ptr, g, D, hist, ch, ko, pout, pad, xcd_map(), 0);
+    KMHG_SCATTER_BM(false, false, false, 1, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
+                    g, D, hist, ntiles, ko, pout, pad, 0);
   else
-    KMHG_SCATTER_BM(false, false, false, 2, nullptr, (int64_t)0, 0, (int64_t)0, 0, ki, pin,
-                    n_ptr, g, D, hist, ch, ko, pout, pad, xcd_map(), 0);
+    KMHG_SCATTER_BM(false, false, false, 2, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
+                    g, D, hist, ntiles, ko, pout, pad, 0);
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
-                       Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
-                       uint32_t pad, hipStream_t s) {
-  KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, pin, n_ptr, g, D,
-               hist, ch, kout, pout, pad, xcd_map(), 0);
+                       Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                       uint32_t* pout, uint32_t pad, hipStream_t s) {
+  KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,
+               hist, ntiles, kout, pout, pad, 0);
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
-                             Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout,
+                             Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                              uint32_t* pout, uint32_t pad, bool nopos, bool skip_empty,
                              hipStream_t s) {
   if (nopos)
-    KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)n_keys, 0, kin, nullptr, n_ptr,
-                 g, D, hist, ch, kout, nullptr, pad, xcd_map(), skip_empty ? 1 : 0);
+    KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr, n_ptr,
+                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0);
   else
-    KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)n_keys, 0, kin, nullptr,
-                 n_ptr, g, D, hist, ch, kout, pout, pad, xcd_map(), skip_empty ? 1 : 0);
+    KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr,
+                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0);
 }
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
-                             const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t pad,
+                             const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t pad,
                              hipStream_t s) {
-  KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, 0, kin, nullptr, n_ptr, g, D,
-               hist, ch, kout, nullptr, pad, xcd_map(), 0);
+  KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr, n_ptr, g, D,
+               hist, ntiles, kout, nullptr, pad, 0);
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s, const uint32_t* bids) {
@@ -2203,71 +1609,30 @@ void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint3
                      bids ? reinterpret_cast<const uint64_t*>(bids) : keys, n_ptr, g, start,
                      bids ? 1 : 0);
 }
-void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
-                      Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                      hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_bucket, dim3(grid_of(g.nb, 4)), dim3(BLOCK), 0, s, keys, pos, start, g,
-                     T, positions, bstats, meta, xcd_map_bucket());
-}
-void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint32_t* start,
-                           Geom g, Slot* T, int32_t* positions, BucketStats* bstats,
-                           BuildMeta* meta, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_bucket_sort, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
-                     positions, bstats, meta);
-}
-// KMHG_BUCKET_TB=512|256: threads of the position-build group bucket kernel (A/B)
-static int bucket_tb() {
-  const char* e = std::getenv("KMHG_BUCKET_TB");     // read per launch: the tests switch it
-  return (e && std::string(e) == "512") ? 512 : 256;
-}
-// KMHG_BUCKET_FP=1: the one-atomic fingerprint insert of pass A, 2: the same with every bucket
-// forced through its collision fallback (tests)
-static int bucket_fp() {
-  const char* e = std::getenv("KMHG_BUCKET_FP");
-  return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-}
-// KMHG_BUCKET_C12=0: the 16-B-per-slot LDS table (GroupTable) instead of the compact one (A/B)
-static bool bucket_c12() {
-  const char* e = std::getenv("KMHG_BUCKET_C12");    // read per launch: the tests switch it
-  return !(e && e[0] == '0');
-}
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         bool count_only, hipStream_t s, uint8_t* TG, uint32_t* mbits,
-                         const uint32_t* code, int k) {
-  const int fp = bucket_fp();
-  const bool c12 = !fp && bucket_c12();
-  if (count_only && c12)
-    hipLaunchKernelGGL((k_v2_bucket_wg<true, BLOCK, false, true>), dim3(g.nb), dim3(BLOCK), 0, s,
-                       keys, pos, start, g, T, positions, bstats, meta, nullptr, nullptr, 0,
-                       nullptr, 0);
-  else if (count_only)
-    hipLaunchKernelGGL(k_v2_bucket_wg<true>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g, T,
-                       positions, bstats, meta, nullptr, nullptr, fp, nullptr, 0);
-  else if (c12 && bucket_tb() == 256 && code)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, BLOCK, true, true>), dim3(g.nb), dim3(BLOCK), 0, s,
-                       keys, pos, start, g, T, positions, bstats, meta, TG, mbits, 0, code, k);
-  else if (c12 && bucket_tb() == 256)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, BLOCK, false, true>), dim3(g.nb), dim3(BLOCK), 0, s,
-                       keys, pos, start, g, T, positions, bstats, meta, TG, mbits, 0, nullptr, 0);
-  else if (bucket_tb() == 512 && code)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, 512, true>), dim3(g.nb), dim3(512), 0, s, keys, pos,
-                       start, g, T, positions, bstats, meta, TG, mbits, fp, code, k);
-  else if (bucket_tb() == 512)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, 512>), dim3(g.nb), dim3(512), 0, s, keys, pos, start,
-                       g, T, positions, bstats, meta, TG, mbits, fp, nullptr, 0);
+                         bool count_only, hipStream_t s, const uint32_t* code, int k) {
+  const bool ballot = ballot_ranks();
+  if (count_only)              // no positions: nothing is ranked
+    hipLaunchKernelGGL((k_v2_bucket_wg<true, false, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
+                       pos, start, g, T, positions, bstats, meta, nullptr, 0);
+  else if (code && !ballot)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, true, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
+                       pos, start, g, T, positions, bstats, meta, code, k);
   else if (code)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, BLOCK, true>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, TG, mbits, fp, code, k);
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, true, true>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
+                       pos, start, g, T, positions, bstats, meta, code, k);
+  else if (!ballot)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, false, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
+                       pos, start, g, T, positions, bstats, meta, nullptr, 0);
   else
-    hipLaunchKernelGGL(k_v2_bucket_wg<false>, dim3(g.nb), dim3(BLOCK), 0, s, keys, pos, start, g,
-                       T, positions, bstats, meta, TG, mbits, fp, nullptr, 0);
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, false, true>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
+                       pos, start, g, T, positions, bstats, meta, nullptr, 0);
 }
 // The hardware property the radix passes' ranks rest on, checked on the device itself
-// (kmhg_check_lds_lane_order; tools/lds_order.hip is the stand-alone probe): the lanes of one
-// returning LDS add that hit the same address get old values in increasing lane order.  Every
-// wave draws skewed random digits, adds, and compares each lane with every lower lane of the
-// same digit.
+// (tools/lds_order.hip is the stand-alone probe): the lanes of one returning LDS add that hit
+// the same address get old values in increasing lane order.  Every wave draws skewed random
+// digits, adds, and compares each lane with every lower lane of the same digit.
 __global__ void __launch_bounds__(BLOCK)
 k_lane_order_check(unsigned long long* __restrict__ res, uint32_t seed, int iters) {
   __shared__ uint32_t cnt[BLOCK / 64][128];
@@ -2296,8 +1661,8 @@ k_lane_order_check(unsigned long long* __restrict__ res, uint32_t seed, int iter
   atomicAdd(&res[0], bad);
   atomicAdd(&res[1], chk);
 }
-void launch_lane_order_check(unsigned long long* res, hipStream_t s) {
-  hipLaunchKernelGGL(k_lane_order_check, dim3(1024), dim3(BLOCK), 0, s, res, 12345u, 64);
+void launch_lane_order_check(unsigned long long* res, hipStream_t s, int blocks) {
+  hipLaunchKernelGGL(k_lane_order_check, dim3(blocks), dim3(BLOCK), 0, s, res, 12345u, 64);
 }
 
 // Test knob (KMHG_TEST_DISORDER=1, tests only): swaps the first two positions of bucket 0's

@@ -662,10 +662,11 @@ struct kmhg_index {
   // part of an owner-computes build (kmhg_build_device_part): holds buckets
   // [geom.b0, geom.b0 + geom.nb) of a table of geom.nbh buckets; exported, never queried
   bool is_part = false;
-  // the build wrote the slot tags (ptag) and the repeated keys' window bits (in the code
-  // block's uniq words): the first diagonal query only derives the window bits (V_diag_valid)
-  bool build_prepped = false;
   std::atomic<bool> ps_ready{false};
+  // how the index was built (kmhg_info.build / .fallback): KMHG_BUILD_* and whether
+  // finish_build() had to rebuild it with the global-atomic build
+  int build_kind = 0;
+  int fallback = 0;
   // copies of this index on other devices for multi-device queries (KMHG_DEVICES), keyed by
   // the query part they serve; made on first use by peer copies over xGMI, freed with the index
   std::map<int, kmhg_index*> replicas;
@@ -737,6 +738,7 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   ReleaseGroup rg(s);
   auto idx = std::make_unique<kmhg_index>();
   idx->stream = s;
+  idx->build_kind = KMHG_BUILD_GLOBAL;
   HIPC(hipGetDevice(&idx->device));
   idx->k = k;
   idx->L = L;
@@ -820,6 +822,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   auto idx = std::make_unique<kmhg_index>();
   idx->stream = s;
   HIPC(hipGetDevice(&idx->device));
+  idx->build_kind = ballot_ranks() ? KMHG_BUILD_PARTITIONED_BALLOT : KMHG_BUILD_PARTITIONED;
   idx->k = k;
   idx->L = L;
   const bool from_keys = d_seq == nullptr;
@@ -836,11 +839,10 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     d_seq = aligned_copy.p;
   }
   const uint32_t ntiles = (uint32_t)((Nw + PTILE - 1) / PTILE);   // partition tiles
-  const Chunks ch = make_chunks(ntiles);
-  // radix plan: fewest passes whose radix fits LDS.  Interleaved tiles of PTILE windows keep
-  // ~PTILE / R elements per digit run: beyond ~300 digits the runs get too short for coalesced
-  // writes and an extra pass is cheaper.
-  uint32_t maxr = ch.interleaved ? V2_MAXR_IL : V2_MAXR;
+  // radix plan: fewest passes whose radix fits LDS.  Tiles of PTILE windows keep ~PTILE / R
+  // elements per digit run: beyond ~300 digits the runs get too short for coalesced writes and
+  // an extra pass is cheaper.
+  uint32_t maxr = V2_MAXR_IL;
   if (const char* e = std::getenv("KMHG_MAXR"))   // testing knob: force more radix passes
     maxr = std::max<uint32_t>(2u, std::min<uint32_t>(maxr, (uint32_t)std::atoi(e)));
   auto plan = [&](uint32_t nbk, uint32_t& R) {
@@ -851,11 +853,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     }
     return 5u;
   };
-  // bucket size: group buckets (1024 windows, one workgroup each) unless wave buckets (256
-  // windows, one wave each) need fewer radix passes (only for tiny inputs).  Measured: group
-  // buckets halve the radix (longer digit runs) -- config 2 26.1 vs 24.8 Gbp/s -- and save a pass
-  // from ~26 M windows -- config 3 26.3 vs 24.5.  KMHG_BUCKET=wave|group forces one.
-  const uint32_t nb_w = (uint32_t)std::max<int64_t>(1, (Nw + V2_BW - 1) / V2_BW);
+  // group buckets: 1024 windows, one workgroup each.  (Wave buckets of 256 windows were
+  // removed in round 4: group buckets halve the radix -- config 2 26.1 vs 24.8 Gbp/s -- and save
+  // a pass from ~26 M windows -- config 3 26.3 vs 24.5.)
   // count-only builds: co_spread x more stream entries per group bucket -- a read batch's
   // distinct keys are a fraction of its key stream, so fewer buckets still fit their LDS
   // sub-tables (co_spread_for); one overflowing bucket fails the whole build (meta->overflow)
@@ -869,31 +869,21 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const uint32_t nb_g =
       co_auto ? (uint32_t)(12 * std::max<int64_t>(1, (Nw + 12 * V2_BW_WG - 1) / (12 * V2_BW_WG)))
               : (uint32_t)std::max<int64_t>(1, (Nw + bw_g - 1) / bw_g);
-  uint32_t R_w = 0, R_g = 0;
-  const uint32_t passes_w = plan(nb_w, R_w), passes_g = plan(nb_g, R_g);
-  bool group = passes_g <= passes_w;
-  bool sorted = false;   // group buckets built by V_bucket_sort instead of the CAS build
-  if (const char* e = std::getenv("KMHG_BUCKET")) {
-    if (std::string(e) == "group") group = true;
-    if (std::string(e) == "sort") group = sorted = true;
-    if (std::string(e) == "wave") group = false;
-  }
-  if (count_only) { group = true; sorted = false; }   // the keys-only group bucket build
-  uint32_t nb = group ? nb_g : nb_w;
-  uint32_t passes = group ? passes_g : passes_w;
-  uint32_t R = group ? R_g : R_w;
+  uint32_t R = 0;
+  uint32_t nb = nb_g;
+  uint32_t passes = plan(nb_g, R);
   // owner-computes part (the reference's reader-pool partition,
   // src/kmer_reader.c:28-39): the whole build's geometry, of which this part keeps the buckets
   // [b0, b1) -- every window is encoded and hashed, only the part's keys are partitioned
   uint32_t b0 = 0, nbh = 0;
   if (n_parts >= 1) {           // n_parts = 0: a whole build
-    if (from_keys || count_only || sorted) fail(KMHG_EINVAL, "part builds index sequences only");
+    if (from_keys || count_only) fail(KMHG_EINVAL, "part builds index sequences only");
     b0 = (uint32_t)((uint64_t)nb * part / n_parts);
     const uint32_t b1 = (uint32_t)((uint64_t)nb * (part + 1) / n_parts);
     nbh = nb;
     idx->is_part = true;
     if (b1 <= b0) {              // more parts than buckets: an empty part (nothing to build)
-      idx->geom = Geom{0u, group ? V2_CAPW : V2_CAPB, b0, nbh};
+      idx->geom = Geom{0u, V2_CAPW, b0, nbh};
       idx->table.reset(1);
       idx->positions.reset(1);
       return idx.release();
@@ -902,9 +892,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     passes = plan(nb, R);
   }
   if (passes > 4) fail(KMHG_EOVERFLOW, "sequence too long for the partitioned build");
-  idx->geom = Geom{nb, group ? V2_CAPW : V2_CAPB, b0, nbh};
+  idx->geom = Geom{nb, V2_CAPW, b0, nbh};
   const Geom g = idx->geom;
-  const uint64_t nhist = (uint64_t)R * ch.C;
+  const uint64_t nhist = (uint64_t)R * ntiles;
   const uint32_t scan_tiles = tiles_for(nhist);
   // bucket-id streams (position builds that keep the code words): the radix passes carry
   // (bucket id, pos) -- 8 B per window instead of 12 -- the last pass positions only, and the
@@ -916,18 +906,21 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   constexpr int64_t BID_MAX_WINDOWS = 12 << 20;
   const char* bide = std::getenv("KMHG_BUILD_BID");
   const bool bid_on = bide ? bide[0] == '1' : Nw <= BID_MAX_WINDOWS;
-  const bool bid = codes && !from_keys && group && !sorted && !count_only && ch.interleaved &&
-                   bid_on;
+  const bool bid = codes && !from_keys && !count_only && bid_on;
   DBuf<uint64_t> kA(bid ? 1 : Nw + PTILE, s), kB(bid ? 1 : Nw + PTILE, s);   // + pad
+  // key-stream position builds write their radix passes line by line (k_v2_scatter_wc) beyond
+  // WC_MIN_WINDOWS; KMHG_SCATTER_WC=0 / 1 forces the tile-by-tile / write-combined passes
+  constexpr int64_t WC_MIN_WINDOWS = 12 << 20;
+  const char* wce = std::getenv("KMHG_SCATTER_WC");
+  const bool wc = !bid && !from_keys && !count_only &&
+                  (wce ? wce[0] == '1' : Nw > WC_MIN_WINDOWS);
   // bucket ids: pass p writes bA / bB alternately; the last pass writes none (the bucket bounds
   // pass V_bounds of 3+ passes reads the last one's, so it is written there)
-  const bool bounds_from_hist = ch.interleaved && passes <= 2 &&
-                                !(std::getenv("KMHG_BOUNDS") &&
-                                  std::string(std::getenv("KMHG_BOUNDS")) == "scan");
+  const bool bounds_from_hist = passes <= 2;
   // (bB first holds V_hist0's per-window ids, the first pass's input)
   DBuf<uint32_t> bA(bid && (passes > 1 || !bounds_from_hist) ? Nw + PTILE : 1, s);
   DBuf<uint32_t> bB(bid ? Nw + PTILE : 1, s);
-  const bool no_pos = count_only && group && !sorted;   // keys only through the passes
+  const bool no_pos = count_only;                        // keys only through the passes
   DBuf<uint32_t> pA(no_pos ? 1 : Nw + PTILE, s), pB(no_pos ? 1 : Nw + PTILE, s);
   const uint32_t pad = (uint32_t)Nw;
   DBuf<uint32_t> hist(nhist, s);
@@ -946,26 +939,17 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   idx->positions.reset(no_pos ? 1 : Nw);
   DBuf<BucketStats> bstats(nb, s);
   // co_auto: HLL rows of the first histogram pass, V_hll's registers + ticket, its pinned record
-  DBuf<uint32_t> hll_rows(co_auto ? (size_t)ch.C * (HLL_REGS / 4) : 1, s);
+  DBuf<uint32_t> hll_rows(co_auto ? (size_t)ntiles * (HLL_REGS / 4) : 1, s);
   DBuf<uint32_t> hll_regs(co_auto ? HLL_PART_WORDS : 1, s);
   PinnedRec hrec;
   if (co_auto) hrec = PinnedPool::get().take();
 
-  // bucket starts straight from the histograms (V_bounds_lo) for one or two passes;
-  // KMHG_BOUNDS=scan (tests) forces the pass over the sorted keys (V_bounds)
+  // bucket starts straight from the histograms (V_bounds_lo) for one or two passes
   const bool bounds_lo = bounds_from_hist;
   DBuf<uint32_t> lo_start(bounds_lo && passes == 2 ? R : 1, s);
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = 1;
-  // KMHG_BUILD_TAGS=1: the diagonal query path's slot tags and repeated-key bits written by the
-  // build itself (V_hist0 zeroes the bits, V_bucket_wg sets them and writes the tags with its
-  // sub-table), so an index's first query pays only V_diag_valid.  Measured (A/B in one run,
-  // config 2): first query of an index 0.21 -> 0.15 ms, build +1-1.5 % (the bucket kernel's
-  // 15 MB of tag stores) -- the build is the headline, so the first query prepares by default.
-  const char* bt = std::getenv("KMHG_BUILD_TAGS");
-  const bool prep = codes && !from_keys && group && !sorted && !count_only && n_parts == 0 &&
-                    bt && bt[0] == '1';
   DiagBlock db{nullptr, nullptr, nullptr};
   if (from_keys) {   // pass 0 reads the caller's key stream in place (positions implicit)
     HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(n_valid), (int)Nw, 1, s));
@@ -977,20 +961,22 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       idx->dcodes.reset(diag_block_words(Nw));
       db = idx->diag_block_of();
     }
-    if (prep) idx->ptag.reset(idx->slots() + 32);   // + the 32-B span the last probe group reads
     LAUNCH("k_v2_hist0", s,
-           launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, status, n_status,
-                           meta, s, db.code, db.nbit, prep ? db.uniq : nullptr,
-                           bid ? bB.p : nullptr));
+           launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, status,
+                           n_status, meta, s, db.code, db.nbit, bid ? bB.p : nullptr));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     if (bid)
       LAUNCH("k_v2_scatter_seq", s,
-             launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ch,
+             launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ntiles,
                                     passes == 1 && bounds_lo ? nullptr : bA.p, pA.p, pad, s));
+    else if (wc)
+      LAUNCH("k_v2_scatter_seq", s,
+             launch_v2_scatter_seq_wc(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
+                                      pA.p, s));
     else
       LAUNCH("k_v2_scatter_seq", s,
-             launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ch, kA.p, pA.p,
-                                   pad, s));
+             launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
+                                   pA.p, pad, s));
     div = R;
   }
   uint32_t *bin = bA.p, *bout = bB.p;
@@ -998,11 +984,11 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const Digit Dp = make_digit(div, R);
     const bool last = p + 1 == passes;
     LAUNCH("k_v2_hist", s,
-           launch_v2_hist_bid(bin, n_valid, g, Dp, hist.p, ch, status, n_status, s,
+           launch_v2_hist_bid(bin, n_valid, g, Dp, hist.p, ntiles, status, n_status, s,
                               bounds_lo && passes == 2 ? lo_start.p : nullptr));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     LAUNCH("k_v2_scatter", s,
-           launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hist.p, ch,
+           launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hist.p, ntiles,
                                  last && bounds_lo ? nullptr : bout, pout, pad, s));
     std::swap(bin, bout);
     std::swap(pin, pout);
@@ -1015,27 +1001,30 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const bool hll = co_auto && p == 0;
     const bool save = bounds_lo && passes == 2 && p == 1;
     LAUNCH("k_v2_hist", s,
-           launch_v2_hist(src, n_valid, g, Dp, hist.p, ch, status, n_status, s,
+           launch_v2_hist(src, n_valid, g, Dp, hist.p, ntiles, status, n_status, s,
                           hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
                           save ? lo_start.p : nullptr, keys0 && skip_empty,
                           /*padded=*/!keys0));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     if (hll) {   // after the scan: the estimate travels with the valid key count
-      LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ch.C, hll_regs.p,
+      LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ntiles, hll_regs.p,
                                           &hrec.meta->distinct_est, n_valid,
                                           &hrec.meta->n_positions, s));
       HIPC(hipEventRecord(hrec.ev, s));
     }
     if (keys0) {
       LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter_keys0(d_keys, (uint64_t)Nw, n_valid, g, Dp, hist.p, ch, kout, pout,
-                                     pad, no_pos, skip_empty, s));
+             launch_v2_scatter_keys0(d_keys, (uint64_t)Nw, n_valid, g, Dp, hist.p, ntiles, kout,
+                                     pout, pad, no_pos, skip_empty, s));
     } else if (no_pos) {
       LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ch, kout, pad, s));
+             launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ntiles, kout, pad, s));
+    } else if (wc) {
+      LAUNCH("k_v2_scatter", s,
+             launch_v2_scatter_wc(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, s));
     } else {
       LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ch, kout, pout, pad, s));
+             launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, pad, s));
     }
     std::swap(kin, kout);
     std::swap(pin, pout);
@@ -1059,7 +1048,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const uint32_t div_last = passes == 2 ? R : 1u;
     LAUNCH("k_v2_bounds", s,
            launch_v2_bounds_lo(passes == 2 ? kout : nullptr, n_valid, g, make_digit(div_last, R),
-                               div_last, hist.p, ch.C, passes == 2 ? lo_start.p : nullptr,
+                               div_last, hist.p, ntiles, passes == 2 ? lo_start.p : nullptr,
                                g.nb / gb.nb, start.p, s,
                                bid && passes == 2 ? bout : nullptr));
   } else {
@@ -1075,20 +1064,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // tests only: bucket 0's stream out of order -> the bucket kernel's check -> v1 rebuild
   if (!no_pos && std::getenv("KMHG_TEST_DISORDER") && std::getenv("KMHG_TEST_DISORDER")[0] == '1')
     launch_v2_test_disorder(pin, start.p, s);
-  if (sorted)
-    LAUNCH("k_v2_bucket_sort", s,
-           launch_v2_bucket_sort(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
-                                 meta, s));
-  else if (group)
-    LAUNCH("k_v2_bucket_wg", s,
-           launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, bstats.p,
-                               meta, no_pos, s, prep ? idx->ptag.p : nullptr,
-                               prep ? db.uniq : nullptr, bid ? db.code : nullptr, k));
-  else
-    LAUNCH("k_v2_bucket", s,
-           launch_v2_bucket(kin, pin, start.p, g, idx->table.p, idx->positions.p, bstats.p,
-                            meta, s));
-  idx->build_prepped = prep;
+  LAUNCH("k_v2_bucket_wg", s,
+         launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, bstats.p,
+                             meta, no_pos, s, bid ? db.code : nullptr, k));
   LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, gb.nb, n_valid, meta, idx->rec.meta, s));
   HIPC(hipEventRecord(idx->rec.ev, s));
 #ifdef KMHG_STAMPS
@@ -1107,6 +1085,50 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 bool tags_on() {
   const char* e = std::getenv("KMHG_QUERY_TAGS");
   return !(e && e[0] == '0');
+}
+
+// The LDS lane-order property the radix ranks rest on (kmhg_build_v2.hip), checked once per
+// device before its first partitioned build: where lanes of one returning LDS add that hit the
+// same counter are not served in lane order, every build takes the ballot-rank kernels.
+// KMHG_TEST_BALLOT=1 (tests) forces them.
+static std::atomic<int> g_lane_state[64];          // 0 unchecked, 1 lane order holds, 2 ballots
+static std::mutex g_lane_mu;
+static void lane_order_run(int blocks, uint64_t* bad, uint64_t* checked) {
+  hipStream_t st = nullptr;
+  HIPC(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  unsigned long long* res = nullptr;
+  hipError_t e = hipMalloc(&res, 2 * sizeof(unsigned long long));
+  unsigned long long h[2] = {0, 0};
+  if (e == hipSuccess) e = hipMemsetAsync(res, 0, sizeof(h), st);
+  if (e == hipSuccess) {
+    launch_lane_order_check(res, st, blocks);
+    e = hipMemcpyAsync(h, res, sizeof(h), hipMemcpyDeviceToHost, st);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (res) (void)hipFree(res);
+  (void)hipStreamDestroy(st);
+  hip_check(e, "LDS lane-order check");
+  *bad = h[0];
+  *checked = h[1];
+}
+bool lane_ballot() {
+  if (const char* e = std::getenv("KMHG_TEST_BALLOT"))
+    if (e[0] == '1') return true;
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  std::atomic<int>& st = g_lane_state[(unsigned)dev % 64];
+  int v = st.load(std::memory_order_acquire);
+  if (v == 0) {
+    std::lock_guard<std::mutex> lk(g_lane_mu);
+    v = st.load(std::memory_order_relaxed);
+    if (v == 0) {
+      uint64_t bad = 0, chk = 0;
+      lane_order_run(256, &bad, &chk);
+      v = (bad == 0 && chk > 0) ? 1 : 2;
+      st.store(v, std::memory_order_release);
+    }
+  }
+  return v == 2;
 }
 
 int build_version() {   // read per build so tests can exercise the fallback (KMHG_BUILD=v1)
@@ -1140,8 +1162,9 @@ void finish_build(kmhg_index* idx) {
   idx->src = nullptr;
   if (hm.overflow) {
     if (idx->is_part) fail(KMHG_EOVERFLOW, "a bucket of a part build overflowed its LDS table");
-    idx->build_prepped = false;             // the table is rebuilt: tags and bits are redone
     std::unique_ptr<kmhg_index> v1(build_device_v1(src, idx->L, idx->k, idx->stream));
+    idx->build_kind = KMHG_BUILD_GLOBAL;
+    idx->fallback = 1;                      // reported by kmhg_index_info (bench.py fails on it)
     idx->geom = v1->geom;
     idx->table.swap_with(v1->table);
     idx->positions.swap_with(v1->positions);
@@ -1178,15 +1201,12 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   // by the two-pass path into an exact buffer
   const uint64_t cap = (uint64_t)Nw + ((uint64_t)Nw >> 3) + 64;
   q->rows.reset(cap);
-  // default: probe / scan / emit.  KMHG_QUERY=fused: one pass with a decoupled look-back
-  // (k_query_fused) -- measured slower (config 2: 0.403 ms against 0.365 ms for the three
-  // kernels; a tile that has probed waits for its predecessors' totals while holding its CU
-  // slot, and the probe is occupancy/latency bound; re-measured round 3 with the diagonal path,
-  // A/B in one run: self query 94 -> 53 Gbp/s), kept for A/B and covered by the tests
-  const char* qe = std::getenv("KMHG_QUERY");
-  const bool classic = !(qe && std::string(qe) == "fused");
+  // probe / scan / emit.  (A one-pass probe + look-back + emit was measured slower and removed
+  // in round 4: config 2 0.403 against 0.365 ms; re-measured round 3 with the diagonal path,
+  // self query 94 -> 53 Gbp/s -- a tile that has probed waits for its predecessors' totals
+  // while holding its CU slot, and the probe is occupancy / latency bound.)
   uint64_t H = 0;
-  // diagonal path (k_query_probe / k_query_fused): a position index queried at its own k
+  // diagonal path (k_query_probe): a position index queried at its own k
   const int64_t nA = idx->L - idx->k + 1;
   const char* de = std::getenv("KMHG_QUERY_DIAG");
   const bool diag_ok = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
@@ -1195,25 +1215,20 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   if (diag && !idx->ps_ready.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> lk(idx->ps_mu);
     if (!idx->ps_ready.load(std::memory_order_relaxed) && !idx->ps_failed) {
-      if (!idx->build_prepped) {
-        try {
-          idx->ptag.reset(idx->slots() + 32);  // + the 32-B span the last probe group reads
-        } catch (const Error& e) {           // no room for the tags: table probes only
-          if (e.code != KMHG_ENOMEM) throw;
-          idx->ps_failed = true;
-          (void)hipGetLastError();
-        }
+      try {
+        idx->ptag.reset(idx->slots() + 32);    // + the 32-B span the last probe group reads
+      } catch (const Error& e) {               // no room for the tags: table probes only
+        if (e.code != KMHG_ENOMEM) throw;
+        idx->ps_failed = true;
+        (void)hipGetLastError();
       }
       if (!idx->ps_failed) {
         idx->ptag.bind(s);
         idx->dcodes.bind(s);
         const DiagBlock db = idx->diag_block_of();
-        if (idx->build_prepped)
-          LAUNCH("k_diag_valid", s, launch_diag_valid_multi(db.nbit, idx->L, idx->k, db.uniq, s));
-        else
-          LAUNCH("k_diag_prep", s,
-                 launch_diag_prep(db.nbit, idx->L, idx->k, db.uniq, idx->table.p, idx->slots(),
-                                  idx->positions.p, idx->ptag.p, s));
+        LAUNCH("k_diag_prep", s,
+               launch_diag_prep(db.nbit, idx->L, idx->k, db.uniq, idx->table.p, idx->slots(),
+                                idx->positions.p, idx->ptag.p, s));
         // once per index: later queries may run on other streams
         HIPC(hipStreamSynchronize(s));
         idx->ps_ready.store(true, std::memory_order_release);
@@ -1222,21 +1237,6 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   }
   diag = diag && idx->ps_ready.load(std::memory_order_acquire);
 
-  if (!classic) {
-    // one pass: probe + look-back + emit (k_query_fused); look-back words + ticket zeroed
-    DBuf<uint64_t> status((size_t)nt + 1, s);
-    HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
-    LAUNCH("k_query_fused", s,
-           launch_query_fused(d_seq, L, kq, idx->table.p, idx->geom, w0, w1, aligned,
-                              idx->positions.p, status.p, q->rows.p, cap, s,
-                              diag ? idx->diag_view() : DiagIdx{nullptr, nullptr, 0},
-                              diag && tags_on() ? idx->ptag.p : nullptr));
-    HIPC(hipMemcpyAsync(&H, status.p + nt - 1, sizeof(H), hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
-    H &= (1ull << 62) - 1;                       // LB_MASK: the last tile's inclusive prefix
-    q->H = (int64_t)H;
-    if (H <= cap) return q.release();
-  }
   DBuf<uint32_t> qrec(Nw, s);         // per window: 0, the one hit's position, or multi
   DBuf<uint2> qmulti(Nw, s);          // {count, first index}: written for multi-hit windows only
   // per-tile rows -> first row; then the long-scan scratch.  The row total goes straight into
@@ -1251,20 +1251,15 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
                             tile_row0, s, diag ? idx->diag_view() : DiagIdx{nullptr, nullptr, 0},
                             diag && tags_on() ? idx->ptag.p : nullptr));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, tiles.p + nt, s));
-  if (classic) {
-    LAUNCH("k_query_emit", s,
-           launch_query_emit(qrec.p, qmulti.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap,
-                             s));
-    HIPC(hipStreamSynchronize(s));
-    H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
-    q->H = (int64_t)H;
-    if (H <= cap) {
-      rg.synced = true;                          // nothing queued behind the synchronize
-      return q.release();
-    }
-  } else {
-    HIPC(hipStreamSynchronize(s));
-    H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
+  LAUNCH("k_query_emit", s,
+         launch_query_emit(qrec.p, qmulti.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap,
+                           s));
+  HIPC(hipStreamSynchronize(s));
+  H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
+  q->H = (int64_t)H;
+  if (H <= cap) {
+    rg.synced = true;                            // nothing queued behind the synchronize
+    return q.release();
   }
   q->rows.bind(s);
   q->rows.reset(H);
@@ -2116,6 +2111,8 @@ void free_index(kmhg_index* idx) {
 
 }  // namespace
 
+bool kmhg::ballot_ranks() { return lane_ballot(); }
+
 // ============================================================================ C-ABI
 extern "C" {
 
@@ -2632,6 +2629,8 @@ int kmhg_index_info(const kmhg_index* cidx, kmhg_info* info) {
     info->sources = (int32_t)idx->sources;
     info->kind = idx->canonical ? 2 : (idx->sources ? 1 : 0);
     info->kmer_count = (int64_t)(idx->sources ? idx->kmer_count : idx->U);
+    info->build = idx->build_kind;
+    info->fallback = idx->fallback;
   });
 }
 

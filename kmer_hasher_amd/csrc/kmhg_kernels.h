@@ -7,17 +7,14 @@ namespace kmhg {
 
 constexpr uint32_t LARGE_MIN = 64;     // keys with >= this many positions sort per workgroup
 // partitioned build (kmhg_build_v2.hip)
-constexpr uint32_t V2_BW = 256;        // mean windows per bucket
-constexpr uint32_t V2_CAPB = 384;      // slots per bucket (LDS sub-table of one wave)
-constexpr uint32_t V2_SLOT_BITS = 9;   // bits to name a slot 0..V2_CAPB
 constexpr uint32_t V2_BW_WG = 1024;    // ... group buckets: mean windows per bucket
 #ifndef KMHG_CAPW
 #define KMHG_CAPW 1536
 #endif
 constexpr uint32_t V2_CAPW = KMHG_CAPW;  // slots per group bucket (LDS sub-table of one workgroup)
 constexpr uint32_t V2_SLOT_BITS_WG = 11;
-constexpr uint32_t V2_MAXR = 640;      // max radix of one partition pass (LDS arrays)
-constexpr uint32_t V2_MAXR_IL = 320;   // ... with the interleaved tile schedule
+constexpr uint32_t V2_MAXR = 640;      // LDS digit arrays of the histogram / bounds kernels
+constexpr uint32_t V2_MAXR_IL = 320;   // max radix of one partition pass (the scatter's LDS)
 constexpr uint32_t SORT_CHUNK = 4096;  // LDS bitonic chunk (16 KiB)
 
 struct BuildMeta {              // written by the build kernels, read once by the host
@@ -96,8 +93,6 @@ void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, co
                       uint64_t nslots, const int32_t* positions, uint8_t* TG, hipStream_t s);
 // An index whose build already wrote the slot tags and set the repeated keys' window bits in
 // the uniq words (V_bucket_wg): uniq = the indexed windows AND NOT those bits
-void launch_diag_valid_multi(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq,
-                             hipStream_t s);
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
 // exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
 // reduce-then-scan with `scratch` = scan_u64_scratch(n) u64
@@ -108,12 +103,6 @@ void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch
 void launch_query_emit(const uint32_t* qrec, const uint2* qmulti, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
                        uint64_t cap, hipStream_t s);
-// probe + emit in one pass (ticketed tiles, decoupled look-back): `status` = grid_for(w1 - w0,
-// TILE) + 1 zeroed u64; the total row count comes back in status[nt - 1] & LB_MASK
-void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
-                        int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
-                        int2* out, uint64_t cap, hipStream_t s,
-                        DiagIdx X = DiagIdx{nullptr, nullptr, 0}, const uint8_t* TG = nullptr);
 // F = L entries {slot, count} preset to slot NONE
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s);
@@ -153,45 +142,33 @@ inline Digit make_digit(uint32_t div, uint32_t R) {
   while ((1u << d.nbits) < R) ++d.nbits;
   return d;
 }
-// Chunked radix passes: chunk c = partition tiles [c*tpc, min((c+1)*tpc, ntiles)), one
-// workgroup per chunk (as many chunks as scatter workgroups are resident); histograms are
-// [digit][chunk] and a chunk's output for a digit is one contiguous run.
-// Interleaved (the default): C = ntiles chunks of one tile each, so histograms are per tile,
-// and the scatter runs a persistent grid whose XCDs each walk one contiguous tile range.
-struct Chunks {
-  uint32_t C;            // chunks = histogram columns (= histogram workgroups)
-  uint32_t tpc;          // tiles per chunk
-  uint32_t ntiles;       // partition tiles (PTILE windows each)
-  uint32_t interleaved;  // 1: per-tile schedule (see above)
-};
-Chunks make_chunks(uint32_t ntiles);
+// Radix passes run over tiles of PTILE windows; histograms are [digit][tile] (ntiles columns),
+// and the persistent scatter grids give every XCD one contiguous tile range (xcd_remap).
 // V_hist0 also zeroes the look-back words of the scan that follows (n_status u64) and `meta`
 // code / nbit (optional, position indices: the diagonal query path, DiagBlock): the sequence's
 // 2-bit code words and N-flag words
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
-                     uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
+                     uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                      BuildMeta* meta, hipStream_t s, uint32_t* code = nullptr,
-                     uint16_t* nbit = nullptr, uint32_t* uniq0 = nullptr,
-                     uint32_t* bids = nullptr);
+                     uint16_t* nbit = nullptr, uint32_t* bids = nullptr);
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
 // exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the histogram kernel
 // launched before it; total <- sum.  Single-pass look-back (8192-entry tiles beyond 64 2048-entry
 // tiles).
-constexpr uint32_t LB_SCAN_MAX_TILES = 256;   // (KMHG_SCAN=8; 8192-entry tiles beyond 64 tiles)
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s);
 // hll_rows (count-only builds, first pass): the histogram workgroups also sketch the distinct
-// keys (HyperLogLog, HLL_REGS registers, 1/64 key-space sample) into one 256-B row each (ch.C
+// keys (HyperLogLog, HLL_REGS registers, 1/64 key-space sample) into one 256-B row each (ntiles
 // rows, HLL_REGS / 4 u32); launch_v2_hll reduces the rows (through hll_regs = HLL_PART_WORDS u32
 // of partial rows) and writes the distinct-key estimate to *host_est (pinned host memory)
 constexpr uint32_t HLL_REGS = 256;
 constexpr uint32_t HLL_PART_WORDS = 256 * 64 + 1;
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
-                    Chunks ch, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
+                    uint32_t ntiles, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr,
                     uint32_t* save_col0 = nullptr, bool skip_empty = false,
                     bool padded = false);
-// bucket starts from the histograms (passes <= 2, interleaved schedule): one workgroup per lo
+// bucket starts from the histograms (passes <= 2): one workgroup per lo
 // value (div of them); kprev = the last pass's input keys, lo_start = the previous pass's digit
 // starts (saved by launch_v2_hist's save_col0; nullptr for one pass); start[b / spread] for
 // buckets b that are multiples of spread, start[nb / spread] = n
@@ -205,33 +182,41 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s);
 // the sequence must be 16-B aligned (the engine copies an unaligned input)
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
-                           const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                           const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s);
+// The same two passes with every output line written whole (k_v2_scatter_wc: chunked tiles,
+// line tails wait in LDS); for key streams beyond the caches.
+void launch_v2_scatter_seq_wc(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
+                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                              uint32_t* pout, hipStream_t s);
+void launch_v2_scatter_wc(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
+                          Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
+                          uint32_t* pout, hipStream_t s);
 // first pass over a caller's key stream of n_keys keys (>= 1): positions are e + 1; nopos:
 // keys only (count-only builds), pout unused; skip_empty: EMPTY_KEY entries are not keys (padded
 // read k-mer streams, k <= 31)
 void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
-                             Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout,
+                             Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                              uint32_t* pout, uint32_t pad, bool nopos, bool skip_empty,
                              hipStream_t s);
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
-                             const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t pad,
+                             const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t pad,
                              hipStream_t s);
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
-                       Digit D, const uint32_t* hist, Chunks ch, uint64_t* kout, uint32_t* pout,
+                       Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s);
 // Bucket-id streams (position builds that keep the sequence's code words): V_hist0 stores
 // every window's bucket id (`bids`, Nw u32, ~0 = not indexed), the radix passes carry (bucket
 // id u32, pos u32) and the last pass writes positions only (bout = nullptr); the bucket kernel
 // cuts the keys from the code words.  Histograms without hashing.
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
-                            const uint32_t* hist, Chunks ch, uint32_t* bout, uint32_t* pout,
+                            const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
                             uint32_t pad, hipStream_t s);
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
-                           Geom g, Digit D, const uint32_t* hist, Chunks ch, uint32_t* bout,
+                           Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
                            uint32_t* pout, uint32_t pad, hipStream_t s);
 void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
-                        uint32_t* hist, Chunks ch, uint64_t* scan_status, uint32_t n_status,
+                        uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                         hipStream_t s, uint32_t* save_col0 = nullptr);
 // bids (bucket-id streams): the sorted bucket ids instead of keys
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
@@ -240,19 +225,16 @@ struct BucketStats {           // per-bucket partials of the build statistics
   uint32_t n_kmers, max_count;
   uint64_t n_pairs;
 };
-void launch_v2_bucket(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
-                      Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                      hipStream_t s);
-void launch_v2_bucket_sort(const uint64_t* keys, const uint32_t* pos, const uint32_t* start,
-                           Geom g, Slot* T, int32_t* positions, BucketStats* bstats,
-                           BuildMeta* meta, hipStream_t s);
 // count_only: occurrence counts only (no positions written; slot aux unspecified)
 // code (bucket-id streams): keys unused, each window's key cut from the code words at its pos
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         bool count_only, hipStream_t s, uint8_t* TG = nullptr,
-                         uint32_t* mbits = nullptr, const uint32_t* code = nullptr, int k = 0);
-void launch_lane_order_check(unsigned long long* res, hipStream_t s);
+                         bool count_only, hipStream_t s, const uint32_t* code = nullptr,
+                         int k = 0);
+// ballot_ranks(): the current device fails the LDS lane-order self-check (or KMHG_TEST_BALLOT):
+// the radix passes and the bucket kernel then rank with ballots (kmhg_engine.cpp)
+bool ballot_ranks();
+void launch_lane_order_check(unsigned long long* res, hipStream_t s, int blocks = 1024);
 void launch_v2_test_disorder(uint32_t* pos, const uint32_t* start, hipStream_t s);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);

@@ -357,13 +357,6 @@ void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, co
                      positions, uniq, TG);
 }
 
-void launch_diag_valid_multi(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq,
-                             hipStream_t s) {
-  const uint64_t nw = diag_uniq_words(L - k + 1);
-  hipLaunchKernelGGL(k_diag_valid, dim3((unsigned)((nw + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
-                     nbit, L, k, uniq, nw, 1);
-}
-
 // A window's probe result as Q_emit reads it: qrec[s] = 0 (no hit), the 1-based index position
 // (one hit: a key seen once keeps its position inline, < 2^31), or QREC_MULTI with qmulti[s] =
 // {count, first index into positions} -- 4 B per window written and read back instead of 8 (only
@@ -801,107 +794,6 @@ k_query_emit(const uint32_t* __restrict__ qrec, const uint2* __restrict__ qmulti
   }
 }
 
-// Q_fused: probe + emit in one pass, no {count, start} record round trip through HBM.  Tiles
-// come from a ticket counter; each tile probes its windows (as Q_probe, results kept in
-// registers), publishes its row total, learns its first row from a decoupled look-back over
-// the preceding tiles (kmhg_device.h) and writes its rows.  A tile never waits before it has
-// published, and every tile it waits on took an earlier ticket (is running or done), so the
-// chain always drains.  Row order inside the tile is Q_emit's: windows in position order, rows
-// of one window by ascending j; windows are visited slice by slice (256 consecutive windows, one
-// per lane), windows with <= EMIT_DIRECT hits write their own rows (one-hit rows of a slice are
-// consecutive, coalesced stores), heavier windows of the slice are dealt to the whole workgroup.
-// `status` (nt look-back words + the ticket) must be zero; rows at or beyond `cap` are dropped
-// and the total comes back in status[nt - 1] (inclusive prefix of the last tile).
-__global__ void __launch_bounds__(BLOCK)
-k_query_fused(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
-              Geom g, int64_t w0, int64_t w1, int aligned, const int32_t* __restrict__ positions,
-              uint64_t* __restrict__ status, uint32_t nt, int2* __restrict__ out, uint64_t cap,
-              DiagIdx X, const uint8_t* __restrict__ TG) {
-  // LDS ~19 KB -> 8 workgroups per CU, as Q_probe: per-window {count, first} records (the
-  // registers would hold them only with all WPT probes unrolled: 100 VGPRs, half the waves), and
-  // the stage shares its bytes with the emit's heavy-window list
-  __shared__ uint2 qi[TILE];
-  __shared__ union {
-    Stage st;
-    struct { uint32_t w[BLOCK]; uint64_t off[BLOCK]; } hv;
-  } u;
-  __shared__ uint64_t sh[8];
-  __shared__ uint32_t tk;
-  __shared__ uint64_t r0_sh;
-  __shared__ uint32_t n_heavy;
-  __shared__ DiagAnchors A;
-  const uint32_t tile = take_ticket(reinterpret_cast<uint32_t*>(status + nt), &tk);
-  const int64_t t_start = w0 + (int64_t)tile * TILE;
-  const int64_t base = (t_start & ~15ll) - HALO;
-  const int o0 = (int)(t_start - base);
-  stage_tile(seq, L, base, u.st, aligned != 0);
-  __syncthreads();
-  if (X.code) diag_anchors(u.st, o0, t_start, w1, L, kq, T, g, A);
-  uint64_t rows = 0;
-  if (X.code) {
-    diag_resolve(u.st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
-                 [&](int w, int64_t, uint32_t count, uint32_t aux) {
-                   qi[w] = make_uint2(count, count == 1 ? aux : aux - count);
-                   rows += count;
-                 });
-  } else {
-#pragma unroll KMHG_PROBE_UNROLL
-    for (int j = 0; j < WPT; ++j) {
-      const int w = j * BLOCK + threadIdx.x;
-      const int64_t s = t_start + w;
-      uint64_t key = 0;
-      uint32_t count = 0, aux = 0;
-      if (s < w1 && window_key(u.st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
-      qi[w] = make_uint2(count, count == 1 ? aux : aux - count);   // position, or list start
-      rows += count;
-    }
-  }
-  uint64_t agg;
-  block_excl_scan(rows, sh, agg);              // (its barriers also retire the stage reads)
-  if (threadIdx.x < 64) {
-    lookback_publish(status, tile, agg);
-    const uint64_t excl = lookback_excl(status, tile, agg, true);
-    if (threadIdx.x == 0) { r0_sh = excl; n_heavy = 0; }
-  }
-  __syncthreads();
-  if (agg == 0) return;
-  uint64_t r = r0_sh;                           // first row of the current slice
-  const int32_t i0 = (int32_t)(t_start + kq);   // i of window w = i0 + w (1-based end)
-#pragma unroll 1
-  for (int j = 0; j < WPT; ++j) {
-    const int w = j * BLOCK + threadIdx.x;
-    const uint2 v = qi[w];
-    uint64_t slice_tot;
-    const uint64_t off = r + block_excl_scan(v.x, sh, slice_tot);
-    r += slice_tot;
-    if (slice_tot == 0) continue;               // uniform
-    if (v.x == 1) {
-      if (off < cap) out[off] = make_int2(i0 + w, (int32_t)v.y);
-    } else if (v.x > EMIT_DIRECT) {
-      const uint32_t h = atomicAdd(&n_heavy, 1u);
-      u.hv.w[h] = (uint32_t)w;
-      u.hv.off[h] = off;
-    } else {
-      for (uint32_t q = 0; q < v.x; ++q)
-        if (off + q < cap) out[off + q] = make_int2(i0 + w, positions[v.y + q]);
-    }
-    __syncthreads();
-    const uint32_t nh = n_heavy;
-    if (nh) {   // uniform: the whole workgroup deals this slice's heavy windows
-      for (uint32_t h = 0; h < nh; ++h) {
-        const uint32_t hw = u.hv.w[h];
-        const uint2 hv = qi[hw];
-        const uint64_t ho = u.hv.off[h];
-        for (uint32_t q = threadIdx.x; q < hv.x; q += BLOCK)
-          if (ho + q < cap) out[ho + q] = make_int2(i0 + (int32_t)hw, positions[hv.y + q]);
-      }
-      __syncthreads();
-      if (threadIdx.x == 0) n_heavy = 0;
-      __syncthreads();
-    }
-  }
-}
-
 // ================================================================== readout kernels
 // The index is the table + positions: a key's slot carries {key, count, end} and its
 // positions are [end - count, end).  Canonical k-mer order (first occurrence) is a slot
@@ -1291,15 +1183,6 @@ void launch_query_emit(const uint32_t* qrec, const uint2* qmulti, int64_t Nw, in
                        uint64_t cap, hipStream_t s) {
   hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qrec, qmulti, Nw, w0,
                      kq, positions, tile_row0, out, cap);
-}
-void launch_query_fused(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g, int64_t w0,
-                        int64_t w1, bool aligned, const int32_t* positions, uint64_t* status,
-                        int2* out, uint64_t cap, hipStream_t s,
-                        DiagIdx X, const uint8_t* TG) {
-  const uint32_t nt = grid_for(w1 - w0, TILE);
-  if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
-  hipLaunchKernelGGL(k_query_fused, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, w0, w1,
-                     aligned ? 1 : 0, positions, status, nt, out, cap, X, TG);
 }
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s) {

@@ -195,23 +195,19 @@ def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
         ptr.free()
 
 
-@pytest.mark.parametrize("bucket", ["wave", "group", "group16", "group512", "groupfp",
-                                    "group512fp", "groupfpforce", "sort"])
-def test_bucket_kernels_vs_oracle(gpu, monkeypatch, bucket):
-    """Both bucket kernels on every size class: one wave per 256-window bucket, and one
-    workgroup per 1024-window bucket (chosen automatically when it saves a radix pass, e.g. at
-    100 Mbp): repeated keys spanning waves, buckets beyond one batch (tandem repeats), N-runs."""
+@pytest.mark.parametrize("ranks", ["lane", "ballot"])
+@pytest.mark.parametrize("stream", ["bid", "keys", "keyswc"])
+def test_bucket_kernels_vs_oracle(gpu, monkeypatch, stream, ranks):
+    """The group bucket kernel (one workgroup per 1024-window bucket) on every size class:
+    repeated keys spanning waves, buckets beyond one batch (tandem repeats), N-runs -- with the
+    radix passes and the bucket kernel ranking by the LDS atomics' lane order (the default on a
+    device that passes the self-check) and by ballots (KMHG_TEST_BALLOT=1, the kernels a device
+    that fails it runs), over bucket-id and key streams, the latter also through the
+    write-combined radix passes (keyswc: KMHG_SCATTER_WC=1, the default beyond 12 M windows)."""
     from kmer_hasher_amd import synth
-    if bucket.startswith("group"):
-        # the 8-wave group bucket kernel (KMHG_BUCKET_TB), the one-atomic fingerprint insert
-        monkeypatch.setenv("KMHG_BUCKET_TB", "512" if "512" in bucket else "256")
-        # KMHG_BUCKET_FP=2 takes every bucket through the fingerprint-collision fallback
-        monkeypatch.setenv("KMHG_BUCKET_FP", "2" if bucket.endswith("force") else
-                           "1" if bucket.endswith("fp") else "0")
-        # group16: the 16-B-per-slot LDS table instead of the compact 12-B one (KMHG_BUCKET_C12)
-        monkeypatch.setenv("KMHG_BUCKET_C12", "0" if bucket == "group16" else "1")
-        bucket = "group"
-    monkeypatch.setenv("KMHG_BUCKET", bucket)
+    monkeypatch.setenv("KMHG_TEST_BALLOT", "1" if ranks == "ballot" else "0")
+    monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
+    monkeypatch.setenv("KMHG_SCATTER_WC", "1" if stream == "keyswc" else "0")
     rng = np.random.default_rng(21)
     for k in (3, 12, 31, 32):
         _check_against_oracle("".join(rng.choice(list("ACGT"), 5000)), k)
@@ -236,6 +232,25 @@ def test_lds_atomic_lane_order(gpu):
     assert bad.value == 0, (bad.value, chk.value)
 
 
+def test_build_kind_reported(gpu, monkeypatch):
+    """kmhg_info.build names the kernels that built the index: partitioned with lane-order
+    ranks on a device that passes the self-check, ballot ranks when forced (KMHG_TEST_BALLOT=1,
+    what a device failing the check runs), the global-atomic build for KMHG_BUILD=v1."""
+    import torch
+    from kmer_hasher_amd import _lib, synth
+    from kmer_hasher_amd.device import DeviceIndex
+    seq = torch.from_numpy(synth.iid(50_000, 5)).cuda()
+    for env, want in ((("KMHG_TEST_BALLOT", "0"), _lib.KMHG_BUILD_PARTITIONED),
+                      (("KMHG_TEST_BALLOT", "1"), _lib.KMHG_BUILD_PARTITIONED_BALLOT),
+                      (("KMHG_BUILD", "v1"), _lib.KMHG_BUILD_GLOBAL)):
+        monkeypatch.setenv(*env)
+        idx = DeviceIndex.build(seq, 31)
+        info = idx.info()
+        assert (info["build"], info["fallback"]) == (want, 0), (env, info)
+        idx.free()
+        monkeypatch.delenv(env[0])
+
+
 @pytest.mark.parametrize("stream", ["bid", "keys"])
 def test_stream_disorder_falls_back(gpu, monkeypatch, stream):
     """The radix passes are stable because same-address LDS count atomics of one instruction
@@ -246,7 +261,7 @@ def test_stream_disorder_falls_back(gpu, monkeypatch, stream):
     import torch
     from kmer_hasher_amd import synth
     from kmer_hasher_amd.device import DeviceIndex
-    monkeypatch.setenv("KMHG_BUCKET", "group")
+    from kmer_hasher_amd import _lib
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
     s = synth.add_n_runs(synth.iid(300_000, 51), 0.002, 9).tobytes().decode("latin-1")
     seq = torch.frombuffer(bytearray(s.encode("latin-1")), dtype=torch.uint8).cuda()
@@ -256,32 +271,31 @@ def test_stream_disorder_falls_back(gpu, monkeypatch, stream):
         meta, _ = idx.export_image()
         nb = int(meta[2].item()) >> 32
         assert (nb == 1) == one_bucket, (disorder, nb)
+        info = idx.info()                  # the rebuild is reported (kmhg_info.fallback / build)
+        assert info["fallback"] == (1 if one_bucket else 0), (disorder, info)
+        assert info["build"] == (_lib.KMHG_BUILD_GLOBAL if one_bucket else
+                                 _lib.KMHG_BUILD_PARTITIONED), (disorder, info)
         idx.free()
         _check_against_oracle(s, 31, pairs=False)
 
 
-@pytest.mark.parametrize("stream", ["bid", "keys"])
-@pytest.mark.parametrize("bounds", ["lo", "scan", "sc8", "h0tile", "histtile"])
+@pytest.mark.parametrize("stream", ["bid", "keys", "keyswc"])
+@pytest.mark.parametrize("ranks", ["lane", "ballot"])
 @pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
-def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds, stream):
+def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, ranks, stream):
     """More radix passes than the input needs (KMHG_MAXR caps the radix): 1-4 passes with N-runs
     and repeat-rich input.  Bucket starts come from the radix histograms for one or two passes
     (k_v2_bounds_lo: the partial-tile count at each low digit's first element; a zero-width
-    tile at a tile boundary) and from a pass over the sorted keys otherwise or with
-    KMHG_BOUNDS=scan; both against the oracle.  Position builds carry bucket ids through the
-    passes and cut the keys from the code words (default); KMHG_BUILD_BID=0 carries the keys."""
+    tile at a tile boundary) and from a pass over the sorted keys for three or more; both against
+    the oracle.  Position builds carry bucket ids through the passes and cut the keys from the
+    code words (default up to 12 M windows); KMHG_BUILD_BID=0 carries the keys, tile by tile
+    or write-combined (keyswc: KMHG_SCATTER_WC=1, line tails waiting in LDS across a chunk's
+    tiles).  Ranks by the LDS atomics' lane order and by ballots (KMHG_TEST_BALLOT=1)."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_MAXR", maxr)
-    monkeypatch.setenv("KMHG_BUCKET", "group")     # bucket-id streams need group buckets
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
-    if bounds == "sc8":                    # the 8-wave radix scatter (KMHG_SC8=1)
-        monkeypatch.setenv("KMHG_SC8", "1")
-    elif bounds == "h0tile":               # the first histogram one workgroup per tile
-        monkeypatch.setenv("KMHG_HIST0P", "0")
-    elif bounds == "histtile":             # the later histograms one workgroup per tile
-        monkeypatch.setenv("KMHG_HISTP", "0")
-    else:
-        monkeypatch.setenv("KMHG_BOUNDS", bounds)
+    monkeypatch.setenv("KMHG_SCATTER_WC", "1" if stream == "keyswc" else "0")
+    monkeypatch.setenv("KMHG_TEST_BALLOT", "1" if ranks == "ballot" else "0")
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
     _check_against_oracle(s, 31, pairs=False)
     rr = synth.repeat_rich(300_000, 42, n_gap_every=100_000).tobytes().decode("latin-1")
@@ -292,21 +306,19 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, bounds, stream):
         _check_against_oracle("".join(rng.choice(list("ACGT"), L)), 31, pairs=False)
 
 
-@pytest.mark.parametrize("path", ["fused", "classic", "nodiag", "notags"])
+@pytest.mark.parametrize("path", ["default", "nodiag", "notags"])
 def test_query_paths_vs_oracle(gpu, monkeypatch, path):
-    """seq.kmer.pos through the probe / scan / emit kernels (default; also the fused path's redo
-    when a query has more rows than the guessed capacity) and through the one-pass probe +
-    look-back + emit kernel (KMHG_QUERY=fused): ragged sizes around the 2048-window tile, windows
-    with 2-4 hits (lane-written) and > 4 hits (workgroup-dealt) in one slice, thousands of tiles
-    chained by the look-back, a query with far more rows than windows, and a query of another
+    """seq.kmer.pos through the probe / scan / emit kernels (the emit's redo into an exact buffer
+    when a query has more rows than the guessed capacity), with the diagonal path off
+    (KMHG_QUERY_DIAG=0) and the slot tags off (KMHG_QUERY_TAGS=0): ragged sizes around the
+    2048-window tile, windows with 2-4 hits (lane-written) and > 4 hits (workgroup-dealt) in one
+    slice, thousands of tiles, a query with far more rows than windows, and a query of another
     sequence (misses)."""
     from kmer_hasher_amd import synth
     if path == "nodiag":
         monkeypatch.setenv("KMHG_QUERY_DIAG", "0")
     elif path == "notags":
         monkeypatch.setenv("KMHG_QUERY_TAGS", "0")
-    else:
-        monkeypatch.setenv("KMHG_QUERY", path)
     make, kpos, sqk = _api()
     rng = np.random.default_rng(77)
     for n in (40, 2047 + 30, 2048 + 30, 2049 + 30, 3 * 2048 + 7):
@@ -339,8 +351,8 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
     ptr.free()
 
 
-@pytest.mark.parametrize("tags,btags", [("1", "1"), ("0", "1"), ("1", "0")])
-def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags, btags):
+@pytest.mark.parametrize("tags", ["1", "0"])
+def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags):
     """The diagonal path of k_query_probe (anchors every 64th window; later windows follow the
     last anchor with a unique hit and take {count 1, aux = predicted position} only when the
     index window there is unique and its key, read from the index's own code words, equals
@@ -349,13 +361,11 @@ def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags, btags):
     inversions, translocations, N-runs), its reverse complement, an unrelated one, repeat-rich
     input (multi-hit anchors predict nothing; keys with > 16 positions have their windows'
     unique bits cleared by a whole wave), shards of the window range that start inside a
-    diagonal, and a query k different from the index k (path off).  btags: the slot tags and
-    repeated-key bits written by the build (V_bucket_wg, default) or by the first query
-    (KMHG_BUILD_TAGS=0, V_diag_prep)."""
+    diagonal, and a query k different from the index k (path off).  The slot tags and the
+    repeated keys' window bits are built by the index's first diagonal query (V_diag_prep)."""
     import torch
     from kmer_hasher_amd import device as D, synth
     monkeypatch.setenv("KMHG_QUERY_TAGS", tags)
-    monkeypatch.setenv("KMHG_BUILD_TAGS", btags)
     make, kpos, sqk = _api()
     A = synth.add_n_runs(synth.iid(300_000, 61), 0.0005, 62, max_run=40)
     B = synth.derived(A, 63)
@@ -405,7 +415,6 @@ def test_query_diagonal_edges_vs_oracle(gpu, monkeypatch, codes):
     in the index, and an index built without the code block (KMHG_DIAG_CODES=0: table probes)."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_DIAG_CODES", codes)
-    monkeypatch.setenv("KMHG_BUILD_TAGS", "1" if codes == "1" else "0")   # (tags need codes)
     make, kpos, sqk = _api()
     rng = np.random.default_rng(91)
 
