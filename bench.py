@@ -13,9 +13,13 @@ seq.kmer.pos self-query of the same sequence is timed the same way and reported 
 sampled from it (packed in HBM) and `depth` seq.kmer.depth.sh of it against that suffix hash
 (SURVEY.md §8 f next-4), each with the reference's own core timed beside it.
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): every rank indexes its own
-sequence (seed = 1 + rank), no data-path collective -> weak scaling; value = all ranks' Mbp
-divided by the max-over-ranks time.
+N > 1 (launched by torch.distributed.run, one rank per GPU): value is the owner-computes build of
+ONE sequence of N x L bases (the reference's reader-pool partition,
+src/kmer_reader.c:28-39): rank 0 holds it and broadcasts it once, every rank builds the k-mers of
+its bucket range (kmhg_build_device_part), no data-path collective inside a step -> weak
+scaling; value = N x L Mbp divided by the max-over-ranks time per step.  The broadcast and the
+assembly of the whole index on every rank are timed beside it; every rank indexing its own L-base
+sequence (replicas) is reported as a side record.
 
 `roofline` prices the dominant build kernel from per-kernel HIP events recorded on the stream
 the kernels run on; `traffic` comes from profiles/pmc_<config>.json (rocprofv3 --pmc passes made
@@ -499,6 +503,8 @@ def main():
         idx = D.DeviceIndex.build(seq, k, stream)
         info = idx.info() if wait else None        # info() waits for the build
         idx.free()
+        if info is not None:
+            check_build(info)
         return info
 
     # ---------------- build: W untimed warmups, 2 steps with events around every kernel (find the
@@ -536,11 +542,12 @@ def main():
     D.timing_enable(False)
     D.timing_select(None)
 
-    # ---------------- N > 1: the owner-computes build of ONE genome of N x L bases:
-    # rank 0 holds it and broadcasts it, every rank builds the k-mers of its bucket range
-    # (kmhg_build_device_part); assembling the whole index on every rank is timed once, apart
+    # ---------------- N > 1: the headline is the owner-computes build of ONE genome of N x L
+    # bases: rank 0 holds it and broadcasts it, every rank builds the k-mers of
+    # its bucket range (kmhg_build_device_part); assembling the whole index on every rank is timed
+    # once, apart.  The replicas above (every rank its own L bases) become a side record.
     sharded = None
-    if world > 1 and not args.profile:
+    if world > 1:
         sharded = bench_sharded_build(args, k, L, dev, world, rank, seed)
 
     # ---------------- query: self seq.kmer.pos against one resident index.  The first query of an
@@ -807,7 +814,31 @@ def main():
             if "k_depth_probe" in dper:
                 out["depth"]["roofline"] = _leg_roofline(
                     dper, "k_depth_probe", depth_algorithmic_bytes("k_depth_probe", L, 2))
+        out["build_path"] = {"build": info["build"], "fallback": info["fallback"],
+                             "note": "kmhg_info of the waited builds: 2 = partitioned, lane-order "
+                                     "ranks; 3 = ballot ranks (the device failed the LDS "
+                                     "lane-order self-check); 1 = global-atomic; fallback = 1 "
+                                     "would mean a rebuild (the run fails instead)"}
+        out["config"]["parallelism"] = "single" if world == 1 else f"replicas{world}"
         if sharded:
+            # the headline at N > 1: the owner-computes build of one genome
+            rep = {f: out[f] for f in ("value", "ms_per_step", "roofline")}
+            rep["parallelism"] = f"replicas{world}"
+            rep["note"] = ("every rank indexes its own L-base sequence (seed 1 + rank), no "
+                           "collective: N independent make.kmer.hash builds")
+            out["replicas"] = rep
+            out["value"] = sharded.pop("value")
+            out["ms_per_step"] = sharded.pop("ms_per_step")
+            out["roofline"] = sharded.pop("roofline")
+            out["config"]["parallelism"] = f"owner{world}"
+            out["config"]["seq_len"] = sharded["seq_len"]
+            out["config"]["distinct_kmers"] = sharded["distinct_kmers"]
+            out["config"]["positions"] = sharded["positions"]
+            out["config"]["workload"] = (f"configs[{args.config - 1}] scaled out: ONE synthetic "
+                                         f"{sharded['seq_len'] / 1e6:.0f} Mbp iid ACGT sequence "
+                                         f"(n_gpus x {L / 1e6:.0f} Mbp, splitmix64 seed "
+                                         f"{1000 + seed - rank}), k={k}, make.kmer.hash as an "
+                                         "owner-computes build over the ranks")
             out["sharded_build"] = sharded
         if not args.profile:
             out["host_boundary"] = host_boundary(host_seq.tobytes(), k)
@@ -831,15 +862,25 @@ def main():
         dist.destroy_process_group()
 
 
+def check_build(info: dict) -> None:
+    """A waited build must not have fallen back to the global-atomic rebuild (kmhg_info.fallback:
+    a bucket's LDS table overflowed or its stream failed the order check): the timed steps would
+    not include that rebuild, so the run fails instead of reporting them."""
+    if info.get("fallback"):
+        raise SystemExit(f"bench: a build fell back to the global-atomic rebuild ({info}); "
+                         "the timed steps would not measure what an R user gets")
+
+
 def bench_sharded_build(args, k, L, dev, world, rank, seed):
     """Owner-computes make.kmer.hash of one (world x L)-base sequence over the ranks: a step is
-    every rank's part build (kmhg_build_device_part), max over ranks.  Returns rank 0's record."""
+    every rank's part build (kmhg_build_device_part), max over ranks.  Returns rank 0's record
+    (value, ms_per_step and the roofline of rank 0's dominant part-build kernel included)."""
     import torch
     import torch.distributed as dist
     from kmer_hasher_amd import device as D
     from kmer_hasher_amd import dist as kd
     from kmer_hasher_amd import synth
-    big = torch.from_numpy(synth.iid(L * world, 1000 + seed)).to(dev) if rank == 0 else None
+    big = torch.from_numpy(synth.iid(L * world, 1000 + seed - rank)).to(dev) if rank == 0 else None
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -848,6 +889,16 @@ def bench_sharded_build(args, k, L, dev, world, rank, seed):
     t_bc = time.perf_counter() - t0
     for _ in range(max(1, args.warmup)):
         D.DeviceIndex.build_part(seq_all, k, rank, world).wait().free()
+    # kernel times of rank 0's part build (dominant kernel -> roofline)
+    D.timing_enable(True)
+    D.timing_select(None)
+    D.timing_reset()
+    for _ in range(2):
+        D.DeviceIndex.build_part(seq_all, k, rank, world).wait().free()
+    wt = D.timing_report()
+    per_step = {n: v[1] / 2 for n, v in wt.items() if v[0]}
+    per_launch = {n: v[1] / v[0] for n, v in wt.items() if v[0]}
+    D.timing_enable(False)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -856,15 +907,16 @@ def bench_sharded_build(args, k, L, dev, world, rank, seed):
     torch.cuda.synchronize()
     dist.barrier()
     t_part = time.perf_counter() - t0
-    part = D.DeviceIndex.build_part(seq_all, k, rank, world).wait()
-    inf = part.part_info()
+    part = D.DeviceIndex.build_part(seq_all, k, rank, world)
+    inf = kd.part_info_all(part, dev)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     idx = kd.assemble_parts(part, dev)
     torch.cuda.synchronize()
     t_asm = time.perf_counter() - t0
-    U = idx.info()["n_kmers"]
+    _ai = idx.info()
+    U, Npos = _ai["n_kmers"], _ai["n_positions"]
     idx.free()
     part.free()
     tt = torch.tensor([t_part, t_bc, t_asm], dtype=torch.float64, device=dev)
@@ -873,15 +925,25 @@ def bench_sharded_build(args, k, L, dev, world, rank, seed):
     if rank != 0:
         return None
     Ltot = L * world
+    step_ms = t_part / args.steps * 1e3
+    dom = max(per_step, key=per_step.get)
+    # rank 0's share of SURVEY.md §8(d)'s build bytes: every rank reads the whole sequence, and
+    # writes its ~1/world of the keys and positions
+    B = Ltot + (12 * U + 4 * Npos) // world
     return {"value": round(Ltot / 1e6 * args.steps / t_part, 2), "unit": "Mbp/s",
-            "ms_per_step": round(t_part / args.steps * 1e3, 4), "seq_len": Ltot, "k": k,
-            "distinct_kmers": U, "rank0_part_kmers": inf["n_kmers"],
+            "ms_per_step": round(step_ms, 4), "seq_len": Ltot, "k": k,
+            "distinct_kmers": U, "positions": Npos, "rank0_part_kmers": inf["n_kmers"],
             "sequence_broadcast_ms": round(t_bc * 1e3, 3),
             "assemble_ms": round(t_asm * 1e3, 3),
+            "rank0_kernels_ms_per_step": {n: round(v, 5) for n, v in per_step.items()},
+            "roofline": dict(roofline(B, dom, per_launch[dom], step_ms, {}), note=(
+                "rank 0's dominant part-build kernel; algorithmic_bytes = the whole sequence "
+                "(every rank reads it) + 1/n_gpus of SURVEY.md §8(d)'s key and position bytes")),
             "note": "owner-computes build of ONE sequence of n_gpus x seq_len bases: each rank "
                     "walks every window and builds the k-mers of its bucket range "
                     "(kmhg_build_device_part); the parts together are the whole index, "
-                    "assembling it on every rank (all-gather) is timed once as assemble_ms"}
+                    "assembling it on every rank (all-gather) is timed once as assemble_ms; the "
+                    "sequence broadcast (once per genome) as sequence_broadcast_ms"}
 
 
 def _emit(out):

@@ -668,7 +668,7 @@ struct kmhg_index {
   int build_kind = 0;
   int fallback = 0;
   // copies of this index on other devices for multi-device queries (KMHG_DEVICES), keyed by
-  // the query part they serve; made on first use by peer copies over xGMI, freed with the index
+  // device (one per device); made on first use by peer copies over xGMI, freed with the index
   std::map<int, kmhg_index*> replicas;
   std::mutex rep_mu;
   bool ps_failed = false;                 // guarded by ps_mu
@@ -1993,21 +1993,22 @@ kmhg_index* make_replica(kmhg_index* home, int dev) {
   return r.release();
 }
 
-kmhg_index* replica_for(kmhg_index* home, int part, int dev) {
+// The index's copy on device `dev` (one per device, shared by every query part that runs
+// there; made on first use, freed with the index).
+kmhg_index* replica_on(kmhg_index* home, int dev) {
   {
     std::lock_guard<std::mutex> lk(home->rep_mu);
-    auto it = home->replicas.find(part);
-    if (it != home->replicas.end() && it->second->device == dev) return it->second;
+    auto it = home->replicas.find(dev);
+    if (it != home->replicas.end()) return it->second;
   }
-  kmhg_index* r = make_replica(home, dev);          // outside the lock: parts copy in parallel
-  kmhg_index* old = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(home->rep_mu);
-    auto& slot = home->replicas[part];
-    old = slot;                                     // a replica on another device (env changed)
-    slot = r;
+  kmhg_index* r = make_replica(home, dev);          // outside the lock: devices copy in parallel
+  std::lock_guard<std::mutex> lk(home->rep_mu);
+  auto& slot = home->replicas[dev];
+  if (slot) {                                       // another thread made it meanwhile
+    free_index(r);
+    return slot;
   }
-  if (old) free_index(old);
+  slot = r;
   return r;
 }
 
@@ -2025,10 +2026,14 @@ kmhg_query* query_multi_device(kmhg_index* idx, const char* seq, int64_t L, int 
   std::vector<kmhg_query*> parts(G, nullptr);
   std::vector<Error> errs(G, Error{KMHG_OK, ""});
   const bool poison = std::getenv("KMHG_SLICE_POISON") != nullptr;   // tests: garbage outside
+  // tests: parts after the first on the index's own device use a same-device replica, so the
+  // copy path runs on a one-GPU box too
+  const bool test_replica = std::getenv("KMHG_TEST_REPLICA") != nullptr;
   auto run = [&](int i) {
     try {
       const int64_t w0 = Nw * i / G, w1 = Nw * (i + 1) / G;
-      kmhg_index* use = (i == 0 && devs[0] == idx->device) ? idx : replica_for(idx, i, devs[i]);
+      const bool home = devs[i] == idx->device && !(test_replica && i > 0);
+      kmhg_index* use = home ? idx : replica_on(idx, devs[i]);
       DeviceGuard g(devs[i]);
       hipStream_t s = lib_stream();
       // a full-length buffer holding only chars [a, b): the window rule of windows [w0, w1)
@@ -2047,9 +2052,18 @@ kmhg_query* query_multi_device(kmhg_index* idx, const char* seq, int64_t L, int 
       errs[i] = Error{KMHG_ENOMEM, "host allocation failed"};
     }
   };
+  // one host thread per distinct device; the parts of one device run in order on its thread
+  // (they share that device's stream and index copy)
+  std::vector<int> uniq;
+  for (int d : devs)
+    if (std::find(uniq.begin(), uniq.end(), d) == uniq.end()) uniq.push_back(d);
+  auto run_device = [&](int d) {
+    for (int i = 0; i < G; ++i)
+      if (devs[i] == d) run(i);
+  };
   std::vector<std::thread> th;
-  for (int i = 1; i < G; ++i) th.emplace_back(run, i);
-  run(0);
+  for (size_t u = 1; u < uniq.size(); ++u) th.emplace_back(run_device, uniq[u]);
+  run_device(uniq[0]);
   for (auto& t : th) t.join();
   q->parts = parts;                                  // freed with q, also on the error path
   for (int i = 0; i < G; ++i)

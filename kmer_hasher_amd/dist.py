@@ -161,6 +161,25 @@ def owner_build(seq: torch.Tensor | None, k: int, device: torch.device, src: int
     return DeviceIndex.build_part(seq, k, rank, world, stream), seq
 
 
+def part_info_all(part, device: torch.device, group=None) -> dict:
+    """part.part_info() (which waits for the part build) on every rank, or an error on EVERY
+    rank: a part whose bucket overflowed raises on its own rank only, and the other ranks would
+    otherwise block forever in the next collective.  The status goes round first (all-reduce
+    MIN), so all ranks raise together."""
+    err = None
+    try:
+        mine = part.part_info()
+    except Exception as e:                  # KmhgError (overflow) or a device error
+        err, mine = e, None
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    if err is not None:
+        raise err
+    if not int(ok.item()):
+        raise RuntimeError("owner-computes build: another rank's part build failed")
+    return mine
+
+
 def assemble_parts(part, device: torch.device, group=None, import_fn=None):
     """All ranks' parts -> the whole index on every rank (all-gather of the rebased slot ranges
     and of the positions, the side slot and code block from their owners), imported with
@@ -168,7 +187,7 @@ def assemble_parts(part, device: torch.device, group=None, import_fn=None):
     from .device import PART_FIELDS, SLOT_BYTES, DeviceIndex
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    mine = part.part_info()
+    mine = part_info_all(part, device, group)
     t = torch.tensor([mine[f] for f in PART_FIELDS], dtype=torch.int64, device=device)
     got = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(got, t, group=group)

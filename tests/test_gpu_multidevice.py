@@ -2,10 +2,11 @@
 "Config / flags"; reference .Call("sequence_kmer_positions"), src/kmer_hash.c:1151-1172).
 
 With KMHG_DEVICES=d0,d1,... the host-pointer kmhg_query_run splits the query's windows over the
-listed devices in one process: the index is peer-copied to each device once (a replica per
-part; with "0,0" the second part's replica is a copy on device 0, so the copy path runs on a
-one-GPU box too), each device receives only its slice of the host sequence, and kmhg_query_fill
-writes every part straight into the caller's buffer.  KMHG_SLICE_POISON fills each device's
+listed devices in one process: the index is peer-copied to each other device once (one replica
+per device, shared by that device's parts, which run in order on its host thread; the index's
+own device uses the index itself -- KMHG_TEST_REPLICA makes its later parts use a same-device
+copy, so the copy path runs on a one-GPU box too), each device receives only its slice of the
+host sequence, and kmhg_query_fill writes every part straight into the caller's buffer.  KMHG_SLICE_POISON fills each device's
 sequence buffer with 'A' outside its slice, so a window that read past its slice would show.
 Rows must equal the oracle's unsharded rows, order included."""
 import ctypes as C
@@ -23,10 +24,13 @@ def _devices_list(torch, reps):
     return ",".join(str(i % n) for i in range(reps))
 
 
+@pytest.mark.parametrize("replica", ["copy", "home"])
 @pytest.mark.parametrize("reps", [2, 3, 8])
-def test_kmhg_devices_query_matches_oracle(gpu, monkeypatch, reps):
+def test_kmhg_devices_query_matches_oracle(gpu, monkeypatch, reps, replica):
     from kmer_hasher_amd import make_kmer_hash, seq_kmer_pos, synth
     monkeypatch.setenv("KMHG_DEVICES", _devices_list(gpu, reps))
+    if replica == "copy":
+        monkeypatch.setenv("KMHG_TEST_REPLICA", "1")
     monkeypatch.setenv("KMHG_SLICE_POISON", "1")
     A = synth.add_n_runs(synth.iid(400_000, 71), 0.0005, 72, max_run=40)
     A[-32] = ord("N")                          # end-drop case in the last part
@@ -56,6 +60,7 @@ def test_kmhg_devices_device_readers(gpu, monkeypatch):
     import torch
     from kmer_hasher_amd import _lib, make_kmer_hash, synth
     monkeypatch.setenv("KMHG_DEVICES", _devices_list(gpu, 3))
+    monkeypatch.setenv("KMHG_TEST_REPLICA", "1")
     s = synth.iid(200_000, 81).tobytes()
     oi = O.OracleIndex(s, 25)
     want = oi.query(s, 25)
