@@ -1096,11 +1096,12 @@ struct Words3 {                                // three consecutive code words, 
   uint32_t a, b, c;
 };
 template <bool COUNT_ONLY, bool CK, bool BALLOT>
-__global__ void __launch_bounds__(BLOCK, BALLOT ? 6 : 2048 / BLOCK)   // 8 workgroups per CU (LDS)
+__global__ void __launch_bounds__(BLOCK, BALLOT ? 4 : 2048 / BLOCK)   // 8 workgroups per CU (LDS)
 k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
                int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
-               BuildMeta* __restrict__ meta, const uint32_t* __restrict__ code, int k) {
+               BuildMeta* __restrict__ meta, const uint32_t* __restrict__ code, int k,
+               const uint32_t* __restrict__ n_ptr, uint32_t nw) {
   static_assert(!(CK && COUNT_ONLY), "code-word keys belong to position builds");
   static_assert(V2_CAPW % BLOCK == 0, "the side slot V2_CAPW is slot q = V2_CAPW / TB of thread 0");
   constexpr int TB = BLOCK;
@@ -1116,6 +1117,12 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   constexpr uint32_t BATCH = TB * PER;
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const uint32_t s0 = start[b], s1 = start[b + 1];
+  // a bucket range outside the stream (a bounds error) is reported like an overflow, never
+  // dereferenced: the index is rebuilt by the global-atomic build
+  if (s0 > s1 || s1 > *n_ptr) {
+    if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
+    return;
+  }
   const bool one_batch = s1 - s0 <= BATCH;
   uint64_t key[PER];
   uint32_t ps[PER];
@@ -1137,7 +1144,9 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
       }
 #pragma unroll
       for (int c = 0; c < PER; ++c) {       // one 12-B load per window (global_load_dwordx3)
-        const Words3 w3 = *reinterpret_cast<const Words3*>(code + ((ps[c] - 1u) >> 4));
+        // clamped: a position outside [1, nw] (a stream error, flagged in pass A) never
+        // turns into a code-word address outside the array
+        const Words3 w3 = *reinterpret_cast<const Words3*>(code + (min(ps[c] - 1u, nw - 1u) >> 4));
         wa[c] = w3.a;
         wb[c] = w3.b;
         wc[c] = w3.c;
@@ -1149,6 +1158,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
       const uint32_t i = elem(i0, c);
       key[c] = i < s1 ? keys[i] : 0;
       ps[c] = (!COUNT_ONLY && i < s1) ? pos[i] : 0;
+      if (!COUNT_ONLY && i < s1 && ps[c] - 1u >= nw) disorder = true;   // outside [1, nw]
       if (!COUNT_ONLY && !one_batch) disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
     }
   };
@@ -1187,6 +1197,11 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
         if (slot[c] < 0) ovf = true;
         else atomicAdd(&W.val[slot[c]], 1u);
       }
+    }
+    if (CK) {                      // positions in [1, nw] (checked after the cut: fewer live VGPRs)
+#pragma unroll
+      for (int c = 0; c < PER; ++c)
+        if (elem(i0, c) < s1 && ps[c] - 1u >= nw) disorder = true;
     }
   }
   // Stream order of a one-batch bucket (multi-batch buckets check it with a neighbour load per
@@ -1611,23 +1626,24 @@ void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint3
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         bool count_only, hipStream_t s, const uint32_t* code, int k) {
+                         bool count_only, hipStream_t s, const uint32_t* n_ptr, uint32_t nw,
+                         const uint32_t* code, int k) {
   const bool ballot = ballot_ranks();
   if (count_only)              // no positions: nothing is ranked
     hipLaunchKernelGGL((k_v2_bucket_wg<true, false, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, nullptr, 0);
+                       pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
   else if (code && !ballot)
     hipLaunchKernelGGL((k_v2_bucket_wg<false, true, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, code, k);
+                       pos, start, g, T, positions, bstats, meta, code, k, n_ptr, nw);
   else if (code)
     hipLaunchKernelGGL((k_v2_bucket_wg<false, true, true>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, code, k);
+                       pos, start, g, T, positions, bstats, meta, code, k, n_ptr, nw);
   else if (!ballot)
     hipLaunchKernelGGL((k_v2_bucket_wg<false, false, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, nullptr, 0);
+                       pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
   else
     hipLaunchKernelGGL((k_v2_bucket_wg<false, false, true>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, nullptr, 0);
+                       pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
 }
 // The hardware property the radix passes' ranks rest on, checked on the device itself
 // (tools/lds_order.hip is the stand-alone probe): the lanes of one returning LDS add that hit
@@ -1665,20 +1681,28 @@ void launch_lane_order_check(unsigned long long* res, hipStream_t s, int blocks)
   hipLaunchKernelGGL(k_lane_order_check, dim3(blocks), dim3(BLOCK), 0, s, res, 12345u, 64);
 }
 
-// Test knob (KMHG_TEST_DISORDER=1, tests only): swaps the first two positions of bucket 0's
-// stream, so the bucket kernel's order check must report it and the build fall back.
-__global__ void k_v2_test_disorder(uint32_t* __restrict__ pos, const uint32_t* __restrict__ start) {
+// Test knob (KMHG_TEST_DISORDER=<mode>, tests only), each of which the bucket kernel must report
+// (the build then falls back) instead of faulting: 1 swaps the first two positions of bucket 0's
+// stream; 2 zeroes its first position (an entry no pass wrote: the pad's value); 3 moves bucket
+// 1's start past the end of the stream.
+__global__ void k_v2_test_disorder(uint32_t* __restrict__ pos, uint32_t* __restrict__ start,
+                                   const uint32_t* __restrict__ n_ptr, int mode) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     const uint32_t a = start[0], b = start[1];
-    if (b - a >= 2) {
+    if (mode == 1 && b - a >= 2) {
       const uint32_t t = pos[a];
       pos[a] = pos[a + 1];
       pos[a + 1] = t;
+    } else if (mode == 2 && b > a) {
+      pos[a] = 0u;
+    } else if (mode == 3) {
+      start[1] = *n_ptr + 4096u;
     }
   }
 }
-void launch_v2_test_disorder(uint32_t* pos, const uint32_t* start, hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_test_disorder, dim3(1), dim3(64), 0, s, pos, start);
+void launch_v2_test_disorder(uint32_t* pos, uint32_t* start, const uint32_t* n_ptr, int mode,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(k_v2_test_disorder, dim3(1), dim3(64), 0, s, pos, start, n_ptr, mode);
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {

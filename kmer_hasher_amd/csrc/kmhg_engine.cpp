@@ -1061,12 +1061,14 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   HIPC(hipMemsetAsync(stamps, 0, sizeof(uint64_t) * 8 * nb, s));
   kmhg::set_stamp_buffer(stamps);
 #endif
-  // tests only: bucket 0's stream out of order -> the bucket kernel's check -> v1 rebuild
-  if (!no_pos && std::getenv("KMHG_TEST_DISORDER") && std::getenv("KMHG_TEST_DISORDER")[0] == '1')
-    launch_v2_test_disorder(pin, start.p, s);
+  // tests only: a corrupted stream or bound (KMHG_TEST_DISORDER=1|2|3) -> the bucket kernel's
+  // checks -> v1 rebuild
+  if (const char* td = std::getenv("KMHG_TEST_DISORDER"))
+    if (!no_pos && td[0] >= '1' && td[0] <= '3')
+      launch_v2_test_disorder(pin, start.p, n_valid, td[0] - '0', s);
   LAUNCH("k_v2_bucket_wg", s,
          launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, bstats.p,
-                             meta, no_pos, s, bid ? db.code : nullptr, k));
+                             meta, no_pos, s, n_valid, (uint32_t)Nw, bid ? db.code : nullptr, k));
   LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, gb.nb, n_valid, meta, idx->rec.meta, s));
   HIPC(hipEventRecord(idx->rec.ev, s));
 #ifdef KMHG_STAMPS

@@ -229,13 +229,14 @@ struct BucketStats {           // per-bucket partials of the build statistics
 // code (bucket-id streams): keys unused, each window's key cut from the code words at its pos
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
-                         bool count_only, hipStream_t s, const uint32_t* code = nullptr,
-                         int k = 0);
+                         bool count_only, hipStream_t s, const uint32_t* n_ptr, uint32_t nw,
+                         const uint32_t* code = nullptr, int k = 0);
 // ballot_ranks(): the current device fails the LDS lane-order self-check (or KMHG_TEST_BALLOT):
 // the radix passes and the bucket kernel then rank with ballots (kmhg_engine.cpp)
 bool ballot_ranks();
 void launch_lane_order_check(unsigned long long* res, hipStream_t s, int blocks = 1024);
-void launch_v2_test_disorder(uint32_t* pos, const uint32_t* start, hipStream_t s);
+void launch_v2_test_disorder(uint32_t* pos, uint32_t* start, const uint32_t* n_ptr, int mode,
+                             hipStream_t s);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);
 

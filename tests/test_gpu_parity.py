@@ -251,21 +251,27 @@ def test_build_kind_reported(gpu, monkeypatch):
         monkeypatch.delenv(env[0])
 
 
-@pytest.mark.parametrize("stream", ["bid", "keys"])
-def test_stream_disorder_falls_back(gpu, monkeypatch, stream):
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
+@pytest.mark.parametrize("stream", ["bid", "keys", "keyswc"])
+def test_stream_disorder_falls_back(gpu, monkeypatch, stream, mode):
     """The radix passes are stable because same-address LDS count atomics of one instruction
-    are served in lane order (tools/lds_order.hip); the bucket kernels check that every
-    bucket's stream is in ascending position order.  KMHG_TEST_DISORDER swaps two positions of
-    bucket 0's stream: the check must report it, and the index is rebuilt by the global-atomic
-    build (image header: one bucket) with results equal to the oracle."""
+    are served in lane order (checked on the device before the first build); the bucket kernel
+    also checks that its stream ascends in position, that every position lies in [1, windows],
+    that every key hashes to the bucket, and that the bucket's range lies inside the stream.
+    KMHG_TEST_DISORDER corrupts the stream after the passes: 1 swaps two positions of bucket 0,
+    2 zeroes one (an entry no pass wrote -- the value a bid-stream build used to turn into a
+    code-word address 1 GB out of range), 3 moves bucket 1's start past the stream's end.  Each
+    must be reported, never faulted on: the index is rebuilt by the global-atomic build (image
+    header: one bucket; kmhg_info.fallback = 1) with results equal to the oracle."""
     import torch
     from kmer_hasher_amd import synth
     from kmer_hasher_amd.device import DeviceIndex
     from kmer_hasher_amd import _lib
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
+    monkeypatch.setenv("KMHG_SCATTER_WC", "1" if stream == "keyswc" else "0")
     s = synth.add_n_runs(synth.iid(300_000, 51), 0.002, 9).tobytes().decode("latin-1")
     seq = torch.frombuffer(bytearray(s.encode("latin-1")), dtype=torch.uint8).cuda()
-    for disorder, one_bucket in (("0", False), ("1", True)):
+    for disorder, one_bucket in (("0", False), (mode, True)):
         monkeypatch.setenv("KMHG_TEST_DISORDER", disorder)
         idx = DeviceIndex.build(seq, 31).wait()
         meta, _ = idx.export_image()
