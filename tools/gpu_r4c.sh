@@ -11,7 +11,7 @@ cd "$REPO"
 timeout -k 10 1000 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_r_glue.py \
   tests/test_gpu_multidevice.py tests/test_gpu_parts.py tests/test_gpu_dist.py -m gpu -x -v \
   --timeout 300 --timeout-method thread -p no:cacheprovider \
-  -k "bucket_kernels or multi_pass or disorder or build_kind or lane_order or golden or config3 or config2 or config4 or glue or multidevice or kmhg_devices or part or dist" \
+  -k "${R4C_K:-bucket_kernels or multi_pass or disorder or build_kind or lane_order or golden or config3 or config2 or config4 or glue or multidevice or kmhg_devices or part or dist}" \
   > "$OUT/pytest.log" 2>&1 || { echo "tests failed"; tail -40 "$OUT/pytest.log"; exit 1; }
 tail -3 "$OUT/pytest.log"
 timeout -k 10 700 bash tools/ab.sh "KMHG_SCATTER_WC=0" "KMHG_SCATTER_WC=1" -- --config 3 --steps 5 --warmup 2 --no-cpu \
