@@ -749,13 +749,12 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
 // registers) writes the waiting elements of a line that completes, the tile's write-out the
 // rest, in the same tile: the line is whole in L2 before it is written back.  Only the first and
 // last line of a digit's range in a chunk are ever partial.
-constexpr int WC_NW = 8;                        // waves per workgroup (512 threads)
-constexpr int WC_TB = WC_NW * 64;
-constexpr uint32_t WC_KL = 16;                  // keys per 128-B line
-constexpr uint32_t WC_PL = 32;                  // positions per 128-B line
+// Geometry variants (A/B, KMHG_SCATTER_WC_GEOM): NW waves per workgroup, KL keys / PL positions
+// per written granule (16 / 32 = whole 128-B lines, 8 / 16 = 64-B halves).
+template <int NW, uint32_t KL, uint32_t PL>
 struct WcLDS {
   static constexpr uint32_t MAXR = V2_MAXR_IL;
-  uint32_t wc[WC_NW][MAXR];    // per-wave digit counts -> per-wave tile-local cursors
+  uint32_t wc[NW][MAXR];       // per-wave digit counts -> per-wave tile-local cursors
   uint32_t tstart[MAXR];       // tile-local start of each digit
   uint32_t ocur[MAXR];         // global index of the digit's first element of this tile
   uint32_t nk0[MAXR];          // keys at global index >= nk0 wait in PK after this tile
@@ -763,11 +762,10 @@ struct WcLDS {
   uint64_t skey[PTILE];
   uint32_t spos[PTILE];
   uint16_t sdig[PTILE];
-  __attribute__((aligned(16))) uint64_t PK[MAXR][WC_KL];
-  __attribute__((aligned(16))) uint32_t PP[MAXR][WC_PL];
+  __attribute__((aligned(16))) uint64_t PK[MAXR][KL];
+  __attribute__((aligned(16))) uint32_t PP[MAXR][PL];
   PStage st;
 };
-static_assert(V2_MAXR_IL <= WC_TB, "one digit per thread");
 
 // elements [0, n) of a pending row to out[g0 ..): 16-B stores where g0 allows
 template <class T>
@@ -781,19 +779,22 @@ __device__ __forceinline__ void wc_flush(T* __restrict__ out, uint64_t g0, const
   for (; j < n; ++j) out[g0 + j] = row[j];
 }
 
-template <bool FROM_SEQ, bool BALLOT>
-__global__ void __launch_bounds__(WC_TB)
+template <bool FROM_SEQ, bool BALLOT, int NW, uint32_t KL, uint32_t PL>
+__global__ void __launch_bounds__(NW * 64)
 k_v2_scatter_wc(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
                 const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
                 const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
                 const uint32_t* __restrict__ hist, uint32_t ntiles,
                 uint64_t* __restrict__ kout, uint32_t* __restrict__ pout) {
-  constexpr int PER = PTILE / WC_TB;            // elements per lane
-  __shared__ WcLDS S;
-  __shared__ uint64_t sh[WC_NW];
+  constexpr int TB = NW * 64;
+  constexpr int PER = PTILE / TB;               // elements per lane
+  using SL = WcLDS<NW, KL, PL>;
+  constexpr int DPT = (int)((SL::MAXR + TB - 1) / TB);   // digits owned per thread
+  __shared__ SL S;
+  __shared__ uint64_t sh[NW];
   const uint32_t R = D.R;
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const uint32_t wbase = (uint32_t)wave * (PTILE / WC_NW);
+  const uint32_t wbase = (uint32_t)wave * (PTILE / NW);
   const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
   // chunk of consecutive tiles; neighbouring chunks on one XCD
   const uint32_t G = gridDim.x;
@@ -802,10 +803,13 @@ k_v2_scatter_wc(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
   const uint32_t t_begin = min(chunk * m, ntiles), t_end = min(t_begin + m, ntiles);
   if (t_begin >= t_end) return;
   const uint32_t n_iter = t_end - t_begin;
-  // the owner thread's digit state (registers)
-  const uint32_t d_own = threadIdx.x;
-  uint32_t gcur = 0, pk0 = 0, pp0 = 0;
-  if (d_own < R) gcur = pk0 = pp0 = hist[(size_t)d_own * ntiles + t_begin];
+  // thread t owns digits [DPT t, DPT t + DPT): their cursors and waiting starts in registers
+  uint32_t gcur[DPT], pk0[DPT], pp0[DPT];
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) {
+    const uint32_t d = threadIdx.x * DPT + q;
+    gcur[q] = pk0[q] = pp0[q] = d < R ? hist[(size_t)d * ntiles + t_begin] : 0u;
+  }
   uint64_t nkey[PER];
   uint32_t npos[PER];
   StageRegs<PSTAGE_W16> nchars;
@@ -868,34 +872,46 @@ k_v2_scatter_wc(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
     }
     __syncthreads();
-    // digit phase: thread d owns digit d
-    uint32_t nd = 0;
-    if (d_own < R) {
+    // digit phase: the owner of each digit
+    uint32_t nd[DPT];
+    uint64_t own = 0;
 #pragma unroll
-      for (int w = 0; w < WC_NW; ++w) nd += S.wc[w][d_own];
+    for (int q = 0; q < DPT; ++q) {
+      const uint32_t d = threadIdx.x * DPT + q;
+      nd[q] = 0;
+      if (d < R) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) nd[q] += S.wc[w][d];
+      }
+      own += nd[q];
     }
     uint64_t tile_n;
-    const uint32_t ts = (uint32_t)block_excl_scan_n<WC_NW>(nd, sh, tile_n);
-    if (d_own < R) {
-      S.tstart[d_own] = ts;
-      uint32_t cur = ts;
+    uint32_t ts = (uint32_t)block_excl_scan_n<NW>(own, sh, tile_n);
 #pragma unroll
-      for (int w = 0; w < WC_NW; ++w) {
-        const uint32_t t = S.wc[w][d_own];
-        S.wc[w][d_own] = cur;
-        cur += t;
+    for (int q = 0; q < DPT; ++q) {
+      const uint32_t d = threadIdx.x * DPT + q;
+      if (d < R) {
+        S.tstart[d] = ts;
+        uint32_t cur = ts;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const uint32_t t = S.wc[w][d];
+          S.wc[w][d] = cur;
+          cur += t;
+        }
+        ts += nd[q];
+        const uint32_t end = gcur[q] + nd[q];
+        const uint32_t nk = max(end & ~(KL - 1), pk0[q]), np = max(end & ~(PL - 1), pp0[q]);
+        // a granule completes: its waiting elements go out now, the new ones in the write-out
+        if (nk > pk0[q]) wc_flush(kout, pk0[q], S.PK[d], gcur[q] - pk0[q]);
+        if (np > pp0[q]) wc_flush(pout, pp0[q], S.PP[d], gcur[q] - pp0[q]);
+        S.ocur[d] = gcur[q];
+        S.nk0[d] = nk;
+        S.np0[d] = np;
+        gcur[q] = end;
+        pk0[q] = nk;
+        pp0[q] = np;
       }
-      const uint32_t end = gcur + nd;
-      const uint32_t nk = max(end & ~(WC_KL - 1), pk0), np = max(end & ~(WC_PL - 1), pp0);
-      // a line completes: its waiting elements go out now, the new ones in the write-out
-      if (nk > pk0) wc_flush(kout, pk0, S.PK[d_own], gcur - pk0);
-      if (np > pp0) wc_flush(pout, pp0, S.PP[d_own], gcur - pp0);
-      S.ocur[d_own] = gcur;
-      S.nk0[d_own] = nk;
-      S.np0[d_own] = np;
-      gcur = end;
-      pk0 = nk;
-      pp0 = np;
     }
     __syncthreads();                       // bases ready; old waiting elements read
     if (!BALLOT) {
@@ -933,7 +949,7 @@ k_v2_scatter_wc(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
     // write-out, run by run: elements below the digit's waiting start go to HBM, the rest wait
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const uint32_t i = (uint32_t)(j * WC_TB) + threadIdx.x;
+      const uint32_t i = (uint32_t)(j * TB) + threadIdx.x;
       if (i < (uint32_t)tile_n) {
         const uint32_t d = S.sdig[i];
         const uint32_t gi = S.ocur[d] + (i - S.tstart[d]);
@@ -946,9 +962,13 @@ k_v2_scatter_wc(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
     }
   }
   __syncthreads();                         // the last tile's waiting elements are in LDS
-  if (d_own < R) {                         // the chunk's last, partial lines
-    wc_flush(kout, pk0, S.PK[d_own], gcur - pk0);
-    wc_flush(pout, pp0, S.PP[d_own], gcur - pp0);
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) {          // the chunk's last, partial granules
+    const uint32_t d = threadIdx.x * DPT + q;
+    if (d < R) {
+      wc_flush(kout, pk0[q], S.PK[d], gcur[q] - pk0[q]);
+      wc_flush(pout, pp0[q], S.PP[d], gcur[q] - pp0[q]);
+    }
   }
 }
 
@@ -1545,29 +1565,43 @@ void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geo
   KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
                kout, pout, pad, 0);
 }
-// write-combined passes (k_v2_scatter_wc): one workgroup per CU, each over a chunk of tiles
-#define KMHG_SCATTER_WC(FS, ...)                                                              \
-  do {                                                                                       \
-    if (ballot_ranks()) {                                                                    \
-      static const unsigned cap_ = resident_blocks((const void*)k_v2_scatter_wc<FS, true>, WC_TB); \
-      hipLaunchKernelGGL((k_v2_scatter_wc<FS, true>), dim3(std::min(ntiles, cap_)), dim3(WC_TB), \
-                         0, s, __VA_ARGS__);                                                 \
-    } else {                                                                                 \
-      static const unsigned cap_ = resident_blocks((const void*)k_v2_scatter_wc<FS, false>, WC_TB); \
-      hipLaunchKernelGGL((k_v2_scatter_wc<FS, false>), dim3(std::min(ntiles, cap_)), dim3(WC_TB), \
-                         0, s, __VA_ARGS__);                                                 \
-    }                                                                                        \
-  } while (0)
+// write-combined passes (k_v2_scatter_wc): persistent workgroups, each over a chunk of tiles.
+// KMHG_SCATTER_WC_GEOM (A/B): 0 = 8 waves, 128-B granules (1 workgroup / CU); 1 = 4 waves,
+// 64-B granules (2 / CU); 2 = 16 waves, 128-B granules (1 / CU)
+static int wc_geom() {
+  const char* e = std::getenv("KMHG_SCATTER_WC_GEOM");
+  return e ? std::atoi(e) : 0;
+}
+template <bool FS, bool B, int NW, uint32_t KL, uint32_t PL, class... A>
+static void launch_wc_one(uint32_t ntiles, hipStream_t s, A... args) {
+  static const unsigned cap = resident_blocks((const void*)k_v2_scatter_wc<FS, B, NW, KL, PL>, NW * 64);
+  hipLaunchKernelGGL((k_v2_scatter_wc<FS, B, NW, KL, PL>), dim3(std::min(ntiles, cap)),
+                     dim3(NW * 64), 0, s, args...);
+}
+template <bool FS, class... A>
+static void launch_wc(uint32_t ntiles, hipStream_t s, A... args) {
+  const int geom = wc_geom();
+  if (ballot_ranks()) {
+    if (geom == 1) launch_wc_one<FS, true, 4, 8, 16>(ntiles, s, args...);
+    else if (geom == 2) launch_wc_one<FS, true, 16, 16, 32>(ntiles, s, args...);
+    else launch_wc_one<FS, true, 8, 16, 32>(ntiles, s, args...);
+  } else {
+    if (geom == 1) launch_wc_one<FS, false, 4, 8, 16>(ntiles, s, args...);
+    else if (geom == 2) launch_wc_one<FS, false, 16, 16, 32>(ntiles, s, args...);
+    else launch_wc_one<FS, false, 8, 16, 32>(ntiles, s, args...);
+  }
+}
 void launch_v2_scatter_seq_wc(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                               const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                               uint32_t* pout, hipStream_t s) {
-  KMHG_SCATTER_WC(true, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles, kout, pout);
+  launch_wc<true>(ntiles, s, seq, L, k, Nw, (const uint64_t*)nullptr, (const uint32_t*)nullptr,
+                  (const uint32_t*)nullptr, g, D, hist, ntiles, kout, pout);
 }
 void launch_v2_scatter_wc(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                           Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                           uint32_t* pout, hipStream_t s) {
-  KMHG_SCATTER_WC(false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D, hist, ntiles,
-                  kout, pout);
+  launch_wc<false>(ntiles, s, (const uint8_t*)nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr,
+                   g, D, hist, ntiles, kout, pout);
 }
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
                             const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
