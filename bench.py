@@ -1020,6 +1020,7 @@ def bench_readout(args, cfg, dev, world, rank):
                                                     if v[0] and n in ("k_read_first", "k_read_order")}},
                "roofline": roofline(B, dom, per[dom], t / args.steps * 1e3, pmc, ab, launches),
                "cpu_baseline": cpu,
+               "index_build": build_rec,
                "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
     idx.free()
 
@@ -1150,6 +1151,39 @@ def bench_sharded_query(args, cfg, dev, world, rank):
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     t, p_b, p_q, p_g = tt.tolist()
+    # the 500 Mbp index build itself (make.kmer.hash of A), rank 0: per-kernel times of one
+    # build, then BUILD5_STEPS timed builds (each waited for and freed)
+    build_rec = None
+    if rank == 0 and not args.profile:
+        ta = torch.from_numpy(synth.iid(L, 4)).to(dev)
+        D.DeviceIndex.build(ta, k).wait().free()
+        D.timing_enable(True)
+        D.timing_select(None)
+        D.timing_reset()
+        D.DeviceIndex.build(ta, k).wait().free()
+        bper = {n: v[1] for n, v in D.timing_report().items() if v[0]}
+        D.timing_enable(False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(BUILD5_STEPS):
+            bi = D.DeviceIndex.build(ta, k)
+            binfo = bi.info()
+            bi.free()
+            check_build(binfo)
+        torch.cuda.synchronize()
+        tb5 = (time.perf_counter() - t0) / BUILD5_STEPS
+        del ta
+        bdom = max(bper, key=bper.get)
+        build_rec = {"value": round(L / 1e6 / tb5, 2), "unit": "Mbp/s",
+                     "ms_per_build": round(tb5 * 1e3, 3), "builds": BUILD5_STEPS,
+                     "kernels_ms_per_build": {n: round(v, 4) for n, v in bper.items()},
+                     "kernel_ms_sum": round(sum(bper.values()), 4),
+                     "roofline": roofline(survey_bytes("build", L=L, U=binfo["n_kmers"],
+                                                       N=binfo["n_positions"]),
+                                          bdom, bper[bdom], tb5 * 1e3, {}),
+                     "build_path": {"build": binfo["build"], "fallback": binfo["fallback"]},
+                     "note": "make.kmer.hash of A alone (500 Mbp, k=31), each build waited for "
+                             "and freed; kernels_ms from HIP events of one build"}
     if rank == 0:
         per = {n: v[1] / v[0] for n, v in kt.items() if v[0]}
         launches = {n: v[0] / args.steps for n, v in kt.items() if v[0]}
@@ -1176,6 +1210,7 @@ def bench_sharded_query(args, cfg, dev, world, rank):
                "roofline": roofline(B_rank, dom, per[dom], t / args.steps * 1e3, _load_pmc(5),
                                     ab, launches),
                "cpu_baseline": cpu,
+               "index_build": build_rec,
                "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
     index.free()
 
@@ -1183,6 +1218,23 @@ def bench_sharded_query(args, cfg, dev, world, rank):
 # config 5's CPU baseline: the reference on a prefix of A and of B (the whole 500 Mbp index needs
 # ~65 GB and minutes of one core)
 CONFIG5_CPU_BP = 20_000_000
+BUILD5_STEPS = 3
+
+
+def _whole_size_config5():
+    """The reference itself on the WHOLE 500 Mbp A / B (tools/ref_config5.py, run once on a GPU
+    box's host: ~65 GB, 3.5 minutes of one core), recorded in profiles/rd4e_ref_config5.json;
+    cited beside the bounded sample, not re-run by every bench."""
+    try:
+        r = json.load(open(os.path.join(ROOT, "profiles", "rd4e_ref_config5.json")))
+        c = r["cpu"]
+        return {"query_value": c["query_mbps"], "build_value": c["build_mbps"], "unit": "Mbp/s",
+                "cores": c["cores"], "build_s": c["build_s"], "query_s": c["query_s"],
+                "teardown_s": c["teardown_s"], "rows": r["query"]["31"]["H"],
+                "rows_sha256": r["query"]["31"]["sha"], "host": c.get("host"),
+                "source": "profiles/rd4e_ref_config5.json (tools/ref_config5.py)"}
+    except Exception:
+        return None
 
 
 def cpu_query_baseline(a: bytes, b: bytes, k: int) -> dict:
@@ -1208,7 +1260,8 @@ def cpu_query_baseline(a: bytes, b: bytes, k: int) -> dict:
                           f"{len(a) / 1e6:.0f} Mbp prefix of A, k={k}, oracle/_ref gcc -O2, "
                           "1 thread pinned",
                 "query_s": round(t_q, 3), "query_rows": n, "build_s": round(t_build, 3),
-                "teardown_s": round(t_free, 3), "host": host_info()}
+                "teardown_s": round(t_free, 3), "host": host_info(),
+                "whole_size_reference": _whole_size_config5()}
     except Exception as e:  # reported, never required
         return {"value": None, "unit": "Mbp/s", "cores": 1, "kind": "reference",
                 "sample": f"unavailable: {e}"}

@@ -535,7 +535,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, uint32_t ntiles,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad,
-             int skip_empty) {
+             int skip_empty, BoundsFuse bf) {
   using KT = typename std::conditional<BM != 0, uint32_t, uint64_t>::type;
   using SL = ScatterLDS<KT>;
   static_assert(BM == 0 || !NOPOS, "bucket-id streams carry positions");
@@ -566,6 +566,11 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
       ngb[q] = hist[(size_t)d * ntiles + tv];
     }
   };
+  // the folded bucket-start work (last pass only), before any tile's loads are issued
+  if (bf.start)
+    for (uint32_t lo = blockIdx.x; lo < bf.div; lo += gridDim.x)
+      bounds_lo_body(lo, &S.wc[0][0], bf.kprev, *n_ptr, g, bf.Dlast, bf.div, hist, ntiles,
+                     bf.lo_start, bf.spread, bf.start, bf.bid, TB);
   // the next tile's inputs are in flight while this one is processed
   KT nkey[PER];
   uint32_t npos[PER];
@@ -1026,24 +1031,23 @@ k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_pt
 // by V_hist) and t = P_lo / PTILE: one workgroup per lo value counts at most one partial tile.
 // Interleaved schedule only (one histogram column per tile).  `spread` (count-only builds):
 // start[b / spread] for the buckets b that are multiples of spread.
-__global__ void __launch_bounds__(BLOCK)
-k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ n_ptr, Geom g,
-               Digit Dlast, uint32_t div, const uint32_t* __restrict__ hist, uint32_t C,
-               const uint32_t* __restrict__ lo_start, uint32_t spread,
-               uint32_t* __restrict__ start, int bid) {
-  __shared__ uint32_t cnt[V2_MAXR];
-  const uint32_t lo = blockIdx.x;
+__device__ __forceinline__ void bounds_lo_body(uint32_t lo, uint32_t* cnt,
+                                               const uint64_t* __restrict__ kprev, uint32_t n,
+                                               Geom g, Digit Dlast, uint32_t div,
+                                               const uint32_t* __restrict__ hist, uint32_t C,
+                                               const uint32_t* __restrict__ lo_start,
+                                               uint32_t spread, uint32_t* __restrict__ start,
+                                               int bid, int tb) {
   const uint32_t R = Dlast.R;
-  const uint32_t n = *n_ptr;
   const uint32_t P = lo_start ? lo_start[lo] : 0u;
-  for (uint32_t d = threadIdx.x; d < R; d += BLOCK) cnt[d] = 0;
+  for (uint32_t d = threadIdx.x; d < R; d += tb) cnt[d] = 0;
   __syncthreads();
   const uint32_t tile = P / PTILE;
-  for (uint32_t i = tile * PTILE + threadIdx.x; i < P; i += BLOCK)
+  for (uint32_t i = tile * PTILE + threadIdx.x; i < P; i += tb)
     atomicAdd(&cnt[bid ? digit_of_b(reinterpret_cast<const uint32_t*>(kprev)[i], Dlast)
                        : digit_of(kprev[i], g, Dlast)], 1u);
   __syncthreads();
-  for (uint32_t hi = threadIdx.x; hi < R; hi += BLOCK) {
+  for (uint32_t hi = threadIdx.x; hi < R; hi += tb) {
     const uint64_t b = (uint64_t)hi * div + lo;
     if (b >= g.nb || b % spread) continue;
     // P == n on a tile boundary past the last column: the end of digit hi
@@ -1052,6 +1056,17 @@ k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ 
     start[b / spread] = base + cnt[hi];
   }
   if (lo == 0 && threadIdx.x == 0) start[g.nb / spread] = n;
+  __syncthreads();                         // cnt is the caller's LDS: free again
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ n_ptr, Geom g,
+               Digit Dlast, uint32_t div, const uint32_t* __restrict__ hist, uint32_t C,
+               const uint32_t* __restrict__ lo_start, uint32_t spread,
+               uint32_t* __restrict__ start, int bid) {
+  __shared__ uint32_t cnt[V2_MAXR];
+  bounds_lo_body(blockIdx.x, cnt, kprev, *n_ptr, g, Dlast, div, hist, C, lo_start, spread, start,
+                 bid, BLOCK);
 }
 
 // The radix passes are stable by the lane order of the LDS count atomics (V_scatter), so a
@@ -1559,11 +1574,12 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
   hipLaunchKernelGGL(k_v2_hll_final, dim3(1), dim3(HLL_T), 0, s, hll_regs, g, host_est, n_valid,
                      host_n);
 }
+static const BoundsFuse kNoFuse{nullptr, nullptr, nullptr, Digit{}, 0u, 1u, 0};
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s) {
   KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
-               kout, pout, pad, 0);
+               kout, pout, pad, 0, kNoFuse);
 }
 // write-combined passes (k_v2_scatter_wc): persistent workgroups, each over a chunk of tiles.
 // KMHG_SCATTER_WC_GEOM (A/B): 0 = 8 waves, 128-B granules (1 workgroup / CU); 1 = 4 waves,
@@ -1610,28 +1626,29 @@ void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
   if (bout)
     KMHG_SCATTER_BM(false, true, false, 1, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0);
+                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse);
   else
     KMHG_SCATTER_BM(false, true, false, 2, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0);
+                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse);
 }
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
-                           uint32_t* pout, uint32_t pad, hipStream_t s) {
+                           uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf) {
   const uint64_t* ki = reinterpret_cast<const uint64_t*>(bin);
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
+  const BoundsFuse f = bf ? *bf : kNoFuse;
   if (bout)
     KMHG_SCATTER_BM(false, false, false, 1, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0);
+                    g, D, hist, ntiles, ko, pout, pad, 0, f);
   else
     KMHG_SCATTER_BM(false, false, false, 2, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0);
+                    g, D, hist, ntiles, ko, pout, pad, 0, f);
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                       uint32_t* pout, uint32_t pad, hipStream_t s) {
+                       uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf) {
   KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,
-               hist, ntiles, kout, pout, pad, 0);
+               hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse);
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
                              Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
@@ -1639,16 +1656,16 @@ void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_
                              hipStream_t s) {
   if (nopos)
     KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr, n_ptr,
-                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0);
+                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0, kNoFuse);
   else
     KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr,
-                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0);
+                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0, kNoFuse);
 }
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t pad,
-                             hipStream_t s) {
+                             hipStream_t s, const BoundsFuse* bf) {
   KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr, n_ptr, g, D,
-               hist, ntiles, kout, nullptr, pad, 0);
+               hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
 }
 void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
                       uint64_t n_max, hipStream_t s, const uint32_t* bids) {

@@ -980,6 +980,14 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     div = R;
   }
   uint32_t *bin = bA.p, *bout = bB.p;
+  // two passes with the spread known at launch: V_bounds_lo rides in the last pass (BoundsFuse);
+  // KMHG_FUSE_BOUNDS=0 (A/B) launches it on its own
+  const char* fbe = std::getenv("KMHG_FUSE_BOUNDS");
+  const bool fuse_bounds = bounds_lo && passes == 2 && !co_auto && !(fbe && fbe[0] == '0');
+  auto fuse_of = [&](const void* kprev, bool is_bid) {
+    return BoundsFuse{reinterpret_cast<const uint64_t*>(kprev), lo_start.p, start.p,
+                      make_digit(R, R), R, 1u, is_bid ? 1 : 0};
+  };
   for (uint32_t p = 1; bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
     const bool last = p + 1 == passes;
@@ -987,9 +995,11 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
            launch_v2_hist_bid(bin, n_valid, g, Dp, hist.p, ntiles, status, n_status, s,
                               bounds_lo && passes == 2 ? lo_start.p : nullptr));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
+    const BoundsFuse bfu = fuse_of(bin, true);
     LAUNCH("k_v2_scatter", s,
            launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hist.p, ntiles,
-                                 last && bounds_lo ? nullptr : bout, pout, pad, s));
+                                 last && bounds_lo ? nullptr : bout, pout, pad, s,
+                                 last && fuse_bounds ? &bfu : nullptr));
     std::swap(bin, bout);
     std::swap(pin, pout);
     div *= R;
@@ -1017,14 +1027,18 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
              launch_v2_scatter_keys0(d_keys, (uint64_t)Nw, n_valid, g, Dp, hist.p, ntiles, kout,
                                      pout, pad, no_pos, skip_empty, s));
     } else if (no_pos) {
+      const BoundsFuse bfu = fuse_of(kin, false);
       LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ntiles, kout, pad, s));
+             launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ntiles, kout, pad, s,
+                                     p + 1 == passes && fuse_bounds ? &bfu : nullptr));
     } else if (wc) {
       LAUNCH("k_v2_scatter", s,
              launch_v2_scatter_wc(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, s));
     } else {
+      const BoundsFuse bfu = fuse_of(kin, false);
       LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, pad, s));
+             launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, pad, s,
+                               p + 1 == passes && fuse_bounds ? &bfu : nullptr));
     }
     std::swap(kin, kout);
     std::swap(pin, pout);
@@ -1042,7 +1056,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     idx->geom = gb;
     idx->table.reset(idx->slots());
   }
-  if (bounds_lo) {
+  if (fuse_bounds && !wc) {
+    // computed by the last pass's first workgroups (the write-combined pass does not fold them)
+  } else if (bounds_lo) {
     // the last pass's input: kout after the final swap (pass 0 of a sequence build reads chars,
     // pass 0 of a key stream the caller's keys: one pass has no partial tile to count)
     const uint32_t div_last = passes == 2 ? R : 1u;

@@ -180,6 +180,19 @@ void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, D
 // also copies *n_valid (launch it after the pass's scan) to *host_n
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s);
+// V_bounds_lo folded into the last radix pass (passes == 2, the spread known at launch): its
+// inputs -- the pass's input stream, its scanned histogram, the previous pass's digit starts --
+// are complete before the pass starts and its output is read only by the bucket kernel, so the
+// pass's first `div` workgroups each compute one low digit's bucket starts before their tiles
+// (one launch fewer).  start == nullptr: not fused.
+struct BoundsFuse {
+  const uint64_t* kprev;       // the pass's input (keys, or bucket ids with bid = 1)
+  const uint32_t* lo_start;    // the previous pass's digit starts
+  uint32_t* start;
+  Digit Dlast;
+  uint32_t div, spread;
+  int bid;
+};
 // the sequence must be 16-B aligned (the engine copies an unaligned input)
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
@@ -201,10 +214,10 @@ void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_
                              hipStream_t s);
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t pad,
-                             hipStream_t s);
+                             hipStream_t s, const BoundsFuse* bf = nullptr);
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
-                       uint32_t pad, hipStream_t s);
+                       uint32_t pad, hipStream_t s, const BoundsFuse* bf = nullptr);
 // Bucket-id streams (position builds that keep the sequence's code words): V_hist0 stores
 // every window's bucket id (`bids`, Nw u32, ~0 = not indexed), the radix passes carry (bucket
 // id u32, pos u32) and the last pass writes positions only (bout = nullptr); the bucket kernel
@@ -214,7 +227,8 @@ void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
                             uint32_t pad, hipStream_t s);
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
-                           uint32_t* pout, uint32_t pad, hipStream_t s);
+                           uint32_t* pout, uint32_t pad, hipStream_t s,
+                           const BoundsFuse* bf = nullptr);
 void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
                         uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                         hipStream_t s, uint32_t* save_col0 = nullptr);

@@ -193,3 +193,47 @@ def test_assemble_parts_places_and_rebases(world):
         p.join(60)
         assert p.exitcode == 0
     assert all(res[r] for r in range(world)), res
+
+
+class FailingPart(FakePart):
+    """A part whose build failed on its own rank (kmhg_part_info raising KMHG_EOVERFLOW)."""
+
+    def part_info(self):
+        from kmer_hasher_amd import _lib
+        raise _lib.KmhgError(_lib.KMHG_EOVERFLOW, "a bucket of a part build overflowed its LDS table")
+
+
+def _failing_worker(rank, world, port, bad, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        part = FailingPart(rank, world) if rank == bad else FakePart(rank, world)
+        try:
+            kd.assemble_parts(part, torch.device("cpu"), import_fn=lambda m, b: (m, b))
+            out_q.put((rank, "assembled"))
+        except Exception as e:                       # every rank must land here, none may hang
+            out_q.put((rank, type(e).__name__ + ": " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,bad", [(2, 1), (3, 0)])
+def test_assemble_parts_failure_reaches_every_rank(world, bad):
+    """A part build that fails on one rank (its bucket overflowed: part_info raises there only)
+    makes every rank raise before the first collective of the assembly, instead of the other
+    ranks blocking forever in the all-gather (dist.part_info_all all-reduces the status first)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_failing_worker, args=(r, world, port, bad, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert "overflowed" in res[bad], res
+    for r in range(world):
+        if r != bad:
+            assert "another rank's part build failed" in res[r], res
