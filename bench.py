@@ -369,17 +369,12 @@ def reads_algorithmic_bytes(kernel: str, n_bases: int, n_reads: int, words: int)
     return None
 
 
-def counts_algorithmic_bytes(kernel: str, L: int, U: int, S: int) -> int | None:
-    """Minimum bytes of the count.kmers kernels (first batch into a new pointer): C_first reads
-    each occupied slot (16 B) and scatters {slot, count, key} (16 B); C_order reads the L-entry
-    first-position array (16 B each) and writes a row per key (key 8 B, S counts, row_slot and
-    slot_row 4 B each); C_slots rereads each occupied slot, its row (4 B) and rewrites 8 B."""
-    if kernel == "k_count_first":
-        return 32 * U
-    if kernel == "k_count_order":
-        return 16 * L + U * (8 + 4 * S + 8)
-    if kernel == "k_count_slots":
-        return 28 * U
+def counts_algorithmic_bytes(kernel: str, L: int, U: int, S: int, nslots: int = 0) -> int | None:
+    """Minimum bytes of the count.kmers kernels (first batch into a new pointer): C_walk reads
+    every slot of the adopted table (16 B) and, per key, writes its row (key 8 B, S counts,
+    row_slot 4 B, order key 8 B), slot_row (4 B) and the slot's count fields (8 B)."""
+    if kernel == "k_count_walk":
+        return 16 * nslots + U * (8 + 4 * S + 4 + 8 + 4 + 8)
     return None
 
 
@@ -475,6 +470,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
+    from kmer_hasher_amd import _lib
     from kmer_hasher_amd import device as D
     from kmer_hasher_amd import synth
 
@@ -619,7 +615,7 @@ def main():
 
     # ---------------- count.kmers (SURVEY.md §8 f next-4) of the same sequence: one call per step
     # into a new counts pointer (k, source 0 of 2)
-    cper, t_count, cU = {}, 0.0, 0
+    cper, t_count, cU, cslots, t_order, order_k = {}, 0.0, 0, 0, 0.0, {}
     if not args.profile:
         for _ in range(max(1, args.warmup)):
             D.DeviceIndex.count(seq, k, 0, 2, stream=stream).free()
@@ -627,7 +623,8 @@ def main():
         D.timing_reset()
         for _ in range(2):
             c = D.DeviceIndex.count(seq, k, 0, 2, stream=stream)
-            cU = c.info()["n_kmers"]
+            ci = c.info()
+            cU, cslots = ci["n_kmers"], ci["table_slots"]
             c.free()
         ct = D.timing_report()
         cper = {n: v[1] / 2 for n, v in ct.items() if v[0]}
@@ -638,6 +635,18 @@ def main():
             D.DeviceIndex.count(seq, k, 0, 2, stream=stream).free()
         barrier()
         t_count = time.perf_counter() - t0
+        # the rows' first-insertion order is restored once, when a readout first asks for rows
+        # (ensure_row_order): timed here on its own (kmhg_counts_export with no output copies)
+        c = D.DeviceIndex.count(seq, k, 0, 2, stream=stream)
+        torch.cuda.synchronize()
+        D.timing_enable(True)
+        D.timing_reset()
+        t0 = time.perf_counter()
+        _lib.check(_lib.lib().kmhg_counts_export(c.handle, None, None))
+        t_order = time.perf_counter() - t0
+        order_k = {n: v[1] for n, v in D.timing_report().items() if v[0]}
+        D.timing_enable(False)
+        c.free()
 
     # ---------------- count.kmers.fq.sh.rp over reads sampled from the same sequence (packed reads
     # resident in HBM, one new suffix hash per step), then seq.kmer.depth.sh of the sequence
@@ -777,13 +786,20 @@ def main():
                 "value": round(mbp_total * leg_steps / t_count, 2), "unit": "Mbp/s",
                 "ms_per_step": round(t_count / leg_steps * 1e3, 4), "distinct_kmers": cU,
                 "kernels_ms_per_step": {n: round(v, 5) for n, v in cper.items()},
+                "first_readout_row_order": {
+                    "ms": round(t_order * 1e3, 4),
+                    "kernels_ms": {n: round(v, 5) for n, v in order_k.items()},
+                    "note": "once per counts pointer (and again after a later batch), when a "
+                            "readout first asks for rows: rows sorted into first-insertion order "
+                            "by their order keys (k_rows_place / k_rows_order)"},
                 "note": "count.kmers(seq, c(k, 0, 2)) into a new pointer per step: partitioned "
-                        "build of the batch, whose table the new pointer adopts (first-occurrence "
-                        "rows from k_count_first / k_count_order / k_count_slots)"}
+                        "build of the batch, whose table the new pointer adopts, its rows "
+                        "written in slot order with their insertion-order keys (k_count_walk); "
+                        "first_readout_row_order is the one-time sort a readout triggers"}
             cdom = max((n for n in cper if n.startswith("k_count_")), key=cper.get, default=None)
             if cdom:
                 out["counts"]["roofline"] = _leg_roofline(
-                    cper, cdom, counts_algorithmic_bytes(cdom, L, cU, 2))
+                    cper, cdom, counts_algorithmic_bytes(cdom, L, cU, 2, cslots))
         if t_reads:
             dom_r = "k_read_kmers_emit"      # the row's own kernel (the batch build is the index's)
             ab_r = reads_algorithmic_bytes(dom_r, n_bases, READS_N, r_words)

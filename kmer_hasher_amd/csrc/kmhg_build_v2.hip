@@ -570,7 +570,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
   if (bf.start)
     for (uint32_t lo = blockIdx.x; lo < bf.div; lo += gridDim.x)
       bounds_lo_body(lo, &S.wc[0][0], bf.kprev, *n_ptr, g, bf.Dlast, bf.div, hist, ntiles,
-                     bf.lo_start, bf.spread, bf.start, bf.bid, TB);
+                     bf.lo_start, bf.spread, bf.start, bf.bid, TB, bf.nlim);
   // the next tile's inputs are in flight while this one is processed
   KT nkey[PER];
   uint32_t npos[PER];
@@ -739,305 +739,27 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
   }
 }
 
-// ---------------------------------------------------------------- V_scatter_wc (write-combined)
-// The same stable pass for key streams beyond the caches, with every output line written whole.
-// Measured (tools/scatter_pattern.hip, profiles/rd4a_scatter_pattern.txt): moving 100 M 12-B
-// elements in the radix-313 digit runs of a 2048-element tile (6.5 elements per run) takes
-// 1.15 ms; the same bytes in whole 128-B lines 0.46 ms -- the scatter passes at config 3 (1.0 and
-// 0.92 ms) were bound by their write pattern, not by their work.  Runs aligned to 64 B still
-// cost 1.3x (keys) / 1.25x (positions) of whole lines.
-// So each workgroup owns a contiguous CHUNK of tiles (one workgroup per CU: the output range of
-// a digit over the chunk is contiguous, its start from the scanned [digit][tile] histogram at
-// the chunk's first tile), and the tail of every digit's output that does not fill a 128-B line
-// (< 16 keys, < 32 positions) waits in LDS (PK / PP) until a later tile completes the line.  The
-// digit's owner thread (thread d owns digit d; its cursor and pending starts live in its
-// registers) writes the waiting elements of a line that completes, the tile's write-out the
-// rest, in the same tile: the line is whole in L2 before it is written back.  Only the first and
-// last line of a digit's range in a chunk are ever partial.
-// Geometry variants (A/B, KMHG_SCATTER_WC_GEOM): NW waves per workgroup, KL keys / PL positions
-// per written granule (16 / 32 = whole 128-B lines, 8 / 16 = 64-B halves).
-template <int NW, uint32_t KL, uint32_t PL>
-struct WcLDS {
-  static constexpr uint32_t MAXR = V2_MAXR_IL;
-  uint32_t wc[NW][MAXR];       // per-wave digit counts -> per-wave tile-local cursors
-  uint32_t tstart[MAXR];       // tile-local start of each digit
-  uint32_t ocur[MAXR];         // global index of the digit's first element of this tile
-  uint32_t nk0[MAXR];          // keys at global index >= nk0 wait in PK after this tile
-  uint32_t np0[MAXR];          // ... positions >= np0 in PP
-  uint64_t skey[PTILE];
-  uint32_t spos[PTILE];
-  uint16_t sdig[PTILE];
-  __attribute__((aligned(16))) uint64_t PK[MAXR][KL];
-  __attribute__((aligned(16))) uint32_t PP[MAXR][PL];
-  PStage st;
-};
-
-// elements [0, n) of a pending row to out[g0 ..): 16-B stores where g0 allows
-template <class T>
-__device__ __forceinline__ void wc_flush(T* __restrict__ out, uint64_t g0, const T* row, uint32_t n) {
-  constexpr uint32_t V = 16 / sizeof(T);        // elements per 16-B store
-  uint32_t j = 0;
-  if (g0 % V == 0) {
-    for (; j + V <= n; j += V)
-      *reinterpret_cast<uint4*>(out + g0 + j) = *reinterpret_cast<const uint4*>(row + j);
-  }
-  for (; j < n; ++j) out[g0 + j] = row[j];
-}
-
-template <bool FROM_SEQ, bool BALLOT, int NW, uint32_t KL, uint32_t PL>
-__global__ void __launch_bounds__(NW * 64)
-k_v2_scatter_wc(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
-                const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
-                const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
-                const uint32_t* __restrict__ hist, uint32_t ntiles,
-                uint64_t* __restrict__ kout, uint32_t* __restrict__ pout) {
-  constexpr int TB = NW * 64;
-  constexpr int PER = PTILE / TB;               // elements per lane
-  using SL = WcLDS<NW, KL, PL>;
-  constexpr int DPT = (int)((SL::MAXR + TB - 1) / TB);   // digits owned per thread
-  __shared__ SL S;
-  __shared__ uint64_t sh[NW];
-  const uint32_t R = D.R;
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  const uint32_t wbase = (uint32_t)wave * (PTILE / NW);
-  const uint64_t n = FROM_SEQ ? (uint64_t)Nw : (uint64_t)*n_ptr;
-  // chunk of consecutive tiles; neighbouring chunks on one XCD
-  const uint32_t G = gridDim.x;
-  const uint32_t chunk = xcd_remap(blockIdx.x, G);
-  const uint32_t m = (ntiles + G - 1) / G;
-  const uint32_t t_begin = min(chunk * m, ntiles), t_end = min(t_begin + m, ntiles);
-  if (t_begin >= t_end) return;
-  const uint32_t n_iter = t_end - t_begin;
-  // thread t owns digits [DPT t, DPT t + DPT): their cursors and waiting starts in registers
-  uint32_t gcur[DPT], pk0[DPT], pp0[DPT];
-#pragma unroll
-  for (int q = 0; q < DPT; ++q) {
-    const uint32_t d = threadIdx.x * DPT + q;
-    gcur[q] = pk0[q] = pp0[q] = d < R ? hist[(size_t)d * ntiles + t_begin] : 0u;
-  }
-  uint64_t nkey[PER];
-  uint32_t npos[PER];
-  StageRegs<PSTAGE_W16> nchars;
-  auto prefetch = [&](uint32_t tv) {
-    const uint64_t t0 = (uint64_t)tv * PTILE;
-    if (FROM_SEQ) {
-      if (threadIdx.x < BLOCK) stage_load<PSTAGE_W16, true>(nchars, seq, L, (int64_t)t0 - HALO, true);
-    } else {
-#pragma unroll
-      for (int cc = 0; cc < PER; ++cc) {       // e < ntiles * PTILE <= n_max + pad: in bounds
-        const uint64_t e = t0 + wbase + (uint32_t)cc * 64 + lane;
-        nkey[cc] = kin[e];
-        npos[cc] = pin[e];
-      }
-    }
-  };
-  prefetch(t_begin);
-  for (uint32_t it = 0; it < n_iter; ++it) {
-    const uint32_t tile = t_begin + it;
-    const uint64_t tile0 = (uint64_t)tile * PTILE;
-    uint64_t key[PER];
-    uint32_t ps[PER], dg[PER];
-    bool act[PER];
-    if (FROM_SEQ) {
-      if (threadIdx.x < BLOCK) stage_pack(nchars, S.st);
-    } else {
-#pragma unroll
-      for (int cc = 0; cc < PER; ++cc) {
-        key[cc] = nkey[cc];
-        ps[cc] = npos[cc];
-      }
-    }
-    if (it + 1 < n_iter) prefetch(tile + 1);
-    for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
-    __syncthreads();                       // stage packed; previous tile's write-out done
-#pragma unroll
-    for (int c = 0; c < PER; ++c) {
-      const uint32_t w = wbase + (uint32_t)c * 64 + lane;     // element index inside the tile
-      const uint64_t e = tile0 + w;
-      if (FROM_SEQ) {
-        uint64_t kk = 0;
-        act[c] = e < n && window_key(S.st, HALO + (int)w, (int64_t)e, L, k, kk);
-        ps[c] = (uint32_t)(e + 1);
-        const uint32_t bl = bucket_local(mix64(kk), g);
-        act[c] = act[c] && bl < g.nb;                        // a part build keeps its buckets
-        key[c] = kk;
-        dg[c] = act[c] ? digit_of_b(bl, D) : 0;
-      } else {
-        act[c] = e < n;
-        dg[c] = act[c] ? digit_of_h(mix64(key[c]), g, D) : 0;
-      }
-    }
-    if (!BALLOT) {     // stable ranks from the count atomics' lane-ordered returns (V_scatter)
-#pragma unroll
-      for (int c = 0; c < PER; ++c)
-        if (act[c]) dg[c] |= atomicAdd(&S.wc[wave][dg[c]], 1u) << 16;
-    } else {
-#pragma unroll
-      for (int c = 0; c < PER; ++c)
-        if (act[c]) atomicAdd(&S.wc[wave][dg[c]], 1u);
-    }
-    __syncthreads();
-    // digit phase: the owner of each digit
-    uint32_t nd[DPT];
-    uint64_t own = 0;
-#pragma unroll
-    for (int q = 0; q < DPT; ++q) {
-      const uint32_t d = threadIdx.x * DPT + q;
-      nd[q] = 0;
-      if (d < R) {
-#pragma unroll
-        for (int w = 0; w < NW; ++w) nd[q] += S.wc[w][d];
-      }
-      own += nd[q];
-    }
-    uint64_t tile_n;
-    uint32_t ts = (uint32_t)block_excl_scan_n<NW>(own, sh, tile_n);
-#pragma unroll
-    for (int q = 0; q < DPT; ++q) {
-      const uint32_t d = threadIdx.x * DPT + q;
-      if (d < R) {
-        S.tstart[d] = ts;
-        uint32_t cur = ts;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-          const uint32_t t = S.wc[w][d];
-          S.wc[w][d] = cur;
-          cur += t;
-        }
-        ts += nd[q];
-        const uint32_t end = gcur[q] + nd[q];
-        const uint32_t nk = max(end & ~(KL - 1), pk0[q]), np = max(end & ~(PL - 1), pp0[q]);
-        // a granule completes: its waiting elements go out now, the new ones in the write-out
-        if (nk > pk0[q]) wc_flush(kout, pk0[q], S.PK[d], gcur[q] - pk0[q]);
-        if (np > pp0[q]) wc_flush(pout, pp0[q], S.PP[d], gcur[q] - pp0[q]);
-        S.ocur[d] = gcur[q];
-        S.nk0[d] = nk;
-        S.np0[d] = np;
-        gcur[q] = end;
-        pk0[q] = nk;
-        pp0[q] = np;
-      }
-    }
-    __syncthreads();                       // bases ready; old waiting elements read
-    if (!BALLOT) {
-#pragma unroll
-      for (int c = 0; c < PER; ++c) {
-        if (act[c]) {
-          const uint32_t d = dg[c] & 0xFFFFu;
-          const uint32_t ld = S.wc[wave][d] + (dg[c] >> 16);
-          S.skey[ld] = key[c];
-          S.spos[ld] = ps[c];
-          S.sdig[ld] = (uint16_t)d;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int c = 0; c < PER; ++c) {        // stable ranks: ballots over the digit bits
-        const uint64_t grp = match_bits(dg[c], D.nbits, act[c]);
-        const int leader = act[c] ? __ffsll((unsigned long long)grp) - 1 : lane;
-        uint32_t cur = 0;
-        if (act[c] && leader == lane) {
-          cur = S.wc[wave][dg[c]];
-          S.wc[wave][dg[c]] = cur + (uint32_t)__popcll(grp);
-        }
-        cur = __shfl(cur, leader);
-        wave_sync();
-        if (act[c]) {
-          const uint32_t ld = cur + (uint32_t)__popcll(grp & lanemask_lt());
-          S.skey[ld] = key[c];
-          S.spos[ld] = ps[c];
-          S.sdig[ld] = (uint16_t)dg[c];
-        }
-      }
-    }
-    __syncthreads();
-    // write-out, run by run: elements below the digit's waiting start go to HBM, the rest wait
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const uint32_t i = (uint32_t)(j * TB) + threadIdx.x;
-      if (i < (uint32_t)tile_n) {
-        const uint32_t d = S.sdig[i];
-        const uint32_t gi = S.ocur[d] + (i - S.tstart[d]);
-        const uint32_t nk = S.nk0[d], np = S.np0[d];
-        if (gi < nk) kout[gi] = S.skey[i];
-        else S.PK[d][gi - nk] = S.skey[i];
-        if (gi < np) pout[gi] = S.spos[i];
-        else S.PP[d][gi - np] = S.spos[i];
-      }
-    }
-  }
-  __syncthreads();                         // the last tile's waiting elements are in LDS
-#pragma unroll
-  for (int q = 0; q < DPT; ++q) {          // the chunk's last, partial granules
-    const uint32_t d = threadIdx.x * DPT + q;
-    if (d < R) {
-      wc_flush(kout, pk0[q], S.PK[d], gcur[q] - pk0[q]);
-      wc_flush(pout, pp0[q], S.PP[d], gcur[q] - pp0[q]);
-    }
-  }
-}
-
-// ---------------------------------------------------------------- V_bounds
-// start[b] = first element of bucket b in the partitioned keys (start[nb] = n).  Each wave walks
-// chunks of 4 x 64 consecutive elements; an element's left neighbour's bucket comes from the lane
-// below by a shuffle (one extra load per chunk), so every key is read and hashed once.
-__global__ void __launch_bounds__(BLOCK)
-k_v2_bounds(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, Geom g,
-            uint32_t* __restrict__ start, int bid) {
-  const uint32_t* __restrict__ bids = reinterpret_cast<const uint32_t*>(keys);
-  auto bucket_at = [&](uint64_t i) -> uint32_t {
-    return bid ? bids[i] : bucket_local(mix64(keys[i]), g);
-  };
-  const uint64_t n = *n_ptr;
-  const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
-  if (n == 0) {
-    for (uint64_t b = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; b <= g.nb; b += stride) start[b] = 0;
-    return;
-  }
-  const int lane = lane_id();
-  const uint64_t nwaves = (uint64_t)gridDim.x * (BLOCK / 64);
-  const uint64_t wid = (uint64_t)blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6);
-  for (uint64_t c0 = wid * 256; c0 < n; c0 += nwaves * 256) {
-    uint32_t bk[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint64_t i = c0 + (uint64_t)j * 64 + lane;
-      bk[j] = i < n ? bucket_at(i) : g.nb;
-    }
-    int64_t before = -1;                       // bucket of element c0 - 1
-    if (c0) before = (int64_t)bucket_at(c0 - 1);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint64_t i = c0 + (uint64_t)j * 64 + lane;
-      const uint32_t up = __shfl_up(bk[j], 1);
-      const uint32_t last_prev = __shfl(j ? bk[j - 1] : 0u, 63);
-      const int64_t bp = lane ? (int64_t)up : (j ? (int64_t)last_prev : before);
-      if (i < n) {
-        for (int64_t x = bp + 1; x <= (int64_t)bk[j]; ++x) start[x] = (uint32_t)i;
-        if (i == n - 1)
-          for (uint64_t x = (uint64_t)bk[j] + 1; x <= g.nb; ++x) start[x] = (uint32_t)n;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------- V_bounds_lo (at most 2 passes)
+// ---------------------------------------------------------------- V_bounds_lo
 // Bucket starts from the radix histograms instead of a pass over the sorted keys.  With LSD
-// passes the last pass's input is sorted by lo = b mod div (div = R^(passes-1)) and that pass
-// places elements by hi = b / div, stably, so
-//   start[hi * div + lo] = #(digit < hi) + #(digit == hi and lo' < lo)
-//                        = hist[hi][t] + #(digit hi among input [t * PTILE, P_lo))
-// where P_lo = #(lo' < lo) is the previous pass's start of digit lo (its scanned column 0, saved
-// by V_hist) and t = P_lo / PTILE: one workgroup per lo value counts at most one partial tile.
-// Interleaved schedule only (one histogram column per tile).  `spread` (count-only builds):
-// start[b / spread] for the buckets b that are multiples of spread.
+// passes, pass p's input is sorted by lo = c mod div (c = the element's digits 0 .. p combined,
+// div = R^p) and the pass places elements by its own digit hi, stably, so
+//   S_p[hi * div + lo] = #(digit < hi) + #(digit == hi and lo' < lo)
+//                      = hist_p[hi][t] + #(digit hi among the pass's input [t * PTILE, P_lo))
+// where P_lo = S_(p-1)[lo] = #(lo' < lo) is the start of lo in that input (for p = 1 pass 0's
+// scanned column 0, saved by V_hist) and t = P_lo / PTILE: one workgroup per lo value counts at
+// most one partial tile.  S_p of the last pass are the bucket starts; the earlier levels (3+
+// passes) keep S_p (R^(p+1) entries, `nlim`) for the next.  Each level rides in its pass's
+// scatter (BoundsFuse) -- it needs that pass's scanned histogram and its input, both live
+// there -- so no key pass and no launch of its own.  Interleaved schedule only (one histogram
+// column per tile).  `spread` (count-only builds): start[b / spread] for the buckets b that are
+// multiples of spread.
 __device__ __forceinline__ void bounds_lo_body(uint32_t lo, uint32_t* cnt,
                                                const uint64_t* __restrict__ kprev, uint32_t n,
                                                Geom g, Digit Dlast, uint32_t div,
                                                const uint32_t* __restrict__ hist, uint32_t C,
                                                const uint32_t* __restrict__ lo_start,
                                                uint32_t spread, uint32_t* __restrict__ start,
-                                               int bid, int tb) {
+                                               int bid, int tb, uint32_t nlim) {
   const uint32_t R = Dlast.R;
   const uint32_t P = lo_start ? lo_start[lo] : 0u;
   for (uint32_t d = threadIdx.x; d < R; d += tb) cnt[d] = 0;
@@ -1049,13 +771,13 @@ __device__ __forceinline__ void bounds_lo_body(uint32_t lo, uint32_t* cnt,
   __syncthreads();
   for (uint32_t hi = threadIdx.x; hi < R; hi += tb) {
     const uint64_t b = (uint64_t)hi * div + lo;
-    if (b >= g.nb || b % spread) continue;
+    if (b >= nlim || b % spread) continue;
     // P == n on a tile boundary past the last column: the end of digit hi
     const uint32_t base = tile < C ? hist[(size_t)hi * C + tile]
                                    : (hi + 1 < R ? hist[(size_t)(hi + 1) * C] : n);
     start[b / spread] = base + cnt[hi];
   }
-  if (lo == 0 && threadIdx.x == 0) start[g.nb / spread] = n;
+  if (lo == 0 && threadIdx.x == 0) start[nlim / spread] = n;
   __syncthreads();                         // cnt is the caller's LDS: free again
 }
 
@@ -1063,10 +785,10 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ n_ptr, Geom g,
                Digit Dlast, uint32_t div, const uint32_t* __restrict__ hist, uint32_t C,
                const uint32_t* __restrict__ lo_start, uint32_t spread,
-               uint32_t* __restrict__ start, int bid) {
+               uint32_t* __restrict__ start, int bid, uint32_t nlim) {
   __shared__ uint32_t cnt[V2_MAXR];
   bounds_lo_body(blockIdx.x, cnt, kprev, *n_ptr, g, Dlast, div, hist, C, lo_start, spread, start,
-                 bid, BLOCK);
+                 bid, BLOCK, nlim);
 }
 
 // The radix passes are stable by the lane order of the LDS count atomics (V_scatter), so a
@@ -1562,10 +1284,11 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 }
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
-                         uint32_t spread, uint32_t* start, hipStream_t s, const uint32_t* bprev) {
+                         uint32_t spread, uint32_t* start, uint32_t nlim, hipStream_t s,
+                         const uint32_t* bprev) {
   hipLaunchKernelGGL(k_v2_bounds_lo, dim3(div), dim3(BLOCK), 0, s,
                      bprev ? reinterpret_cast<const uint64_t*>(bprev) : kprev, n_ptr, g, Dlast,
-                     div, hist, C, lo_start, spread, start, bprev ? 1 : 0);
+                     div, hist, C, lo_start, spread, start, bprev ? 1 : 0, nlim);
 }
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s) {
@@ -1574,50 +1297,12 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
   hipLaunchKernelGGL(k_v2_hll_final, dim3(1), dim3(HLL_T), 0, s, hll_regs, g, host_est, n_valid,
                      host_n);
 }
-static const BoundsFuse kNoFuse{nullptr, nullptr, nullptr, Digit{}, 0u, 1u, 0};
+static const BoundsFuse kNoFuse{nullptr, nullptr, nullptr, Digit{}, 0u, 1u, 0, 0u};
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s) {
   KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
                kout, pout, pad, 0, kNoFuse);
-}
-// write-combined passes (k_v2_scatter_wc): persistent workgroups, each over a chunk of tiles.
-// KMHG_SCATTER_WC_GEOM (A/B): 0 = 8 waves, 128-B granules (1 workgroup / CU); 1 = 4 waves,
-// 64-B granules (2 / CU); 2 = 16 waves, 128-B granules (1 / CU)
-static int wc_geom() {
-  const char* e = std::getenv("KMHG_SCATTER_WC_GEOM");
-  return e ? std::atoi(e) : 0;
-}
-template <bool FS, bool B, int NW, uint32_t KL, uint32_t PL, class... A>
-static void launch_wc_one(uint32_t ntiles, hipStream_t s, A... args) {
-  static const unsigned cap = resident_blocks((const void*)k_v2_scatter_wc<FS, B, NW, KL, PL>, NW * 64);
-  hipLaunchKernelGGL((k_v2_scatter_wc<FS, B, NW, KL, PL>), dim3(std::min(ntiles, cap)),
-                     dim3(NW * 64), 0, s, args...);
-}
-template <bool FS, class... A>
-static void launch_wc(uint32_t ntiles, hipStream_t s, A... args) {
-  const int geom = wc_geom();
-  if (ballot_ranks()) {
-    if (geom == 1) launch_wc_one<FS, true, 4, 8, 16>(ntiles, s, args...);
-    else if (geom == 2) launch_wc_one<FS, true, 16, 16, 32>(ntiles, s, args...);
-    else launch_wc_one<FS, true, 8, 16, 32>(ntiles, s, args...);
-  } else {
-    if (geom == 1) launch_wc_one<FS, false, 4, 8, 16>(ntiles, s, args...);
-    else if (geom == 2) launch_wc_one<FS, false, 16, 16, 32>(ntiles, s, args...);
-    else launch_wc_one<FS, false, 8, 16, 32>(ntiles, s, args...);
-  }
-}
-void launch_v2_scatter_seq_wc(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
-                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                              uint32_t* pout, hipStream_t s) {
-  launch_wc<true>(ntiles, s, seq, L, k, Nw, (const uint64_t*)nullptr, (const uint32_t*)nullptr,
-                  (const uint32_t*)nullptr, g, D, hist, ntiles, kout, pout);
-}
-void launch_v2_scatter_wc(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
-                          Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                          uint32_t* pout, hipStream_t s) {
-  launch_wc<false>(ntiles, s, (const uint8_t*)nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr,
-                   g, D, hist, ntiles, kout, pout);
 }
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
                             const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
@@ -1666,14 +1351,6 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
                              hipStream_t s, const BoundsFuse* bf) {
   KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr, n_ptr, g, D,
                hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
-}
-void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
-                      uint64_t n_max, hipStream_t s, const uint32_t* bids) {
-  unsigned gr = grid_of(n_max > g.nb ? n_max : g.nb, BLOCK);
-  if (gr > 16384) gr = 16384;
-  hipLaunchKernelGGL(k_v2_bounds, dim3(gr), dim3(BLOCK), 0, s,
-                     bids ? reinterpret_cast<const uint64_t*>(bids) : keys, n_ptr, g, start,
-                     bids ? 1 : 0);
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,

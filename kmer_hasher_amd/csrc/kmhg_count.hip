@@ -2,18 +2,21 @@
 //
 // Replaces count_kmers (reference src/kmer_hash.c:548-591) with seq_to_counts (:220-251) and
 // kmer_count_insert (:185-208): every valid window of a sequence adds one to slot `source` of
-// its key's vector of `source_n` counts; keys are kept in first-insertion order.
+// its key's vector of `source_n` counts; keys are read out in first-insertion order.
 //
 // A count.kmers call is one partitioned build of the batch (the distinct keys with their
-// occurrence counts, in first-occurrence order = the readout permutation) merged into the
-// counts index:
-// perm_b = nullptr walks the batch table's slots instead (order-free merges: the read counts of
-// kmhg_sh.hip), empty slots contributing nothing.
-//   C_probe   batch key r -> one probe of the counts table; a known key adds its count to its
+// occurrence counts in the slots of its table) merged into the counts index, the batch table's
+// slots walked in slot order (perm_b = nullptr; empty slots contribute nothing).  Rows are
+// appended in that order, each with its insertion-order key (rord, below), and sorted into
+// first-insertion order only when a readout asks for rows (round 4: the batch's
+// first-occurrence permutation used to come first -- one random 16-B store per key and a
+// compaction of an L-entry array -- on every count.kmers call):
+//   C_probe   batch item r -> one probe of the counts table; a known key adds its count to its
 //             row (distinct keys own distinct rows: a plain read-modify-write), a new key
 //             raises its flag
-//   (k_scan_u32 of the flags: new rows keep first-occurrence order)
-//   C_append  new key r -> row U0 + rank: key + a count vector with only `source` set
+//   (k_scan_u32 of the flags)
+//   C_append  new key r -> row U0 + rank: key + a count vector with only `source` set, and its
+//             order key
 //   (table)   the table is rebuilt for the grown key list by the partitioned build run over the
 //             key stream (values = row + 1), then C_fix gives each slot {key, count = source_n,
 //             aux}, aux = the count itself for source_n = 1 (the inline convention of the
@@ -51,11 +54,18 @@ k_count_probe(const uint32_t* __restrict__ perm_b, uint32_t Ub, const Slot* __re
   newf[r] = f;
 }
 
+// A batch slot's first position (1-based): a key seen once holds it inline, a repeated key's
+// position list [aux - count, aux) starts with it.
+__device__ __forceinline__ uint64_t first_pos(uint4 v, const int32_t* __restrict__ pos) {
+  return v.z == 1 ? (uint64_t)v.w : (uint64_t)(uint32_t)pos[v.w - v.z];
+}
+
 __global__ void __launch_bounds__(BLOCK)
 k_count_append(const uint32_t* __restrict__ perm_b, uint32_t Ub, const Slot* __restrict__ Tb,
                const uint32_t* __restrict__ rank, const uint32_t* __restrict__ n_new,
                uint32_t U0, uint32_t S, uint32_t source, uint64_t* __restrict__ ckeys,
-               int32_t* __restrict__ M) {
+               int32_t* __restrict__ M, const int32_t* __restrict__ bpos,
+               uint64_t* __restrict__ rord, uint64_t base) {
   const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
   if (r >= Ub) return;
   const uint32_t o = rank[r];
@@ -65,6 +75,7 @@ k_count_append(const uint32_t* __restrict__ perm_b, uint32_t Ub, const Slot* __r
   const uint64_t row = (uint64_t)U0 + o;
   ckeys[row] = ((uint64_t)v.y << 32) | v.x;
   for (uint32_t j = 0; j < S; ++j) M[row * S + j] = j == source ? (int32_t)v.z : 0;
+  if (rord) rord[row] = base + first_pos(v, bpos) - 1;
 }
 
 __global__ void __launch_bounds__(BLOCK)
@@ -94,23 +105,6 @@ k_count_canon(const uint32_t* __restrict__ row_slot, const int32_t* __restrict__
   if (S >= 2) {
     pkeys[r] = r;
     pair_off[r] = (uint64_t)r * ((uint64_t)S * (S - 1) / 2);
-  }
-}
-
-// The first batch of count.kmers into a new pointer, rows in first-occurrence order without a
-// slot permutation: C_first scatters {slot, count, key} to the key's first position, C_order
-// compacts that array in position order straight into the rows (key, count vector, row_slot,
-// slot_row), C_slots rewrites the adopted table's slots in slot order.  The only random
-// accesses left are C_first's 16-B stores and C_order's slot_row stores.
-__global__ void __launch_bounds__(BLOCK)
-k_count_first(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restrict__ positions,
-              uint4* __restrict__ F) {
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
-       i += (uint64_t)gridDim.x * BLOCK) {
-    const uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
-    if (v.z)
-      F[(v.z == 1 ? (int32_t)v.w : positions[v.w - v.z]) - 1] =
-          make_uint4((uint32_t)i, v.z, v.x, v.y);
   }
 }
 
@@ -144,41 +138,59 @@ __device__ __forceinline__ void tile_compact(const bool (&flag)[J], uint64_t (&r
     rk[j] = cw[j * NW + wave] + (uint64_t)__popcll(m[j] & lanemask_lt());
 }
 
-// F: L entries in position order, slot NONE where no key starts.  `ticket` orders the tiles.
+// Row order of a count.kmers index (first insertion, the order kh_put saw the keys in, which the
+// khash readout order replays): a batch's rows are written in slot order, each with its order
+// key rord = base + first position - 1 (base = the characters counted before the batch), and
+// sorted once when a readout needs them (kmhg_engine.cpp ensure_row_order): C_place puts row r at
+// F[rord[r]] (F preset to NONE), C_rows compacts F in order into the new rows, moving each row's
+// key, counts, order key and slot, and pointing its slot at it.
 __global__ void __launch_bounds__(BLOCK)
-k_count_order(const uint4* __restrict__ F, int64_t L, uint64_t* __restrict__ status,
-              uint32_t* __restrict__ ticket, uint32_t S, uint32_t source,
-              uint64_t* __restrict__ ckeys, int32_t* __restrict__ M,
-              uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot) {
+k_rows_place(const uint64_t* __restrict__ rord, uint32_t U, uint32_t* __restrict__ F) {
+  const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
+  if (r < U) F[rord[r]] = r;
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_rows_order(const uint32_t* __restrict__ F, int64_t n, uint64_t* __restrict__ status,
+             uint32_t* __restrict__ ticket, uint32_t S, const uint64_t* __restrict__ ckeys,
+             const int32_t* __restrict__ M, const uint64_t* __restrict__ rord,
+             const uint32_t* __restrict__ row_slot, uint64_t* __restrict__ nkeys,
+             int32_t* __restrict__ nM, uint64_t* __restrict__ nrord,
+             uint32_t* __restrict__ nrow_slot, uint32_t* __restrict__ slot_row,
+             Slot* __restrict__ T) {
   __shared__ uint64_t cw[WPT * (BLOCK / 64)];
   __shared__ uint32_t tk;
   const uint32_t tile = take_ticket(ticket, &tk);
   const int64_t t0 = (int64_t)tile * TILE;
-  uint4 f[WPT];
+  uint32_t o[WPT];
   bool fl[WPT];
 #pragma unroll
   for (int j = 0; j < WPT; ++j) {
     const int64_t p = t0 + (int64_t)j * BLOCK + threadIdx.x;
-    f[j] = p < L ? F[p] : make_uint4(NONE, 0u, 0u, 0u);
-    fl[j] = f[j].x != NONE;
+    o[j] = p < n ? F[p] : NONE;
+    fl[j] = o[j] != NONE;
   }
   uint64_t rk[WPT];
   tile_compact(fl, rk, cw, status, tile);
 #pragma unroll
   for (int j = 0; j < WPT; ++j) {
     if (!fl[j]) continue;
-    const uint64_t row = rk[j];
-    ckeys[row] = ((uint64_t)f[j].w << 32) | f[j].z;
-    int32_t* m = M + row * S;
-    for (uint32_t q = 0; q < S; ++q) m[q] = q == source ? (int32_t)f[j].y : 0;
-    row_slot[row] = f[j].x;
-    slot_row[f[j].x] = (uint32_t)row;
+    const uint64_t i = rk[j], r = o[j];
+    nkeys[i] = ckeys[r];
+    for (uint32_t q = 0; q < S; ++q) nM[i * S + q] = M[r * S + q];
+    nrord[i] = rord[r];
+    const uint32_t sl = row_slot[r];
+    nrow_slot[i] = sl;
+    slot_row[sl] = (uint32_t)i;
+    if (S > 1) T[sl].aux = ((uint32_t)i + 1) * S;     // the row's counts end (S = 1: the count)
   }
 }
 
-// The first batch into an empty suffix hash (order-free rows: slot order).  One pass over the
-// adopted table in tiles of TILE slots: occupied slots are compacted into rows, each writes its
-// row (key, count vector, row_slot), slot_row and its own slot fields -- every access coalesced.
+// The first batch into an empty counts index or suffix hash: the batch table becomes the counts
+// table and its rows are written in slot order.  One pass over the adopted table in tiles of
+// TILE slots: occupied slots are compacted into rows, each writes its row (key, count vector,
+// row_slot, and for count.kmers its order key), slot_row and its own slot fields -- every access
+// coalesced but the first-position load of a repeated key.
 // WALK_PER slots per thread: a longer tile halves the look-back chain over the sparse table
 #ifndef KMHG_WALK_PER
 #define KMHG_WALK_PER 16
@@ -199,7 +211,8 @@ __global__ void WALK_BOUNDS
 k_count_walk(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ status,
              uint32_t* __restrict__ ticket, uint32_t S, uint32_t source,
              uint64_t* __restrict__ ckeys, int32_t* __restrict__ M,
-             uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot) {
+             uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot,
+             const int32_t* __restrict__ bpos, uint64_t* __restrict__ rord, uint64_t base) {
   __shared__ uint64_t cw[WALK_PER * (BLOCK / 64)];
   __shared__ uint32_t tk;
   const uint32_t tile = take_ticket(ticket, &tk);
@@ -224,19 +237,9 @@ k_count_walk(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ statu
     for (uint32_t q = 0; q < S; ++q) m[q] = q == source ? (int32_t)v[j].z : 0;
     row_slot[row] = (uint32_t)i;
     slot_row[i] = (uint32_t)row;
+    if (rord) rord[row] = base + first_pos(v[j], bpos) - 1;
     *reinterpret_cast<uint2*>(&T[i].count) =
         make_uint2(S, S == 1 ? v[j].z : ((uint32_t)row + 1) * S);
-  }
-}
-
-__global__ void __launch_bounds__(BLOCK)
-k_count_slots(Slot* __restrict__ T, uint64_t nslots, uint32_t S,
-              const uint32_t* __restrict__ slot_row) {
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < nslots;
-       i += (uint64_t)gridDim.x * BLOCK) {
-    const uint32_t c = T[i].count;
-    if (!c) continue;
-    *reinterpret_cast<uint2*>(&T[i].count) = make_uint2(S, S == 1 ? c : (slot_row[i] + 1) * S);
   }
 }
 
@@ -271,9 +274,10 @@ void launch_count_probe(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb, con
 }
 void launch_count_append(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb,
                          const uint32_t* rank, const uint32_t* n_new, uint32_t U0, uint32_t S,
-                         uint32_t source, uint64_t* ckeys, int32_t* M, hipStream_t s) {
+                         uint32_t source, uint64_t* ckeys, int32_t* M, const int32_t* bpos,
+                         uint64_t* rord, uint64_t base, hipStream_t s) {
   hipLaunchKernelGGL(k_count_append, dim3(grid_of(Ub)), dim3(BLOCK), 0, s, perm_b, Ub, Tb, rank,
-                     n_new, U0, S, source, ckeys, M);
+                     n_new, U0, S, source, ckeys, M, bpos, rord, base);
 }
 void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uint32_t S,
                          const int32_t* M, uint32_t* slot_row, uint32_t* row_slot,
@@ -281,30 +285,25 @@ void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uin
   hipLaunchKernelGGL(k_count_insert, dim3(grid_of(U)), dim3(BLOCK), 0, s, ckeys, U, T, g, S, M,
                      slot_row, row_slot);
 }
-void launch_count_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint4* F,
-                        hipStream_t s) {
-  hipLaunchKernelGGL(k_count_first, dim3(grid_cap(nslots)), dim3(BLOCK), 0, s, T, nslots,
-                     positions, F);
+void launch_rows_place(const uint64_t* rord, uint32_t U, uint32_t* F, hipStream_t s) {
+  hipLaunchKernelGGL(k_rows_place, dim3(grid_of(U)), dim3(BLOCK), 0, s, rord, U, F);
 }
-void launch_count_order(const uint4* F, int64_t L, uint64_t* status, uint32_t* ticket, uint32_t S,
-                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
-                        uint32_t* row_slot, hipStream_t s) {
-  const unsigned nt = (unsigned)(((uint64_t)L + TILE - 1) / TILE);
-  hipLaunchKernelGGL(k_count_order, dim3(nt), dim3(BLOCK), 0, s, F, L, status, ticket, S, source,
-                     ckeys, M, slot_row, row_slot);
+void launch_rows_order(const uint32_t* F, int64_t n, uint64_t* status, uint32_t* ticket,
+                       uint32_t S, const uint64_t* ckeys, const int32_t* M, const uint64_t* rord,
+                       const uint32_t* row_slot, uint64_t* nkeys, int32_t* nM, uint64_t* nrord,
+                       uint32_t* nrow_slot, uint32_t* slot_row, Slot* T, hipStream_t s) {
+  const unsigned nt = (unsigned)(((uint64_t)n + TILE - 1) / TILE);
+  hipLaunchKernelGGL(k_rows_order, dim3(nt), dim3(BLOCK), 0, s, F, n, status, ticket, S, ckeys,
+                     M, rord, row_slot, nkeys, nM, nrord, nrow_slot, slot_row, T);
 }
 uint64_t count_walk_tiles(uint64_t nslots) { return (nslots + WALK_TILE - 1) / WALK_TILE; }
 void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
-                       uint32_t* row_slot, hipStream_t s) {
+                       uint32_t* row_slot, const int32_t* bpos, uint64_t* rord, uint64_t base,
+                       hipStream_t s) {
   const unsigned nt = (unsigned)((nslots + WALK_TILE - 1) / WALK_TILE);
   hipLaunchKernelGGL(k_count_walk, dim3(nt), dim3(BLOCK), 0, s, T, nslots, status, ticket, S,
-                     source, ckeys, M, slot_row, row_slot);
-}
-void launch_count_slots(Slot* T, uint64_t nslots, uint32_t S, const uint32_t* slot_row,
-                        hipStream_t s) {
-  hipLaunchKernelGGL(k_count_slots, dim3(grid_cap(nslots)), dim3(BLOCK), 0, s, T, nslots, S,
-                     slot_row);
+                     source, ckeys, M, slot_row, row_slot, bpos, rord, base);
 }
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s) {

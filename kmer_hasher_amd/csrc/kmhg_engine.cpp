@@ -641,8 +641,10 @@ struct kmhg_index {
   PinnedRec rec;
   const uint8_t* src = nullptr;
   // counts index (count.kmers, kmhg_count.hip): sources > 0.  `positions` then holds the
-  // U x sources count matrix (row-major, rows in first-insertion order, rows_cap allocated),
-  // `ckeys` the keys of the rows, slot_row / row_slot the table <-> row maps.
+  // U x sources count matrix (row-major, rows_cap allocated), `ckeys` the keys of the rows,
+  // slot_row / row_slot the table <-> row maps.  count.kmers rows are appended in slot order with
+  // their insertion-order keys `rord` and sorted into first-insertion order before a readout
+  // (ensure_row_order; rows_sorted); a suffix hash's rows are order-free (no rord).
   uint32_t sources = 0;
   bool canonical = false;         // suffix hash (count.kmers.fq.sh.rp): canonical k-mer counts
   uint64_t rows_cap = 0, kmer_count = 0;
@@ -650,7 +652,8 @@ struct kmhg_index {
   // last read batch (kmhg_sh_last_batch): HLL distinct estimate, bucket spread, build path
   double co_est = 0;
   int co_spread = 0, co_path = 0;
-  DBuf<uint64_t> ckeys;
+  DBuf<uint64_t> ckeys, rord;
+  bool rows_sorted = true;
   DBuf<uint32_t> slot_row, row_slot;
   // seq.kmer.pos diagonal path (DiagIdx, kmhg_kernels.h): the index sequence's 2-bit code words
   // and window bits, written by the build (V_hist0); the bits of repeated keys' windows are
@@ -680,8 +683,8 @@ struct kmhg_index {
   }
   // stream-ordered release of everything the index holds (work queued on `s` may still read it)
   void bind_all(hipStream_t s) {
-    table.bind(s); positions.bind(s); ckeys.bind(s); slot_row.bind(s); row_slot.bind(s);
-    dcodes.bind(s); ptag.bind(s);
+    table.bind(s); positions.bind(s); ckeys.bind(s); rord.bind(s); slot_row.bind(s);
+    row_slot.bind(s); dcodes.bind(s); ptag.bind(s);
     canon.perm.bind(s); canon.canon_off.bind(s); canon.pkeys.bind(s); canon.pair_off.bind(s);
     canon.rinfo.bind(s);
   }
@@ -908,17 +911,13 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const bool bid_on = bide ? bide[0] == '1' : Nw <= BID_MAX_WINDOWS;
   const bool bid = codes && !from_keys && !count_only && bid_on;
   DBuf<uint64_t> kA(bid ? 1 : Nw + PTILE, s), kB(bid ? 1 : Nw + PTILE, s);   // + pad
-  // key-stream position builds write their radix passes line by line (k_v2_scatter_wc) beyond
-  // WC_MIN_WINDOWS; KMHG_SCATTER_WC=0 / 1 forces the tile-by-tile / write-combined passes
-  constexpr int64_t WC_MIN_WINDOWS = 12 << 20;
-  const char* wce = std::getenv("KMHG_SCATTER_WC");
-  const bool wc = !bid && !from_keys && !count_only &&
-                  (wce ? wce[0] == '1' : Nw > WC_MIN_WINDOWS);
-  // bucket ids: pass p writes bA / bB alternately; the last pass writes none (the bucket bounds
-  // pass V_bounds of 3+ passes reads the last one's, so it is written there)
-  const bool bounds_from_hist = passes <= 2;
+  // (Removed in round 4 after measurement, DESIGN.md §5: radix passes writing whole 128-B lines
+  // through LDS write-combining buffers -- config 3 29.2 -> 25.0-28.7 Gbp/s, the 500 Mbp build
+  // 18.1 -> 18.9-22.7 ms.)
+  // bucket ids: pass p writes bA / bB alternately; the last pass writes none (the bucket starts
+  // come from the histograms)
   // (bB first holds V_hist0's per-window ids, the first pass's input)
-  DBuf<uint32_t> bA(bid && (passes > 1 || !bounds_from_hist) ? Nw + PTILE : 1, s);
+  DBuf<uint32_t> bA(bid && passes > 1 ? Nw + PTILE : 1, s);
   DBuf<uint32_t> bB(bid ? Nw + PTILE : 1, s);
   const bool no_pos = count_only;                        // keys only through the passes
   DBuf<uint32_t> pA(no_pos ? 1 : Nw + PTILE, s), pB(no_pos ? 1 : Nw + PTILE, s);
@@ -944,9 +943,13 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   PinnedRec hrec;
   if (co_auto) hrec = PinnedPool::get().take();
 
-  // bucket starts straight from the histograms (V_bounds_lo) for one or two passes
-  const bool bounds_lo = bounds_from_hist;
-  DBuf<uint32_t> lo_start(bounds_lo && passes == 2 ? R : 1, s);
+  // bucket starts straight from the histograms (V_bounds_lo), one level per pass p >= 1:
+  // lo_save = pass 0's digit starts (saved by pass 1's V_hist), lvA / lvB = S_p of the passes
+  // before the last (3+ passes), the last level writes `start`
+  DBuf<uint32_t> lo_save(passes >= 2 ? R : 1, s);
+  uint64_t r_top = 1;                                   // R^(passes - 1)
+  for (uint32_t i = 1; i < passes; ++i) r_top *= R;
+  DBuf<uint32_t> lvA(passes >= 3 ? r_top + 1 : 1, s), lvB(passes >= 4 ? r_top + 1 : 1, s);
   uint64_t *kin = kA.p, *kout = kB.p;
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = 1;
@@ -968,11 +971,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     if (bid)
       LAUNCH("k_v2_scatter_seq", s,
              launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ntiles,
-                                    passes == 1 && bounds_lo ? nullptr : bA.p, pA.p, pad, s));
-    else if (wc)
-      LAUNCH("k_v2_scatter_seq", s,
-             launch_v2_scatter_seq_wc(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
-                                      pA.p, s));
+                                    passes == 1 ? nullptr : bA.p, pA.p, pad, s));
     else
       LAUNCH("k_v2_scatter_seq", s,
              launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
@@ -980,26 +979,40 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     div = R;
   }
   uint32_t *bin = bA.p, *bout = bB.p;
-  // two passes with the spread known at launch: V_bounds_lo rides in the last pass (BoundsFuse);
-  // KMHG_FUSE_BOUNDS=0 (A/B) launches it on its own
+  // each level of the bucket starts rides in its pass (BoundsFuse), except the last one of a
+  // count-only build whose spread is chosen after the passes (co_auto); KMHG_FUSE_BOUNDS=0
+  // (A/B) launches every level on its own
   const char* fbe = std::getenv("KMHG_FUSE_BOUNDS");
-  const bool fuse_bounds = bounds_lo && passes == 2 && !co_auto && !(fbe && fbe[0] == '0');
-  auto fuse_of = [&](const void* kprev, bool is_bid) {
-    return BoundsFuse{reinterpret_cast<const uint64_t*>(kprev), lo_start.p, start.p,
-                      make_digit(R, R), R, 1u, is_bid ? 1 : 0};
+  const bool fuse_on = !(fbe && fbe[0] == '0');
+  auto level_of = [&](uint32_t p, const void* kprev, bool is_bid, uint32_t spread) {
+    uint64_t dv = 1;                                    // R^p lower-digit values
+    for (uint32_t i = 0; i < p; ++i) dv *= R;
+    const bool last = p + 1 == passes;
+    const uint32_t* lin = p == 1 ? lo_save.p : ((p - 1) % 2 ? lvA.p : lvB.p);
+    uint32_t* lout = last ? start.p : (p % 2 ? lvA.p : lvB.p);
+    return BoundsFuse{reinterpret_cast<const uint64_t*>(kprev), lin, lout,
+                      make_digit((uint32_t)dv, R), (uint32_t)dv, spread, is_bid ? 1 : 0,
+                      last ? g.nb : (uint32_t)(dv * R)};
+  };
+  auto fused = [&](uint32_t p) { return fuse_on && !(co_auto && p + 1 == passes); };
+  auto launch_level = [&](const BoundsFuse& f) {
+    const uint64_t* kp = f.bid ? nullptr : f.kprev;
+    const uint32_t* bp = f.bid ? reinterpret_cast<const uint32_t*>(f.kprev) : nullptr;
+    LAUNCH("k_v2_bounds", s, launch_v2_bounds_lo(kp, n_valid, g, f.Dlast, f.div, hist.p, ntiles,
+                                                 f.lo_start, f.spread, f.start, f.nlim, s, bp));
   };
   for (uint32_t p = 1; bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
     const bool last = p + 1 == passes;
     LAUNCH("k_v2_hist", s,
            launch_v2_hist_bid(bin, n_valid, g, Dp, hist.p, ntiles, status, n_status, s,
-                              bounds_lo && passes == 2 ? lo_start.p : nullptr));
+                              p == 1 ? lo_save.p : nullptr));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
-    const BoundsFuse bfu = fuse_of(bin, true);
+    const BoundsFuse lv = level_of(p, bin, true, 1u);
     LAUNCH("k_v2_scatter", s,
-           launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hist.p, ntiles,
-                                 last && bounds_lo ? nullptr : bout, pout, pad, s,
-                                 last && fuse_bounds ? &bfu : nullptr));
+           launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hist.p, ntiles, last ? nullptr : bout,
+                                 pout, pad, s, fused(p) ? &lv : nullptr));
+    if (!fused(p) && !last) launch_level(lv);
     std::swap(bin, bout);
     std::swap(pin, pout);
     div *= R;
@@ -1007,13 +1020,13 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   for (uint32_t p = from_keys ? 0 : 1; !bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
     const bool keys0 = from_keys && p == 0;
+    const bool last = p + 1 == passes;
     const uint64_t* src = keys0 ? d_keys : kin;
     const bool hll = co_auto && p == 0;
-    const bool save = bounds_lo && passes == 2 && p == 1;
     LAUNCH("k_v2_hist", s,
            launch_v2_hist(src, n_valid, g, Dp, hist.p, ntiles, status, n_status, s,
                           hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
-                          save ? lo_start.p : nullptr, keys0 && skip_empty,
+                          p == 1 ? lo_save.p : nullptr, keys0 && skip_empty,
                           /*padded=*/!keys0));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     if (hll) {   // after the scan: the estimate travels with the valid key count
@@ -1026,19 +1039,17 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       LAUNCH("k_v2_scatter", s,
              launch_v2_scatter_keys0(d_keys, (uint64_t)Nw, n_valid, g, Dp, hist.p, ntiles, kout,
                                      pout, pad, no_pos, skip_empty, s));
-    } else if (no_pos) {
-      const BoundsFuse bfu = fuse_of(kin, false);
-      LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ntiles, kout, pad, s,
-                                     p + 1 == passes && fuse_bounds ? &bfu : nullptr));
-    } else if (wc) {
-      LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter_wc(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, s));
     } else {
-      const BoundsFuse bfu = fuse_of(kin, false);
-      LAUNCH("k_v2_scatter", s,
-             launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, pad, s,
-                               p + 1 == passes && fuse_bounds ? &bfu : nullptr));
+      const BoundsFuse lv = level_of(p, kin, false, 1u);
+      if (no_pos)
+        LAUNCH("k_v2_scatter", s,
+               launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ntiles, kout, pad, s,
+                                       fused(p) ? &lv : nullptr));
+      else
+        LAUNCH("k_v2_scatter", s,
+               launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, pad, s,
+                                 fused(p) ? &lv : nullptr));
+      if (!fused(p) && !last) launch_level(lv);
     }
     std::swap(kin, kout);
     std::swap(pin, pout);
@@ -1056,20 +1067,15 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     idx->geom = gb;
     idx->table.reset(idx->slots());
   }
-  if (fuse_bounds && !wc) {
-    // computed by the last pass's first workgroups (the write-combined pass does not fold them)
-  } else if (bounds_lo) {
-    // the last pass's input: kout after the final swap (pass 0 of a sequence build reads chars,
-    // pass 0 of a key stream the caller's keys: one pass has no partial tile to count)
-    const uint32_t div_last = passes == 2 ? R : 1u;
+  if (passes == 1) {
+    // one pass (pass 0 reads chars or the caller's keys): the starts are the scanned column 0
     LAUNCH("k_v2_bounds", s,
-           launch_v2_bounds_lo(passes == 2 ? kout : nullptr, n_valid, g, make_digit(div_last, R),
-                               div_last, hist.p, ntiles, passes == 2 ? lo_start.p : nullptr,
-                               g.nb / gb.nb, start.p, s,
-                               bid && passes == 2 ? bout : nullptr));
-  } else {
-    LAUNCH("k_v2_bounds", s, launch_v2_bounds(kin, n_valid, gb, start.p, (uint64_t)Nw, s,
-                                              bid ? bin : nullptr));
+           launch_v2_bounds_lo(nullptr, n_valid, g, make_digit(1, R), 1u, hist.p, ntiles, nullptr,
+                               g.nb / gb.nb, start.p, g.nb, s, nullptr));
+  } else if (!fused(passes - 1)) {
+    // the last pass's input: kout / bout after the final swap
+    launch_level(level_of(passes - 1, bid ? static_cast<const void*>(bout) : kout, bid,
+                          g.nb / gb.nb));
   }
 #ifdef KMHG_STAMPS
   static uint64_t* stamps = nullptr;
@@ -1334,8 +1340,7 @@ struct Release {                   // a batch index dies in stream order
   ~Release() { b->bind_all(s); }
 };
 
-void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_t n_items,
-                 uint32_t source, hipStream_t s);
+void merge_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint64_t base, hipStream_t s);
 
 // Room for `need` rows in the count matrix (grown geometrically: repeated calls amortise the copy).
 void reserve_rows(kmhg_index* idx, uint64_t need, hipStream_t s) {
@@ -1345,54 +1350,66 @@ void reserve_rows(kmhg_index* idx, uint64_t need, hipStream_t s) {
     fail(KMHG_EOVERFLOW, "counts index larger than 2^31-1 counts (R vector limit)");
   if (need <= idx->rows_cap) return;
   const uint64_t cap = std::max<uint64_t>(need, idx->rows_cap * 2);
-  DBuf<uint64_t> nk(cap);
+  const bool ord = !idx->canonical;               // count.kmers rows carry order keys
+  DBuf<uint64_t> nk(cap), nr(ord ? cap : 0);
   DBuf<int32_t> nm(cap * S);
   if (U0) {
     HIPC(hipMemcpyAsync(nk.p, idx->ckeys.p, U0 * 8, hipMemcpyDeviceToDevice, s));
     HIPC(hipMemcpyAsync(nm.p, idx->positions.p, U0 * S * 4, hipMemcpyDeviceToDevice, s));
+    if (ord) HIPC(hipMemcpyAsync(nr.p, idx->rord.p, U0 * 8, hipMemcpyDeviceToDevice, s));
   }
   idx->ckeys.bind(s);
   idx->positions.bind(s);
+  idx->rord.bind(s);
   idx->ckeys.swap_with(nk);
   idx->positions.swap_with(nm);
+  idx->rord.swap_with(nr);
   idx->rows_cap = cap;
 }
 
-// The first batch into an empty counts index: every key is new, the batch table becomes the
-// counts table, and the rows (first-occurrence order) come from C_first / C_order / C_slots
-// (kmhg_count.hip) -- no slot permutation, probe, append, table rebuild or C_fix.
-void adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, hipStream_t s) {
+// The first batch into an empty counts index or suffix hash: every key is new, the batch table
+// becomes the counts table, and its occupied slots are compacted into rows in slot order in one
+// pass (k_count_walk) -- no probe, append, table rebuild or C_fix.  count.kmers rows get their
+// order keys (base + first position - 1); a suffix hash's rows are order-free.  Returns the
+// rows written (B->U, exact, when the batch was built from a sequence).
+uint64_t adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint64_t base,
+                           hipStream_t s) {
   ReleaseGroup rg(s);
   const uint32_t S = idx->sources;
   const uint64_t Ub = B->U;
-  const int64_t L = B->L;
   reserve_rows(idx, Ub, s);
-  DBuf<uint4> F(L, s);
-  HIPC(hipMemsetAsync(F.p, 0xFF, (size_t)L * 16, s));
-  LAUNCH("k_count_first", s,
-         launch_count_first(B->table.p, B->slots(), B->positions.p, F.p, s));
-  const uint64_t nt = ((uint64_t)L + TILE - 1) / TILE;
-  DBuf<uint64_t> status(nt + 1, s);                // look-back words + the tile ticket
-  HIPC(hipMemsetAsync(status.p, 0, (nt + 1) * 8, s));
+  const bool ord = !idx->canonical;
+  const uint64_t ns = B->slots();
+  const uint64_t nw = count_walk_tiles(ns);
+  DBuf<uint64_t> status(nw + 1, s);                // look-back words + the tile ticket
+  HIPC(hipMemsetAsync(status.p, 0, (nw + 1) * 8, s));
   idx->table.bind(s);
   idx->slot_row.bind(s);
   idx->row_slot.bind(s);
   idx->geom = B->geom;
   idx->table.swap_with(B->table);                  // B's release frees the old (empty) table
-  idx->slot_row.reset(idx->slots());
+  idx->slot_row.reset(ns);
   idx->row_slot.reset(Ub);
-  LAUNCH("k_count_order", s,
-         launch_count_order(F.p, L, status.p, reinterpret_cast<uint32_t*>(status.p + nt), S,
-                            source, idx->ckeys.p, idx->positions.p, idx->slot_row.p,
-                            idx->row_slot.p, s));
-  LAUNCH("k_count_slots", s,
-         launch_count_slots(idx->table.p, idx->slots(), S, idx->slot_row.p, s));
-  idx->U = Ub;
-  idx->N = Ub * S;
-  idx->P = Ub * ((uint64_t)S * (S - 1) / 2);
-  idx->max_n = Ub ? S : 0;
-  idx->kmer_count += Ub;
+  LAUNCH("k_count_walk", s,
+         launch_count_walk(idx->table.p, ns, status.p, reinterpret_cast<uint32_t*>(status.p + nw),
+                           S, source, idx->ckeys.p, idx->positions.p, idx->slot_row.p,
+                           idx->row_slot.p, ord ? B->positions.p : nullptr,
+                           ord ? idx->rord.p : nullptr, base, s));
+  uint64_t n_new = Ub;
+  if (!ord) {                                      // a read batch: the last tile's prefix
+    uint64_t last = 0;
+    HIPC(hipMemcpyAsync(&last, status.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    n_new = last & ((1ull << 62) - 1);             // LB_MASK: payload of a status word
+  }
+  idx->U = n_new;
+  idx->N = n_new * S;
+  idx->P = n_new * ((uint64_t)S * (S - 1) / 2);
+  idx->max_n = n_new ? S : 0;
+  idx->kmer_count += n_new;
+  idx->rows_sorted = !ord;
   idx->canon.ready = false;
+  return n_new;
 }
 
 // Adopting a batch table keeps its size, set by the batch's windows / k-mer words; the rebuild
@@ -1417,72 +1434,45 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
   finish_build(B.get());
   B->stream = s;
   if (!B->U) return;
-  if (adoptable(idx, B.get())) {
-    adopt_first_batch(idx, B.get(), source, s);
-  } else {
-    prepare_canon(B.get(), s);     // batch keys in first-occurrence order
-    merge_batch(idx, B.get(), B->canon.perm.p, B->U, source, s);
-  }
-  idx->L += L;
+  if (adoptable(idx, B.get()))
+    adopt_first_batch(idx, B.get(), source, (uint64_t)idx->L, s);
+  else
+    merge_batch(idx, B.get(), source, (uint64_t)idx->L, s);
+  idx->L += L;                     // the next batch's order keys start here
 }
 
-// Merge a batch index B (distinct keys with their counts in the slots) into the counts index:
-// items r < n_items are B's slots perm_b[r] (or slot r itself when perm_b is null: order-free,
-// empty slots skipped).  New keys get rows in item order.
-void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_t n_items,
-                 uint32_t source, hipStream_t s) {
+// Merge a batch index B (distinct keys with their counts in the slots) into the counts index,
+// B's slots walked in slot order (empty slots skipped).  New keys get rows in that order;
+// count.kmers rows get order keys base + first position - 1 (base = characters counted before
+// the batch), so ensure_row_order can restore first-insertion order for a readout.
+void merge_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint64_t base, hipStream_t s) {
   ReleaseGroup rg(s);
   const int k = idx->k;
   const uint32_t S = idx->sources;
   const uint64_t Ub = B->U;
   const uint64_t U0 = idx->U;
-  reserve_rows(idx, U0 + Ub, s);
-  const uint64_t ni = n_items;
-  const uint32_t nt = tiles_for(ni);
+  const bool ord = !idx->canonical;
   // KMHG_COUNT_TABLE (tests): "rebuild" / "probe" take the general merge even for the first batch
   const char* ct = std::getenv("KMHG_COUNT_TABLE");
-  if (!perm_b && adoptable(idx, B)) {
-    // first batch into an empty suffix hash: every key is new and the batch table becomes the
-    // counts table, its occupied slots compacted into rows in slot order in one pass
-    // (k_count_walk) -- no probe, append, table rebuild or C_fix.  (count.kmers batches take
-    // adopt_first_batch: rows in first-occurrence order.)
-    const uint64_t ns = B->slots();
-    const uint64_t nw = count_walk_tiles(ns);
-    DBuf<uint64_t> status(nw + 1, s);            // look-back words + the tile ticket
-    HIPC(hipMemsetAsync(status.p, 0, (nw + 1) * 8, s));
-    idx->table.bind(s);
-    idx->slot_row.bind(s);
-    idx->row_slot.bind(s);
-    idx->geom = B->geom;
-    idx->table.swap_with(B->table);          // B's release frees the old (empty) table
-    idx->slot_row.reset(ns);
-    idx->row_slot.reset(Ub);                 // B->U: exact, or an upper bound after an overflow
-    LAUNCH("k_count_walk", s,
-           launch_count_walk(idx->table.p, ns, status.p, reinterpret_cast<uint32_t*>(status.p + nw),
-                             S, source, idx->ckeys.p, idx->positions.p, idx->slot_row.p,
-                             idx->row_slot.p, s));
-    uint64_t last = 0;                       // the last tile's inclusive prefix = rows written
-    HIPC(hipMemcpyAsync(&last, status.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
-    const uint64_t n_new = last & ((1ull << 62) - 1);   // LB_MASK: payload of a status word
-    idx->U = n_new;
-    idx->N = (uint64_t)n_new * S;
-    idx->P = (uint64_t)n_new * ((uint64_t)S * (S - 1) / 2);
-    idx->max_n = n_new ? S : 0;
-    idx->kmer_count += n_new;
-    idx->canon.ready = false;
+  if (adoptable(idx, B)) {         // first batch into an empty suffix hash
+    adopt_first_batch(idx, B, source, base, s);
     return;
   }
+  reserve_rows(idx, U0 + Ub, s);
+  const uint64_t ni = B->slots();
+  const uint32_t nt = tiles_for(ni);
   DBuf<uint32_t> rank(ni + 1, s);                 // flags -> ranks of the new keys; [ni] = total
   DBuf<uint64_t> status((size_t)nt + 1, s);
   HIPC(hipMemsetAsync(status.p, 0, ((size_t)nt + 1) * 8, s));
   LAUNCH("k_count_probe", s,
-         launch_count_probe(perm_b, (uint32_t)ni, B->table.p, U0 ? idx->table.p : nullptr,
+         launch_count_probe(nullptr, (uint32_t)ni, B->table.p, U0 ? idx->table.p : nullptr,
                             idx->geom, idx->slot_row.p, S, source, idx->positions.p, rank.p, s));
   LAUNCH("k_scan_u32", s, launch_scan_u32(rank.p, ni, status.p, rank.p + ni, s));
   LAUNCH("k_count_append", s,
-         launch_count_append(perm_b, (uint32_t)ni, B->table.p, rank.p, rank.p + ni,
-                             (uint32_t)U0, S, source, idx->ckeys.p, idx->positions.p, s));
+         launch_count_append(nullptr, (uint32_t)ni, B->table.p, rank.p, rank.p + ni,
+                             (uint32_t)U0, S, source, idx->ckeys.p, idx->positions.p,
+                             ord ? B->positions.p : nullptr, ord ? idx->rord.p : nullptr, base,
+                             s));
   uint32_t n_new = 0;
   HIPC(hipMemcpyAsync(&n_new, rank.p + ni, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -1527,7 +1517,42 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, const uint32_t* perm_b, uint64_
   idx->P = U1 * ((uint64_t)S * (S - 1) / 2);
   idx->max_n = U1 ? S : 0;
   idx->kmer_count += n_new;
+  if (ord && n_new) idx->rows_sorted = false;
   idx->canon.ready = false;
+}
+
+// Rows of a count.kmers index in first-insertion order (the order of their order keys, rord):
+// C_place scatters each row's index to F[rord], C_rows compacts F in order into new row arrays
+// and repoints the slots.  Run only when a readout asks for rows, once per batch at most.
+void ensure_row_order(kmhg_index* idx, hipStream_t s) {
+  if (idx->rows_sorted || idx->canonical || !idx->U) return;
+  ReleaseGroup rg(s);
+  const uint32_t S = idx->sources;
+  const uint64_t U = idx->U;
+  const int64_t n = idx->L;                       // every order key is < the characters counted
+  DBuf<uint32_t> F((size_t)n, s);
+  HIPC(hipMemsetAsync(F.p, 0xFF, (size_t)n * 4, s));
+  LAUNCH("k_rows_place", s, launch_rows_place(idx->rord.p, (uint32_t)U, F.p, s));
+  const uint64_t nt = ((uint64_t)n + TILE - 1) / TILE;
+  DBuf<uint64_t> status(nt + 1, s);               // look-back words + the tile ticket
+  HIPC(hipMemsetAsync(status.p, 0, (nt + 1) * 8, s));
+  const uint64_t cap = idx->rows_cap;
+  DBuf<uint64_t> nk(cap), nr(cap);
+  DBuf<int32_t> nm(cap * S);
+  DBuf<uint32_t> nrs(U);
+  LAUNCH("k_rows_order", s,
+         launch_rows_order(F.p, n, status.p, reinterpret_cast<uint32_t*>(status.p + nt), S,
+                           idx->ckeys.p, idx->positions.p, idx->rord.p, idx->row_slot.p, nk.p,
+                           nm.p, nr.p, nrs.p, idx->slot_row.p, idx->table.p, s));
+  idx->ckeys.bind(s);
+  idx->positions.bind(s);
+  idx->rord.bind(s);
+  idx->row_slot.bind(s);
+  idx->ckeys.swap_with(nk);
+  idx->positions.swap_with(nm);
+  idx->rord.swap_with(nr);
+  idx->row_slot.swap_with(nrs);
+  idx->rows_sorted = true;
 }
 
 // ---------------------------------------------------------------------------- read counting
@@ -1677,7 +1702,7 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   idx->co_spread = spread;
   idx->co_path = path;
   if (B->U == 0) return;                         // every window of the batch rejected
-  merge_batch(idx, B.get(), nullptr, B->slots(), source, s);
+  merge_batch(idx, B.get(), source, 0, s);
 }
 
 // Host reads packed for the GPU: bases and qualities concatenated, read r = [off[r], off[r+1]).
@@ -1795,7 +1820,8 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
   idx->stream = s;
   Canon& c = idx->canon;
   if (c.ready) return;
-  if (idx->sources) {            // counts index: rows are already in first-insertion order
+  if (idx->sources) {            // counts index: rows in first-insertion order (ensure_row_order)
+    ensure_row_order(idx, s);
     const uint32_t U = (uint32_t)idx->U, S = idx->sources;
     c.perm.reset(U);
     c.canon_off.reset(U + 1);
@@ -2615,6 +2641,8 @@ int kmhg_counts_export(kmhg_index* idx, uint64_t* keys, int32_t* counts) {
     if (!idx || !idx->sources) fail(KMHG_EINVAL, "not a counts index");
     DeviceGuard g(idx->device);
     hipStream_t s = lib_stream();
+    idx->stream = s;
+    ensure_row_order(idx, s);
     if (idx->U && keys)
       HIPC(hipMemcpyAsync(keys, idx->ckeys.p, idx->U * 8, hipMemcpyDeviceToHost, s));
     if (idx->U && counts)

@@ -168,43 +168,37 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
                     uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr,
                     uint32_t* save_col0 = nullptr, bool skip_empty = false,
                     bool padded = false);
-// bucket starts from the histograms (passes <= 2): one workgroup per lo
-// value (div of them); kprev = the last pass's input keys, lo_start = the previous pass's digit
-// starts (saved by launch_v2_hist's save_col0; nullptr for one pass); start[b / spread] for
-// buckets b that are multiples of spread, start[nb / spread] = n
-// bprev (bucket-id streams): the last pass's input bucket ids instead of kprev
+// one level of the bucket starts from the histograms (the unfused form of BoundsFuse): one
+// workgroup per lo value (div of them); kprev = pass p's input keys, lo_start = S_(p-1) (pass 0's
+// column 0 saved by launch_v2_hist's save_col0 for p = 1; nullptr for one pass); start[c / spread]
+// for c < nlim that are multiples of spread, start[nlim / spread] = n
+// bprev (bucket-id streams): the pass's input bucket ids instead of kprev
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
-                         uint32_t spread, uint32_t* start, hipStream_t s,
+                         uint32_t spread, uint32_t* start, uint32_t nlim, hipStream_t s,
                          const uint32_t* bprev = nullptr);
 // also copies *n_valid (launch it after the pass's scan) to *host_n
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s);
-// V_bounds_lo folded into the last radix pass (passes == 2, the spread known at launch): its
-// inputs -- the pass's input stream, its scanned histogram, the previous pass's digit starts --
-// are complete before the pass starts and its output is read only by the bucket kernel, so the
-// pass's first `div` workgroups each compute one low digit's bucket starts before their tiles
-// (one launch fewer).  start == nullptr: not fused.
+// One level of V_bounds_lo folded into radix pass p >= 1: its inputs -- the pass's input
+// stream, its scanned histogram, the starts of the input's combined lower digits (S_(p-1)) --
+// are complete before the pass starts, and its output (S_p: the bucket starts for the last pass)
+// is read only by the next level or the bucket kernel, so the pass's workgroups each compute
+// the starts of a few lower-digit values before their tiles (no launch, no key pass).
+// start == nullptr: not fused.
 struct BoundsFuse {
   const uint64_t* kprev;       // the pass's input (keys, or bucket ids with bid = 1)
-  const uint32_t* lo_start;    // the previous pass's digit starts
-  uint32_t* start;
-  Digit Dlast;
-  uint32_t div, spread;
+  const uint32_t* lo_start;    // S_(p-1): starts of the input's combined lower digits
+  uint32_t* start;             // S_p
+  Digit Dlast;                 // the pass's own digit
+  uint32_t div, spread;        // div = R^p lower-digit values
   int bid;
+  uint32_t nlim;               // entries of S_p: nb for the last pass, R^(p+1) before
 };
 // the sequence must be 16-B aligned (the engine copies an unaligned input)
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s);
-// The same two passes with every output line written whole (k_v2_scatter_wc: chunked tiles,
-// line tails wait in LDS); for key streams beyond the caches.
-void launch_v2_scatter_seq_wc(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
-                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                              uint32_t* pout, hipStream_t s);
-void launch_v2_scatter_wc(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
-                          Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                          uint32_t* pout, hipStream_t s);
 // first pass over a caller's key stream of n_keys keys (>= 1): positions are e + 1; nopos:
 // keys only (count-only builds), pout unused; skip_empty: EMPTY_KEY entries are not keys (padded
 // read k-mer streams, k <= 31)
@@ -232,9 +226,6 @@ void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint3
 void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
                         uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                         hipStream_t s, uint32_t* save_col0 = nullptr);
-// bids (bucket-id streams): the sorted bucket ids instead of keys
-void launch_v2_bounds(const uint64_t* keys, const uint32_t* n_ptr, Geom g, uint32_t* start,
-                      uint64_t n_max, hipStream_t s, const uint32_t* bids = nullptr);
 struct BucketStats {           // per-bucket partials of the build statistics
   uint32_t n_kmers, max_count;
   uint64_t n_pairs;
@@ -264,27 +255,30 @@ void launch_join_emit(const uint4* jinfo, uint32_t Ua, const int32_t* pos_a, con
 void launch_count_probe(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb, const Slot* Tc,
                         Geom gc, const uint32_t* slot_row, uint32_t S, uint32_t source,
                         int32_t* M, uint32_t* newf, hipStream_t s);
+// rord (count.kmers; nullptr for a suffix hash): new row's order key = base + its key's first
+// position in the batch (bpos: the batch's position lists) - 1
 void launch_count_append(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb,
                          const uint32_t* rank, const uint32_t* n_new, uint32_t U0, uint32_t S,
-                         uint32_t source, uint64_t* ckeys, int32_t* M, hipStream_t s);
+                         uint32_t source, uint64_t* ckeys, int32_t* M, const int32_t* bpos,
+                         uint64_t* rord, uint64_t base, hipStream_t s);
 void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uint32_t S,
                          const int32_t* M, uint32_t* slot_row, uint32_t* row_slot,
                          hipStream_t s);
-// first batch into a new count.kmers pointer: F = L entries {slot, count, key} preset to slot
-// NONE; `status` = ceil(L / TILE) zeroed look-back words, `ticket` a zeroed u32
-void launch_count_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint4* F,
-                        hipStream_t s);
-void launch_count_order(const uint4* F, int64_t L, uint64_t* status, uint32_t* ticket, uint32_t S,
-                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
-                        uint32_t* row_slot, hipStream_t s);
-void launch_count_slots(Slot* T, uint64_t nslots, uint32_t S, const uint32_t* slot_row,
-                        hipStream_t s);
-// first batch into a new suffix hash: rows in slot order; `status` = ceil(nslots / TILE) zeroed
-// look-back words, `ticket` a zeroed u32
+// rows of a count.kmers index into first-insertion order: F = n u32 preset to NONE, n > every
+// order key; `status` = ceil(n / TILE) zeroed look-back words, `ticket` a zeroed u32
+void launch_rows_place(const uint64_t* rord, uint32_t U, uint32_t* F, hipStream_t s);
+void launch_rows_order(const uint32_t* F, int64_t n, uint64_t* status, uint32_t* ticket,
+                       uint32_t S, const uint64_t* ckeys, const int32_t* M, const uint64_t* rord,
+                       const uint32_t* row_slot, uint64_t* nkeys, int32_t* nM, uint64_t* nrord,
+                       uint32_t* nrow_slot, uint32_t* slot_row, Slot* T, hipStream_t s);
+// first batch into a new counts index / suffix hash: rows in slot order; `status` =
+// count_walk_tiles zeroed look-back words, `ticket` a zeroed u32; rord (count.kmers; nullptr for a
+// suffix hash): each row's order key, base + its first position in the batch (bpos) - 1
 uint64_t count_walk_tiles(uint64_t nslots);   // look-back words launch_count_walk needs
 void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
-                       uint32_t* row_slot, hipStream_t s);
+                       uint32_t* row_slot, const int32_t* bpos, uint64_t* rord, uint64_t base,
+                       hipStream_t s);
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s);
 void launch_count_canon(const uint32_t* row_slot, const int32_t* M, uint32_t U, uint32_t S,

@@ -169,6 +169,38 @@ def test_gpu_counts_first_order_vs_oracle(gpu, cgold, monkeypatch, table):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("table", ["adopt", "rebuild"])
+def test_gpu_counts_readout_between_batches(gpu, cgold, monkeypatch, table):
+    """A batch's new rows are written in slot order with their insertion-order keys and sorted
+    into first-insertion order only when a readout asks for rows (ensure_row_order).  A readout
+    after every call -- rows sorted, then more appended unsorted and sorted again, the earlier
+    rows' counts changed by later sources -- equals the oracle each time; golden cases plus
+    200 kbp batches that share half their sequence (known and new keys in one batch)."""
+    from kmer_hasher_amd import count_kmers, kmer_pos, synth
+    monkeypatch.setenv("KMHG_COUNT_TABLE", table)
+    base = synth.add_n_runs(synth.iid(300_000, 61), 0.001, 7).tobytes().decode("latin-1")
+    big = {"name": "overlap", "k": 19, "source_n": 3,
+           "calls": [(0, [base[:200_000]]), (1, [base[100_000:300_000], base[:5_000]]),
+                     (2, [base[250_000:], base[50_000:60_000]])]}
+    for case in [c for c, _ in cgold] + [big]:
+        oc = O.OracleCounts(case["k"], case["source_n"])
+        ptr = None
+        for source, seqs in case["calls"]:
+            if source < 0:
+                with pytest.warns(UserWarning):
+                    ptr = count_kmers(seqs, (case["k"], source, case["source_n"]), ptr)
+            else:
+                ptr = count_kmers(seqs, (case["k"], source, case["source_n"]), ptr)
+            oc.add(seqs, source)
+            ix = oc.index()
+            res = kmer_pos(ptr, 15)
+            assert np.array_equal(res["count"], ix.counts), case["name"]
+            assert np.array_equal(res["pos"].reshape(-1), ix.pos_rows()), case["name"]
+            assert res["kmer"] == ix.kmer_strings(), case["name"]
+        ptr.free()
+
+
+@pytest.mark.gpu
 def test_gpu_counts_errors_and_identity(gpu):
     from kmer_hasher_amd import KmerHashError, count_kmers, make_kmer_hash
     p = count_kmers(["ACGTACGTAA"], (4, 0, 2))

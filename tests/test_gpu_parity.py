@@ -196,18 +196,16 @@ def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
 
 
 @pytest.mark.parametrize("ranks", ["lane", "ballot"])
-@pytest.mark.parametrize("stream", ["bid", "keys", "keyswc"])
+@pytest.mark.parametrize("stream", ["bid", "keys"])
 def test_bucket_kernels_vs_oracle(gpu, monkeypatch, stream, ranks):
     """The group bucket kernel (one workgroup per 1024-window bucket) on every size class:
     repeated keys spanning waves, buckets beyond one batch (tandem repeats), N-runs -- with the
     radix passes and the bucket kernel ranking by the LDS atomics' lane order (the default on a
     device that passes the self-check) and by ballots (KMHG_TEST_BALLOT=1, the kernels a device
-    that fails it runs), over bucket-id and key streams, the latter also through the
-    write-combined radix passes (keyswc: KMHG_SCATTER_WC=1, the default beyond 12 M windows)."""
+    that fails it runs), over bucket-id and key streams."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_TEST_BALLOT", "1" if ranks == "ballot" else "0")
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
-    monkeypatch.setenv("KMHG_SCATTER_WC", "1" if stream == "keyswc" else "0")
     rng = np.random.default_rng(21)
     for k in (3, 12, 31, 32):
         _check_against_oracle("".join(rng.choice(list("ACGT"), 5000)), k)
@@ -252,7 +250,7 @@ def test_build_kind_reported(gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["1", "2", "3"])
-@pytest.mark.parametrize("stream", ["bid", "keys", "keyswc"])
+@pytest.mark.parametrize("stream", ["bid", "keys"])
 def test_stream_disorder_falls_back(gpu, monkeypatch, stream, mode):
     """The radix passes are stable because same-address LDS count atomics of one instruction
     are served in lane order (checked on the device before the first build); the bucket kernel
@@ -268,7 +266,6 @@ def test_stream_disorder_falls_back(gpu, monkeypatch, stream, mode):
     from kmer_hasher_amd.device import DeviceIndex
     from kmer_hasher_amd import _lib
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
-    monkeypatch.setenv("KMHG_SCATTER_WC", "1" if stream == "keyswc" else "0")
     s = synth.add_n_runs(synth.iid(300_000, 51), 0.002, 9).tobytes().decode("latin-1")
     seq = torch.frombuffer(bytearray(s.encode("latin-1")), dtype=torch.uint8).cuda()
     for disorder, one_bucket in (("0", False), (mode, True)):
@@ -285,22 +282,23 @@ def test_stream_disorder_falls_back(gpu, monkeypatch, stream, mode):
         _check_against_oracle(s, 31, pairs=False)
 
 
-@pytest.mark.parametrize("stream", ["bid", "keys", "keyswc"])
+@pytest.mark.parametrize("stream", ["bid", "keys", "keys-levels"])
 @pytest.mark.parametrize("ranks", ["lane", "ballot"])
 @pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
 def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, ranks, stream):
     """More radix passes than the input needs (KMHG_MAXR caps the radix): 1-4 passes with N-runs
-    and repeat-rich input.  Bucket starts come from the radix histograms for one or two passes
-    (k_v2_bounds_lo: the partial-tile count at each low digit's first element; a zero-width
-    tile at a tile boundary) and from a pass over the sorted keys for three or more; both against
-    the oracle.  Position builds carry bucket ids through the passes and cut the keys from the
-    code words (default up to 12 M windows); KMHG_BUILD_BID=0 carries the keys, tile by tile
-    or write-combined (keyswc: KMHG_SCATTER_WC=1, line tails waiting in LDS across a chunk's
-    tiles).  Ranks by the LDS atomics' lane order and by ballots (KMHG_TEST_BALLOT=1)."""
+    and repeat-rich input (700 K windows: maxr 6 -> 4 passes, 12 -> 3, 40 and 640 -> 2; the tiny
+    inputs 1).  Bucket starts come from the radix histograms level by level (V_bounds_lo: pass p
+    turns the starts of its input's lower digits into its output's by one partial-tile count per
+    lower-digit value; a zero-width tile at a tile boundary), each level inside its pass's
+    scatter, or launched on its own (keys-levels: KMHG_FUSE_BOUNDS=0).  Position builds carry
+    bucket ids through the passes and cut the keys from the code words (default up to 12 M
+    windows); KMHG_BUILD_BID=0 carries the keys.  Ranks by the LDS atomics' lane order and by
+    ballots (KMHG_TEST_BALLOT=1)."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_MAXR", maxr)
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
-    monkeypatch.setenv("KMHG_SCATTER_WC", "1" if stream == "keyswc" else "0")
+    monkeypatch.setenv("KMHG_FUSE_BOUNDS", "0" if stream == "keys-levels" else "1")
     monkeypatch.setenv("KMHG_TEST_BALLOT", "1" if ranks == "ballot" else "0")
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
     _check_against_oracle(s, 31, pairs=False)

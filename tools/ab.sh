@@ -32,6 +32,8 @@ for line in open(sys.argv[1]):
               "reads", rd.get("value"), "walk", rd.get("kernels_ms_per_step", {}).get("k_count_walk"),
               "rk", rd.get("kernels_ms_per_step", {}).get("k_read_kmers_emit"),
               "counts", d.get("counts", {}).get("value"),
+              "counts_k", d.get("counts", {}).get("kernels_ms_per_step"),
+              "order_ms", d.get("counts", {}).get("first_readout_row_order", {}).get("ms"),
               "depth", d.get("depth", {}).get("value"),
               "dprobe", d.get("depth", {}).get("kernels_ms_per_step", {}).get("k_depth_probe"),
               "hb_build_ms", d.get("host_boundary", {}).get("build", {}).get("ms"),
