@@ -243,6 +243,105 @@ k_count_walk(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ statu
   }
 }
 
+// Bucket-aligned walk (round 4, the default for a batch from the partitioned build): a tile is
+// WALK_B buckets of the adopted table (WALK_B * capb slots; the last tile also holds the side
+// slot), and its rows start at the count of the distinct keys of the buckets before it -- the
+// bucket kernel's per-bucket statistics, summed per tile (C_wcount) and scanned -- so the tiles
+// need no look-back chain.  The slot-tiled walk above chains 36 K tiles at config 3 and was
+// bound by that chain's hand-offs (~80 ns per tile, 2.9 ms).  A tile whose occupied slots
+// disagree with the statistics raises `err` (the host fails loudly: an internal error).
+constexpr uint32_t WALK_B = 2;
+constexpr int WALK_BPER = (int)(WALK_B * V2_CAPW / BLOCK);
+static_assert(WALK_B * V2_CAPW % BLOCK == 0 && WALK_BPER * (BLOCK / 64) < 64, "walk tile shape");
+
+// tile_compact with the tile's first rank known (no look-back); returns the tile's flag count
+template <int J>
+__device__ __forceinline__ uint32_t tile_rank_at(const bool (&flag)[J], uint64_t (&rk)[J],
+                                                 uint64_t* cw, uint64_t base) {
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  constexpr int NW = BLOCK / 64;
+  uint64_t m[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) m[j] = __ballot(flag[j]);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) cw[j * NW + wave] = (uint64_t)__popcll(m[j]);
+  }
+  __syncthreads();
+  if (wave == 0) {                       // lanes 0 .. J*NW-1 own one (j, wave) count each
+    const uint64_t c = lane < J * NW ? cw[lane] : 0;
+    const uint64_t inc = wave_incl_scan(c);
+    if (lane < J * NW) cw[lane] = base + inc - c;
+    if (lane == 63) cw[J * NW] = inc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+    rk[j] = cw[j * NW + wave] + (uint64_t)__popcll(m[j] & lanemask_lt());
+  return (uint32_t)cw[J * NW];
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_walk_counts(const BucketStats* __restrict__ bs, const Slot* __restrict__ T, Geom g,
+              uint32_t* __restrict__ tc, uint32_t nt, uint32_t* __restrict__ err) {
+  const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+  if (t == 0) *err = 0;
+  if (t >= nt) return;
+  uint32_t c = 0;
+  const uint32_t b1 = min(g.nb, (t + 1) * WALK_B);
+  for (uint32_t b = t * WALK_B; b < b1; ++b) c += bs[b].n_kmers;
+  if (T[side_slot(g)].count) {           // the side key is counted by its bucket, stored last
+    const uint32_t sb = bucket_of(mix64(EMPTY_KEY), g.nbh ? g.nbh : g.nb) - g.b0;
+    if (sb / WALK_B == t) c -= 1;
+    if (t == nt - 1) c += 1;
+  }
+  tc[t] = c;
+}
+
+__global__ void WALK_BOUNDS
+k_count_walk_b(Slot* __restrict__ T, Geom g, const uint32_t* __restrict__ tbase, uint32_t S,
+               uint32_t source,
+               uint64_t* __restrict__ ckeys, int32_t* __restrict__ M,
+               uint32_t* __restrict__ slot_row, uint32_t* __restrict__ row_slot,
+               const int32_t* __restrict__ bpos, uint64_t* __restrict__ rord, uint64_t base,
+               uint32_t* __restrict__ err) {
+  __shared__ uint64_t cw[WALK_BPER * (BLOCK / 64) + 1];
+  const uint32_t tile = blockIdx.x;
+  const uint64_t side = side_slot(g);
+  const uint64_t t0 = (uint64_t)tile * WALK_B * V2_CAPW;
+  const uint64_t t1 = min(t0 + (uint64_t)WALK_B * V2_CAPW, side);
+  const bool last = tile + 1 == gridDim.x;
+  uint4 v[WALK_BPER];
+  bool fl[WALK_BPER];
+#pragma unroll
+  for (int j = 0; j < WALK_BPER; ++j) {
+    const uint64_t i = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    v[j] = i < t1 ? *reinterpret_cast<const uint4*>(&T[i]) : make_uint4(0u, 0u, 0u, 0u);
+    fl[j] = v[j].z != 0;
+  }
+  const uint64_t r0 = tbase[tile];
+  uint64_t rk[WALK_BPER];
+  const uint32_t n = tile_rank_at<WALK_BPER>(fl, rk, cw, r0);
+  uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+  if (last) sv = *reinterpret_cast<const uint4*>(&T[side]);
+  const uint32_t ns = last && sv.z ? 1u : 0u;
+  if (threadIdx.x == 0 && n + ns != tbase[tile + 1] - (uint32_t)r0) *err = 1;
+  auto put = [&](uint64_t i, uint4 x, uint64_t row) {
+    ckeys[row] = ((uint64_t)x.y << 32) | x.x;
+    int32_t* m = M + row * S;
+    for (uint32_t q = 0; q < S; ++q) m[q] = q == source ? (int32_t)x.z : 0;
+    row_slot[row] = (uint32_t)i;
+    slot_row[i] = (uint32_t)row;
+    if (rord) rord[row] = base + first_pos(x, bpos) - 1;
+    *reinterpret_cast<uint2*>(&T[i].count) =
+        make_uint2(S, S == 1 ? x.z : ((uint32_t)row + 1) * S);
+  };
+#pragma unroll
+  for (int j = 0; j < WALK_BPER; ++j)
+    if (fl[j]) put(t0 + (uint64_t)j * BLOCK + threadIdx.x, v[j], rk[j]);
+  if (ns && threadIdx.x == 0) put(side, sv, r0 + n);
+}
+
 // C_fix: a table rebuilt by the partitioned build from the key list holds {key, 1, row + 1};
 // give every occupied slot its counts-index fields and record the slot <-> row maps.
 __global__ void __launch_bounds__(BLOCK)
@@ -304,6 +403,18 @@ void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* tic
   const unsigned nt = (unsigned)((nslots + WALK_TILE - 1) / WALK_TILE);
   hipLaunchKernelGGL(k_count_walk, dim3(nt), dim3(BLOCK), 0, s, T, nslots, status, ticket, S,
                      source, ckeys, M, slot_row, row_slot, bpos, rord, base);
+}
+uint32_t count_walk_b_tiles(uint32_t nb) { return (nb + WALK_B - 1) / WALK_B; }
+void launch_walk_counts(const BucketStats* bs, const Slot* T, Geom g, uint32_t* tc, uint32_t nt,
+                        uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(k_walk_counts, dim3(grid_of(nt)), dim3(BLOCK), 0, s, bs, T, g, tc, nt, err);
+}
+void launch_count_walk_b(Slot* T, Geom g, const uint32_t* tbase, uint32_t nt, uint32_t S,
+                         uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
+                         uint32_t* row_slot, const int32_t* bpos, uint64_t* rord, uint64_t base,
+                         uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(k_count_walk_b, dim3(nt), dim3(BLOCK), 0, s, T, g, tbase, S, source, ckeys, M,
+                     slot_row, row_slot, bpos, rord, base, err);
 }
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s) {

@@ -654,6 +654,10 @@ struct kmhg_index {
   int co_spread = 0, co_path = 0;
   DBuf<uint64_t> ckeys, rord;
   bool rows_sorted = true;
+  // per-bucket statistics of a partitioned build (bstats_nb buckets, 0 for other builds): a
+  // batch index adopted by a counts index takes its row offsets from them (k_count_walk_b)
+  DBuf<BucketStats> bstats;
+  uint32_t bstats_nb = 0;
   DBuf<uint32_t> slot_row, row_slot;
   // seq.kmer.pos diagonal path (DiagIdx, kmhg_kernels.h): the index sequence's 2-bit code words
   // and window bits, written by the build (V_hist0); the bits of repeated keys' windows are
@@ -683,7 +687,7 @@ struct kmhg_index {
   }
   // stream-ordered release of everything the index holds (work queued on `s` may still read it)
   void bind_all(hipStream_t s) {
-    table.bind(s); positions.bind(s); ckeys.bind(s); rord.bind(s); slot_row.bind(s);
+    table.bind(s); positions.bind(s); ckeys.bind(s); rord.bind(s); bstats.bind(s); slot_row.bind(s);
     row_slot.bind(s); dcodes.bind(s); ptag.bind(s);
     canon.perm.bind(s); canon.canon_off.bind(s); canon.pkeys.bind(s); canon.pair_off.bind(s);
     canon.rinfo.bind(s);
@@ -936,7 +940,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   idx->rec = PinnedPool::get().take();                     // V_stats writes the totals here
   if (!co_auto) idx->table.reset(idx->slots());
   idx->positions.reset(no_pos ? 1 : Nw);
-  DBuf<BucketStats> bstats(nb, s);
+  idx->bstats.reset(nb);            // kept: a batch index's walk takes its row offsets from it
   // co_auto: HLL rows of the first histogram pass, V_hll's registers + ticket, its pinned record
   DBuf<uint32_t> hll_rows(co_auto ? (size_t)ntiles * (HLL_REGS / 4) : 1, s);
   DBuf<uint32_t> hll_regs(co_auto ? HLL_PART_WORDS : 1, s);
@@ -1089,9 +1093,10 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     if (!no_pos && td[0] >= '1' && td[0] <= '3')
       launch_v2_test_disorder(pin, start.p, n_valid, td[0] - '0', s);
   LAUNCH("k_v2_bucket_wg", s,
-         launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, bstats.p,
+         launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, idx->bstats.p,
                              meta, no_pos, s, n_valid, (uint32_t)Nw, bid ? db.code : nullptr, k));
-  LAUNCH("k_v2_stats", s, launch_v2_stats(bstats.p, gb.nb, n_valid, meta, idx->rec.meta, s));
+  LAUNCH("k_v2_stats", s, launch_v2_stats(idx->bstats.p, gb.nb, n_valid, meta, idx->rec.meta, s));
+  idx->bstats_nb = gb.nb;
   HIPC(hipEventRecord(idx->rec.ev, s));
 #ifdef KMHG_STAMPS
   if (const char* f = std::getenv("KMHG_STAMP_FILE")) {
@@ -1188,6 +1193,7 @@ void finish_build(kmhg_index* idx) {
     if (idx->is_part) fail(KMHG_EOVERFLOW, "a bucket of a part build overflowed its LDS table");
     std::unique_ptr<kmhg_index> v1(build_device_v1(src, idx->L, idx->k, idx->stream));
     idx->build_kind = KMHG_BUILD_GLOBAL;
+    idx->bstats_nb = 0;                          // one global bucket: no per-bucket statistics
     idx->fallback = 1;                      // reported by kmhg_index_info (bench.py fails on it)
     idx->geom = v1->geom;
     idx->table.swap_with(v1->table);
@@ -1380,9 +1386,6 @@ uint64_t adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint
   reserve_rows(idx, Ub, s);
   const bool ord = !idx->canonical;
   const uint64_t ns = B->slots();
-  const uint64_t nw = count_walk_tiles(ns);
-  DBuf<uint64_t> status(nw + 1, s);                // look-back words + the tile ticket
-  HIPC(hipMemsetAsync(status.p, 0, (nw + 1) * 8, s));
   idx->table.bind(s);
   idx->slot_row.bind(s);
   idx->row_slot.bind(s);
@@ -1390,14 +1393,39 @@ uint64_t adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint
   idx->table.swap_with(B->table);                  // B's release frees the old (empty) table
   idx->slot_row.reset(ns);
   idx->row_slot.reset(Ub);
-  LAUNCH("k_count_walk", s,
-         launch_count_walk(idx->table.p, ns, status.p, reinterpret_cast<uint32_t*>(status.p + nw),
-                           S, source, idx->ckeys.p, idx->positions.p, idx->slot_row.p,
-                           idx->row_slot.p, ord ? B->positions.p : nullptr,
-                           ord ? idx->rord.p : nullptr, base, s));
+  const int32_t* bpos = ord ? B->positions.p : nullptr;
+  uint64_t* rord = ord ? idx->rord.p : nullptr;
   uint64_t n_new = Ub;
-  if (!ord) {                                      // a read batch: the last tile's prefix
-    uint64_t last = 0;
+  const char* we = std::getenv("KMHG_COUNT_WALK");   // "lb": the look-back walk (A/B, tests)
+  if (B->bstats_nb == B->geom.nb && B->geom.nb > 0 && !(we && std::string(we) == "lb")) {
+    // bucket-aligned tiles, row offsets from the bucket statistics: no look-back chain
+    const uint32_t nt = count_walk_b_tiles(B->geom.nb);
+    const uint32_t st = tiles_for(nt);
+    DBuf<uint32_t> tc(nt + 2, s);                  // tile counts -> offsets; [nt] total, [nt+1] err
+    DBuf<uint64_t> status((size_t)st + 1, s);
+    HIPC(hipMemsetAsync(status.p, 0, ((size_t)st + 1) * 8, s));
+    LAUNCH("k_walk_counts", s,
+           launch_walk_counts(B->bstats.p, idx->table.p, idx->geom, tc.p, nt, tc.p + nt + 1, s));
+    LAUNCH("k_scan_u32", s, launch_scan_u32(tc.p, nt, status.p, tc.p + nt, s));
+    LAUNCH("k_count_walk_b", s,
+           launch_count_walk_b(idx->table.p, idx->geom, tc.p, nt, S, source, idx->ckeys.p,
+                               idx->positions.p, idx->slot_row.p, idx->row_slot.p, bpos, rord,
+                               base, tc.p + nt + 1, s));   // tc: offsets, [nt] = total
+    uint32_t h[2] = {0, 0};                        // rows written, consistency flag
+    HIPC(hipMemcpyAsync(h, tc.p + nt, 8, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    if (h[1]) fail(KMHG_EDEVICE, "counts walk: bucket statistics disagree with the table (internal error)");
+    n_new = h[0];
+  } else {
+    const uint64_t nw = count_walk_tiles(ns);
+    DBuf<uint64_t> status(nw + 1, s);              // look-back words + the tile ticket
+    HIPC(hipMemsetAsync(status.p, 0, (nw + 1) * 8, s));
+    LAUNCH("k_count_walk", s,
+           launch_count_walk(idx->table.p, ns, status.p,
+                             reinterpret_cast<uint32_t*>(status.p + nw), S, source, idx->ckeys.p,
+                             idx->positions.p, idx->slot_row.p, idx->row_slot.p, bpos, rord, base,
+                             s));
+    uint64_t last = 0;                             // the last tile's inclusive prefix
     HIPC(hipMemcpyAsync(&last, status.p + nw - 1, 8, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     n_new = last & ((1ull << 62) - 1);             // LB_MASK: payload of a status word

@@ -275,6 +275,17 @@ void launch_rows_order(const uint32_t* F, int64_t n, uint64_t* status, uint32_t*
 // count_walk_tiles zeroed look-back words, `ticket` a zeroed u32; rord (count.kmers; nullptr for a
 // suffix hash): each row's order key, base + its first position in the batch (bpos) - 1
 uint64_t count_walk_tiles(uint64_t nslots);   // look-back words launch_count_walk needs
+// the same walk with bucket-aligned tiles (a batch from the partitioned build, bstats = its
+// per-bucket statistics): C_wcount writes count_walk_b_tiles(nb) tile counts to tc (and zeroes
+// *err), k_scan_u32 turns them into offsets (nt + 1 entries, [nt] = total), C_walk_b writes the
+// rows and raises *err if a tile's occupied slots disagree with the statistics
+uint32_t count_walk_b_tiles(uint32_t nb);
+void launch_walk_counts(const BucketStats* bs, const Slot* T, Geom g, uint32_t* tc, uint32_t nt,
+                        uint32_t* err, hipStream_t s);
+void launch_count_walk_b(Slot* T, Geom g, const uint32_t* tbase, uint32_t nt, uint32_t S,
+                         uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
+                         uint32_t* row_slot, const int32_t* bpos, uint64_t* rord, uint64_t base,
+                         uint32_t* err, hipStream_t s);
 void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
                        uint32_t source, uint64_t* ckeys, int32_t* M, uint32_t* slot_row,
                        uint32_t* row_slot, const int32_t* bpos, uint64_t* rord, uint64_t base,

@@ -148,14 +148,16 @@ def test_gpu_counts_golden_khash_order(gpu, cgold):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("table", ["adopt", "rebuild", "probe"])
+@pytest.mark.parametrize("table", ["adopt", "adopt-lb", "rebuild", "probe"])
 def test_gpu_counts_first_order_vs_oracle(gpu, cgold, monkeypatch, table):
     """Every way of making the counts table: the first batch's own table adopted (the default
-    for a new pointer), the partitioned build over the key list (KMHG_COUNT_TABLE=rebuild; the
-    default for later batches) and global linear probing (its overflow fallback,
-    KMHG_COUNT_TABLE=probe)."""
+    for a new pointer; its rows from bucket-aligned tiles offset by the bucket statistics, or by
+    the look-back walk, adopt-lb: KMHG_COUNT_WALK=lb), the partitioned build over the key list
+    (KMHG_COUNT_TABLE=rebuild; the default for later batches) and global linear probing (its
+    overflow fallback, KMHG_COUNT_TABLE=probe)."""
     from kmer_hasher_amd import kmer_pos
-    monkeypatch.setenv("KMHG_COUNT_TABLE", table)
+    monkeypatch.setenv("KMHG_COUNT_TABLE", table.split("-")[0])
+    monkeypatch.setenv("KMHG_COUNT_WALK", "lb" if table.endswith("-lb") else "b")
     for case, _ in cgold:
         oc = _oracle(case)
         ix = oc.index()

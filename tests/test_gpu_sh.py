@@ -32,13 +32,15 @@ def _sorted_table(ptr):
     return keys[o], M[o]
 
 
-@pytest.mark.parametrize("table", ["adopt", "rebuild"])
+@pytest.mark.parametrize("table", ["adopt", "adopt-lb", "rebuild"])
 @pytest.mark.parametrize("case", GOLD["cases"], ids=lambda c: c["name"])
 def test_sh_golden(gpu, case, inputs, monkeypatch, table):
-    """`table`: the first batch's table adopted as the suffix hash (default) or rebuilt from
-    the key list (KMHG_COUNT_TABLE=rebuild, the path of every later batch)."""
+    """`table`: the first batch's table adopted as the suffix hash (default; rows from
+    bucket-aligned tiles, or from the look-back walk with adopt-lb: KMHG_COUNT_WALK=lb) or
+    rebuilt from the key list (KMHG_COUNT_TABLE=rebuild, the path of every later batch)."""
     from kmer_hasher_amd import api
-    monkeypatch.setenv("KMHG_COUNT_TABLE", table)
+    monkeypatch.setenv("KMHG_COUNT_TABLE", table.split("-")[0])
+    monkeypatch.setenv("KMHG_COUNT_WALK", "lb" if table.endswith("-lb") else "b")
     files, genome = inputs
     ptr = None
     for f, pb, mq, mr, src in case["calls"]:
