@@ -1036,7 +1036,6 @@ def bench_readout(args, cfg, dev, world, rank):
                                                     if v[0] and n in ("k_read_first", "k_read_order")}},
                "roofline": roofline(B, dom, per[dom], t / args.steps * 1e3, pmc, ab, launches),
                "cpu_baseline": cpu,
-               "index_build": build_rec,
                "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
     idx.free()
 
