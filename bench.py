@@ -790,12 +790,12 @@ def main():
                     "ms": round(t_order * 1e3, 4),
                     "kernels_ms": {n: round(v, 5) for n, v in order_k.items()},
                     "note": "once per counts pointer (and again after a later batch), when a "
-                            "readout first asks for rows: rows sorted into first-insertion order "
-                            "by their order keys (k_rows_place / k_rows_order)"},
+                            "readout first asks for rows: the rows' first-insertion order derived "
+                            "from their order keys (k_rows_place / k_rows_order)"},
                 "note": "count.kmers(seq, c(k, 0, 2)) into a new pointer per step: partitioned "
                         "build of the batch, whose table the new pointer adopts, its rows "
                         "written in slot order with their insertion-order keys (k_count_walk); "
-                        "first_readout_row_order is the one-time sort a readout triggers"}
+                        "first_readout_row_order is the one-time ordering a readout triggers"}
             cdom = max((n for n in cper if n.startswith("k_count_")), key=cper.get, default=None)
             if cdom:
                 out["counts"]["roofline"] = _leg_roofline(

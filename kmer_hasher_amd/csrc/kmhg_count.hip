@@ -92,16 +92,17 @@ k_count_insert(const uint64_t* __restrict__ ckeys, uint32_t U, Slot* __restrict_
 }
 
 __global__ void __launch_bounds__(BLOCK)
-k_count_canon(const uint32_t* __restrict__ row_slot, const int32_t* __restrict__ M, uint32_t U,
-              uint32_t S, uint32_t* __restrict__ perm, uint32_t* __restrict__ canon_off,
-              uint32_t* __restrict__ pkeys, uint64_t* __restrict__ pair_off,
-              uint2* __restrict__ rinfo) {
+k_count_canon(const uint32_t* __restrict__ rorder, const uint32_t* __restrict__ row_slot,
+              const int32_t* __restrict__ M, uint32_t U, uint32_t S, uint32_t* __restrict__ perm,
+              uint32_t* __restrict__ canon_off, uint32_t* __restrict__ pkeys,
+              uint64_t* __restrict__ pair_off, uint2* __restrict__ rinfo) {
   const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
   if (r > U) return;
-  canon_off[r] = r * S;
+  canon_off[r] = r * S;                  // output rows: S per key in readout order
   if (r == U) return;
-  perm[r] = row_slot[r];
-  rinfo[r] = make_uint2(S, S == 1 ? (uint32_t)M[r] : (r + 1) * S);   // the slot's {count, aux}
+  const uint32_t o = rorder ? rorder[r] : r;   // the row (in the count matrix) read out r-th
+  perm[r] = row_slot[o];
+  rinfo[r] = make_uint2(S, S == 1 ? (uint32_t)M[o] : (o + 1) * S);   // the slot's {count, aux}
   if (S >= 2) {
     pkeys[r] = r;
     pair_off[r] = (uint64_t)r * ((uint64_t)S * (S - 1) / 2);
@@ -140,10 +141,10 @@ __device__ __forceinline__ void tile_compact(const bool (&flag)[J], uint64_t (&r
 
 // Row order of a count.kmers index (first insertion, the order kh_put saw the keys in, which the
 // khash readout order replays): a batch's rows are written in slot order, each with its order
-// key rord = base + first position - 1 (base = the characters counted before the batch), and
-// sorted once when a readout needs them (kmhg_engine.cpp ensure_row_order): C_place puts row r at
-// F[rord[r]] (F preset to NONE), C_rows compacts F in order into the new rows, moving each row's
-// key, counts, order key and slot, and pointing its slot at it.
+// key rord = base + first position - 1 (base = the characters counted before the batch); when a
+// readout needs the order (kmhg_engine.cpp ensure_row_order), C_place puts row r at F[rord[r]]
+// (F preset to NONE) and C_rows compacts F in order into rorder (rank -> row).  The rows never
+// move: the readout arrays (C_canon) and the export (C_gather) go through rorder.
 __global__ void __launch_bounds__(BLOCK)
 k_rows_place(const uint64_t* __restrict__ rord, uint32_t U, uint32_t* __restrict__ F) {
   const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
@@ -152,12 +153,7 @@ k_rows_place(const uint64_t* __restrict__ rord, uint32_t U, uint32_t* __restrict
 
 __global__ void __launch_bounds__(BLOCK)
 k_rows_order(const uint32_t* __restrict__ F, int64_t n, uint64_t* __restrict__ status,
-             uint32_t* __restrict__ ticket, uint32_t S, const uint64_t* __restrict__ ckeys,
-             const int32_t* __restrict__ M, const uint64_t* __restrict__ rord,
-             const uint32_t* __restrict__ row_slot, uint64_t* __restrict__ nkeys,
-             int32_t* __restrict__ nM, uint64_t* __restrict__ nrord,
-             uint32_t* __restrict__ nrow_slot, uint32_t* __restrict__ slot_row,
-             Slot* __restrict__ T) {
+             uint32_t* __restrict__ ticket, uint32_t* __restrict__ rorder) {
   __shared__ uint64_t cw[WPT * (BLOCK / 64)];
   __shared__ uint32_t tk;
   const uint32_t tile = take_ticket(ticket, &tk);
@@ -173,17 +169,20 @@ k_rows_order(const uint32_t* __restrict__ F, int64_t n, uint64_t* __restrict__ s
   uint64_t rk[WPT];
   tile_compact(fl, rk, cw, status, tile);
 #pragma unroll
-  for (int j = 0; j < WPT; ++j) {
-    if (!fl[j]) continue;
-    const uint64_t i = rk[j], r = o[j];
-    nkeys[i] = ckeys[r];
-    for (uint32_t q = 0; q < S; ++q) nM[i * S + q] = M[r * S + q];
-    nrord[i] = rord[r];
-    const uint32_t sl = row_slot[r];
-    nrow_slot[i] = sl;
-    slot_row[sl] = (uint32_t)i;
-    if (S > 1) T[sl].aux = ((uint32_t)i + 1) * S;     // the row's counts end (S = 1: the count)
-  }
+  for (int j = 0; j < WPT; ++j)
+    if (fl[j]) rorder[rk[j]] = o[j];
+}
+
+// rows in first-insertion order for an export: row r of the output is row rorder[r]
+__global__ void __launch_bounds__(BLOCK)
+k_rows_gather(const uint32_t* __restrict__ rorder, const uint64_t* __restrict__ ckeys,
+              const int32_t* __restrict__ M, uint32_t U, uint32_t S, uint64_t* __restrict__ okeys,
+              int32_t* __restrict__ oM) {
+  const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
+  if (r >= U) return;
+  const uint64_t o = rorder[r];
+  okeys[r] = ckeys[o];
+  for (uint32_t q = 0; q < S; ++q) oM[(uint64_t)r * S + q] = M[o * S + q];
 }
 
 // The first batch into an empty counts index or suffix hash: the batch table becomes the counts
@@ -388,12 +387,14 @@ void launch_rows_place(const uint64_t* rord, uint32_t U, uint32_t* F, hipStream_
   hipLaunchKernelGGL(k_rows_place, dim3(grid_of(U)), dim3(BLOCK), 0, s, rord, U, F);
 }
 void launch_rows_order(const uint32_t* F, int64_t n, uint64_t* status, uint32_t* ticket,
-                       uint32_t S, const uint64_t* ckeys, const int32_t* M, const uint64_t* rord,
-                       const uint32_t* row_slot, uint64_t* nkeys, int32_t* nM, uint64_t* nrord,
-                       uint32_t* nrow_slot, uint32_t* slot_row, Slot* T, hipStream_t s) {
+                       uint32_t* rorder, hipStream_t s) {
   const unsigned nt = (unsigned)(((uint64_t)n + TILE - 1) / TILE);
-  hipLaunchKernelGGL(k_rows_order, dim3(nt), dim3(BLOCK), 0, s, F, n, status, ticket, S, ckeys,
-                     M, rord, row_slot, nkeys, nM, nrord, nrow_slot, slot_row, T);
+  hipLaunchKernelGGL(k_rows_order, dim3(nt), dim3(BLOCK), 0, s, F, n, status, ticket, rorder);
+}
+void launch_rows_gather(const uint32_t* rorder, const uint64_t* ckeys, const int32_t* M,
+                        uint32_t U, uint32_t S, uint64_t* okeys, int32_t* oM, hipStream_t s) {
+  hipLaunchKernelGGL(k_rows_gather, dim3(grid_of(U)), dim3(BLOCK), 0, s, rorder, ckeys, M, U, S,
+                     okeys, oM);
 }
 uint64_t count_walk_tiles(uint64_t nslots) { return (nslots + WALK_TILE - 1) / WALK_TILE; }
 void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* ticket, uint32_t S,
@@ -421,11 +422,11 @@ void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, ui
   hipLaunchKernelGGL(k_count_fix, dim3(grid_cap(nslots)), dim3(BLOCK), 0, s, T, nslots, S, M,
                      slot_row, row_slot);
 }
-void launch_count_canon(const uint32_t* row_slot, const int32_t* M, uint32_t U, uint32_t S,
-                        uint32_t* perm, uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
-                        uint2* rinfo, hipStream_t s) {
-  hipLaunchKernelGGL(k_count_canon, dim3(grid_of((uint64_t)U + 1)), dim3(BLOCK), 0, s, row_slot,
-                     M, U, S, perm, canon_off, pkeys, pair_off, rinfo);
+void launch_count_canon(const uint32_t* rorder, const uint32_t* row_slot, const int32_t* M,
+                        uint32_t U, uint32_t S, uint32_t* perm, uint32_t* canon_off,
+                        uint32_t* pkeys, uint64_t* pair_off, uint2* rinfo, hipStream_t s) {
+  hipLaunchKernelGGL(k_count_canon, dim3(grid_of((uint64_t)U + 1)), dim3(BLOCK), 0, s, rorder,
+                     row_slot, M, U, S, perm, canon_off, pkeys, pair_off, rinfo);
 }
 
 }  // namespace kmhg

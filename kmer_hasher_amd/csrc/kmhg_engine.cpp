@@ -643,8 +643,9 @@ struct kmhg_index {
   // counts index (count.kmers, kmhg_count.hip): sources > 0.  `positions` then holds the
   // U x sources count matrix (row-major, rows_cap allocated), `ckeys` the keys of the rows,
   // slot_row / row_slot the table <-> row maps.  count.kmers rows are appended in slot order with
-  // their insertion-order keys `rord` and sorted into first-insertion order before a readout
-  // (ensure_row_order; rows_sorted); a suffix hash's rows are order-free (no rord).
+  // their insertion-order keys `rord`; before a readout, `rorder` (first-insertion rank -> row)
+  // is derived from them (ensure_row_order; order_ready) -- the rows themselves never move.  A
+  // suffix hash's rows are order-free (no rord, no rorder).
   uint32_t sources = 0;
   bool canonical = false;         // suffix hash (count.kmers.fq.sh.rp): canonical k-mer counts
   uint64_t rows_cap = 0, kmer_count = 0;
@@ -653,7 +654,8 @@ struct kmhg_index {
   double co_est = 0;
   int co_spread = 0, co_path = 0;
   DBuf<uint64_t> ckeys, rord;
-  bool rows_sorted = true;
+  DBuf<uint32_t> rorder;
+  bool order_ready = true;
   // per-bucket statistics of a partitioned build (bstats_nb buckets, 0 for other builds): a
   // batch index adopted by a counts index takes its row offsets from them (k_count_walk_b)
   DBuf<BucketStats> bstats;
@@ -687,7 +689,8 @@ struct kmhg_index {
   }
   // stream-ordered release of everything the index holds (work queued on `s` may still read it)
   void bind_all(hipStream_t s) {
-    table.bind(s); positions.bind(s); ckeys.bind(s); rord.bind(s); bstats.bind(s); slot_row.bind(s);
+    table.bind(s); positions.bind(s); ckeys.bind(s); rord.bind(s); rorder.bind(s); bstats.bind(s);
+    slot_row.bind(s);
     row_slot.bind(s); dcodes.bind(s); ptag.bind(s);
     canon.perm.bind(s); canon.canon_off.bind(s); canon.pkeys.bind(s); canon.pair_off.bind(s);
     canon.rinfo.bind(s);
@@ -1435,7 +1438,7 @@ uint64_t adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint
   idx->P = n_new * ((uint64_t)S * (S - 1) / 2);
   idx->max_n = n_new ? S : 0;
   idx->kmer_count += n_new;
-  idx->rows_sorted = !ord;
+  idx->order_ready = !ord;
   idx->canon.ready = false;
   return n_new;
 }
@@ -1545,17 +1548,17 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint64_t base,
   idx->P = U1 * ((uint64_t)S * (S - 1) / 2);
   idx->max_n = U1 ? S : 0;
   idx->kmer_count += n_new;
-  if (ord && n_new) idx->rows_sorted = false;
+  if (ord && n_new) idx->order_ready = false;
   idx->canon.ready = false;
 }
 
-// Rows of a count.kmers index in first-insertion order (the order of their order keys, rord):
-// C_place scatters each row's index to F[rord], C_rows compacts F in order into new row arrays
-// and repoints the slots.  Run only when a readout asks for rows, once per batch at most.
+// First-insertion order of a count.kmers index's rows (the order of their order keys, rord):
+// C_place puts each row's index at F[rord], C_rows compacts F in order into rorder (rank ->
+// row).  The rows stay where they are: the readout arrays (k_count_canon) and the export take
+// them through rorder.  Run when a readout first asks for rows after a batch.
 void ensure_row_order(kmhg_index* idx, hipStream_t s) {
-  if (idx->rows_sorted || idx->canonical || !idx->U) return;
+  if (idx->order_ready || idx->canonical || !idx->U) return;
   ReleaseGroup rg(s);
-  const uint32_t S = idx->sources;
   const uint64_t U = idx->U;
   const int64_t n = idx->L;                       // every order key is < the characters counted
   DBuf<uint32_t> F((size_t)n, s);
@@ -1564,23 +1567,17 @@ void ensure_row_order(kmhg_index* idx, hipStream_t s) {
   const uint64_t nt = ((uint64_t)n + TILE - 1) / TILE;
   DBuf<uint64_t> status(nt + 1, s);               // look-back words + the tile ticket
   HIPC(hipMemsetAsync(status.p, 0, (nt + 1) * 8, s));
-  const uint64_t cap = idx->rows_cap;
-  DBuf<uint64_t> nk(cap), nr(cap);
-  DBuf<int32_t> nm(cap * S);
-  DBuf<uint32_t> nrs(U);
+  idx->rorder.bind(s);
+  idx->rorder.reset(U);
   LAUNCH("k_rows_order", s,
-         launch_rows_order(F.p, n, status.p, reinterpret_cast<uint32_t*>(status.p + nt), S,
-                           idx->ckeys.p, idx->positions.p, idx->rord.p, idx->row_slot.p, nk.p,
-                           nm.p, nr.p, nrs.p, idx->slot_row.p, idx->table.p, s));
-  idx->ckeys.bind(s);
-  idx->positions.bind(s);
-  idx->rord.bind(s);
-  idx->row_slot.bind(s);
-  idx->ckeys.swap_with(nk);
-  idx->positions.swap_with(nm);
-  idx->rord.swap_with(nr);
-  idx->row_slot.swap_with(nrs);
-  idx->rows_sorted = true;
+         launch_rows_order(F.p, n, status.p, reinterpret_cast<uint32_t*>(status.p + nt),
+                           idx->rorder.p, s));
+  idx->order_ready = true;
+}
+
+// rorder of a counts index, or nullptr when its rows are already in order (a suffix hash)
+const uint32_t* row_order_of(const kmhg_index* idx) {
+  return idx->canonical ? nullptr : idx->rorder.p;
 }
 
 // ---------------------------------------------------------------------------- read counting
@@ -1856,7 +1853,8 @@ void prepare_canon(kmhg_index* idx, hipStream_t s) {
     c.pkeys.reset(S >= 2 ? U : 1);
     c.pair_off.reset(S >= 2 ? U : 1);
     c.rinfo.reset(U);
-    LAUNCH("k_count_canon", s, launch_count_canon(idx->row_slot.p, idx->positions.p, U, S, c.perm.p,
+    LAUNCH("k_count_canon", s, launch_count_canon(row_order_of(idx), idx->row_slot.p,
+                                                  idx->positions.p, U, S, c.perm.p,
                                                   c.canon_off.p, c.pkeys.p, c.pair_off.p,
                                                   c.rinfo.p, s));
     c.n_multi = S >= 2 ? U : 0;
@@ -2670,12 +2668,26 @@ int kmhg_counts_export(kmhg_index* idx, uint64_t* keys, int32_t* counts) {
     DeviceGuard g(idx->device);
     hipStream_t s = lib_stream();
     idx->stream = s;
+    ReleaseGroup rg(s);
     ensure_row_order(idx, s);
-    if (idx->U && keys)
-      HIPC(hipMemcpyAsync(keys, idx->ckeys.p, idx->U * 8, hipMemcpyDeviceToHost, s));
-    if (idx->U && counts)
-      HIPC(hipMemcpyAsync(counts, idx->positions.p, idx->U * idx->sources * 4,
-                          hipMemcpyDeviceToHost, s));
+    const uint64_t U = idx->U, S = idx->sources;
+    const uint64_t* k = idx->ckeys.p;
+    const int32_t* m = idx->positions.p;
+    DBuf<uint64_t> gk;
+    DBuf<int32_t> gm;
+    if (U && row_order_of(idx) && (keys || counts)) {   // rows in first-insertion order
+      gk.reset(U);
+      gm.reset(U * S);
+      gk.bind(s);
+      gm.bind(s);
+      LAUNCH("k_rows_gather", s, launch_rows_gather(row_order_of(idx), idx->ckeys.p,
+                                                    idx->positions.p, (uint32_t)U, (uint32_t)S,
+                                                    gk.p, gm.p, s));
+      k = gk.p;
+      m = gm.p;
+    }
+    if (U && keys) HIPC(hipMemcpyAsync(keys, k, U * 8, hipMemcpyDeviceToHost, s));
+    if (U && counts) HIPC(hipMemcpyAsync(counts, m, U * S * 4, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
   });
 }

@@ -264,13 +264,14 @@ void launch_count_append(const uint32_t* perm_b, uint32_t Ub, const Slot* Tb,
 void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uint32_t S,
                          const int32_t* M, uint32_t* slot_row, uint32_t* row_slot,
                          hipStream_t s);
-// rows of a count.kmers index into first-insertion order: F = n u32 preset to NONE, n > every
-// order key; `status` = ceil(n / TILE) zeroed look-back words, `ticket` a zeroed u32
+// first-insertion order of a count.kmers index's rows: F = n u32 preset to NONE, n > every
+// order key; `status` = ceil(n / TILE) zeroed look-back words, `ticket` a zeroed u32; rorder[i] =
+// the row read out i-th.  C_gather copies the rows out in that order.
 void launch_rows_place(const uint64_t* rord, uint32_t U, uint32_t* F, hipStream_t s);
 void launch_rows_order(const uint32_t* F, int64_t n, uint64_t* status, uint32_t* ticket,
-                       uint32_t S, const uint64_t* ckeys, const int32_t* M, const uint64_t* rord,
-                       const uint32_t* row_slot, uint64_t* nkeys, int32_t* nM, uint64_t* nrord,
-                       uint32_t* nrow_slot, uint32_t* slot_row, Slot* T, hipStream_t s);
+                       uint32_t* rorder, hipStream_t s);
+void launch_rows_gather(const uint32_t* rorder, const uint64_t* ckeys, const int32_t* M,
+                        uint32_t U, uint32_t S, uint64_t* okeys, int32_t* oM, hipStream_t s);
 // first batch into a new counts index / suffix hash: rows in slot order; `status` =
 // count_walk_tiles zeroed look-back words, `ticket` a zeroed u32; rord (count.kmers; nullptr for a
 // suffix hash): each row's order key, base + its first position in the batch (bpos) - 1
@@ -292,9 +293,10 @@ void launch_count_walk(Slot* T, uint64_t nslots, uint64_t* status, uint32_t* tic
                        hipStream_t s);
 void launch_count_fix(Slot* T, uint64_t nslots, uint32_t S, const int32_t* M, uint32_t* slot_row,
                       uint32_t* row_slot, hipStream_t s);
-void launch_count_canon(const uint32_t* row_slot, const int32_t* M, uint32_t U, uint32_t S,
-                        uint32_t* perm, uint32_t* canon_off, uint32_t* pkeys, uint64_t* pair_off,
-                        uint2* rinfo, hipStream_t s);
+// rorder: the rows in readout order (nullptr: the row order itself)
+void launch_count_canon(const uint32_t* rorder, const uint32_t* row_slot, const int32_t* M,
+                        uint32_t U, uint32_t S, uint32_t* perm, uint32_t* canon_off,
+                        uint32_t* pkeys, uint64_t* pair_off, uint2* rinfo, hipStream_t s);
 
 #ifdef KMHG_STAMPS
 void set_stamp_buffer(uint64_t* p);
