@@ -373,7 +373,7 @@ def counts_algorithmic_bytes(kernel: str, L: int, U: int, S: int, nslots: int = 
     """Minimum bytes of the count.kmers kernels (first batch into a new pointer): C_walk reads
     every slot of the adopted table (16 B) and, per key, writes its row (key 8 B, S counts,
     row_slot 4 B, order key 8 B), slot_row (4 B) and the slot's count fields (8 B)."""
-    if kernel == "k_count_walk":
+    if kernel in ("k_count_walk", "k_count_walk_b"):
         return 16 * nslots + U * (8 + 4 * S + 4 + 8 + 4 + 8)
     return None
 
