@@ -986,6 +986,29 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     div = R;
   }
   uint32_t *bin = bA.p, *bout = bB.p;
+  // the later passes' histogram layout: [digit][tile] over the tiles of their input.  A part
+  // build keeps ~1/n_parts of the windows after pass 0, so it reads that count back and sizes
+  // the later passes to it (a separate histogram, so pass 0's column 0 stays readable) instead
+  // of walking every window's tile again -- one host round trip per part build.
+  uint32_t* hp = hist.p;
+  uint32_t C = ntiles, nst = n_status;
+  uint64_t nh = nhist;
+  DBuf<uint32_t> hist1;
+  if (n_parts >= 1 && passes > 1) {
+    uint32_t nv = 0;
+    HIPC(hipMemcpyAsync(&nv, n_valid, 4, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    C = std::max<uint32_t>(1u, (uint32_t)(((uint64_t)nv + PTILE - 1) / PTILE));
+    nh = (uint64_t)R * C;
+    nst = tiles_for(nh) + 1;
+    hist1.reset(nh);
+    hist1.bind(s);
+    hp = hist1.p;
+    // pass 0's digit starts (its scanned column 0), which pass 1's V_hist saves otherwise
+    HIPC(hipMemcpy2DAsync(lo_save.p, 4, hist.p, (size_t)ntiles * 4, 4, R,
+                          hipMemcpyDeviceToDevice, s));
+  }
+  uint32_t* save1 = hp == hist.p ? lo_save.p : nullptr;   // where pass 1 saves column 0
   // each level of the bucket starts rides in its pass (BoundsFuse), except the last one of a
   // count-only build whose spread is chosen after the passes (co_auto); KMHG_FUSE_BOUNDS=0
   // (A/B) launches every level on its own
@@ -1005,19 +1028,19 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   auto launch_level = [&](const BoundsFuse& f) {
     const uint64_t* kp = f.bid ? nullptr : f.kprev;
     const uint32_t* bp = f.bid ? reinterpret_cast<const uint32_t*>(f.kprev) : nullptr;
-    LAUNCH("k_v2_bounds", s, launch_v2_bounds_lo(kp, n_valid, g, f.Dlast, f.div, hist.p, ntiles,
+    LAUNCH("k_v2_bounds", s, launch_v2_bounds_lo(kp, n_valid, g, f.Dlast, f.div, hp, C,
                                                  f.lo_start, f.spread, f.start, f.nlim, s, bp));
   };
   for (uint32_t p = 1; bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
     const bool last = p + 1 == passes;
     LAUNCH("k_v2_hist", s,
-           launch_v2_hist_bid(bin, n_valid, g, Dp, hist.p, ntiles, status, n_status, s,
-                              p == 1 ? lo_save.p : nullptr));
-    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
+           launch_v2_hist_bid(bin, n_valid, g, Dp, hp, C, status, nst, s,
+                              p == 1 ? save1 : nullptr));
+    LAUNCH("k_scan_u32", s, launch_scan_u32(hp, nh, status, n_valid, s));
     const BoundsFuse lv = level_of(p, bin, true, 1u);
     LAUNCH("k_v2_scatter", s,
-           launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hist.p, ntiles, last ? nullptr : bout,
+           launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hp, C, last ? nullptr : bout,
                                  pout, pad, s, fused(p) ? &lv : nullptr));
     if (!fused(p) && !last) launch_level(lv);
     std::swap(bin, bout);
@@ -1031,11 +1054,11 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const uint64_t* src = keys0 ? d_keys : kin;
     const bool hll = co_auto && p == 0;
     LAUNCH("k_v2_hist", s,
-           launch_v2_hist(src, n_valid, g, Dp, hist.p, ntiles, status, n_status, s,
+           launch_v2_hist(src, n_valid, g, Dp, hp, C, status, nst, s,
                           hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
-                          p == 1 ? lo_save.p : nullptr, keys0 && skip_empty,
+                          p == 1 ? save1 : nullptr, keys0 && skip_empty,
                           /*padded=*/!keys0));
-    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
+    LAUNCH("k_scan_u32", s, launch_scan_u32(hp, nh, status, n_valid, s));
     if (hll) {   // after the scan: the estimate travels with the valid key count
       LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ntiles, hll_regs.p,
                                           &hrec.meta->distinct_est, n_valid,
@@ -1050,11 +1073,11 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       const BoundsFuse lv = level_of(p, kin, false, 1u);
       if (no_pos)
         LAUNCH("k_v2_scatter", s,
-               launch_v2_scatter_nopos(kin, n_valid, g, Dp, hist.p, ntiles, kout, pad, s,
+               launch_v2_scatter_nopos(kin, n_valid, g, Dp, hp, C, kout, pad, s,
                                        fused(p) ? &lv : nullptr));
       else
         LAUNCH("k_v2_scatter", s,
-               launch_v2_scatter(kin, pin, n_valid, g, Dp, hist.p, ntiles, kout, pout, pad, s,
+               launch_v2_scatter(kin, pin, n_valid, g, Dp, hp, C, kout, pout, pad, s,
                                  fused(p) ? &lv : nullptr));
       if (!fused(p) && !last) launch_level(lv);
     }
