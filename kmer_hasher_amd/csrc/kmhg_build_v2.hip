@@ -136,14 +136,21 @@ __device__ __forceinline__ void diag_words_out(const PStage& st, uint32_t tile, 
 #ifndef KMHG_HIST0_WAVES
 #define KMHG_HIST0_WAVES 6   // Win8: 80 VGPRs without spills (7 spills 44 B / lane)
 #endif
-template <bool CODES, bool BIDS = false>
-__global__ void __launch_bounds__(BLOCK, KMHG_HIST0_WAVES)
+// PARTC (a part build of an owner-computes build, key streams): the windows this part owns are
+// also written compacted per tile -- (key, position) of tile t's owned windows in window order at
+// [t * PTILE, t * PTILE + tcnt[t]) -- so the first scatter reads ~1/n_parts of the windows
+// instead of encoding and hashing every window of the sequence a second time.
+template <bool CODES, bool BIDS = false, bool PARTC = false>
+__global__ void __launch_bounds__(BLOCK, PARTC ? 5 : KMHG_HIST0_WAVES)   // PARTC: no spills
 k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
             uint32_t* __restrict__ hist, uint32_t ntiles, uint64_t* __restrict__ scan_status,
             uint32_t n_status, BuildMeta* __restrict__ meta, uint32_t* __restrict__ code,
-            uint16_t* __restrict__ nbit, uint32_t* __restrict__ bids) {
+            uint16_t* __restrict__ nbit, uint32_t* __restrict__ bids,
+            uint64_t* __restrict__ ckeys, uint32_t* __restrict__ cpos,
+            uint32_t* __restrict__ tcnt) {
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
+  __shared__ uint64_t scs[5];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
     scan_status[i] = 0;
   if (blockIdx.x == 0 && threadIdx.x < sizeof(BuildMeta) / 4)
@@ -181,6 +188,23 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
             bl[j] = b;
           }
         }
+      }
+      if (PARTC) {                 // this part's windows, compacted in window order
+        uint32_t own = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) own |= (bl[j] != ~0u ? 1u : 0u) << j;
+        uint64_t tot;
+        uint32_t at = (uint32_t)block_excl_scan((uint64_t)__popc(own), scs, tot);
+        const uint64_t base = (uint64_t)tile * PTILE;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (own >> j & 1u) {
+            ckeys[base + at] = win.key(j);
+            cpos[base + at] = (uint32_t)(s0 + j + 1);
+            ++at;
+          }
+        }
+        if (threadIdx.x == 0) tcnt[tile] = (uint32_t)tot;
       }
       // the id array holds Nw + PTILE entries: a tile's last 16-B stores stay inside it
       if (BIDS && s0 < Nw) {
@@ -535,7 +559,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, uint32_t ntiles,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad,
-             int skip_empty, BoundsFuse bf) {
+             int skip_empty, BoundsFuse bf, const uint32_t* __restrict__ tcnt) {
   using KT = typename std::conditional<BM != 0, uint32_t, uint64_t>::type;
   using SL = ScatterLDS<KT>;
   static_assert(BM == 0 || !NOPOS, "bucket-id streams carry positions");
@@ -571,13 +595,16 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
     for (uint32_t lo = blockIdx.x; lo < bf.div; lo += gridDim.x)
       bounds_lo_body(lo, &S.wc[0][0], bf.kprev, *n_ptr, g, bf.Dlast, bf.div, hist, ntiles,
                      bf.lo_start, bf.spread, bf.start, bf.bid, TB, bf.nlim);
-  // the next tile's inputs are in flight while this one is processed
+  // the next tile's inputs are in flight while this one is processed.  tcnt (a part build's first
+  // pass over V_hist0's compacted tiles): tile t holds tcnt[t] elements at [t * PTILE, ...)
+  uint32_t tc_next = 0, tc_cur = 0;
   KT nkey[PER];
   uint32_t npos[PER];
   StageRegs<PSTAGE_W16> nchars;
   auto prefetch = [&](uint32_t tv) {
     const uint64_t t0 = (uint64_t)tv * PTILE;
     load_bases(tv);
+    if (tcnt) tc_next = tcnt[tv];
     if (FROM_SEQ) {
       stage_load<PSTAGE_W16, true>(nchars, seq, L, (int64_t)t0 - HALO, true);
     } else {
@@ -620,6 +647,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         ps[cc] = KEYS0 ? (uint32_t)(tile0 + wbase + (uint32_t)cc * 64 + lane + 1) : npos[cc];
       }
     }
+    tc_cur = tc_next;
     prefetch(tile_at(min(it + 1, n_iter - 1)));   // unconditional: static vmcnt
     for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
     __syncthreads();                       // stage packed; previous tile's write-out done
@@ -637,10 +665,10 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         key[c] = BM ? (KT)bl : (KT)kk;
         dg[c] = act[c] ? digit_of_b(bl, D) : 0;
       } else if (BM) {
-        act[c] = e < n && !(KEYS0 && (uint32_t)key[c] == ~0u);
+        act[c] = (tcnt ? w < tc_cur : e < n) && !(KEYS0 && (uint32_t)key[c] == ~0u);
         dg[c] = act[c] ? digit_of_b((uint32_t)key[c], D) : 0;
       } else {
-        act[c] = e < n && !(KEYS0 && skip_empty && key[c] == EMPTY_KEY);
+        act[c] = (tcnt ? w < tc_cur : e < n) && !(KEYS0 && skip_empty && key[c] == EMPTY_KEY);
         dg[c] = act[c] ? digit_of_h(mix64((uint64_t)key[c]), g, D) : 0;
       }
     }
@@ -1225,22 +1253,27 @@ bool ballot_ranks();
 void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                      uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                      BuildMeta* meta, hipStream_t s, uint32_t* code, uint16_t* nbit,
-                     uint32_t* bids) {
-  if (bids) {                  // bucket-id builds (keep the code words)
+                     uint32_t* bids, uint64_t* ckeys, uint32_t* cpos, uint32_t* tcnt) {
+  if (ckeys) {                 // a part build's compacted windows (keep the code words)
+    static const unsigned cap_p = resident_blocks((const void*)k_v2_hist0p<true, false, true>);
+    hipLaunchKernelGGL((k_v2_hist0p<true, false, true>), dim3(std::min<unsigned>(ntiles, cap_p)),
+                       dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ntiles, scan_status,
+                       n_status, meta, code, nbit, nullptr, ckeys, cpos, tcnt);
+  } else if (bids) {           // bucket-id builds (keep the code words)
     static const unsigned cap_b = resident_blocks((const void*)k_v2_hist0p<true, true>);
     hipLaunchKernelGGL((k_v2_hist0p<true, true>), dim3(std::min<unsigned>(ntiles, cap_b)),
                        dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ntiles, scan_status,
-                       n_status, meta, code, nbit, bids);
+                       n_status, meta, code, nbit, bids, nullptr, nullptr, nullptr);
   } else if (code && nbit) {
     static const unsigned cap_c = resident_blocks((const void*)k_v2_hist0p<true, false>);
     hipLaunchKernelGGL((k_v2_hist0p<true, false>), dim3(std::min<unsigned>(ntiles, cap_c)),
                        dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ntiles, scan_status,
-                       n_status, meta, code, nbit, nullptr);
+                       n_status, meta, code, nbit, nullptr, nullptr, nullptr, nullptr);
   } else {
     static const unsigned cap_n = resident_blocks((const void*)k_v2_hist0p<false, false>);
     hipLaunchKernelGGL((k_v2_hist0p<false, false>), dim3(std::min<unsigned>(ntiles, cap_n)),
                        dim3(BLOCK), 0, s, seq, L, k, Nw, g, D, hist, ntiles, scan_status,
-                       n_status, meta, nullptr, nullptr, nullptr);
+                       n_status, meta, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
   }
 }
 // Beyond 64 tiles of 2048 entries: the 32-per-thread look-back scan at any length.  Measured
@@ -1302,7 +1335,7 @@ void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geo
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s) {
   KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
-               kout, pout, pad, 0, kNoFuse);
+               kout, pout, pad, 0, kNoFuse, nullptr);
 }
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
                             const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
@@ -1311,10 +1344,10 @@ void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
   if (bout)
     KMHG_SCATTER_BM(false, true, false, 1, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse);
+                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse, nullptr);
   else
     KMHG_SCATTER_BM(false, true, false, 2, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse);
+                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse, nullptr);
 }
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
@@ -1324,16 +1357,17 @@ void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint3
   const BoundsFuse f = bf ? *bf : kNoFuse;
   if (bout)
     KMHG_SCATTER_BM(false, false, false, 1, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0, f);
+                    g, D, hist, ntiles, ko, pout, pad, 0, f, nullptr);
   else
     KMHG_SCATTER_BM(false, false, false, 2, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0, f);
+                    g, D, hist, ntiles, ko, pout, pad, 0, f, nullptr);
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                       uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf) {
+                       uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf,
+                       const uint32_t* tcnt) {
   KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,
-               hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse);
+               hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse, tcnt);
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
                              Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
@@ -1341,16 +1375,16 @@ void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_
                              hipStream_t s) {
   if (nopos)
     KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr, n_ptr,
-                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0, kNoFuse);
+                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0, kNoFuse, nullptr);
   else
     KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr,
-                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0, kNoFuse);
+                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0, kNoFuse, nullptr);
 }
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t pad,
                              hipStream_t s, const BoundsFuse* bf) {
   KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr, n_ptr, g, D,
-               hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
+               hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, nullptr);
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,

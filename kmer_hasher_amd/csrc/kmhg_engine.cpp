@@ -971,14 +971,26 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       idx->dcodes.reset(diag_block_words(Nw));
       db = idx->diag_block_of();
     }
+    // a part of 2+ (key streams): V_hist0 also writes the part's windows compacted per tile
+    // into kB / pB (free until pass 1), and the first scatter reads those instead of encoding
+    // and hashing every window again; KMHG_PART_COMPACT=0 (A/B) re-encodes
+    const char* pce = std::getenv("KMHG_PART_COMPACT");
+    const bool partc = n_parts >= 2 && !bid && codes && !(pce && pce[0] == '0');
+    DBuf<uint32_t> tcnt(partc ? ntiles : 1, s);
     LAUNCH("k_v2_hist0", s,
            launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, status,
-                           n_status, meta, s, db.code, db.nbit, bid ? bB.p : nullptr));
+                           n_status, meta, s, db.code, db.nbit, bid ? bB.p : nullptr,
+                           partc ? kB.p : nullptr, partc ? pB.p : nullptr,
+                           partc ? tcnt.p : nullptr));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
     if (bid)
       LAUNCH("k_v2_scatter_seq", s,
              launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ntiles,
                                     passes == 1 ? nullptr : bA.p, pA.p, pad, s));
+    else if (partc)
+      LAUNCH("k_v2_scatter_seq", s,
+             launch_v2_scatter(kB.p, pB.p, n_valid, g, make_digit(1, R), hist.p, ntiles, kA.p,
+                               pA.p, pad, s, nullptr, tcnt.p));
     else
       LAUNCH("k_v2_scatter_seq", s,
              launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
@@ -994,7 +1006,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint32_t C = ntiles, nst = n_status;
   uint64_t nh = nhist;
   DBuf<uint32_t> hist1;
-  if (n_parts >= 1 && passes > 1) {
+  if (n_parts >= 2 && passes > 1) {
     uint32_t nv = 0;
     HIPC(hipMemcpyAsync(&nv, n_valid, 4, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
