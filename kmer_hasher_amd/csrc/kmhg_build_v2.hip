@@ -137,9 +137,10 @@ __device__ __forceinline__ void diag_words_out(const PStage& st, uint32_t tile, 
 #define KMHG_HIST0_WAVES 6   // Win8: 80 VGPRs without spills (7 spills 44 B / lane)
 #endif
 // PARTC (a part build of an owner-computes build, key streams): the windows this part owns are
-// also written compacted per tile -- (key, position) of tile t's owned windows in window order at
-// [t * PTILE, t * PTILE + tcnt[t]) -- so the first scatter reads ~1/n_parts of the windows
-// instead of encoding and hashing every window of the sequence a second time.
+// written compacted per tile instead of counted -- (key, position) of tile t's owned windows in
+// window order at [t * PTILE, t * PTILE + tcnt[t]) -- and V_part_dense packs them into one
+// stream, which the radix passes read: ~1/n_parts of the windows instead of encoding and hashing
+// every window of the sequence a second time.
 template <bool CODES, bool BIDS = false, bool PARTC = false>
 __global__ void __launch_bounds__(BLOCK, PARTC ? 5 : KMHG_HIST0_WAVES)   // PARTC: no spills
 k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
@@ -184,7 +185,7 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
         if (s0 + j < Nw && win.valid(j)) {
           const uint32_t b = bucket_local(mix64(win.key(j)), g);
           if (b < g.nb) {
-            atomicAdd(&lh[digit_of_b(b, D)], 1u);
+            if (!PARTC) atomicAdd(&lh[digit_of_b(b, D)], 1u);
             bl[j] = b;
           }
         }
@@ -214,7 +215,7 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
       }
     }
     __syncthreads();
-    for (uint32_t d = threadIdx.x; d < D.R; d += BLOCK) {
+    for (uint32_t d = threadIdx.x; !PARTC && d < D.R; d += BLOCK) {
       hist[(size_t)d * ntiles + tile] = lh[d];
       lh[d] = 0;                               // next tile's atomics follow a barrier
     }
@@ -559,7 +560,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, uint32_t ntiles,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad,
-             int skip_empty, BoundsFuse bf, const uint32_t* __restrict__ tcnt) {
+             int skip_empty, BoundsFuse bf) {
   using KT = typename std::conditional<BM != 0, uint32_t, uint64_t>::type;
   using SL = ScatterLDS<KT>;
   static_assert(BM == 0 || !NOPOS, "bucket-id streams carry positions");
@@ -595,16 +596,13 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
     for (uint32_t lo = blockIdx.x; lo < bf.div; lo += gridDim.x)
       bounds_lo_body(lo, &S.wc[0][0], bf.kprev, *n_ptr, g, bf.Dlast, bf.div, hist, ntiles,
                      bf.lo_start, bf.spread, bf.start, bf.bid, TB, bf.nlim);
-  // the next tile's inputs are in flight while this one is processed.  tcnt (a part build's first
-  // pass over V_hist0's compacted tiles): tile t holds tcnt[t] elements at [t * PTILE, ...)
-  uint32_t tc_next = 0, tc_cur = 0;
+  // the next tile's inputs are in flight while this one is processed
   KT nkey[PER];
   uint32_t npos[PER];
   StageRegs<PSTAGE_W16> nchars;
   auto prefetch = [&](uint32_t tv) {
     const uint64_t t0 = (uint64_t)tv * PTILE;
     load_bases(tv);
-    if (tcnt) tc_next = tcnt[tv];
     if (FROM_SEQ) {
       stage_load<PSTAGE_W16, true>(nchars, seq, L, (int64_t)t0 - HALO, true);
     } else {
@@ -647,7 +645,6 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         ps[cc] = KEYS0 ? (uint32_t)(tile0 + wbase + (uint32_t)cc * 64 + lane + 1) : npos[cc];
       }
     }
-    tc_cur = tc_next;
     prefetch(tile_at(min(it + 1, n_iter - 1)));   // unconditional: static vmcnt
     for (uint32_t d = lane; d < R; d += 64) S.wc[wave][d] = 0;
     __syncthreads();                       // stage packed; previous tile's write-out done
@@ -665,10 +662,10 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         key[c] = BM ? (KT)bl : (KT)kk;
         dg[c] = act[c] ? digit_of_b(bl, D) : 0;
       } else if (BM) {
-        act[c] = (tcnt ? w < tc_cur : e < n) && !(KEYS0 && (uint32_t)key[c] == ~0u);
+        act[c] = e < n && !(KEYS0 && (uint32_t)key[c] == ~0u);
         dg[c] = act[c] ? digit_of_b((uint32_t)key[c], D) : 0;
       } else {
-        act[c] = (tcnt ? w < tc_cur : e < n) && !(KEYS0 && skip_empty && key[c] == EMPTY_KEY);
+        act[c] = e < n && !(KEYS0 && skip_empty && key[c] == EMPTY_KEY);
         dg[c] = act[c] ? digit_of_h(mix64((uint64_t)key[c]), g, D) : 0;
       }
     }
@@ -1211,6 +1208,25 @@ k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __re
 void set_stamp_buffer(uint64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
 #endif
 
+// ---------------------------------------------------------------- V_part_dense
+// A part build's compacted tiles (V_hist0 PARTC) into one dense stream: tile t's off[t+1] -
+// off[t] elements (off = the scanned tile counts, off[ntiles] = *n_total) move from
+// [t * PTILE, ...) to [off[t], ...), keys and positions, order kept.
+__global__ void __launch_bounds__(BLOCK)
+k_part_dense(const uint64_t* __restrict__ ck, const uint32_t* __restrict__ cp,
+             const uint32_t* __restrict__ off, uint32_t ntiles,
+             const uint32_t* __restrict__ n_total, uint64_t* __restrict__ dk,
+             uint32_t* __restrict__ dp) {
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint32_t o0 = off[t], o1 = t + 1 < ntiles ? off[t + 1] : *n_total;
+    const uint64_t src = (uint64_t)t * PTILE;
+    for (uint32_t i = threadIdx.x; i < o1 - o0; i += BLOCK) {
+      dk[o0 + i] = ck[src + i];
+      dp[o0 + i] = cp[src + i];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 // Persistent grids: as many workgroups as are resident at once (CUs x the occupancy the
 // kernel's VGPR/LDS budget allows), so no workgroup waits for another to finish.
@@ -1335,7 +1351,13 @@ void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geo
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s) {
   KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
-               kout, pout, pad, 0, kNoFuse, nullptr);
+               kout, pout, pad, 0, kNoFuse);
+}
+void launch_part_dense(const uint64_t* ck, const uint32_t* cp, const uint32_t* off,
+                       uint32_t ntiles, const uint32_t* n_total, uint64_t* dk, uint32_t* dp,
+                       hipStream_t s) {
+  hipLaunchKernelGGL(k_part_dense, dim3(std::min<uint32_t>(ntiles, 8192u)), dim3(BLOCK), 0, s, ck,
+                     cp, off, ntiles, n_total, dk, dp);
 }
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
                             const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
@@ -1344,10 +1366,10 @@ void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
   if (bout)
     KMHG_SCATTER_BM(false, true, false, 1, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse, nullptr);
+                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse);
   else
     KMHG_SCATTER_BM(false, true, false, 2, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse, nullptr);
+                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse);
 }
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
@@ -1357,17 +1379,16 @@ void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint3
   const BoundsFuse f = bf ? *bf : kNoFuse;
   if (bout)
     KMHG_SCATTER_BM(false, false, false, 1, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0, f, nullptr);
+                    g, D, hist, ntiles, ko, pout, pad, 0, f);
   else
     KMHG_SCATTER_BM(false, false, false, 2, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0, f, nullptr);
+                    g, D, hist, ntiles, ko, pout, pad, 0, f);
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                       uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf,
-                       const uint32_t* tcnt) {
+                       uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf) {
   KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,
-               hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse, tcnt);
+               hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse);
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
                              Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
@@ -1375,16 +1396,16 @@ void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_
                              hipStream_t s) {
   if (nopos)
     KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr, n_ptr,
-                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0, kNoFuse, nullptr);
+                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0, kNoFuse);
   else
     KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr,
-                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0, kNoFuse, nullptr);
+                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0, kNoFuse);
 }
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t pad,
                              hipStream_t s, const BoundsFuse* bf) {
   KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr, n_ptr, g, D,
-               hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, nullptr);
+               hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,

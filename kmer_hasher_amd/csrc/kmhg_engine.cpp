@@ -961,6 +961,14 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = 1;
   DiagBlock db{nullptr, nullptr, nullptr};
+  // a part of 2+ (key streams): V_hist0 also writes the part's windows compacted per tile into
+  // kB / pB (free until then) with their counts; a scan of the counts and one copy make them a
+  // dense (key, position) stream of ~1/n_parts of the windows, and every radix pass runs over
+  // that alone -- instead of encoding and hashing every window again in a first pass over all
+  // of them.  KMHG_PART_COMPACT=0 (A/B) keeps that first pass.
+  const char* pce = std::getenv("KMHG_PART_COMPACT");
+  const bool partc = !from_keys && n_parts >= 2 && !bid && codes && !(pce && pce[0] == '0');
+  DBuf<uint32_t> tcnt(partc ? ntiles : 1, s);
   if (from_keys) {   // pass 0 reads the caller's key stream in place (positions implicit)
     HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(n_valid), (int)Nw, 1, s));
     HIPC(hipMemsetAsync(meta, 0, sizeof(BuildMeta), s));
@@ -971,31 +979,25 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       idx->dcodes.reset(diag_block_words(Nw));
       db = idx->diag_block_of();
     }
-    // a part of 2+ (key streams): V_hist0 also writes the part's windows compacted per tile
-    // into kB / pB (free until pass 1), and the first scatter reads those instead of encoding
-    // and hashing every window again; KMHG_PART_COMPACT=0 (A/B) re-encodes
-    const char* pce = std::getenv("KMHG_PART_COMPACT");
-    const bool partc = n_parts >= 2 && !bid && codes && !(pce && pce[0] == '0');
-    DBuf<uint32_t> tcnt(partc ? ntiles : 1, s);
     LAUNCH("k_v2_hist0", s,
            launch_v2_hist0(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, status,
                            n_status, meta, s, db.code, db.nbit, bid ? bB.p : nullptr,
                            partc ? kB.p : nullptr, partc ? pB.p : nullptr,
                            partc ? tcnt.p : nullptr));
-    LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
-    if (bid)
-      LAUNCH("k_v2_scatter_seq", s,
-             launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ntiles,
-                                    passes == 1 ? nullptr : bA.p, pA.p, pad, s));
-    else if (partc)
-      LAUNCH("k_v2_scatter_seq", s,
-             launch_v2_scatter(kB.p, pB.p, n_valid, g, make_digit(1, R), hist.p, ntiles, kA.p,
-                               pA.p, pad, s, nullptr, tcnt.p));
-    else
-      LAUNCH("k_v2_scatter_seq", s,
-             launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
-                                   pA.p, pad, s));
-    div = R;
+    if (partc) {   // tile counts -> tile offsets, the part's window count -> n_valid
+      LAUNCH("k_scan_u32", s, launch_scan_u32(tcnt.p, ntiles, status, n_valid, s));
+    } else {
+      LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
+      if (bid)
+        LAUNCH("k_v2_scatter_seq", s,
+               launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ntiles,
+                                      passes == 1 ? nullptr : bA.p, pA.p, pad, s));
+      else
+        LAUNCH("k_v2_scatter_seq", s,
+               launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
+                                     pA.p, pad, s));
+      div = R;
+    }
   }
   uint32_t *bin = bA.p, *bout = bB.p;
   // the later passes' histogram layout: [digit][tile] over the tiles of their input.  A part
@@ -1006,7 +1008,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint32_t C = ntiles, nst = n_status;
   uint64_t nh = nhist;
   DBuf<uint32_t> hist1;
-  if (n_parts >= 2 && passes > 1) {
+  if (n_parts >= 2 && (passes > 1 || partc)) {
     uint32_t nv = 0;
     HIPC(hipMemcpyAsync(&nv, n_valid, 4, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
@@ -1017,10 +1019,16 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     hist1.bind(s);
     hp = hist1.p;
     // pass 0's digit starts (its scanned column 0), which pass 1's V_hist saves otherwise
-    HIPC(hipMemcpy2DAsync(lo_save.p, 4, hist.p, (size_t)ntiles * 4, 4, R,
-                          hipMemcpyDeviceToDevice, s));
+    if (!partc)
+      HIPC(hipMemcpy2DAsync(lo_save.p, 4, hist.p, (size_t)ntiles * 4, 4, R,
+                            hipMemcpyDeviceToDevice, s));
   }
-  uint32_t* save1 = hp == hist.p ? lo_save.p : nullptr;   // where pass 1 saves column 0
+  if (partc)   // the part's windows, dense in window order: every radix pass reads these
+    LAUNCH("k_part_dense", s, launch_part_dense(kB.p, pB.p, tcnt.p, ntiles, n_valid, kA.p, pA.p,
+                                                s));
+  // where pass 1 saves column 0: pass 0's histogram is hp's unless pass 0 was the one over
+  // every window (its own layout, copied above)
+  uint32_t* save1 = hp == hist.p || partc ? lo_save.p : nullptr;
   // each level of the bucket starts rides in its pass (BoundsFuse), except the last one of a
   // count-only build whose spread is chosen after the passes (co_auto); KMHG_FUSE_BOUNDS=0
   // (A/B) launches every level on its own
@@ -1036,7 +1044,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
                       make_digit((uint32_t)dv, R), (uint32_t)dv, spread, is_bid ? 1 : 0,
                       last ? g.nb : (uint32_t)(dv * R)};
   };
-  auto fused = [&](uint32_t p) { return fuse_on && !(co_auto && p + 1 == passes); };
+  auto fused = [&](uint32_t p) { return p >= 1 && fuse_on && !(co_auto && p + 1 == passes); };
   auto launch_level = [&](const BoundsFuse& f) {
     const uint64_t* kp = f.bid ? nullptr : f.kprev;
     const uint32_t* bp = f.bid ? reinterpret_cast<const uint32_t*>(f.kprev) : nullptr;
@@ -1059,7 +1067,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     std::swap(pin, pout);
     div *= R;
   }
-  for (uint32_t p = from_keys ? 0 : 1; !bid && p < passes; ++p) {
+  for (uint32_t p = from_keys || partc ? 0 : 1; !bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
     const bool keys0 = from_keys && p == 0;
     const bool last = p + 1 == passes;
@@ -1091,7 +1099,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
         LAUNCH("k_v2_scatter", s,
                launch_v2_scatter(kin, pin, n_valid, g, Dp, hp, C, kout, pout, pad, s,
                                  fused(p) ? &lv : nullptr));
-      if (!fused(p) && !last) launch_level(lv);
+      if (p >= 1 && !fused(p) && !last) launch_level(lv);
     }
     std::swap(kin, kout);
     std::swap(pin, pout);
@@ -1112,8 +1120,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   if (passes == 1) {
     // one pass (pass 0 reads chars or the caller's keys): the starts are the scanned column 0
     LAUNCH("k_v2_bounds", s,
-           launch_v2_bounds_lo(nullptr, n_valid, g, make_digit(1, R), 1u, hist.p, ntiles, nullptr,
-                               g.nb / gb.nb, start.p, g.nb, s, nullptr));
+           launch_v2_bounds_lo(nullptr, n_valid, g, make_digit(1, R), 1u, partc ? hp : hist.p,
+                               partc ? C : ntiles, nullptr, g.nb / gb.nb, start.p, g.nb, s,
+                               nullptr));
   } else if (!fused(passes - 1)) {
     // the last pass's input: kout / bout after the final swap
     launch_level(level_of(passes - 1, bid ? static_cast<const void*>(bout) : kout, bid,

@@ -153,9 +153,13 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
                      uint16_t* nbit = nullptr, uint32_t* bids = nullptr,
                      uint64_t* ckeys = nullptr, uint32_t* cpos = nullptr,
                      uint32_t* tcnt = nullptr);
-// ckeys (a part build, key streams): the part's windows compacted per tile, (key, position) at
-// [t * PTILE, t * PTILE + tcnt[t]) in window order (ckeys / cpos hold Nw + PTILE entries); the
-// first scatter reads them with launch_v2_scatter(..., tcnt)
+// ckeys (a part build, key streams): instead of the histogram, the part's windows compacted
+// per tile, (key, position) at [t * PTILE, t * PTILE + tcnt[t]) in window order (ckeys / cpos
+// hold Nw + PTILE entries); after a scan of tcnt (offsets, total in n_total) launch_part_dense
+// packs them into dk / dp
+void launch_part_dense(const uint64_t* ck, const uint32_t* cp, const uint32_t* off,
+                       uint32_t ntiles, const uint32_t* n_total, uint64_t* dk, uint32_t* dp,
+                       hipStream_t s);
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
 // exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the histogram kernel
@@ -216,8 +220,7 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
                              hipStream_t s, const BoundsFuse* bf = nullptr);
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
-                       uint32_t pad, hipStream_t s, const BoundsFuse* bf = nullptr,
-                       const uint32_t* tcnt = nullptr);
+                       uint32_t pad, hipStream_t s, const BoundsFuse* bf = nullptr);
 // Bucket-id streams (position builds that keep the sequence's code words): V_hist0 stores
 // every window's bucket id (`bids`, Nw u32, ~0 = not indexed), the radix passes carry (bucket
 // id u32, pos u32) and the last pass writes positions only (bout = nullptr); the bucket kernel

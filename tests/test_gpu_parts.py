@@ -52,9 +52,16 @@ def _slot_sets(table, positions, capb):
     return sorted(out)
 
 
+@pytest.mark.parametrize("stream", ["bid", "keys", "keys-first-pass"])
 @pytest.mark.parametrize("n_parts", [1, 2, 3, 5, 8])
-def test_parts_reassemble_to_the_single_build(gpu, n_parts):
+def test_parts_reassemble_to_the_single_build(gpu, monkeypatch, n_parts, stream):
+    """`stream`: bucket-id streams (the default up to 12 M windows), key streams whose parts
+    compact their own windows in the first histogram pass and run every radix pass over those
+    alone (the default beyond), and key streams with the older first pass over every window
+    (KMHG_PART_COMPACT=0)."""
     torch = gpu
+    monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
+    monkeypatch.setenv("KMHG_PART_COMPACT", "0" if stream == "keys-first-pass" else "1")
     from kmer_hasher_amd import synth
     from kmer_hasher_amd.device import DeviceIndex
     rr = synth.add_n_runs(synth.repeat_rich(400_000, 31, n_gap_every=70_000), 0.001, 32)
