@@ -961,13 +961,17 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   uint32_t *pin = pA.p, *pout = pB.p;
   uint32_t div = 1;
   DiagBlock db{nullptr, nullptr, nullptr};
-  // a part of 2+ (key streams): V_hist0 also writes the part's windows compacted per tile into
+  // a part of 4+ (key streams): V_hist0 also writes the part's windows compacted per tile into
   // kB / pB (free until then) with their counts; a scan of the counts and one copy make them a
   // dense (key, position) stream of ~1/n_parts of the windows, and every radix pass runs over
   // that alone -- instead of encoding and hashing every window again in a first pass over all
-  // of them.  KMHG_PART_COMPACT=0 (A/B) keeps that first pass.
+  // of them.  It costs a copy and one more pass over the part's windows, so it pays from 4
+  // parts on (one-GPU rehearsal, tools/part_step.py, per-rank step of 10 Mbp per part: 2 parts
+  // 0.397 -> 0.467 ms, 4 parts 0.504 -> 0.495, 8 parts 0.749 -> 0.581).  KMHG_PART_COMPACT=0 / 1
+  // forces the first pass over every window / the compaction (tests).
   const char* pce = std::getenv("KMHG_PART_COMPACT");
-  const bool partc = !from_keys && n_parts >= 2 && !bid && codes && !(pce && pce[0] == '0');
+  const bool partc = !from_keys && n_parts >= 2 && !bid && codes &&
+                     (pce ? pce[0] == '1' : n_parts >= 4);
   DBuf<uint32_t> tcnt(partc ? ntiles : 1, s);
   if (from_keys) {   // pass 0 reads the caller's key stream in place (positions implicit)
     HIPC(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(n_valid), (int)Nw, 1, s));
