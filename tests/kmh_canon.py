@@ -54,3 +54,50 @@ def canon_from_raw(raw: dict):
             q = np.empty((0, 3), np.int32)
         out["pair.pos"] = q.reshape(-1).astype(np.int32)
     return out, order
+
+
+class _MemoOracle:
+    """An oracle index whose derived outputs are computed once per test session: the parity
+    tests run the same inputs through several kernel variants (streams x ranks x radix caps), and
+    the CPU oracle -- not the GPU -- dominated their time."""
+
+    def __init__(self, oi):
+        self._oi = oi
+        self._memo = {}
+        self.U, self.N, self.P, self.max_n = oi.U, oi.N, oi.P, oi.max_n
+        self.counts = oi.counts
+
+    def _get(self, name, fn):
+        if name not in self._memo:
+            self._memo[name] = fn()
+        return self._memo[name]
+
+    def pos_rows(self):
+        return self._get("pos", self._oi.pos_rows)
+
+    def pair_rows(self):
+        return self._get("pairs", self._oi.pair_rows)
+
+    def kmer_strings(self):
+        return self._get("kmer", self._oi.kmer_strings)
+
+    def query(self, seq, kq):
+        qb = seq.encode("latin-1") if isinstance(seq, str) else bytes(seq)
+        return self._get(("q", hashlib.sha1(qb).digest(), kq), lambda: self._oi.query(seq, kq))
+
+
+_ORACLES: dict = {}
+
+
+def oracle_index(s, k: int, cap: int = 24):
+    """OracleIndex(s, k) (oracle/oracle.py), memoised per (sequence, k) for the session."""
+    from oracle import oracle as O
+    b = s.encode("latin-1") if isinstance(s, str) else bytes(s)
+    key = (hashlib.sha1(b).digest(), len(b), k)
+    hit = _ORACLES.pop(key, None)
+    if hit is None:
+        hit = _MemoOracle(O.OracleIndex(s, k))
+    _ORACLES[key] = hit                           # most recently used last
+    while len(_ORACLES) > cap:
+        _ORACLES.pop(next(iter(_ORACLES)))
+    return hit

@@ -3,7 +3,7 @@ oracle on seeded inputs.  Integer work: everything is compared bit-exactly."""
 import numpy as np
 import pytest
 
-from kmh_canon import sha
+from kmh_canon import oracle_index, sha
 from oracle import oracle as O
 from synth_inputs import sequence
 
@@ -18,7 +18,7 @@ def _api():
 def _check_against_oracle(s, k, qks=None, pairs=True):
     make, kpos, sqk = _api()
     ptr = make(s, k)
-    oi = O.OracleIndex(s, k)
+    oi = oracle_index(s, k)
     res = kpos(ptr, 15 if pairs else 11)
     assert np.array_equal(res["count"], oi.counts)
     assert np.array_equal(res["pos"].reshape(-1), oi.pos_rows())
@@ -138,20 +138,9 @@ def test_determinism(gpu):
     assert a["kmer"] == b["kmer"]
 
 
-@pytest.mark.slow
-def test_10mbp_k31_vs_oracle(gpu):
-    """Config 2 (BASELINE.json configs[1]) at full size: bit-exact vs the oracle."""
-    from kmer_hasher_amd import synth
-    s = synth.iid(10_000_000, 1).tobytes().decode()
-    make, kpos, sqk = _api()
-    ptr = make(s, 31)
-    oi = O.OracleIndex(s, 31)
-    res = kpos(ptr, 11)
-    assert np.array_equal(res["count"], oi.counts)
-    assert np.array_equal(res["pos"].reshape(-1), oi.pos_rows())
-    assert sha(res["kmer"]) == sha(oi.kmer_strings())
-    q = sqk(ptr, s, 31)
-    assert np.array_equal(q.reshape(-1), oi.query(s, 31))
+# (Config 2 at full size is checked against the reference's own digests in
+# tests/test_gpu_fullsize.py::test_config2_10mbp_k31_reference_digests; the oracle copy of that
+# check was removed in round 4 to keep the suite under three minutes.)
 
 
 def test_fallback_build_v1_matches_oracle(gpu, monkeypatch):
@@ -214,7 +203,7 @@ def test_bucket_kernels_vs_oracle(gpu, monkeypatch, stream, ranks):
         _check_against_oracle(s, k, qks=[k], pairs=(k != 5))
     rr = synth.add_n_runs(synth.repeat_rich(400_000, 13, n_gap_every=100_000), 0.001, 5)
     _check_against_oracle(rr.tobytes().decode("latin-1"), 21, qks=[21], pairs=True)
-    _check_against_oracle(synth.iid(3_000_000, 17).tobytes().decode(), 31, pairs=False)
+    _check_against_oracle(synth.iid(1_200_000, 17).tobytes().decode(), 31, pairs=False)
     _check_against_oracle("G" * 40, 32, qks=[31])
 
 

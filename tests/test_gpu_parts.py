@@ -6,7 +6,7 @@ does.  Includes parts that own no bucket (more parts than buckets) and the k = 3
 import numpy as np
 import pytest
 
-from oracle import oracle as O
+from kmh_canon import oracle_index
 
 pytestmark = pytest.mark.gpu
 
@@ -83,7 +83,7 @@ def test_parts_reassemble_to_the_single_build(gpu, monkeypatch, n_parts, stream)
         assert _slot_sets(table, positions, lay["capb"]) == \
             _slot_sets(bufs_w[0][:table.numel()], bufs_w[1], lay["capb"]), (k, n_parts)
         s = seq_np.tobytes()
-        oi = O.OracleIndex(s, k)
+        oi = oracle_index(s, k)
         res = idx.positions(14)
         assert np.array_equal(res["count"].cpu().numpy(), oi.counts)
         assert np.array_equal(res["pos"].cpu().numpy().reshape(-1), oi.pos_rows())
