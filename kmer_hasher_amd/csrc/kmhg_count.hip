@@ -253,33 +253,6 @@ constexpr uint32_t WALK_B = 2;
 constexpr int WALK_BPER = (int)(WALK_B * V2_CAPW / BLOCK);
 static_assert(WALK_B * V2_CAPW % BLOCK == 0 && WALK_BPER * (BLOCK / 64) < 64, "walk tile shape");
 
-// tile_compact with the tile's first rank known (no look-back); returns the tile's flag count
-template <int J>
-__device__ __forceinline__ uint32_t tile_rank_at(const bool (&flag)[J], uint64_t (&rk)[J],
-                                                 uint64_t* cw, uint64_t base) {
-  const int wave = threadIdx.x >> 6, lane = lane_id();
-  constexpr int NW = BLOCK / 64;
-  uint64_t m[J];
-#pragma unroll
-  for (int j = 0; j < J; ++j) m[j] = __ballot(flag[j]);
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < J; ++j) cw[j * NW + wave] = (uint64_t)__popcll(m[j]);
-  }
-  __syncthreads();
-  if (wave == 0) {                       // lanes 0 .. J*NW-1 own one (j, wave) count each
-    const uint64_t c = lane < J * NW ? cw[lane] : 0;
-    const uint64_t inc = wave_incl_scan(c);
-    if (lane < J * NW) cw[lane] = base + inc - c;
-    if (lane == 63) cw[J * NW] = inc;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < J; ++j)
-    rk[j] = cw[j * NW + wave] + (uint64_t)__popcll(m[j] & lanemask_lt());
-  return (uint32_t)cw[J * NW];
-}
-
 __global__ void __launch_bounds__(BLOCK)
 k_walk_counts(const BucketStats* __restrict__ bs, const Slot* __restrict__ T, Geom g,
               uint32_t* __restrict__ tc, uint32_t nt, uint32_t* __restrict__ err) {

@@ -54,6 +54,36 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* lds, u
   return off + inc - v;
 }
 
+// Ranks of the flagged elements of a tile of J x BLOCK elements, element e = j * BLOCK + t
+// (lane-contiguous), in element order, from `base` on: per-(j, wave) ballots and one wave scan,
+// no look-back (the caller knows the tile's first rank).  `cw` = LDS for J * (BLOCK / 64) + 1
+// u64 (J * BLOCK / 64 < 64).  Returns the tile's flag count.
+template <int J>
+__device__ __forceinline__ uint32_t tile_rank_at(const bool (&flag)[J], uint64_t (&rk)[J],
+                                                 uint64_t* cw, uint64_t base) {
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  constexpr int NW = BLOCK / 64;
+  uint64_t m[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) m[j] = __ballot(flag[j]);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < J; ++j) cw[j * NW + wave] = (uint64_t)__popcll(m[j]);
+  }
+  __syncthreads();
+  if (wave == 0) {                       // lanes 0 .. J*NW-1 own one (j, wave) count each
+    const uint64_t c = lane < J * NW ? cw[lane] : 0;
+    const uint64_t inc = wave_incl_scan(c);
+    if (lane < J * NW) cw[lane] = base + inc - c;
+    if (lane == 63) cw[J * NW] = inc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+    rk[j] = cw[j * NW + wave] + (uint64_t)__popcll(m[j] & lanemask_lt());
+  return (uint32_t)cw[J * NW];
+}
+
 // ------------------------------------------------------------------ decoupled look-back
 // status word: [63:62] = 0 not ready / 1 aggregate / 2 inclusive prefix, [61:0] payload.
 // Each word is a self-describing 8-B granule written by ONE relaxed agent-scope store and read

@@ -1324,17 +1324,18 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   // pinned host memory (no copy launch before the host reads it).
   DBuf<uint64_t> tiles((size_t)nt + scan_u64_scratch(nt), s);
   uint64_t* tile_row0 = tiles.p;
+  DBuf<uint32_t> elist((size_t)nt + 1, s);   // tiles with a multi-hit window; [nt] = their count
   PinnedRec hrec = PinnedPool::get().take();
   GiveBack give_back{hrec, s};
   uint64_t* total = &hrec.meta->n_kmers;
   LAUNCH("k_query_probe", s,
          launch_query_probe(d_seq, L, kq, idx->table.p, idx->geom, qrec.p, qmulti.p, w0, w1, aligned,
                             tile_row0, s, diag ? idx->diag_view() : DiagIdx{nullptr, nullptr, 0},
-                            diag && tags_on() ? idx->ptag.p : nullptr));
+                            diag && tags_on() ? idx->ptag.p : nullptr, elist.p + nt));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, tiles.p + nt, s));
   LAUNCH("k_query_emit", s,
          launch_query_emit(qrec.p, qmulti.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap,
-                           s));
+                           elist.p, elist.p + nt, true, s));
   HIPC(hipStreamSynchronize(s));
   H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
   q->H = (int64_t)H;
@@ -1345,7 +1346,8 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   q->rows.bind(s);
   q->rows.reset(H);
   LAUNCH("k_query_emit", s,
-         launch_query_emit(qrec.p, qmulti.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, H, s));
+         launch_query_emit(qrec.p, qmulti.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, H,
+                           elist.p, elist.p + nt, false, s));
   return q.release();
 }
 

@@ -85,7 +85,7 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
                         uint32_t* qrec, uint2* qmulti, int64_t w0, int64_t w1, bool aligned,
                         uint64_t* tile_rows,
                         hipStream_t s, DiagIdx X = DiagIdx{nullptr, nullptr, 0},
-                        const uint8_t* TG = nullptr);
+                        const uint8_t* TG = nullptr, uint32_t* ecount = nullptr);
 // Once per index, before its first diagonal query: `uniq` = the indexed windows (from the N
 // flags: the reference's window rule), then TG[i] = slot_tag of slot i (0 empty), all nslots
 // slots, and the `uniq` bits of every position of a key seen more than once cleared
@@ -99,10 +99,14 @@ void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t
 constexpr uint64_t SCAN1_MAX = 16384;
 inline uint64_t scan_u64_scratch(uint64_t n) { return (n + TILE - 1) / TILE + 1; }
 void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch, hipStream_t s);
-// rows >= cap are dropped (the caller re-runs the emit into an exact buffer if the total exceeds cap)
+// rows >= cap are dropped (the caller re-runs the emit into an exact buffer if the total exceeds
+// cap).  Two kernels: Q_emit1 writes the tiles whose windows have <= 1 hit and lists the others
+// in elist (nt entries; *ecount zeroed by the probe), Q_emit writes the listed tiles.  A re-emit
+// passes append = false (the list is already complete).
 void launch_query_emit(const uint32_t* qrec, const uint2* qmulti, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
-                       uint64_t cap, hipStream_t s);
+                       uint64_t cap, uint32_t* elist, uint32_t* ecount, bool append,
+                       hipStream_t s);
 // F = L entries {slot, count} preset to slot NONE
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s);

@@ -601,7 +601,8 @@ __global__ void PROBE_BOUNDS
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint32_t* __restrict__ qrec, uint2* __restrict__ qmulti, int64_t w0,
               int64_t w1, int aligned,
-              uint64_t* __restrict__ tile_rows, DiagIdx X, const uint8_t* __restrict__ TG) {
+              uint64_t* __restrict__ tile_rows, DiagIdx X, const uint8_t* __restrict__ TG,
+              uint32_t* __restrict__ ecount) {
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
   __shared__ DiagAnchors A;
@@ -609,6 +610,7 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   __shared__ DiagProbeLDS PL;
 #endif
   const uint32_t tile = blockIdx.x;
+  if (tile == 0 && threadIdx.x == 0 && ecount) *ecount = 0;   // Q_emit1's list, filled later
   // windows [w0, w1) of the FULL sequence: halo chars come from the real neighbours, so the
   // N / end-of-sequence rules at a shard boundary are those of the unsharded walk
   const int64_t t_start = w0 + (int64_t)tile * TILE;
@@ -729,7 +731,8 @@ __global__ void __launch_bounds__(BLOCK)
 k_query_emit(const uint32_t* __restrict__ qrec, const uint2* __restrict__ qmulti, int64_t Nw,
              int64_t w0, int kq,
              const int32_t* __restrict__ positions, const uint64_t* __restrict__ tile_row0,
-             int2* __restrict__ out, uint64_t cap) {
+             int2* __restrict__ out, uint64_t cap, const uint32_t* __restrict__ elist,
+             const uint32_t* __restrict__ ecount) {
   __shared__ uint64_t incl[TILE];
   __shared__ uint32_t start[TILE];
   using HeavyT = uint16_t;            // a window of the tile (< TILE): 28.7 KB of LDS, 5 groups / CU
@@ -737,7 +740,11 @@ k_query_emit(const uint32_t* __restrict__ qrec, const uint2* __restrict__ qmulti
   __shared__ HeavyT heavy[TILE];
   __shared__ uint32_t n_heavy;
   __shared__ uint64_t sh[8];
-  const int64_t tile0 = (int64_t)blockIdx.x * TILE;
+  const uint32_t nlist = *ecount;
+  for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
+  const uint32_t tile = elist[li];
+  const int64_t tile0 = (int64_t)tile * TILE;
+  __syncthreads();                      // the previous tile's reads of the LDS arrays are done
   if (threadIdx.x == 0) n_heavy = 0;
   // load counts / starts (coalesced), then thread-contiguous prefix over WPT entries
   for (int j = 0; j < WPT; ++j) {
@@ -759,8 +766,8 @@ k_query_emit(const uint32_t* __restrict__ qrec, const uint2* __restrict__ qmulti
 #pragma unroll
   for (int j = 0; j < WPT; ++j) incl[threadIdx.x * WPT + j] = loc[j] + ex;
   __syncthreads();
-  if (tot == 0) return;
-  const uint64_t r0 = tile_row0[blockIdx.x];
+  if (tot == 0) continue;               // uniform: every thread skips the tile
+  const uint64_t r0 = tile_row0[tile];
   const int32_t i0 = (int32_t)(w0 + tile0 + kq);
 #pragma unroll 2
   for (int j = 0; j < WPT; ++j) {
@@ -792,6 +799,42 @@ k_query_emit(const uint32_t* __restrict__ qrec, const uint2* __restrict__ qmulti
     for (uint64_t q = threadIdx.x; q < n; q += BLOCK)
       if (r + q < cap) out[r + q] = make_int2(i0 + (int32_t)w, positions[st0 + (uint32_t)q]);
   }
+  }
+}
+
+// Q_emit1 (round 4): the tiles whose windows have at most one hit each -- a dot plot's
+// diagonals, an unrelated query's misses, most of any query.  The rows of such a tile are its
+// hit windows in window order, so one ballot per (element row, wave) and one wave scan from the
+// tile's first row place them: no LDS arrays (Q_emit's 29 KB hold it to 5 workgroups per CU),
+// 8-B rows from consecutive lanes to consecutive rows.  A tile with a multi-hit window goes on
+// `elist` for Q_emit instead (append = 0 on a re-emit into an exact buffer: the list is complete).
+__global__ void __launch_bounds__(BLOCK)
+k_query_emit1(const uint32_t* __restrict__ qrec, int64_t Nw, int64_t w0, int kq,
+              const uint64_t* __restrict__ tile_row0, int2* __restrict__ out, uint64_t cap,
+              uint32_t* __restrict__ elist, uint32_t* __restrict__ ecount, int append) {
+  __shared__ uint64_t cw[WPT * (BLOCK / 64) + 1];
+  const uint32_t tile = blockIdx.x;
+  const int64_t tile0 = (int64_t)tile * TILE;
+  uint32_t rec[WPT];
+  bool hit[WPT];
+  int multi = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const int64_t e = tile0 + j * BLOCK + threadIdx.x;
+    rec[j] = e < Nw ? qrec[e] : 0u;
+    multi |= rec[j] == QREC_MULTI;
+    hit[j] = rec[j] != 0u;
+  }
+  if (__syncthreads_or(multi)) {
+    if (append && threadIdx.x == 0) elist[atomicAdd(ecount, 1u)] = tile;
+    return;
+  }
+  uint64_t rk[WPT];
+  tile_rank_at<WPT>(hit, rk, cw, tile_row0[tile]);
+  const int32_t i0 = (int32_t)(w0 + tile0 + kq);
+#pragma unroll
+  for (int j = 0; j < WPT; ++j)
+    if (hit[j] && rk[j] < cap) out[rk[j]] = make_int2(i0 + j * BLOCK + (int)threadIdx.x, (int32_t)rec[j]);
 }
 
 // ================================================================== readout kernels
@@ -1154,15 +1197,16 @@ void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, h
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint32_t* qrec, uint2* qmulti, int64_t w0, int64_t w1, bool aligned,
                         uint64_t* tile_rows,
-                        hipStream_t s, DiagIdx X, const uint8_t* TG) {
+                        hipStream_t s, DiagIdx X, const uint8_t* TG, uint32_t* ecount) {
   uint32_t nt = grid_for(w1 - w0, TILE);
   if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
   if (X.code)
     hipLaunchKernelGGL(k_query_probe<true>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti,
-                       w0, w1, aligned ? 1 : 0, tile_rows, X, TG);
+                       w0, w1, aligned ? 1 : 0, tile_rows, X, TG, ecount);
   else
     hipLaunchKernelGGL(k_query_probe<false>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti,
-                       w0, w1, aligned ? 1 : 0, tile_rows, DiagIdx{nullptr, nullptr, 0}, nullptr);
+                       w0, w1, aligned ? 1 : 0, tile_rows, DiagIdx{nullptr, nullptr, 0}, nullptr,
+                       ecount);
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
@@ -1180,9 +1224,23 @@ void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch
 }
 void launch_query_emit(const uint32_t* qrec, const uint2* qmulti, int64_t Nw, int64_t w0, int kq,
                        const int32_t* positions, const uint64_t* tile_row0, int2* out,
-                       uint64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_query_emit, dim3(grid_for(Nw, TILE)), dim3(BLOCK), 0, s, qrec, qmulti, Nw, w0,
-                     kq, positions, tile_row0, out, cap);
+                       uint64_t cap, uint32_t* elist, uint32_t* ecount, bool append,
+                       hipStream_t s) {
+  const uint32_t nt = grid_for(Nw, TILE);
+  hipLaunchKernelGGL(k_query_emit1, dim3(nt), dim3(BLOCK), 0, s, qrec, Nw, w0, kq, tile_row0, out,
+                     cap, elist, ecount, append ? 1 : 0);
+  static const unsigned cap_g = [] {
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_query_emit, BLOCK, 0) !=
+            hipSuccess || per < 1)
+      per = 1;
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    return (unsigned)(per * (cus > 0 ? cus : 1));
+  }();
+  hipLaunchKernelGGL(k_query_emit, dim3(std::min<unsigned>(nt, cap_g)), dim3(BLOCK), 0, s, qrec,
+                     qmulti, Nw, w0, kq, positions, tile_row0, out, cap, elist, ecount);
 }
 void launch_read_first(const Slot* T, uint64_t nslots, const int32_t* positions, uint2* F,
                        hipStream_t s) {
