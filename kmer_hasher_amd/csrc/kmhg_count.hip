@@ -249,7 +249,7 @@ k_count_walk(Slot* __restrict__ T, uint64_t nslots, uint64_t* __restrict__ statu
 // need no look-back chain.  The slot-tiled walk above chains 36 K tiles at config 3 and was
 // bound by that chain's hand-offs (~80 ns per tile, 2.9 ms).  A tile whose occupied slots
 // disagree with the statistics raises `err` (the host fails loudly: an internal error).
-constexpr uint32_t WALK_B = 2;
+constexpr uint32_t WALK_B = V2_CAPW <= 1536 ? 2 : 1;
 constexpr int WALK_BPER = (int)(WALK_B * V2_CAPW / BLOCK);
 static_assert(WALK_B * V2_CAPW % BLOCK == 0 && WALK_BPER * (BLOCK / 64) < 64, "walk tile shape");
 

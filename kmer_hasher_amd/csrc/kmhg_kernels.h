@@ -7,12 +7,18 @@ namespace kmhg {
 
 constexpr uint32_t LARGE_MIN = 64;     // keys with >= this many positions sort per workgroup
 // partitioned build (kmhg_build_v2.hip)
-constexpr uint32_t V2_BW_WG = 1024;    // ... group buckets: mean windows per bucket
+// group buckets: mean windows per bucket and LDS sub-table slots (load 2/3).  Variant builds
+// (A/B, `make variant`) may set -DKMHG_BW_WG=2048 -DKMHG_CAPW=3072 -DKMHG_BUCKET_WGS=4.
+#ifndef KMHG_BW_WG
+#define KMHG_BW_WG 1024
+#endif
 #ifndef KMHG_CAPW
 #define KMHG_CAPW 1536
 #endif
+constexpr uint32_t V2_BW_WG = KMHG_BW_WG;
 constexpr uint32_t V2_CAPW = KMHG_CAPW;  // slots per group bucket (LDS sub-table of one workgroup)
-constexpr uint32_t V2_SLOT_BITS_WG = 11;
+constexpr uint32_t V2_SLOT_BITS_WG = V2_CAPW >= 2048 ? 12 : 11;
+static_assert(V2_CAPW < (1u << V2_SLOT_BITS_WG), "slot index bits");
 constexpr uint32_t V2_MAXR = 640;      // LDS digit arrays of the histogram / bounds kernels
 constexpr uint32_t V2_MAXR_IL = 320;   // max radix of one partition pass (the scatter's LDS)
 constexpr uint32_t SORT_CHUNK = 4096;  // LDS bitonic chunk (16 KiB)
