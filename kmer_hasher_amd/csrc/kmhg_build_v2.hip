@@ -152,6 +152,8 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
   __shared__ PStage st;
   __shared__ uint32_t lh[V2_MAXR];
   __shared__ uint64_t scs[5];
+  __shared__ uint64_t sk[PARTC ? PTILE : 1];     // PARTC: the tile's own windows, compacted
+  __shared__ uint32_t sp[PARTC ? PTILE : 1];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
     scan_status[i] = 0;
   if (blockIdx.x == 0 && threadIdx.x < sizeof(BuildMeta) / 4)
@@ -196,14 +198,20 @@ k_v2_hist0p(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw, Geom 
         for (int j = 0; j < 8; ++j) own |= (bl[j] != ~0u ? 1u : 0u) << j;
         uint64_t tot;
         uint32_t at = (uint32_t)block_excl_scan((uint64_t)__popc(own), scs, tot);
-        const uint64_t base = (uint64_t)tile * PTILE;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           if (own >> j & 1u) {
-            ckeys[base + at] = win.key(j);
-            cpos[base + at] = (uint32_t)(s0 + j + 1);
+            sk[at] = win.key(j);
+            sp[at] = (uint32_t)(s0 + j + 1);
             ++at;
           }
+        }
+        __syncthreads();
+        // out of LDS in order: consecutive lanes, consecutive entries
+        const uint64_t base = (uint64_t)tile * PTILE;
+        for (uint32_t i = threadIdx.x; i < (uint32_t)tot; i += BLOCK) {
+          ckeys[base + i] = sk[i];
+          cpos[base + i] = sp[i];
         }
         if (threadIdx.x == 0) tcnt[tile] = (uint32_t)tot;
       }

@@ -301,7 +301,10 @@ k_count_walk_b(Slot* __restrict__ T, Geom g, const uint32_t* __restrict__ tbase,
   auto put = [&](uint64_t i, uint4 x, uint64_t row) {
     ckeys[row] = ((uint64_t)x.y << 32) | x.x;
     int32_t* m = M + row * S;
-    for (uint32_t q = 0; q < S; ++q) m[q] = q == source ? (int32_t)x.z : 0;
+    if (S == 2)                        // the common two-source matrix: one 8-B store per row
+      *reinterpret_cast<int2*>(m) = source ? make_int2(0, (int32_t)x.z) : make_int2((int32_t)x.z, 0);
+    else
+      for (uint32_t q = 0; q < S; ++q) m[q] = q == source ? (int32_t)x.z : 0;
     row_slot[row] = (uint32_t)i;
     slot_row[i] = (uint32_t)row;
     if (rord) rord[row] = base + first_pos(x, bpos) - 1;
