@@ -465,10 +465,13 @@ constexpr size_t D2H_CHUNK = 16u << 20;
 constexpr size_t H2D_CHUNK = 4u << 20;
 constexpr size_t H2D_STAGE_MIN = 2u << 20;
 constexpr size_t D2H_STAGE_MIN = 4u << 20;
-static int d2h_threads() {                           // KMHG_D2H_THREADS (A/B), default 4
+// KMHG_D2H_THREADS (A/B), default 8: A/B in one run (`profiles/rd4n_ab_d2h.log`, config 2
+// host-boundary query, 10 M rows into a fresh array): 4 threads 7.9 / 8.4 ms, 8 threads 7.0 /
+// 6.7 ms, 16 threads 7.7 / 10.1 ms
+static int d2h_threads() {
   static const int n = [] {
     const char* e = std::getenv("KMHG_D2H_THREADS");
-    return e ? std::max(1, std::min(16, std::atoi(e))) : 4;
+    return e ? std::max(1, std::min(16, std::atoi(e))) : 8;
   }();
   return n;
 }
