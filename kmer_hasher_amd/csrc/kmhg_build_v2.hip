@@ -902,11 +902,12 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   __shared__ GroupTableC W;
   __shared__ uint64_t sh[2 * NW];
   __shared__ uint32_t red[2][NW];
-  __shared__ __attribute__((aligned(16))) uint32_t edge[8 * NW + 1];   // stream-order check
   const uint32_t b = blockIdx.x;
   // elements per thread per batch: 2x the mean (code words: 1.5x, for the VGPR budget of
   // 8 waves / SIMD); a larger bucket takes more batches
   constexpr int PER = (CK ? 3 : 4) * V2_BW_WG / 2 / TB;
+  constexpr int EW = (PER + 1) & ~1;                  // edge row: PER positions, written as pairs
+  __shared__ __attribute__((aligned(16))) uint32_t edge[EW * NW + 1];   // stream-order check
   constexpr uint32_t BATCH = TB * PER;
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const uint32_t s0 = start[b], s1 = start[b + 1];
@@ -1003,11 +1004,11 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   // `edge` and read after the barrier below.  Here, after pass A, the positions have long
   // arrived, so the check makes no load wait earlier than it did.
   const bool chk = !COUNT_ONLY && one_batch;
-  // (edge: row `wave` holds that wave's lane-63 positions, 8 per row, written and read as
+  // (edge: row `wave` holds that wave's lane-63 positions, EW per row, written and read as
   // pairs -- a handful of LDS instructions per wave: single-lane LDS instructions cost nearly a
   // full one each in this LDS-bound kernel)
   if (chk) {
-    if (threadIdx.x == 0) edge[8 * NW] = 0u;
+    if (threadIdx.x == 0) edge[EW * NW] = 0u;
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       // lane - 1's position by a DPP wave shift (a VALU move; __shfl_up is an LDS permute)
@@ -1018,7 +1019,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     if (lane == 63) {
 #pragma unroll
       for (int q = 0; q < PER; q += 2)
-        *reinterpret_cast<uint2*>(&edge[8 * wave + q]) = make_uint2(ps[q], q + 1 < PER ? ps[q + 1] : 0u);
+        *reinterpret_cast<uint2*>(&edge[EW * wave + q]) = make_uint2(ps[q], q + 1 < PER ? ps[q + 1] : 0u);
     }
   }
   if (__syncthreads_or(ovf || disorder)) {
@@ -1027,7 +1028,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   }
   if (chk && lane == 0) {
     // lane 0 of wave w follows lane 63 of wave w - 1 (same row); wave 0 follows wave NW - 1
-    const uint32_t* row = edge + 8 * (wave ? wave - 1 : NW - 1);
+    const uint32_t* row = edge + EW * (wave ? wave - 1 : NW - 1);
     uint32_t pv[PER + 1];
 #pragma unroll
     for (int q = 0; q < PER; q += 2) {
@@ -1042,7 +1043,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
       const uint32_t prev = wave ? pv[c] : (c ? pv[c - 1] : 0u);   // wave 0: row c - 1
       bad |= e > s0 && e < s1 && prev >= ps[c];
     }
-    if (bad) edge[8 * NW] = 1u;              // read after the counts pass's barrier
+    if (bad) edge[EW * NW] = 1u;             // read after the counts pass's barrier
   }
   STAMP_WG(b, 2);
   // counts: thread t owns slots t, t + TB, ... (lane-contiguous: conflict-free LDS; thread-
@@ -1072,7 +1073,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     sh[NW + wave] = pairs;                 // sh[NW..2NW): the block scan below uses sh[0..NW)
   }
   const bool has_multi = __syncthreads_or(mx > 1);
-  if (chk && edge[8 * NW]) {                 // stream out of order at a wave / row boundary
+  if (chk && edge[EW * NW]) {                // stream out of order at a wave / row boundary
     if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
     return;
   }
