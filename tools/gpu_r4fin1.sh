@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-4 closing evidence, part 1: whole GPU suite + smoke + default bench, then configs 3-5.
+set -uo pipefail
+REPO=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$REPO"
+bash tools/gpu_check.sh rd4fin || exit 1
+OUT=$REPO/gpurun_out/cfg_rd4fin
+mkdir -p "$OUT"
+for c in 3 4 5; do
+  timeout -k 10 300 python -u bench.py --config $c --steps 5 --warmup 2 > "$OUT/config$c.json" \
+    2> "$OUT/config$c.err" || { echo "config $c failed"; tail -20 "$OUT/config$c.err"; exit 1; }
+  echo "config $c ok"
+done
