@@ -14,9 +14,6 @@
 // Integer/byte work only: every kernel is bounded by HBM (or by random-access latency on the
 // table), none by arithmetic; nothing here is matmul-shaped.
 #include <hip/hip_runtime.h>
-
-#include <map>
-
 #include "kmhg_common.h"
 #include "kmhg_kernels.h"
 #include "kmhg_device.h"
@@ -591,102 +588,77 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
 // At least 6 waves per SIMD: the diagonal probe needs 81 VGPRs unconstrained (5 waves / SIMD);
 // capped it fits 72 with no spill (7 waves).  A/B in one run, config 2: self query 87.0 / 90.0 ->
 // 90.9 / 95.4 Gbp/s, unrelated 41.4 -> 44.3; 8 waves (64 VGPRs) spills 44 B / lane and is slower.
-#ifndef KMHG_PROBE_PERSIST
-#define KMHG_PROBE_PERSIST 1
-#endif
 #ifndef KMHG_PROBE_WAVES
-#if KMHG_PROBE_PERSIST
-#define KMHG_PROBE_WAVES 5   // the persistent loop holds 84 VGPRs; capped at 6 waves it spills
-#else
 #define KMHG_PROBE_WAVES 6
-#endif
 #endif
 #if KMHG_PROBE_WAVES
 #define PROBE_BOUNDS __launch_bounds__(BLOCK, KMHG_PROBE_WAVES)
 #else
 #define PROBE_BOUNDS __launch_bounds__(BLOCK)
 #endif
-// Persistent (round 4): as many workgroups as are resident walk the tiles XCD-contiguously
-// (neighbouring query tiles on one XCD read neighbouring index code words through one L2), and
-// each loads the next tile's chars into registers while it resolves the current one, so the
-// stage load leaves every tile's dependent chain (chars -> anchor probes -> verification words
-// -> records).  KMHG_PROBE_PERSIST=0 (variant builds, A/B): one workgroup per tile.
 template <bool DIAG>
 __global__ void PROBE_BOUNDS
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint32_t* __restrict__ qrec, uint2* __restrict__ qmulti, int64_t w0,
               int64_t w1, int aligned,
               uint64_t* __restrict__ tile_rows, DiagIdx X, const uint8_t* __restrict__ TG,
-              uint32_t* __restrict__ ecount, uint32_t nt) {
+              uint32_t* __restrict__ ecount) {
   __shared__ Stage st;
   __shared__ uint64_t sh[8];
   __shared__ DiagAnchors A;
 #ifndef KMHG_PROBE_STRIDED
   __shared__ DiagProbeLDS PL;
 #endif
-  if (blockIdx.x == 0 && threadIdx.x == 0 && ecount) *ecount = 0;   // Q_emit1's list
+  const uint32_t tile = blockIdx.x;
+  if (tile == 0 && threadIdx.x == 0 && ecount) *ecount = 0;   // Q_emit1's list, filled later
   // windows [w0, w1) of the FULL sequence: halo chars come from the real neighbours, so the
   // N / end-of-sequence rules at a shard boundary are those of the unsharded walk
-  auto base_of = [&](uint32_t tile) { return ((w0 + (int64_t)tile * TILE) & ~15ll) - HALO; };
-  auto process = [&](uint32_t tile) {
-    const int64_t t_start = w0 + (int64_t)tile * TILE;
-    const int o0 = (int)(t_start - base_of(tile));
-    if (DIAG) diag_anchors(st, o0, t_start, w1, L, kq, T, g, A);
-    uint64_t rows = 0;
+  const int64_t t_start = w0 + (int64_t)tile * TILE;
+  const int64_t base = (t_start & ~15ll) - HALO;
+  const int o0 = (int)(t_start - base);
+  stage_tile(seq, L, base, st, aligned != 0);
+  __syncthreads();
+  if (DIAG) diag_anchors(st, o0, t_start, w1, L, kq, T, g, A);
+  uint64_t rows = 0;
 #ifndef KMHG_PROBE_UNROLL
 #define KMHG_PROBE_UNROLL 2
 #endif
-    if (DIAG) {
+  if (DIAG) {
 #ifndef KMHG_PROBE_STRIDED
-      rows = diag_resolve8(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A, qrec, qmulti, PL);
-#else
-      diag_resolve(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
-                   [&](int w, int64_t s, uint32_t count, uint32_t aux) {
-                     if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
-                     rows += count;
-                   });
+    rows = diag_resolve8(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A, qrec, qmulti, PL);
+    uint64_t tot8;
+    block_excl_scan(rows, sh, tot8);
+    if (threadIdx.x == 0) tile_rows[tile] = tot8;
+    return;
 #endif
-    } else {
-      // (measured: issuing all WPT home-slot loads before resolving any cost occupancy -- 94
-      // VGPRs, 5 waves/SIMD -- and ran 15 % slower than this two-deep loop; a per-lane state
-      // machine walking two probe streams one slot per step ran 30 % slower, and compacting the
-      // windows not resolved at their home slot into LDS queue rounds 40 % slower)
-#pragma unroll KMHG_PROBE_UNROLL
-      for (int j = 0; j < WPT; ++j) {
-        const int w = j * BLOCK + threadIdx.x;
-        const int64_t s = t_start + w;
-        uint64_t key = 0;
-        uint32_t count = 0, aux = 0;
-        if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
-        // {count, position} for a key seen once, {count, first index} otherwise
-        if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
-        rows += count;
-      }
-    }
+    diag_resolve(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
+                 [&](int w, int64_t s, uint32_t count, uint32_t aux) {
+                   if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
+                   rows += count;
+                 });
     uint64_t tot;
-    block_excl_scan(rows, sh, tot);       // its barriers also end this tile's LDS reads
+    block_excl_scan(rows, sh, tot);
     if (threadIdx.x == 0) tile_rows[tile] = tot;
-  };
-#if KMHG_PROBE_PERSIST
-  const uint32_t G = gridDim.x;
-  const uint32_t n_iter = (nt - blockIdx.x + G - 1) / G;
-  auto tile_at = [&](uint32_t i) -> uint32_t { return xcd_remap(blockIdx.x + i * G, nt); };
-  StageRegs<STAGE_W16> regs;
-  stage_load<STAGE_W16, false>(regs, seq, L, base_of(tile_at(0)), aligned != 0);
-  for (uint32_t it = 0; it < n_iter; ++it) {
-    const uint32_t tile = tile_at(it);
-    __syncthreads();                      // the previous tile's reads of st / A / PL are done
-    stage_pack(regs, st);
-    if (it + 1 < n_iter)
-      stage_load<STAGE_W16, false>(regs, seq, L, base_of(tile_at(it + 1)), aligned != 0);
-    __syncthreads();
-    process(tile);
+    return;
   }
-#else
-  stage_tile(seq, L, base_of(blockIdx.x), st, aligned != 0);
-  __syncthreads();
-  process(blockIdx.x);
-#endif
+  // (measured: issuing all WPT home-slot loads before resolving any cost occupancy -- 94
+  // VGPRs, 5 waves/SIMD -- and ran 15 % slower than this two-deep loop; a per-lane state
+  // machine walking two probe streams one slot per step ran 30 % slower, and compacting the
+  // windows not resolved at their home slot into LDS queue rounds 40 % slower)
+#pragma unroll KMHG_PROBE_UNROLL
+  for (int j = 0; j < WPT; ++j) {
+    const int w = j * BLOCK + threadIdx.x;
+    const int64_t s = t_start + w;
+    uint64_t key = 0;
+    uint32_t count = 0, aux = 0;
+    if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
+    // {count, position} for a key seen once, {count, first index} otherwise
+    if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
+    rows += count;
+  }
+  uint64_t tot;
+  block_excl_scan(rows, sh, tot);
+  if (threadIdx.x == 0) tile_rows[tile] = tot;
 }
 
 // Exclusive scan of n per-tile u64 totals in one workgroup (n = tiles, at most ~1M).
@@ -1228,33 +1200,13 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
                         hipStream_t s, DiagIdx X, const uint8_t* TG, uint32_t* ecount) {
   uint32_t nt = grid_for(w1 - w0, TILE);
   if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
-  auto grid_of_probe = [&](const void* kern) -> unsigned {
-#if KMHG_PROBE_PERSIST
-    static std::map<const void*, unsigned> caps;
-    auto it = caps.find(kern);
-    if (it == caps.end()) {
-      int per = 0, dev = 0, cus = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, BLOCK, 0) != hipSuccess ||
-          per < 1)
-        per = 1;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      it = caps.emplace(kern, (unsigned)per * (unsigned)(cus > 0 ? cus : 1)).first;
-    }
-    return std::min<unsigned>(nt, it->second);
-#else
-    (void)kern;
-    return nt;
-#endif
-  };
   if (X.code)
-    hipLaunchKernelGGL(k_query_probe<true>, dim3(grid_of_probe((const void*)k_query_probe<true>)),
-                       dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti, w0, w1, aligned ? 1 : 0,
-                       tile_rows, X, TG, ecount, nt);
+    hipLaunchKernelGGL(k_query_probe<true>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti,
+                       w0, w1, aligned ? 1 : 0, tile_rows, X, TG, ecount);
   else
-    hipLaunchKernelGGL(k_query_probe<false>, dim3(grid_of_probe((const void*)k_query_probe<false>)),
-                       dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti, w0, w1, aligned ? 1 : 0,
-                       tile_rows, DiagIdx{nullptr, nullptr, 0}, nullptr, ecount, nt);
+    hipLaunchKernelGGL(k_query_probe<false>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti,
+                       w0, w1, aligned ? 1 : 0, tile_rows, DiagIdx{nullptr, nullptr, 0}, nullptr,
+                       ecount);
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
