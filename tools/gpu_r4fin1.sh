@@ -11,3 +11,5 @@ for c in 3 4 5; do
     2> "$OUT/config$c.err" || { echo "config $c failed"; tail -20 "$OUT/config$c.err"; exit 1; }
   echo "config $c ok"
 done
+timeout -k 10 300 python -u tools/part_step.py 10 10 > "$OUT/part_step.log" 2>&1 || { echo "part_step failed"; tail -20 "$OUT/part_step.log"; exit 1; }
+cat "$OUT/part_step.log"
