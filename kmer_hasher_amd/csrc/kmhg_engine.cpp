@@ -1513,7 +1513,10 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
   idx->stream = s;
   const int k = idx->k;
   if (L <= k) return;
-  std::unique_ptr<kmhg_index> B(build_device(d_seq, L, k, s, false));
+  // the batch keeps its code words only to be eligible for bucket-id radix streams (<= 12 M
+  // windows); KMHG_COUNT_BID=0 (A/B) builds it with key streams
+  const char* cbe = std::getenv("KMHG_COUNT_BID");
+  std::unique_ptr<kmhg_index> B(build_device(d_seq, L, k, s, !(cbe && cbe[0] == '0')));
   Release rel{B.get(), s};
   finish_build(B.get());
   B->stream = s;
