@@ -13,3 +13,6 @@ for c in 3 4 5; do
 done
 timeout -k 10 300 python -u tools/part_step.py 10 10 > "$OUT/part_step.log" 2>&1 || { echo "part_step failed"; tail -20 "$OUT/part_step.log"; exit 1; }
 cat "$OUT/part_step.log"
+timeout -k 10 500 bash tools/ab.sh "KMHG_COUNT_BID=1" "KMHG_COUNT_BID=0" -- --no-cpu --no-reads \
+  || { echo "ab count bid failed"; exit 1; }
+cp gpurun_out/ab.log "$OUT/ab_count_bid.log"
