@@ -383,9 +383,15 @@ __device__ __forceinline__ void put_qrec(uint32_t* qrec, uint2* qmulti, int64_t 
 // this replaced streamed 16 B per window (and took 16 B per index window of HBM, built by a
 // random scatter on the first query).  Queries unrelated to the index pay the anchors and one
 // failed check.
+// Anchor stride.  Round 2 (config 2 self dot plot, probe): 16 / 32 / 64 / 128 -> 97 / 86 / 82 /
+// 76 us, 64 kept for short misses after a tile start.  Round 4, A/B in one run against variant
+// builds (`profiles/rd4w_ab_dg_stride_*`): 128 beats 64 at every size -- config 2 probe 42-44 ->
+// 37-39 us (query 117-120 -> 123-125 Gbp/s, unrelated 46.5 -> 47.6), config 3 0.346-0.350 ->
+// 0.319-0.320 ms (167 -> 175 Gbp/s), config 5 4.75-4.77 -> 4.55-4.56 ms (72.1 -> 74.1 Gbp/s);
+// 32 loses (config 2 111 Gbp/s).
 #ifndef KMHG_DG_STRIDE
-#define KMHG_DG_STRIDE 64        // A/B (config 2 self dot plot, probe): 16 / 32 / 64 / 128 ->
-#endif                           //   97 / 86 / 82 / 76 us; 64 keeps misses after a tile start short
+#define KMHG_DG_STRIDE 128
+#endif
 constexpr int DG_STRIDE = KMHG_DG_STRIDE;
 constexpr int DG_ANCHORS = TILE / DG_STRIDE;
 constexpr int DG_SCAN = (DG_ANCHORS + 63) / 64 * 64;   // whole waves run the anchor scan
