@@ -388,9 +388,13 @@ __device__ __forceinline__ void put_qrec(uint32_t* qrec, uint2* qmulti, int64_t 
 // builds (`profiles/rd4w_ab_dg_stride_*`): 128 beats 64 at every size -- config 2 probe 42-44 ->
 // 37-39 us (query 117-120 -> 123-125 Gbp/s, unrelated 46.5 -> 47.6), config 3 0.346-0.350 ->
 // 0.319-0.320 ms (167 -> 175 Gbp/s), config 5 4.75-4.77 -> 4.55-4.56 ms (72.1 -> 74.1 Gbp/s);
-// 32 loses (config 2 111 Gbp/s).
+// 32 loses (config 2 111 Gbp/s).  256 against 128 (`profiles/rd4x_ab_dg_stride_*`): config 3
+// probe 0.319-0.321 -> 0.297-0.298 ms (174 -> 181 Gbp/s), config 5 4.55-4.56 -> 4.52-4.53 ms,
+// config 2 probe 38.8-40.0 -> 37.2-39.9 us; 64 again slower.  Anchors only establish a
+// diagonal: a window after an SNV is verified again against the same anchor's prediction, and
+// only a shifted diagonal (an indel, a rearrangement) probes until the next anchor.
 #ifndef KMHG_DG_STRIDE
-#define KMHG_DG_STRIDE 128
+#define KMHG_DG_STRIDE 256
 #endif
 constexpr int DG_STRIDE = KMHG_DG_STRIDE;
 constexpr int DG_ANCHORS = TILE / DG_STRIDE;
