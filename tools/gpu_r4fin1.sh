@@ -3,8 +3,8 @@
 set -uo pipefail
 REPO=${GRAFT_REPO_ROOT:-/root/repo}
 cd "$REPO"
-bash tools/gpu_check.sh rd4fin || exit 1
-OUT=$REPO/gpurun_out/cfg_rd4fin
+bash tools/gpu_check.sh rd4end || exit 1
+OUT=$REPO/gpurun_out/cfg_rd4end
 mkdir -p "$OUT"
 for c in 3 4 5; do
   timeout -k 10 300 python -u bench.py --config $c --steps 5 --warmup 2 > "$OUT/config$c.json" \
