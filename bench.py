@@ -201,8 +201,9 @@ def host_info() -> dict:
 
 def query_roofline(qper: dict, L: int, Nw: int, H: int, pmc: dict, step_ms: float,
                    launches: dict | None = None) -> dict | None:
-    """Roofline of the dominant query kernel from its HIP-event average duration, priced with
-    SURVEY.md §8(d)'s query bytes."""
+    """Roofline of the query: SURVEY.md §8(d)'s query bytes over the summed HIP-event averages of
+    the query's kernels (probe, scan, emit); the dominant kernel's own time, PMC traffic and
+    kernel_model ride along."""
     if not qper:
         return None
     dom = max(qper, key=qper.get)
