@@ -8,3 +8,11 @@ bash tools/profile.sh rd4end2 --steps 10 --warmup 2 --profile || { echo "profile
 bash tools/profile.sh rd4endlegs --steps 3 --warmup 1 --no-cpu || { echo "profile legs failed"; exit 1; }
 bash tools/profile.sh rd4end3 --config 3 --steps 3 --warmup 1 --profile --no-cpu || { echo "profile 3 failed"; exit 1; }
 echo "profiles done"
+# bench lines again after the query roofline's pricing change (bench.py only; same library)
+OUT=$REPO/gpurun_out/cfg_rd4end
+mkdir -p "$OUT"
+for c in 2 3 5; do
+  timeout -k 10 300 python -u bench.py --config $c --steps 5 --warmup 2 > "$OUT/config${c}_b.json" \
+    2> "$OUT/config${c}_b.err" || { echo "config $c failed"; tail -20 "$OUT/config${c}_b.err"; exit 1; }
+  echo "config $c ok"
+done
