@@ -247,6 +247,18 @@ class DeviceQuery:
             self.copy_to(t)
         return t
 
+    def rows_view(self) -> torch.Tensor:
+        """The (H, 2) int32 rows where the emit kernel wrote them (kmhg_query_rows_device), as a
+        tensor that owns this query: no copy, and the rows' buffer goes back to the library's pool
+        (stream-ordered on the query's stream) when the last tensor using it is gone.  Used on
+        the query's stream, as every result of the library is."""
+        if not self.n_rows:
+            return torch.empty((0, 2), dtype=torch.int32,
+                               device=torch.device("cuda", torch.cuda.current_device()))
+        d = C.c_void_p()
+        _lib.check(_lib.lib().kmhg_query_rows_device(self._h, C.byref(d)))
+        return torch.as_tensor(_RowsBuffer(self, d.value), device="cuda")
+
     def free(self):
         if self._h:
             _lib.lib().kmhg_query_free(self._h)
@@ -257,6 +269,17 @@ class DeviceQuery:
             self.free()
         except Exception:
             pass
+
+
+class _RowsBuffer:
+    """__cuda_array_interface__ of a query's device rows; torch keeps this object (and so the
+    query) alive for as long as the tensor made from it."""
+
+    def __init__(self, q: DeviceQuery, ptr: int):
+        self.q = q
+        self.__cuda_array_interface__ = {"shape": (q.n_rows, 2), "typestr": "<i4",
+                                         "data": (ptr, False), "version": 3, "strides": None,
+                                         "stream": None}
 
 
 def timing_enable(on: bool = True):

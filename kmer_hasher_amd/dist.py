@@ -236,11 +236,9 @@ class HipQueryEngine:
         self.index = index
 
     def query_range(self, seq: torch.Tensor, k: int, w0: int, w1: int) -> torch.Tensor:
-        q = self.index.query_range(seq, k, w0, w1)
-        try:
-            return q.rows(seq.device)
-        finally:
-            q.free()
+        # the rows stay where the emit kernel wrote them (a 3 GB device copy per query at
+        # config 5 otherwise); the tensor owns the query
+        return self.index.query_range(seq, k, w0, w1).rows_view()
 
 
 def broadcast_index(index, device: torch.device, src: int = 0, group=None):

@@ -48,6 +48,28 @@ def test_range_shards_concatenate_to_full_query(gpu, nshards):
     assert np.array_equal(got, want)
 
 
+def test_rows_view_owns_its_query(gpu):
+    """DeviceQuery.rows_view: the rows where the emit wrote them, alive after the query object,
+    the index and further queries (whose buffers must not reuse the view's) are gone."""
+    import gc
+    torch = gpu
+    from kmer_hasher_amd.device import DeviceIndex
+    s, t = _seq(torch, 120_000, 12)
+    idx = DeviceIndex.build(t, 23)
+    want = O.OracleIndex(s.tobytes(), 23).query(s.tobytes(), 23)
+    v = idx.query(t, 23).rows_view()
+    gc.collect()
+    for _ in range(3):                       # pool traffic while the view is alive
+        idx.query(t, 23).rows_view()
+    idx.free()
+    gc.collect()
+    assert v.dtype == torch.int32 and v.shape == (len(want) // 2, 2)
+    assert np.array_equal(v.cpu().numpy().reshape(-1), want)
+    empty = DeviceIndex.build(t[:1000], 31)
+    z = empty.query(torch.full((500,), ord("N"), dtype=torch.uint8, device=t.device), 31)
+    assert z.n_rows == 0 and z.rows_view().shape == (0, 2)
+
+
 def test_image_export_import_roundtrip(gpu):
     torch = gpu
     from kmer_hasher_amd.device import DeviceIndex
