@@ -1059,20 +1059,28 @@ k_read_pos(const uint2* __restrict__ rinfo, const uint32_t* __restrict__ canon_o
 // R_pairs: rows (i, x, y), x < y, j-outer / k-inner inside a key (src/kmer_hash.c:1113-1121).
 // Keys without pairs are excluded from pkeys, so again every listed key owns >= 1 row.  A
 // workgroup owns PR_TILE rows; R_tiles has recorded the key holding each tile's first row, so
-// no workgroup binary-searches the global offsets.  Thread t produces the PR_PER consecutive
-// rows r0 + t*PR_PER ...: one LDS binary search and one triangular-root inversion for the first,
-// then (j, q) advance row by row; all position loads are issued before any is used; rows are
-// staged in LDS and leave as 16-B stores over the tile's contiguous 12*PR_TILE bytes.
+// no workgroup binary-searches the global offsets.  The tile is produced in two halves; in each,
+// thread t makes the PR_HALF consecutive rows h0 + t*PR_HALF ...: one LDS binary search and one
+// triangular-root inversion for the first, then (j, q) advance row by row; all position loads
+// are issued before any is used; the half's rows are staged in LDS and leave as 16-B stores
+// over its contiguous 12*BLOCK*PR_HALF bytes.  (Round 4: the kernel waits on its chain of
+// dependent loads -- tile key, offsets, key, run, positions -- so what counts is the rows in
+// flight per CU.  The whole-tile 24-KB stage ran 4 waves per SIMD; the 12-KB half stage and
+// 16-bit offsets run 6 (80 VGPRs): config 4 2.49 -> 2.29 ms.  Forcing 8 (64 VGPRs, spills)
+// 4.19 ms; stores straight from registers -- each lane's 96 contiguous bytes -- 3.57 ms.
+// A/B in one run, profiles/rd4z_*.)
 constexpr int PR_PER = 8;
+constexpr int PR_HALF = PR_PER / 2;
 constexpr int PR_TILE = BLOCK * PR_PER;
+static_assert(PR_TILE <= 65536, "offsets inside a tile are 16-bit");
 
-__global__ void __launch_bounds__(BLOCK)
+__global__ void __launch_bounds__(BLOCK, 6)
 k_read_pairs(const uint32_t* __restrict__ pkeys, const uint64_t* __restrict__ pair_off,
              const uint32_t* __restrict__ tile_key, uint64_t nrows,
              const uint2* __restrict__ rinfo, const int32_t* __restrict__ positions,
              int32_t* __restrict__ out) {
-  __shared__ uint32_t offr[PR_TILE];        // key start rows - r0 (the first key's clamped to 0)
-  __shared__ __attribute__((aligned(16))) int32_t stage[3 * PR_TILE];
+  __shared__ uint16_t offr[PR_TILE];        // key start rows - r0 (the first key's clamped to 0)
+  __shared__ __attribute__((aligned(16))) int32_t stage[3 * BLOCK * PR_HALF];
   __shared__ uint64_t first_off;
   const uint32_t b = blockIdx.x;
   const uint64_t r0 = (uint64_t)b * PR_TILE;
@@ -1084,72 +1092,78 @@ k_read_pairs(const uint32_t* __restrict__ pkeys, const uint64_t* __restrict__ pa
   const uint32_t nk = m1 - m0 + 1;
   for (uint32_t i = threadIdx.x; i < nk; i += BLOCK) {
     const uint64_t o = pair_off[m0 + i];
-    offr[i] = o > r0 ? (uint32_t)(o - r0) : 0u;
+    offr[i] = (uint16_t)(o > r0 ? o - r0 : 0u);
     if (i == 0) first_off = o;
   }
   __syncthreads();
-  const uint32_t rel = threadIdx.x * PR_PER;
-  const uint64_t rb = r0 + rel;
-  if (rb < r1) {
-    uint32_t lo = 0, hi = nk - 1;
-    while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (offr[mid] <= rel) lo = mid; else hi = mid - 1; }
-    uint32_t c = pkeys[m0 + lo];
-    uint2 v = rinfo[c];
-    uint32_t n = v.x;
-    const uint64_t t = lo == 0 ? rb - first_off : (uint64_t)(rel - offr[lo]);
-    // largest j with S(j) = j*(2n-j-1)/2 <= t
-    const uint64_t n64 = n;
-    double dn = (double)(2 * n64 - 1);
-    double disc = dn * dn - 8.0 * (double)t;
-    int64_t jj = (int64_t)((dn - sqrt(disc > 0 ? disc : 0)) * 0.5);
-    if (jj < 0) jj = 0;
-    if (jj > (int64_t)n64 - 2) jj = (int64_t)n64 - 2;
-    auto S = [n64](int64_t x) -> uint64_t { return (uint64_t)x * (2 * n64 - (uint64_t)x - 1) / 2; };
-    while (jj > 0 && S(jj) > t) --jj;
-    while (jj + 1 <= (int64_t)n64 - 2 && S(jj + 1) <= t) ++jj;
-    uint32_t j = (uint32_t)jj;
-    uint32_t q = j + 1 + (uint32_t)(t - S(jj));
-    uint32_t base = v.y - v.x;
-    const uint32_t nr = (uint32_t)min<uint64_t>(PR_PER, r1 - rb);
-    uint32_t ij[PR_PER], iq[PR_PER], cc[PR_PER];
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {
+    const uint32_t hrel = (uint32_t)half * BLOCK * PR_HALF;
+    const uint32_t rel = hrel + threadIdx.x * PR_HALF;
+    const uint64_t rb = r0 + rel;
+    if (rb < r1) {
+      uint32_t lo = 0, hi = nk - 1;
+      while (lo < hi) { uint32_t mid = (lo + hi + 1) >> 1; if (offr[mid] <= rel) lo = mid; else hi = mid - 1; }
+      uint32_t c = pkeys[m0 + lo];
+      uint2 v = rinfo[c];
+      uint32_t n = v.x;
+      const uint64_t t = lo == 0 ? rb - first_off : (uint64_t)(rel - offr[lo]);
+      // largest j with S(j) = j*(2n-j-1)/2 <= t
+      const uint64_t n64 = n;
+      double dn = (double)(2 * n64 - 1);
+      double disc = dn * dn - 8.0 * (double)t;
+      int64_t jj = (int64_t)((dn - sqrt(disc > 0 ? disc : 0)) * 0.5);
+      if (jj < 0) jj = 0;
+      if (jj > (int64_t)n64 - 2) jj = (int64_t)n64 - 2;
+      auto S = [n64](int64_t x) -> uint64_t { return (uint64_t)x * (2 * n64 - (uint64_t)x - 1) / 2; };
+      while (jj > 0 && S(jj) > t) --jj;
+      while (jj + 1 <= (int64_t)n64 - 2 && S(jj + 1) <= t) ++jj;
+      uint32_t j = (uint32_t)jj;
+      uint32_t q = j + 1 + (uint32_t)(t - S(jj));
+      uint32_t base = v.y - v.x;
+      const uint32_t nr = (uint32_t)min<uint64_t>(PR_HALF, r1 - rb);
+      uint32_t ij[PR_HALF], iq[PR_HALF], cc[PR_HALF];
 #pragma unroll
-    for (int i = 0; i < PR_PER; ++i) {
-      if ((uint32_t)i >= nr) break;
-      // advance before every row but the first (no key past this thread's rows is touched)
-      if (i > 0 && ++q == n) {               // next j; past the last pair: the next key
-        if (++j == n - 1) {
-          c = pkeys[m0 + ++lo];
-          v = rinfo[c];
-          n = v.x;
-          base = v.y - v.x;
-          j = 0;
+      for (int i = 0; i < PR_HALF; ++i) {
+        if ((uint32_t)i >= nr) break;
+        // advance before every row but the first (no key past this thread's rows is touched)
+        if (i > 0 && ++q == n) {               // next j; past the last pair: the next key
+          if (++j == n - 1) {
+            c = pkeys[m0 + ++lo];
+            v = rinfo[c];
+            n = v.x;
+            base = v.y - v.x;
+            j = 0;
+          }
+          q = j + 1;
         }
-        q = j + 1;
+        ij[i] = base + j;
+        iq[i] = base + q;
+        cc[i] = c + 1;
       }
-      ij[i] = base + j;
-      iq[i] = base + q;
-      cc[i] = c + 1;
+      int32_t pj[PR_HALF], pq[PR_HALF];
+#pragma unroll
+      for (int i = 0; i < PR_HALF; ++i)
+        if ((uint32_t)i < nr) { pj[i] = positions[ij[i]]; pq[i] = positions[iq[i]]; }
+      int32_t* o = stage + 3 * threadIdx.x * PR_HALF;
+#pragma unroll
+      for (int i = 0; i < PR_HALF; ++i)
+        if ((uint32_t)i < nr) { o[3 * i] = (int32_t)cc[i]; o[3 * i + 1] = pj[i]; o[3 * i + 2] = pq[i]; }
     }
-    int32_t pj[PR_PER], pq[PR_PER];
-#pragma unroll
-    for (int i = 0; i < PR_PER; ++i)
-      if ((uint32_t)i < nr) { pj[i] = positions[ij[i]]; pq[i] = positions[iq[i]]; }
-    int32_t* o = stage + 3 * rel;
-#pragma unroll
-    for (int i = 0; i < PR_PER; ++i)
-      if ((uint32_t)i < nr) { o[3 * i] = (int32_t)cc[i]; o[3 * i + 1] = pj[i]; o[3 * i + 2] = pq[i]; }
-  }
-  __syncthreads();
-  // the tile's rows are the contiguous ints [3 r0, 3 r1) of out
-  const uint32_t nint = 3 * (uint32_t)(r1 - r0);
-  int32_t* dst = out + 3 * r0;
-  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
-    const uint32_t n4 = nint / 4;
-    for (uint32_t i = threadIdx.x; i < n4; i += BLOCK)
-      reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(stage)[i];
-    for (uint32_t i = 4 * n4 + threadIdx.x; i < nint; i += BLOCK) dst[i] = stage[i];
-  } else {
-    for (uint32_t i = threadIdx.x; i < nint; i += BLOCK) dst[i] = stage[i];
+    __syncthreads();
+    // the half's rows are the contiguous ints [3 h0, 3 h1) of out
+    const uint64_t h0 = r0 + hrel;
+    const uint32_t nint = h0 < r1 ? 3 * (uint32_t)(min<uint64_t>(r1, h0 + BLOCK * PR_HALF) - h0) : 0u;
+    int32_t* dst = out + 3 * h0;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+      const uint32_t n4 = nint / 4;
+      for (uint32_t i = threadIdx.x; i < n4; i += BLOCK)
+        reinterpret_cast<int4*>(dst)[i] = reinterpret_cast<const int4*>(stage)[i];
+      for (uint32_t i = 4 * n4 + threadIdx.x; i < nint; i += BLOCK) dst[i] = stage[i];
+    } else {
+      for (uint32_t i = threadIdx.x; i < nint; i += BLOCK) dst[i] = stage[i];
+    }
+    if (half == 0) __syncthreads();          // the stage is refilled by the second half
   }
 }
 
