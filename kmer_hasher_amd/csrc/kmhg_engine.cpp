@@ -462,8 +462,6 @@ hipStream_t lib_stream() {
 // the host copy of chunk i, which d2h_threads() threads split (they also take the destination's
 // first-touch page faults in parallel).  Synchronous: returns once dst holds the bytes.
 constexpr size_t D2H_CHUNK = 16u << 20;
-constexpr size_t H2D_CHUNK = 4u << 20;
-constexpr size_t H2D_STAGE_MIN = 2u << 20;
 constexpr size_t D2H_STAGE_MIN = 4u << 20;
 // KMHG_D2H_THREADS (A/B), default 8: A/B in one run (`profiles/rd4n_ab_d2h.log`, config 2
 // host-boundary query, 10 M rows into a fresh array): 4 threads 7.9 / 8.4 ms, 8 threads 7.0 /
@@ -549,56 +547,16 @@ void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
   }
 }
 
-
+// Pageable host -> device copy for the host-pointer entry points (the R string of make.kmer.hash
+// / seq.kmer.pos), ordered on `s`.
 void h2d_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (!bytes) return;
-  // measured (A/B in one run, config 2 host build): pageable hipMemcpy 0.632 ms, this staging
-  // 0.81-0.92 ms -- the runtime's own pageable path already overlaps its copy and DMA, and a
-  // thread start per chunk costs more than the second copier saves.  Opt-in only.
-  static const bool staged = [] {
-    const char* e = std::getenv("KMHG_H2D");
-    return e && std::string(e) == "staged";
-  }();
-  if (!staged || bytes < H2D_STAGE_MIN) {
-    HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
-    return;                                      // pageable: the runtime stages it
-  }
-  PinStage& st = pin_stage();
-  std::lock_guard<std::mutex> g(st.mu);
-  char** pin = st.pin;
-  if (!pin[0])
-    for (int i = 0; i < 2; ++i)
-      HIPC(hipHostMalloc(reinterpret_cast<void**>(&pin[i]), D2H_CHUNK, hipHostMallocPortable));
-  struct Ev2 {
-    hipEvent_t e[2] = {nullptr, nullptr};
-    bool used[2] = {false, false};
-    ~Ev2() {   // every exit: the DMAs out of the pinned chunks have finished, events destroyed
-      for (int i = 0; i < 2; ++i)
-        if (e[i]) {
-          if (used[i]) (void)hipEventSynchronize(e[i]);
-          (void)hipEventDestroy(e[i]);
-        }
-    }
-  } ev;
-  for (int i = 0; i < 2; ++i) HIPC(hipEventCreateWithFlags(&ev.e[i], hipEventDisableTiming));
-  const size_t nch = (bytes + H2D_CHUNK - 1) / H2D_CHUNK;
-  for (size_t i = 0; i < nch; ++i) {
-    const int b = (int)(i & 1);
-    if (ev.used[b]) HIPC(hipEventSynchronize(ev.e[b]));     // its previous DMA is done
-    const size_t off = i * H2D_CHUNK, n = std::min(H2D_CHUNK, bytes - off);
-    host_copy_par(pin[b], static_cast<const char*>(src) + off, n);
-    HIPC(hipMemcpyAsync(static_cast<char*>(dst) + off, pin[b], n, hipMemcpyHostToDevice, s));
-    HIPC(hipEventRecord(ev.e[b], s));
-    ev.used[b] = true;
-  }
+  // pageable: the runtime stages it at the link's rate (10 MB in 0.194 ms, 54 GB/s,
+  // tools/h2d_probe.hip).  Measured and removed: two pinned chunks filled by host threads while
+  // the previous chunk's DMA runs (round 3: 0.81-0.92 ms against 0.63 for the config-2 host
+  // build), and pinning the caller's pages in place (hipHostRegister: the same 0.194 ms).
+  HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
 }
-
-// Pageable host -> device copy for the host-pointer entry points (the R string of make.kmer.hash
-// / seq.kmer.pos): inputs above H2D_STAGE_MIN go through the device's two pinned chunks,
-// d2h_threads() threads filling chunk i + 1 while the DMA of chunk i runs.  Returns once the
-// DMAs have completed (the pinned chunks are reused by the next caller).  KMHG_H2D=staged turns
-// it on; the default is one pageable hipMemcpyAsync (faster, see below).
-void h2d_host(void* dst, const void* src, size_t bytes, hipStream_t s);
 
 // The hash table is sized from the number of windows (an upper bound on distinct k-mers) for a
 // load factor <= 0.7; capacity is not a power of two (slot = mulhi(hash, cap)).
