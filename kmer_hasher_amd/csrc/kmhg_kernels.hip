@@ -390,7 +390,10 @@ __device__ __forceinline__ void put_qrec(uint32_t* qrec, uint2* qmulti, int64_t 
 // 0.319-0.320 ms (167 -> 175 Gbp/s), config 5 4.75-4.77 -> 4.55-4.56 ms (72.1 -> 74.1 Gbp/s);
 // 32 loses (config 2 111 Gbp/s).  256 against 128 (`profiles/rd4x_ab_dg_stride_*`): config 3
 // probe 0.319-0.321 -> 0.297-0.298 ms (174 -> 181 Gbp/s), config 5 4.55-4.56 -> 4.52-4.53 ms,
-// config 2 probe 38.8-40.0 -> 37.2-39.9 us; 64 again slower.  Anchors only establish a
+// config 2 probe 38.8-40.0 -> 37.2-39.9 us; 64 again slower.  512 / 1024 against 256
+// (`profiles/rd4ae_ab_dg_stride_*`): config 3 181 -> 186 Gbp/s, but config 5 (the cross query:
+// an anchor on an SNV leaves the windows up to the next one to probe) 90.9 -> 86.0 / 73.8.
+// Anchors only establish a
 // diagonal: a window after an SNV is verified again against the same anchor's prediction, and
 // only a shifted diagonal (an indel, a rearrangement) probes until the next anchor.
 #ifndef KMHG_DG_STRIDE
