@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdint>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -65,6 +66,46 @@ __global__ void __launch_bounds__(TB) k_pattern(const uint64_t* __restrict__ kin
   }
 }
 
+// Supertiles (round 4): workgroup w owns supertiles of S consecutive tiles and writes them one
+// tile after another; the histogram unit is the supertile, so digit d's runs of the S tiles are
+// adjacent in the output (one run of S * 2048 / R elements, written in S pieces by one
+// workgroup a few microseconds apart) -- the layout a scatter with per-supertile histograms and
+// running digit offsets in LDS would produce.
+template <int S>
+__global__ void __launch_bounds__(TB) k_super(const uint64_t* __restrict__ kin,
+                                              const uint32_t* __restrict__ pin,
+                                              uint64_t* __restrict__ kout,
+                                              uint32_t* __restrict__ pout, uint32_t ntiles,
+                                              uint32_t R) {
+  const uint32_t G = gridDim.x;
+  const uint32_t nsup = ntiles / S;
+  for (uint32_t it = blockIdx.x; it < nsup; it += G) {
+    const uint32_t T = xcd_remap(it, nsup);
+    for (int sub = 0; sub < S; ++sub) {
+      const uint32_t t = T * S + sub;
+      uint64_t k[PER];
+      uint32_t p[PER];
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const uint64_t e = (uint64_t)t * PT + j * TB + threadIdx.x;
+        k[j] = kin[e];
+        p[j] = pin[e];
+      }
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const uint32_t i = j * TB + threadIdx.x;
+        const uint32_t d = (uint32_t)(((uint64_t)i * R) / PT);
+        const uint32_t ts = (uint32_t)(((uint64_t)d * PT + R - 1) / R);
+        const uint32_t te = (uint32_t)(((uint64_t)(d + 1) * PT + R - 1) / R);
+        const uint64_t c = te - ts;                      // run length per tile
+        const uint64_t dst = (uint64_t)nsup * S * ts + (uint64_t)T * S * c + sub * c + (i - ts);
+        kout[dst] = k[j];
+        pout[dst] = p[j];
+      }
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const uint64_t n_req = argc > 1 ? std::strtoull(argv[1], nullptr, 10) : 100000000ull;
   const uint32_t ntiles = (uint32_t)(n_req / PT);
@@ -103,6 +144,16 @@ int main(int argc, char** argv) {
       run((const void*)k_pattern<false, 0>, "interleaved", R, wpc, 24);
       run((const void*)k_pattern<false, 1>, "chunked", R, wpc, 24);
     }
+  if (argc > 2 && std::string(argv[2]) == "super") {
+    for (uint32_t R : {79u, 313u}) {
+      run((const void*)k_super<1>, "super S=1", R, 4, 24);
+      run((const void*)k_super<2>, "super S=2", R, 4, 24);
+      run((const void*)k_super<4>, "super S=4", R, 4, 24);
+      run((const void*)k_super<8>, "super S=8", R, 4, 24);
+      run((const void*)k_super<4>, "super S=4 wg2", R, 2, 24);
+    }
+    return 0;
+  }
   // aligned runs of G elements (R = 2048 / G): the write granularity each array needs
   for (uint32_t G : {2u, 4u, 8u, 16u, 32u, 64u}) {
     run((const void*)k_pattern<false, 0, true, false>, "keys-only aligned", PT / G, 3, 20);
