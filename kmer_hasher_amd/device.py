@@ -257,7 +257,7 @@ class DeviceQuery:
                                device=torch.device("cuda", torch.cuda.current_device()))
         d = C.c_void_p()
         _lib.check(_lib.lib().kmhg_query_rows_device(self._h, C.byref(d)))
-        return torch.as_tensor(_RowsBuffer(self, d.value), device="cuda")
+        return torch.as_tensor(_RowsBuffer(self, d.value))   # on the rows' own device
 
     def free(self):
         if self._h:
