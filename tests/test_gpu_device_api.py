@@ -63,6 +63,7 @@ def test_rows_view_owns_its_query(gpu):
         idx.query(t, 23).rows_view()
     idx.free()
     gc.collect()
+    assert v.is_cuda and v.device == t.device
     assert v.dtype == torch.int32 and v.shape == (len(want) // 2, 2)
     assert np.array_equal(v.cpu().numpy().reshape(-1), want)
     empty = DeviceIndex.build(t[:1000], 31)
