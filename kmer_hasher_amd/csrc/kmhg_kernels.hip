@@ -404,10 +404,13 @@ constexpr int DG_ANCHORS = TILE / DG_STRIDE;
 constexpr int DG_SCAN = (DG_ANCHORS + 63) / 64 * 64;   // whole waves run the anchor scan
 static_assert(DG_SCAN <= BLOCK && DG_SCAN <= 128, "anchors: one thread each, at most two waves");
 
+static_assert(DG_ANCHORS <= 64, "the probed-anchor mask is one wave's ballot");
 struct DiagAnchors {
   uint32_t anc[DG_ANCHORS];      // anchor's unique hit (1-based index position), 0 none
   int32_t last[DG_ANCHORS];      // last anchor <= a that predicts, -1 none
-  uint2 info[DG_ANCHORS];        // anchor's {count, aux}
+  uint2 info[DG_ANCHORS];        // anchor's {count, aux} (probed anchors)
+  uint64_t probed;               // bit a: anchor a's window was probed
+  __device__ __forceinline__ bool was_probed(int a) const { return (probed >> a) & 1ull; }
 };
 
 // Anchor probes of a staged tile (threads < DG_ANCHORS) and the last-predicting-anchor scan;
@@ -422,8 +425,18 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
     const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
-    if (is_anchor && s < w1 && window_key(st, o0 + w, s, L, kq, key))
-      table_find(T, g, key, count, aux);
+    const bool kv = is_anchor && s < w1 && window_key(st, o0 + w, s, L, kq, key);
+    // Adaptive anchors: the even ones are always probed; an odd one only while no even anchor
+    // before it predicts (the tile's head after a miss), since behind a predicting anchor the
+    // windows verify against its diagonal anyway.  A self dot plot probes every 512th window, a
+    // cross query keeps every 256th where the tile head needs it.
+    const bool primary = (threadIdx.x & 1) == 0;
+    if (kv && primary) table_find(T, g, key, count, aux);
+    const uint64_t pm = __ballot(is_anchor && primary && count == 1);
+    const bool second = kv && !primary && (pm & lanemask_lt()) == 0;
+    if (second) table_find(T, g, key, count, aux);
+    const uint64_t probed = __ballot(is_anchor && (primary || second));
+    if (threadIdx.x == 0) A.probed = probed;
     if (is_anchor) {
       A.anc[threadIdx.x] = count == 1 ? aux : 0u;
       A.info[threadIdx.x] = make_uint2(count, aux);
@@ -463,7 +476,7 @@ __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_sta
     const int w = j * BLOCK + threadIdx.x;
     const int la = A.last[w / DG_STRIDE];
     int64_t pj = la >= 0 ? (int64_t)A.anc[la] + (w - la * DG_STRIDE) : 1;
-    if (pj > X.nA || w % DG_STRIDE == 0) pj = 1;
+    if (pj > X.nA || (w % DG_STRIDE == 0 && A.was_probed(w / DG_STRIDE))) pj = 1;
     const uint64_t q0 = (uint64_t)(pj - 1) >> 4;
     ca[j] = X.code[q0];
     cb[j] = X.code[q0 + 1];
@@ -478,7 +491,7 @@ __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_sta
     uint32_t count = 0, aux = 0;
     if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) {
       bool hit;
-      if (w % DG_STRIDE == 0) {
+      if (w % DG_STRIDE == 0 && A.was_probed(w / DG_STRIDE)) {
         const uint2 ai = A.info[w / DG_STRIDE];
         count = ai.x; aux = ai.y;
         hit = true;
@@ -547,7 +560,7 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
     if (s < w1 && win.valid(j)) {
       const uint64_t key = win.key(j);
       bool hit;
-      if (j == 0 && w0 % DG_STRIDE == 0) {               // an anchor: probed already
+      if (j == 0 && w0 % DG_STRIDE == 0 && A.was_probed(w0 / DG_STRIDE)) {   // probed already
         const uint2 ai = A.info[w0 / DG_STRIDE];
         count = ai.x; aux = ai.y;
         hit = true;
