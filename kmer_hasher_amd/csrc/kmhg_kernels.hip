@@ -433,7 +433,9 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
     const bool primary = (threadIdx.x & 1) == 0;
     if (kv && primary) table_find(T, g, key, count, aux);
     const uint64_t pm = __ballot(is_anchor && primary && count == 1);
-    const bool second = kv && !primary && (pm & lanemask_lt()) == 0;
+    // (and only in a tile where some even anchor predicts: with none, the tile is unrelated to
+    // the index and its windows probe the table whatever the odd anchors find)
+    const bool second = kv && !primary && pm != 0 && (pm & lanemask_lt()) == 0;
     if (second) table_find(T, g, key, count, aux);
     const uint64_t probed = __ballot(is_anchor && (primary || second));
     if (threadIdx.x == 0) A.probed = probed;

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Round 4: adaptive diagonal anchors (odd anchors probed only at a tile head without a
 # predicting even anchor) -- query parity (incl. the full-size config 3 / 5 digests), then A/B
-# against the previous library (preanc) at configs 2, 3 and 5.
+# against the previous library (preanc; round 2: odd anchors skipped in tiles where no even anchor predicts) at configs 2, 3 and 5.
 set -uo pipefail
 REPO=${GRAFT_REPO_ROOT:-/root/repo}
 cd "$REPO"
-OUT=$REPO/gpurun_out/r4ag
+OUT=$REPO/gpurun_out/r4ag2
 mkdir -p "$OUT"
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_parity.py tests/test_gpu_device_api.py tests/test_gpu_multidevice.py tests/test_gpu_dist.py \
