@@ -138,16 +138,22 @@ def survey_bytes(kind: str, L: int = 0, U: int = 0, N: int = 0, Nq: int = 0, H: 
     raise ValueError(kind)
 
 
+# HIP-event labels that cover several kernels (one LAUNCH of two kernels), by PMC kernel name
+PMC_GROUP = {"k_query_emit": ("k_query_emit", "k_query_emit1"),
+             "k_scan_tiles_u64": ("k_scan_tiles_u64", "k_block_sum_u64", "k_block_scan_u64")}
+
+
 def pmc_step_traffic(pmc: dict, kernels) -> int | None:
     """Summed PMC HBM bytes of one step's kernels (per-launch averages x launches per step)."""
     if not pmc:
         return None
     tot, seen = 0, False
     for name, launches in kernels.items():
-        t = pmc_traffic(pmc, name)
-        if t is not None:
-            tot += t * launches
-            seen = True
+        for part in PMC_GROUP.get(name, (name,)):
+            t = pmc_traffic(pmc, part)
+            if t is not None:
+                tot += t * launches
+                seen = True
     return tot if seen else None
 
 
