@@ -102,6 +102,8 @@ void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, co
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
 // exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
 // reduce-then-scan with `scratch` = scan_u64_scratch(n) u64
+// (round 4: one workgroup up to 64 K / 256 K totals instead -- config 3 query 185 -> 162 Gbp/s,
+// config 5 92.5 -> 82.4; profiles/rd4ak_*)
 constexpr uint64_t SCAN1_MAX = 16384;
 inline uint64_t scan_u64_scratch(uint64_t n) { return (n + TILE - 1) / TILE + 1; }
 void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch, hipStream_t s);
