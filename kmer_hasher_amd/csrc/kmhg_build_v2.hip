@@ -363,7 +363,14 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
 // while this one is counted -- the one-tile-per-workgroup form exposed every workgroup's load
 // latency (config 2: 14.5 us for 40 MB).  `in` holds n + PTILE elements (the passes' padded
 // streams), so whole-tile loads stay inside it.
-template <bool BID>
+// MODE: 0 = u64 keys, 1 = u32 bucket ids, 2 = packed 12-B {key lo, key hi, pos} elements (the
+// position builds' key streams: 96 B = six 16-B loads per thread and tile).
+template <int MODE>
+__device__ __forceinline__ uint32_t word_of(const uint4* v, int i) {   // i: compile-time after unroll
+  const uint4 w = v[i >> 2];
+  return (i & 3) == 0 ? w.x : (i & 3) == 1 ? w.y : (i & 3) == 2 ? w.z : w.w;
+}
+template <int MODE>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
            uint32_t* __restrict__ hist, uint32_t ntiles, uint64_t* __restrict__ scan_status,
@@ -380,11 +387,12 @@ k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, 
   if (save_col0 && tile_at(0) == 0)
     for (uint32_t d = threadIdx.x; d < R; d += BLOCK) save_col0[d] = hist[(size_t)d * ntiles];
   for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
-  constexpr int NV = BID ? 2 : 4;                      // 16-B loads per thread per tile
+  constexpr bool BID = MODE == 1;
+  constexpr int NV = MODE == 1 ? 2 : MODE == 2 ? 6 : 4;   // 16-B loads per thread per tile
   uint4 nx[NV];
   auto prefetch = [&](uint32_t tile) {
     const uint4* src = reinterpret_cast<const uint4*>(in) +
-                       ((uint64_t)tile * PTILE + 8u * threadIdx.x) / (BID ? 4 : 2);
+                       ((uint64_t)tile * PTILE + 8u * threadIdx.x) * (uint64_t)(NV * 2) / 16;
 #pragma unroll
     for (int v = 0; v < NV; ++v) nx[v] = src[v];
   };
@@ -405,6 +413,9 @@ k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, 
           const uint4 w = cur[j >> 2];
           const uint32_t id = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
           dg = digit_of_b(id, D);
+        } else if (MODE == 2) {
+          const uint64_t key = ((uint64_t)word_of<MODE>(cur, 3 * j + 1) << 32) | word_of<MODE>(cur, 3 * j);
+          dg = digit_of_h(mix64(key), g, D);
         } else {
           const uint4 w = cur[j >> 1];
           const uint64_t key = (j & 1) ? (((uint64_t)w.w << 32) | w.z) : (((uint64_t)w.y << 32) | w.x);
@@ -559,6 +570,11 @@ __device__ __forceinline__ uint64_t block_excl_scan_n(uint64_t v, uint64_t* lds,
 // code words by the bucket kernel; 2 = the last pass: (bucket id, pos) in, positions only out.
 // kin / kout then point at u32 arrays.  8 B per element instead of 12 through the middle passes,
 // 4 B out of the last.
+// 3 = packed (key, pos) elements, 12 B each in kin / kout ({key lo, key hi, pos}; pin / pout
+// unused): a tile's digit run leaves as ONE contiguous piece instead of an 8 c-byte piece of
+// keys and a 4 c-byte piece of positions in two arrays.  Write-pattern probe
+// (tools/scatter_pattern.hip layout, profiles/r5a_scatter_layout.txt, 100 M elements): radix 313
+// 1.09 -> 0.87 ms, radix 79 0.72 -> 0.61 ms.
 // BALLOT: stable ranks from one ballot per digit bit instead of the count atomics' lane-ordered
 // returns -- chosen at run time where the device self-check finds that order violated.
 template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false, int BM = 0, bool BALLOT = false>
@@ -569,9 +585,12 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
              const uint32_t* __restrict__ hist, uint32_t ntiles,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad,
              int skip_empty, BoundsFuse bf) {
-  using KT = typename std::conditional<BM != 0, uint32_t, uint64_t>::type;
+  constexpr bool BIDS = BM == 1 || BM == 2;      // bucket-id streams
+  constexpr bool AOS = BM == 3;                   // packed 12-B (key, pos) elements
+  using KT = typename std::conditional<BIDS, uint32_t, uint64_t>::type;
   using SL = ScatterLDS<KT>;
-  static_assert(BM == 0 || !NOPOS, "bucket-id streams carry positions");
+  static_assert(BM == 0 || !NOPOS, "bucket-id and packed streams carry positions");
+  static_assert(!(AOS && KEYS0), "packed streams start from the sequence");
   // KEYS0 with BM: the first pass over V_hist0's per-window bucket ids (~0: not indexed)
   const KT* __restrict__ kinT = reinterpret_cast<const KT*>(kin);
   KT* __restrict__ koutT = reinterpret_cast<KT*>(kout);
@@ -619,6 +638,10 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         const uint64_t e = t0 + wbase + (uint32_t)cc * 64 + lane;
         if (KEYS0) {
           nkey[cc] = kinT[e < n ? e : n - 1];    // positions implicit: e + 1 (below)
+        } else if (AOS) {
+          const uint3 v = reinterpret_cast<const uint3*>(kin)[e];
+          nkey[cc] = ((uint64_t)v.y << 32) | v.x;
+          npos[cc] = v.z;
         } else {
           nkey[cc] = kinT[e];
           npos[cc] = NOPOS ? 0u : pin[e];
@@ -632,8 +655,12 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
   prefetch(tile_at(0));
 #pragma unroll
   for (int j = 0; j < PTILE / TB; ++j) {
-    if (BM != 2) koutT[pad + threadIdx.x] = 0;
-    if (!NOPOS) pout[pad + threadIdx.x] = 0;
+    if (AOS) {
+      reinterpret_cast<uint3*>(kout)[pad + threadIdx.x] = make_uint3(0u, 0u, 0u);
+    } else {
+      if (BM != 2) koutT[pad + threadIdx.x] = 0;
+      if (!NOPOS) pout[pad + threadIdx.x] = 0;
+    }
   }
   for (uint32_t it = 0; it < n_iter; ++it) {
     const uint32_t tile = tile_at(it);
@@ -667,9 +694,9 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         const uint64_t h = mix64(kk);
         const uint32_t bl = bucket_local(h, g);
         act[c] = act[c] && bl < g.nb;                        // a part build keeps its buckets
-        key[c] = BM ? (KT)bl : (KT)kk;
+        key[c] = BIDS ? (KT)bl : (KT)kk;
         dg[c] = act[c] ? digit_of_b(bl, D) : 0;
-      } else if (BM) {
+      } else if (BIDS) {
         act[c] = e < n && !(KEYS0 && (uint32_t)key[c] == ~0u);
         dg[c] = act[c] ? digit_of_b((uint32_t)key[c], D) : 0;
       } else {
@@ -766,8 +793,13 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
       const uint32_t i = (uint32_t)(j * TB) + threadIdx.x;
       // lanes past the tile's end store into the PTILE-element pad behind the outputs
       const uint32_t dst = i < (uint32_t)tile_n ? S.sdst[i] : pad + threadIdx.x;
-      if (BM != 2) koutT[dst] = S.skey[i];
-      if (!NOPOS) pout[dst] = S.spos[i];
+      if (AOS) {
+        const uint64_t kk = S.skey[i];
+        reinterpret_cast<uint3*>(kout)[dst] = make_uint3((uint32_t)kk, (uint32_t)(kk >> 32), S.spos[i]);
+      } else {
+        if (BM != 2) koutT[dst] = S.skey[i];
+        if (!NOPOS) pout[dst] = S.spos[i];
+      }
     }
   }
 }
@@ -798,9 +830,18 @@ __device__ __forceinline__ void bounds_lo_body(uint32_t lo, uint32_t* cnt,
   for (uint32_t d = threadIdx.x; d < R; d += tb) cnt[d] = 0;
   __syncthreads();
   const uint32_t tile = P / PTILE;
-  for (uint32_t i = tile * PTILE + threadIdx.x; i < P; i += tb)
-    atomicAdd(&cnt[bid ? digit_of_b(reinterpret_cast<const uint32_t*>(kprev)[i], Dlast)
-                       : digit_of(kprev[i], g, Dlast)], 1u);
+  for (uint32_t i = tile * PTILE + threadIdx.x; i < P; i += tb) {
+    uint32_t dg;
+    if (bid == 1) {                        // bucket ids
+      dg = digit_of_b(reinterpret_cast<const uint32_t*>(kprev)[i], Dlast);
+    } else if (bid == 2) {                 // packed (key, pos) elements
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(kprev) + 3 * (uint64_t)i;
+      dg = digit_of(((uint64_t)w[1] << 32) | w[0], g, Dlast);
+    } else {
+      dg = digit_of(kprev[i], g, Dlast);
+    }
+    atomicAdd(&cnt[dg], 1u);
+  }
   __syncthreads();
   for (uint32_t hi = threadIdx.x; hi < R; hi += tb) {
     const uint64_t b = (uint64_t)hi * div + lo;
@@ -828,9 +869,11 @@ k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ 
 // bucket's stream lists its windows in ascending position -- the order the position lists keep.
 // The bucket kernels check it with one neighbour load per element and report a violation like
 // an LDS table overflow, which rebuilds the index with the global-atomic build (finish_build).
+// (pos: the stream's positions, every `stride`-th word: 3 in a packed (key, pos) stream)
+template <int STRIDE = 1>
 __device__ __forceinline__ bool stream_out_of_order(const uint32_t* __restrict__ pos, uint32_t i,
                                                     uint32_t s0, uint32_t s1, uint32_t p) {
-  return i > s0 && i < s1 && pos[i - 1] >= p;
+  return i > s0 && i < s1 && pos[(uint64_t)(i - 1) * STRIDE] >= p;
 }
 
 // ---------------------------------------------------------------- V_bucket_wg (group per bucket)
@@ -885,7 +928,8 @@ __device__ __forceinline__ int lds_find_g(const GroupTableC& W, uint64_t key) {
 struct Words3 {                                // three consecutive code words, 4-B aligned
   uint32_t a, b, c;
 };
-template <bool COUNT_ONLY, bool CK, bool BALLOT>
+// AOS: the stream is packed 12-B (key, pos) elements in `keys` (`pos` unused).
+template <bool COUNT_ONLY, bool CK, bool BALLOT, bool AOS = false>
 #ifndef KMHG_BUCKET_WGS
 #define KMHG_BUCKET_WGS 8      // workgroups per CU the compact LDS table allows (1,536 slots)
 #endif
@@ -896,6 +940,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
                BuildMeta* __restrict__ meta, const uint32_t* __restrict__ code, int k,
                const uint32_t* __restrict__ n_ptr, uint32_t nw) {
   static_assert(!(CK && COUNT_ONLY), "code-word keys belong to position builds");
+  static_assert(!(AOS && (CK || COUNT_ONLY)), "packed streams carry keys and positions");
   static_assert(V2_CAPW % BLOCK == 0, "the side slot V2_CAPW is slot q = V2_CAPW / TB of thread 0");
   constexpr int TB = BLOCK;
   constexpr int NW = TB / 64;                         // waves of the workgroup
@@ -950,10 +995,19 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
 #pragma unroll
     for (int c = 0; c < PER; ++c) {
       const uint32_t i = elem(i0, c);
-      key[c] = i < s1 ? keys[i] : 0;
-      ps[c] = (!COUNT_ONLY && i < s1) ? pos[i] : 0;
+      if (AOS) {
+        const uint3 v = i < s1 ? reinterpret_cast<const uint3*>(keys)[i] : make_uint3(0u, 0u, 0u);
+        key[c] = ((uint64_t)v.y << 32) | v.x;
+        ps[c] = v.z;
+      } else {
+        key[c] = i < s1 ? keys[i] : 0;
+        ps[c] = (!COUNT_ONLY && i < s1) ? pos[i] : 0;
+      }
       if (!COUNT_ONLY && i < s1 && ps[c] - 1u >= nw) disorder = true;   // outside [1, nw]
-      if (!COUNT_ONLY && !one_batch) disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
+      if (!COUNT_ONLY && !one_batch)
+        disorder |= AOS ? stream_out_of_order<3>(reinterpret_cast<const uint32_t*>(keys) + 2, i,
+                                                  s0, s1, ps[c])
+                        : stream_out_of_order(pos, i, s0, s1, ps[c]);
     }
   };
   auto cut = [&](uint32_t i0) {
@@ -1224,6 +1278,8 @@ void set_stamp_buffer(uint64_t* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamps
 // A part build's compacted tiles (V_hist0 PARTC) into one dense stream: tile t's off[t+1] -
 // off[t] elements (off = the scanned tile counts, off[ntiles] = *n_total) move from
 // [t * PTILE, ...) to [off[t], ...), keys and positions, order kept.
+// AOS: the dense stream is packed 12-B (key, pos) elements in dk (dp unused).
+template <bool AOS>
 __global__ void __launch_bounds__(BLOCK)
 k_part_dense(const uint64_t* __restrict__ ck, const uint32_t* __restrict__ cp,
              const uint32_t* __restrict__ off, uint32_t ntiles,
@@ -1233,8 +1289,13 @@ k_part_dense(const uint64_t* __restrict__ ck, const uint32_t* __restrict__ cp,
     const uint32_t o0 = off[t], o1 = t + 1 < ntiles ? off[t + 1] : *n_total;
     const uint64_t src = (uint64_t)t * PTILE;
     for (uint32_t i = threadIdx.x; i < o1 - o0; i += BLOCK) {
-      dk[o0 + i] = ck[src + i];
-      dp[o0 + i] = cp[src + i];
+      if (AOS) {
+        const uint64_t kk = ck[src + i];
+        reinterpret_cast<uint3*>(dk)[o0 + i] = make_uint3((uint32_t)kk, (uint32_t)(kk >> 32), cp[src + i]);
+      } else {
+        dk[o0 + i] = ck[src + i];
+        dp[o0 + i] = cp[src + i];
+      }
     }
   }
 }
@@ -1319,18 +1380,24 @@ void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total,
 void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
                         uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                         hipStream_t s, uint32_t* save_col0) {
-  static const unsigned cap = resident_blocks((const void*)k_v2_histp<true>);
-  hipLaunchKernelGGL(k_v2_histp<true>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0, s,
+  static const unsigned cap = resident_blocks((const void*)k_v2_histp<1>);
+  hipLaunchKernelGGL(k_v2_histp<1>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0, s,
                      reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ntiles,
                      scan_status, n_status, save_col0);
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     uint32_t ntiles, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0, bool skip_empty,
-                    bool padded) {
+                    bool padded, bool aos) {
+  if (aos) {                   // packed (key, pos) stream (padded by construction)
+    static const unsigned cap = resident_blocks((const void*)k_v2_histp<2>);
+    hipLaunchKernelGGL(k_v2_histp<2>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0,
+                       s, keys, n_ptr, g, D, hist, ntiles, scan_status, n_status, save_col0);
+    return;
+  }
   if (padded && !hll_rows && !skip_empty) {
-    static const unsigned cap = resident_blocks((const void*)k_v2_histp<false>);
-    hipLaunchKernelGGL(k_v2_histp<false>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0,
+    static const unsigned cap = resident_blocks((const void*)k_v2_histp<0>);
+    hipLaunchKernelGGL(k_v2_histp<0>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0,
                        s, keys, n_ptr, g, D, hist, ntiles, scan_status, n_status, save_col0);
     return;
   }
@@ -1346,10 +1413,10 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
                          uint32_t spread, uint32_t* start, uint32_t nlim, hipStream_t s,
-                         const uint32_t* bprev) {
+                         const uint32_t* bprev, bool aos) {
   hipLaunchKernelGGL(k_v2_bounds_lo, dim3(div), dim3(BLOCK), 0, s,
                      bprev ? reinterpret_cast<const uint64_t*>(bprev) : kprev, n_ptr, g, Dlast,
-                     div, hist, C, lo_start, spread, start, bprev ? 1 : 0, nlim);
+                     div, hist, C, lo_start, spread, start, bprev ? 1 : aos ? 2 : 0, nlim);
 }
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s) {
@@ -1361,15 +1428,23 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
 static const BoundsFuse kNoFuse{nullptr, nullptr, nullptr, Digit{}, 0u, 1u, 0, 0u};
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
-                           uint32_t pad, hipStream_t s) {
-  KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
-               kout, pout, pad, 0, kNoFuse);
+                           uint32_t pad, hipStream_t s, bool aos) {
+  if (aos)
+    KMHG_SCATTER_BM(true, false, false, 3, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist,
+                    ntiles, kout, nullptr, pad, 0, kNoFuse);
+  else
+    KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
+                 kout, pout, pad, 0, kNoFuse);
 }
 void launch_part_dense(const uint64_t* ck, const uint32_t* cp, const uint32_t* off,
                        uint32_t ntiles, const uint32_t* n_total, uint64_t* dk, uint32_t* dp,
-                       hipStream_t s) {
-  hipLaunchKernelGGL(k_part_dense, dim3(std::min<uint32_t>(ntiles, 8192u)), dim3(BLOCK), 0, s, ck,
-                     cp, off, ntiles, n_total, dk, dp);
+                       hipStream_t s, bool aos) {
+  if (aos)
+    hipLaunchKernelGGL(k_part_dense<true>, dim3(std::min<uint32_t>(ntiles, 8192u)), dim3(BLOCK), 0,
+                       s, ck, cp, off, ntiles, n_total, dk, dp);
+  else
+    hipLaunchKernelGGL(k_part_dense<false>, dim3(std::min<uint32_t>(ntiles, 8192u)), dim3(BLOCK), 0,
+                       s, ck, cp, off, ntiles, n_total, dk, dp);
 }
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
                             const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
@@ -1398,9 +1473,14 @@ void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint3
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
-                       uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf) {
-  KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,
-               hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse);
+                       uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf,
+                       bool aos) {
+  if (aos)
+    KMHG_SCATTER_BM(false, false, false, 3, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr,
+                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
+  else
+    KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,
+                 hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse);
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
                              Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
@@ -1422,9 +1502,15 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, const uint32_t* n_ptr, uint32_t nw,
-                         const uint32_t* code, int k) {
+                         const uint32_t* code, int k, bool aos) {
   const bool ballot = ballot_ranks();
-  if (count_only)              // no positions: nothing is ranked
+  if (aos && !ballot)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, false, false, true>), dim3(g.nb), dim3(BLOCK), 0, s,
+                       keys, pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
+  else if (aos)
+    hipLaunchKernelGGL((k_v2_bucket_wg<false, false, true, true>), dim3(g.nb), dim3(BLOCK), 0, s,
+                       keys, pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
+  else if (count_only)              // no positions: nothing is ranked
     hipLaunchKernelGGL((k_v2_bucket_wg<true, false, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
                        pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
   else if (code && !ballot)
@@ -1480,24 +1566,25 @@ void launch_lane_order_check(unsigned long long* res, hipStream_t s, int blocks)
 // (the build then falls back) instead of faulting: 1 swaps the first two positions of bucket 0's
 // stream; 2 zeroes its first position (an entry no pass wrote: the pad's value); 3 moves bucket
 // 1's start past the end of the stream.
+// (pos: the stream's positions, every `stride`-th word)
 __global__ void k_v2_test_disorder(uint32_t* __restrict__ pos, uint32_t* __restrict__ start,
-                                   const uint32_t* __restrict__ n_ptr, int mode) {
+                                   const uint32_t* __restrict__ n_ptr, int mode, uint32_t stride) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
-    const uint32_t a = start[0], b = start[1];
+    const uint64_t a = start[0], b = start[1];
     if (mode == 1 && b - a >= 2) {
-      const uint32_t t = pos[a];
-      pos[a] = pos[a + 1];
-      pos[a + 1] = t;
+      const uint32_t t = pos[a * stride];
+      pos[a * stride] = pos[(a + 1) * stride];
+      pos[(a + 1) * stride] = t;
     } else if (mode == 2 && b > a) {
-      pos[a] = 0u;
+      pos[a * stride] = 0u;
     } else if (mode == 3) {
       start[1] = *n_ptr + 4096u;
     }
   }
 }
 void launch_v2_test_disorder(uint32_t* pos, uint32_t* start, const uint32_t* n_ptr, int mode,
-                             hipStream_t s) {
-  hipLaunchKernelGGL(k_v2_test_disorder, dim3(1), dim3(64), 0, s, pos, start, n_ptr, mode);
+                             hipStream_t s, uint32_t stride) {
+  hipLaunchKernelGGL(k_v2_test_disorder, dim3(1), dim3(64), 0, s, pos, start, n_ptr, mode, stride);
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {

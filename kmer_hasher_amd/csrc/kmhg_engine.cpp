@@ -878,7 +878,17 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const char* bide = std::getenv("KMHG_BUILD_BID");
   const bool bid_on = bide ? bide[0] == '1' : Nw <= BID_MAX_WINDOWS;
   const bool bid = codes && !from_keys && !count_only && bid_on;
-  DBuf<uint64_t> kA(bid ? 1 : Nw + PTILE, s), kB(bid ? 1 : Nw + PTILE, s);   // + pad
+  // position builds on key streams carry packed 12-B (key, pos) elements: a tile's digit run is
+  // one contiguous write instead of a key piece and a position piece in two arrays
+  // (tools/scatter_pattern.hip layout, profiles/r5a_scatter_layout.txt: radix 313 1.09 -> 0.87
+  // ms per 100 M elements, radix 79 0.72 -> 0.61).  Built with -DKMHG_NO_AOS: SoA streams (A/B).
+#ifdef KMHG_NO_AOS
+  const bool aos = false;
+#else
+  const bool aos = !from_keys && !count_only && !bid;
+#endif
+  const uint64_t kwords = bid ? 1 : aos ? ((uint64_t)(Nw + PTILE) * 3 + 1) / 2 : (uint64_t)(Nw + PTILE);
+  DBuf<uint64_t> kA(kwords, s), kB(kwords, s);   // + pad
   // (Removed in round 4 after measurement, DESIGN.md §5: radix passes writing whole 128-B lines
   // through LDS write-combining buffers -- config 3 29.2 -> 25.0-28.7 Gbp/s, the 500 Mbp build
   // 18.1 -> 18.9-22.7 ms.)
@@ -888,7 +898,10 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   DBuf<uint32_t> bA(bid && passes > 1 ? Nw + PTILE : 1, s);
   DBuf<uint32_t> bB(bid ? Nw + PTILE : 1, s);
   const bool no_pos = count_only;                        // keys only through the passes
-  DBuf<uint32_t> pA(no_pos ? 1 : Nw + PTILE, s), pB(no_pos ? 1 : Nw + PTILE, s);
+  // (a part build's compacted windows land in kB / pB before they are packed: pB stays)
+  const bool partc_pos = !from_keys && n_parts >= 2 && codes;
+  DBuf<uint32_t> pA(no_pos || aos ? 1 : Nw + PTILE, s),
+      pB(no_pos || (aos && !partc_pos) ? 1 : Nw + PTILE, s);
   const uint32_t pad = (uint32_t)Nw;
   DBuf<uint32_t> hist(nhist, s);
   DBuf<uint32_t> start((uint64_t)nb + 1, s);
@@ -960,7 +973,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       else
         LAUNCH("k_v2_scatter_seq", s,
                launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
-                                     pA.p, pad, s));
+                                     pA.p, pad, s, aos));
       div = R;
     }
   }
@@ -990,7 +1003,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   }
   if (partc)   // the part's windows, dense in window order: every radix pass reads these
     LAUNCH("k_part_dense", s, launch_part_dense(kB.p, pB.p, tcnt.p, ntiles, n_valid, kA.p, pA.p,
-                                                s));
+                                                s, aos));
   // where pass 1 saves column 0: pass 0's histogram is hp's unless pass 0 was the one over
   // every window (its own layout, copied above)
   uint32_t* save1 = hp == hist.p || partc ? lo_save.p : nullptr;
@@ -1006,7 +1019,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const uint32_t* lin = p == 1 ? lo_save.p : ((p - 1) % 2 ? lvA.p : lvB.p);
     uint32_t* lout = last ? start.p : (p % 2 ? lvA.p : lvB.p);
     return BoundsFuse{reinterpret_cast<const uint64_t*>(kprev), lin, lout,
-                      make_digit((uint32_t)dv, R), (uint32_t)dv, spread, is_bid ? 1 : 0,
+                      make_digit((uint32_t)dv, R), (uint32_t)dv, spread, is_bid ? 1 : aos ? 2 : 0,
                       last ? g.nb : (uint32_t)(dv * R)};
   };
   auto fused = [&](uint32_t p) { return p >= 1 && fuse_on && !(co_auto && p + 1 == passes); };
@@ -1014,7 +1027,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const uint64_t* kp = f.bid ? nullptr : f.kprev;
     const uint32_t* bp = f.bid ? reinterpret_cast<const uint32_t*>(f.kprev) : nullptr;
     LAUNCH("k_v2_bounds", s, launch_v2_bounds_lo(kp, n_valid, g, f.Dlast, f.div, hp, C,
-                                                 f.lo_start, f.spread, f.start, f.nlim, s, bp));
+                                                 f.lo_start, f.spread, f.start, f.nlim, s, bp,
+                                                 f.bid == 2));
   };
   for (uint32_t p = 1; bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
@@ -1042,7 +1056,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
            launch_v2_hist(src, n_valid, g, Dp, hp, C, status, nst, s,
                           hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
                           p == 1 ? save1 : nullptr, keys0 && skip_empty,
-                          /*padded=*/!keys0));
+                          /*padded=*/!keys0, aos));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hp, nh, status, n_valid, s));
     if (hll) {   // after the scan: the estimate travels with the valid key count
       LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ntiles, hll_regs.p,
@@ -1063,7 +1077,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       else
         LAUNCH("k_v2_scatter", s,
                launch_v2_scatter(kin, pin, n_valid, g, Dp, hp, C, kout, pout, pad, s,
-                                 fused(p) ? &lv : nullptr));
+                                 fused(p) ? &lv : nullptr, aos));
       if (p >= 1 && !fused(p) && !last) launch_level(lv);
     }
     std::swap(kin, kout);
@@ -1103,10 +1117,12 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // checks -> v1 rebuild
   if (const char* td = std::getenv("KMHG_TEST_DISORDER"))
     if (!no_pos && td[0] >= '1' && td[0] <= '3')
-      launch_v2_test_disorder(pin, start.p, n_valid, td[0] - '0', s);
+      launch_v2_test_disorder(aos ? reinterpret_cast<uint32_t*>(kin) + 2 : pin, start.p, n_valid,
+                              td[0] - '0', s, aos ? 3u : 1u);
   LAUNCH("k_v2_bucket_wg", s,
          launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, idx->bstats.p,
-                             meta, no_pos, s, n_valid, (uint32_t)Nw, bid ? db.code : nullptr, k));
+                             meta, no_pos, s, n_valid, (uint32_t)Nw, bid ? db.code : nullptr, k,
+                             aos));
   LAUNCH("k_v2_stats", s, launch_v2_stats(idx->bstats.p, gb.nb, n_valid, meta, idx->rec.meta, s));
   idx->bstats_nb = gb.nb;
   HIPC(hipEventRecord(idx->rec.ev, s));

@@ -171,7 +171,7 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
 // packs them into dk / dp
 void launch_part_dense(const uint64_t* ck, const uint32_t* cp, const uint32_t* off,
                        uint32_t ntiles, const uint32_t* n_total, uint64_t* dk, uint32_t* dp,
-                       hipStream_t s);
+                       hipStream_t s, bool aos = false);
 // The scatter passes' outputs hold n_max + PTILE elements: lanes past a tile's end store into the
 // pad at [pad, pad + BLOCK) so every lane issues the same stores (see k_v2_scatter).
 // exclusive scan of a u32 array; status = tiles_for(n) + 1 u64, zeroed by the histogram kernel
@@ -188,7 +188,7 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
                     uint32_t ntiles, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr,
                     uint32_t* save_col0 = nullptr, bool skip_empty = false,
-                    bool padded = false);
+                    bool padded = false, bool aos = false);
 // one level of the bucket starts from the histograms (the unfused form of BoundsFuse): one
 // workgroup per lo value (div of them); kprev = pass p's input keys, lo_start = S_(p-1) (pass 0's
 // column 0 saved by launch_v2_hist's save_col0 for p = 1; nullptr for one pass); start[c / spread]
@@ -197,7 +197,7 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
                          uint32_t spread, uint32_t* start, uint32_t nlim, hipStream_t s,
-                         const uint32_t* bprev = nullptr);
+                         const uint32_t* bprev = nullptr, bool aos = false);
 // also copies *n_valid (launch it after the pass's scan) to *host_n
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s);
@@ -213,13 +213,13 @@ struct BoundsFuse {
   uint32_t* start;             // S_p
   Digit Dlast;                 // the pass's own digit
   uint32_t div, spread;        // div = R^p lower-digit values
-  int bid;
+  int bid;                     // 0 u64 keys, 1 u32 bucket ids, 2 packed 12-B (key, pos) elements
   uint32_t nlim;               // entries of S_p: nb for the last pass, R^(p+1) before
 };
 // the sequence must be 16-B aligned (the engine copies an unaligned input)
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
-                           uint32_t pad, hipStream_t s);
+                           uint32_t pad, hipStream_t s, bool aos = false);
 // first pass over a caller's key stream of n_keys keys (>= 1): positions are e + 1; nopos:
 // keys only (count-only builds), pout unused; skip_empty: EMPTY_KEY entries are not keys (padded
 // read k-mer streams, k <= 31)
@@ -232,7 +232,11 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
                              hipStream_t s, const BoundsFuse* bf = nullptr);
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
-                       uint32_t pad, hipStream_t s, const BoundsFuse* bf = nullptr);
+                       uint32_t pad, hipStream_t s, const BoundsFuse* bf = nullptr,
+                       bool aos = false);
+// Packed key streams (aos): position builds on key streams carry each window as ONE 12-B
+// element {key lo, key hi, pos} (kin / kout hold n + PTILE of them; pin / pout unused), so a
+// tile's digit run is one contiguous write.
 // Bucket-id streams (position builds that keep the sequence's code words): V_hist0 stores
 // every window's bucket id (`bids`, Nw u32, ~0 = not indexed), the radix passes carry (bucket
 // id u32, pos u32) and the last pass writes positions only (bout = nullptr); the bucket kernel
@@ -256,13 +260,13 @@ struct BucketStats {           // per-bucket partials of the build statistics
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, const uint32_t* n_ptr, uint32_t nw,
-                         const uint32_t* code = nullptr, int k = 0);
+                         const uint32_t* code = nullptr, int k = 0, bool aos = false);
 // ballot_ranks(): the current device fails the LDS lane-order self-check (or KMHG_TEST_BALLOT):
 // the radix passes and the bucket kernel then rank with ballots (kmhg_engine.cpp)
 bool ballot_ranks();
 void launch_lane_order_check(unsigned long long* res, hipStream_t s, int blocks = 1024);
 void launch_v2_test_disorder(uint32_t* pos, uint32_t* start, const uint32_t* n_ptr, int mode,
-                             hipStream_t s);
+                             hipStream_t s, uint32_t stride = 1);
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s);
 

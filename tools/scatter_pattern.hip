@@ -66,6 +66,56 @@ __global__ void __launch_bounds__(TB) k_pattern(const uint64_t* __restrict__ kin
   }
 }
 
+// Element layouts (round 5): LAY 1 = one packed 12-B element {key lo, key hi, pos} per index
+// (AoS, a run is one contiguous 12 c-byte piece instead of an 8 c- and a 4 c-byte piece in two
+// arrays); LAY 2 = one 8-B element per index (a key stream with the position folded in); LAY 3 =
+// 16-B elements {key, pos, pad}.
+template <int LAY>
+__global__ void __launch_bounds__(TB) k_layout(const uint64_t* __restrict__ kin,
+                                               const uint32_t* __restrict__ pin,
+                                               uint64_t* __restrict__ kout,
+                                               uint32_t* __restrict__ pout, uint32_t ntiles,
+                                               uint32_t R) {
+  (void)pout;
+  const uint32_t G = gridDim.x;
+  const uint32_t n_iter = (ntiles - blockIdx.x + G - 1) / G;
+  for (uint32_t it = 0; it < n_iter; ++it) {
+    const uint32_t t = xcd_remap(blockIdx.x + it * G, ntiles);
+    uint64_t k[PER];
+    uint32_t p[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint64_t e = (uint64_t)t * PT + j * TB + threadIdx.x;
+      if (LAY == 1) {
+        const uint3 v = reinterpret_cast<const uint3*>(kin)[e];
+        k[j] = ((uint64_t)v.y << 32) | v.x;
+        p[j] = v.z;
+      } else if (LAY == 3) {
+        const uint4 v = reinterpret_cast<const uint4*>(kin)[e];
+        k[j] = ((uint64_t)v.y << 32) | v.x;
+        p[j] = v.z;
+      } else {
+        k[j] = kin[e];
+        p[j] = 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t i = j * TB + threadIdx.x;
+      const uint32_t d = (uint32_t)(((uint64_t)i * R) / PT);
+      const uint32_t ts = (uint32_t)(((uint64_t)d * PT + R - 1) / R);
+      const uint32_t te = (uint32_t)(((uint64_t)(d + 1) * PT + R - 1) / R);
+      const uint64_t dst = (uint64_t)ntiles * ts + (uint64_t)t * (te - ts) + (i - ts);
+      if (LAY == 1)
+        reinterpret_cast<uint3*>(kout)[dst] = make_uint3((uint32_t)k[j], (uint32_t)(k[j] >> 32), p[j]);
+      else if (LAY == 3)
+        reinterpret_cast<uint4*>(kout)[dst] = make_uint4((uint32_t)k[j], (uint32_t)(k[j] >> 32), p[j], 0u);
+      else
+        kout[dst] = k[j] ^ p[j];
+    }
+  }
+}
+
 // Supertiles (round 4): workgroup w owns supertiles of S consecutive tiles and writes them one
 // tile after another; the histogram unit is the supertile, so digit d's runs of the S tiles are
 // adjacent in the output (one run of S * 2048 / R elements, written in S pieces by one
@@ -112,9 +162,9 @@ int main(int argc, char** argv) {
   const uint64_t n = (uint64_t)ntiles * PT;
   uint64_t *ka, *kb;
   uint32_t *pa, *pb;
-  CK(hipMalloc(&ka, n * 8)); CK(hipMalloc(&kb, n * 8));
+  CK(hipMalloc(&ka, n * 16)); CK(hipMalloc(&kb, n * 16));   // LAY 3: 16 B per element
   CK(hipMalloc(&pa, n * 4)); CK(hipMalloc(&pb, n * 4));
-  CK(hipMemset(ka, 1, n * 8)); CK(hipMemset(pa, 2, n * 4));
+  CK(hipMemset(ka, 1, n * 16)); CK(hipMemset(pa, 2, n * 4));
   int cus = 256, per = 1;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   hipEvent_t e0, e1;
@@ -138,6 +188,16 @@ int main(int argc, char** argv) {
                 bytes_per_elt);
     std::fflush(stdout);
   };
+  if (argc > 2 && std::string(argv[2]) == "layout") {
+    for (uint32_t R : {1u, 47u, 79u, 156u, 313u}) {
+      run((const void*)k_pattern<false, 0>, "SoA 8+4 (build)", R, 3, 24);
+      run((const void*)k_layout<1>, "AoS 12 packed", R, 3, 24);
+      run((const void*)k_layout<1>, "AoS 12 packed wg4", R, 4, 24);
+      run((const void*)k_layout<2>, "8-B elements", R, 3, 16);
+      run((const void*)k_layout<3>, "AoS 16", R, 3, 32);
+    }
+    return 0;
+  }
   const uint32_t Rs[] = {1, 47, 156, 313};
   for (int wpc : {1, 2, 3})
     for (uint32_t R : Rs) {
