@@ -572,7 +572,8 @@ __device__ __forceinline__ uint64_t block_excl_scan_n(uint64_t v, uint64_t* lds,
 // 4 B out of the last.
 // 3 = packed (key, pos) elements, 12 B each in kin / kout ({key lo, key hi, pos}; pin / pout
 // unused): a tile's digit run leaves as ONE contiguous piece instead of an 8 c-byte piece of
-// keys and a 4 c-byte piece of positions in two arrays.  Write-pattern probe
+// keys and a 4 c-byte piece of positions in two arrays; 4 = (key, pos) arrays in, packed out
+// (the last pass of a build whose earlier streams stay unpacked for their histogram passes).  Write-pattern probe
 // (tools/scatter_pattern.hip layout, profiles/r5a_scatter_layout.txt, 100 M elements): radix 313
 // 1.09 -> 0.87 ms, radix 79 0.72 -> 0.61 ms.
 // BALLOT: stable ranks from one ballot per digit bit instead of the count atomics' lane-ordered
@@ -586,7 +587,8 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad,
              int skip_empty, BoundsFuse bf) {
   constexpr bool BIDS = BM == 1 || BM == 2;      // bucket-id streams
-  constexpr bool AOS = BM == 3;                   // packed 12-B (key, pos) elements
+  constexpr bool AOS = BM == 3 || BM == 4;        // packed 12-B (key, pos) elements out
+  constexpr bool AIN = BM == 3;                   // ... and in
   using KT = typename std::conditional<BIDS, uint32_t, uint64_t>::type;
   using SL = ScatterLDS<KT>;
   static_assert(BM == 0 || !NOPOS, "bucket-id and packed streams carry positions");
@@ -638,7 +640,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         const uint64_t e = t0 + wbase + (uint32_t)cc * 64 + lane;
         if (KEYS0) {
           nkey[cc] = kinT[e < n ? e : n - 1];    // positions implicit: e + 1 (below)
-        } else if (AOS) {
+        } else if (AIN) {
           const uint3 v = reinterpret_cast<const uint3*>(kin)[e];
           nkey[cc] = ((uint64_t)v.y << 32) | v.x;
           npos[cc] = v.z;
@@ -1203,6 +1205,15 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   STAMP_WG(b, 4);
   // the bucket's sub-table, coalesced 16-B slots, counts from the registers of the slot's owner
   Slot* Tb = T + (uint64_t)b * V2_CAPW;
+#ifdef KMHG_EXP_SLOT8
+  // EXPERIMENT ONLY (timing variant, wrong tables): the write-out of 8-B {count, aux} slots
+  uint2* T8 = reinterpret_cast<uint2*>(T) + (uint64_t)b * V2_CAPW;
+#pragma unroll
+  for (uint32_t q = 0; q < SPT; ++q) {
+    const uint32_t j = q * TB + threadIdx.x;
+    if (j < V2_CAPW) T8[j] = make_uint2(cnt[q], COUNT_ONLY ? 0u : (W.val[j] & ~VAL_MULTI));
+  }
+#else
 #pragma unroll
   for (uint32_t q = 0; q < SPT; ++q) {
     const uint32_t j = q * TB + threadIdx.x;
@@ -1212,6 +1223,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
       *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), cnt[q], aux);
     }
   }
+#endif
   if (threadIdx.x == 0 && side_bucket(b, g)) {
     const uint2 c = make_uint2(cnt[V2_CAPW / TB], COUNT_ONLY ? 0u : (W.val[V2_CAPW] & ~VAL_MULTI));
     *reinterpret_cast<uint4*>(&T[side_slot(g)]) = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, c.x, c.y);
@@ -1474,9 +1486,12 @@ void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint3
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                        uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf,
-                       bool aos) {
-  if (aos)
+                       bool aos, bool aos_in) {
+  if (aos && aos_in)
     KMHG_SCATTER_BM(false, false, false, 3, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr,
+                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
+  else if (aos)
+    KMHG_SCATTER_BM(false, false, false, 4, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin,
                     n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
   else
     KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,

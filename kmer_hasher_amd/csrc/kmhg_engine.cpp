@@ -28,6 +28,26 @@
 #include "kmhg_fastx.h"
 #include "kmhg_khash.h"
 #include "kmhg_sh.h"
+
+// Environment knobs.  Product: KMHG_TIMING (per-kernel events), KMHG_DEVICES (multi-device
+// query), KMHG_ROW_ORDER, KMHG_D2H_THREADS.  Path selectors the GPU suite uses to force each
+// build / query / counts path against the oracle (KMHG_BUILD, KMHG_BUILD_BID, KMHG_MAXR,
+// KMHG_FUSE_BOUNDS, KMHG_TEST_BALLOT, KMHG_QUERY_TAGS, KMHG_QUERY_DIAG, KMHG_DIAG_CODES,
+// KMHG_COUNT_TABLE, KMHG_COUNT_WALK, KMHG_CO_SPREAD, KMHG_CO_GLOBAL, KMHG_PART_COMPACT,
+// KMHG_SLICE_POISON, KMHG_TEST_REPLICA) choose between equivalent paths and change no result.
+// Fault injection (KMHG_TEST_DISORDER) and the A/B-only switches (KMHG_D2H, KMHG_COUNT_BID,
+// KMHG_RK_CAP) exist only in the test build (-DKMHG_TEST_BUILD: libkmhgpu_test.so, make test):
+// the product library never reads them.
+namespace kmhg {
+inline const char* test_build_knob(const char* name) {
+#ifdef KMHG_TEST_BUILD
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+}  // namespace kmhg
 #include "../../include/kmhgpu.h"
 
 using namespace kmhg;
@@ -502,7 +522,7 @@ static PinStage& pin_stage() {           // the device's two pinned D2H_CHUNK bu
 void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (!bytes) return;
   static const bool staged = [] {
-    const char* e = std::getenv("KMHG_D2H");          // A/B knob: "direct" = one hipMemcpy
+    const char* e = test_build_knob("KMHG_D2H");      // A/B knob: "direct" = one hipMemcpy
     return !(e && std::string(e) == "direct");
   }();
   if (!staged || bytes < D2H_STAGE_MIN) {
@@ -755,6 +775,14 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   return idx.release();
 }
 
+// Bucket-id radix streams (position builds that keep their code words) up to this many windows
+// (build_device_v2); KMHG_BUILD_BID=0 / 1 forces key / bucket-id streams.
+constexpr int64_t BID_MAX_WINDOWS = 12 << 20;
+bool bid_streams_for(int64_t Nw) {
+  const char* bide = std::getenv("KMHG_BUILD_BID");
+  return bide ? bide[0] == '1' : Nw <= BID_MAX_WINDOWS;
+}
+
 constexpr double CO_FILL = 0.6;                  // target mean occupancy of a count-only bucket
 
 // Stream entries per group bucket (in units of V2_BW_WG) for a batch of `total` keys with
@@ -874,10 +902,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // line per window beyond.  Measured (A/B in one run): config 2 (10 M windows, 2.5 MB of code)
   // 30.1 -> 31.1 Gbp/s; config 3 (100 M, 25 MB) 28.5 -> 24.0 (bucket kernel 0.84 -> 2.0 ms).
   // So on up to BID_MAX_WINDOWS; KMHG_BUILD_BID=0 / 1 forces key / bucket-id streams.
-  constexpr int64_t BID_MAX_WINDOWS = 12 << 20;
-  const char* bide = std::getenv("KMHG_BUILD_BID");
-  const bool bid_on = bide ? bide[0] == '1' : Nw <= BID_MAX_WINDOWS;
-  const bool bid = codes && !from_keys && !count_only && bid_on;
+  const bool bid = codes && !from_keys && !count_only && bid_streams_for(Nw);
   // position builds on key streams carry packed 12-B (key, pos) elements: a tile's digit run is
   // one contiguous write instead of a key piece and a position piece in two arrays
   // (tools/scatter_pattern.hip layout, profiles/r5a_scatter_layout.txt: radix 313 1.09 -> 0.87
@@ -887,6 +912,17 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 #else
   const bool aos = !from_keys && !count_only && !bid;
 #endif
+  // Which streams are packed (stream p = pass p's output; -1 = a part build's dense stream):
+  // the last one, which only the bucket kernel reads, always; an earlier one only at a radix
+  // where the scatter's saving beats the 4 more bytes per element its histogram pass then reads.
+  // Measured: config 3 (2 passes, radix 313) every stream packed 3.49 -> 3.21 ms per build
+  // (scatters 0.94 + 1.03 -> 0.75 + 0.91 ms, histogram 0.27 -> 0.36); the 500 Mbp build (3
+  // passes, radix 79) 18.2 -> 18.6 ms (histograms 1.9 -> 2.8 ms, scatters 11.2 -> 10.3), A/B
+  // in one run (profiles/r5b_ab_aos_config3.log, r5c_ab_aos_config5.log).
+  constexpr uint32_t AOS_MIN_RADIX = 160;
+  auto packed = [&](int p) { return aos && (p + 1 == (int)passes || R >= AOS_MIN_RADIX); };
+  bool any_unpacked = !aos;
+  for (int p = -1; p + 1 < (int)passes; ++p) any_unpacked |= !packed(p);
   const uint64_t kwords = bid ? 1 : aos ? ((uint64_t)(Nw + PTILE) * 3 + 1) / 2 : (uint64_t)(Nw + PTILE);
   DBuf<uint64_t> kA(kwords, s), kB(kwords, s);   // + pad
   // (Removed in round 4 after measurement, DESIGN.md §5: radix passes writing whole 128-B lines
@@ -900,8 +936,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const bool no_pos = count_only;                        // keys only through the passes
   // (a part build's compacted windows land in kB / pB before they are packed: pB stays)
   const bool partc_pos = !from_keys && n_parts >= 2 && codes;
-  DBuf<uint32_t> pA(no_pos || aos ? 1 : Nw + PTILE, s),
-      pB(no_pos || (aos && !partc_pos) ? 1 : Nw + PTILE, s);
+  DBuf<uint32_t> pA(no_pos || !any_unpacked ? 1 : Nw + PTILE, s),
+      pB(no_pos || (!any_unpacked && !partc_pos) ? 1 : Nw + PTILE, s);
   const uint32_t pad = (uint32_t)Nw;
   DBuf<uint32_t> hist(nhist, s);
   DBuf<uint32_t> start((uint64_t)nb + 1, s);
@@ -973,7 +1009,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       else
         LAUNCH("k_v2_scatter_seq", s,
                launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
-                                     pA.p, pad, s, aos));
+                                     pA.p, pad, s, packed(0)));
       div = R;
     }
   }
@@ -1003,7 +1039,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   }
   if (partc)   // the part's windows, dense in window order: every radix pass reads these
     LAUNCH("k_part_dense", s, launch_part_dense(kB.p, pB.p, tcnt.p, ntiles, n_valid, kA.p, pA.p,
-                                                s, aos));
+                                                s, packed(-1)));
   // where pass 1 saves column 0: pass 0's histogram is hp's unless pass 0 was the one over
   // every window (its own layout, copied above)
   uint32_t* save1 = hp == hist.p || partc ? lo_save.p : nullptr;
@@ -1019,7 +1055,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const uint32_t* lin = p == 1 ? lo_save.p : ((p - 1) % 2 ? lvA.p : lvB.p);
     uint32_t* lout = last ? start.p : (p % 2 ? lvA.p : lvB.p);
     return BoundsFuse{reinterpret_cast<const uint64_t*>(kprev), lin, lout,
-                      make_digit((uint32_t)dv, R), (uint32_t)dv, spread, is_bid ? 1 : aos ? 2 : 0,
+                      make_digit((uint32_t)dv, R), (uint32_t)dv, spread,
+                      is_bid ? 1 : packed((int)p - 1) ? 2 : 0,
                       last ? g.nb : (uint32_t)(dv * R)};
   };
   auto fused = [&](uint32_t p) { return p >= 1 && fuse_on && !(co_auto && p + 1 == passes); };
@@ -1056,7 +1093,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
            launch_v2_hist(src, n_valid, g, Dp, hp, C, status, nst, s,
                           hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
                           p == 1 ? save1 : nullptr, keys0 && skip_empty,
-                          /*padded=*/!keys0, aos));
+                          /*padded=*/!keys0, !keys0 && packed((int)p - 1)));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hp, nh, status, n_valid, s));
     if (hll) {   // after the scan: the estimate travels with the valid key count
       LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ntiles, hll_regs.p,
@@ -1077,7 +1114,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       else
         LAUNCH("k_v2_scatter", s,
                launch_v2_scatter(kin, pin, n_valid, g, Dp, hp, C, kout, pout, pad, s,
-                                 fused(p) ? &lv : nullptr, aos));
+                                 fused(p) ? &lv : nullptr, packed((int)p), packed((int)p - 1)));
       if (p >= 1 && !fused(p) && !last) launch_level(lv);
     }
     std::swap(kin, kout);
@@ -1115,7 +1152,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 #endif
   // tests only: a corrupted stream or bound (KMHG_TEST_DISORDER=1|2|3) -> the bucket kernel's
   // checks -> v1 rebuild
-  if (const char* td = std::getenv("KMHG_TEST_DISORDER"))
+  if (const char* td = test_build_knob("KMHG_TEST_DISORDER"))
     if (!no_pos && td[0] >= '1' && td[0] <= '3')
       launch_v2_test_disorder(aos ? reinterpret_cast<uint32_t*>(kin) + 2 : pin, start.p, n_valid,
                               td[0] - '0', s, aos ? 3u : 1u);
@@ -1150,20 +1187,27 @@ bool tags_on() {
 // KMHG_TEST_BALLOT=1 (tests) forces them.
 static std::atomic<int> g_lane_state[64];          // 0 unchecked, 1 lane order holds, 2 ballots
 static std::mutex g_lane_mu;
+// The check's stream and result buffer are made once per device and kept: no hipFree (which
+// waits for the whole device, stalling work other streams have in flight) and only the check's
+// own stream is synchronized.
 static void lane_order_run(int blocks, uint64_t* bad, uint64_t* checked) {
-  hipStream_t st = nullptr;
-  HIPC(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  unsigned long long* res = nullptr;
-  hipError_t e = hipMalloc(&res, 2 * sizeof(unsigned long long));
+  struct Probe {
+    hipStream_t st = nullptr;
+    unsigned long long* res = nullptr;
+  };
+  static Probe probes[64];                         // under g_lane_mu (callers hold it)
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  Probe& pr = probes[(unsigned)dev % 64];
+  if (!pr.st) HIPC(hipStreamCreateWithFlags(&pr.st, hipStreamNonBlocking));
+  if (!pr.res) HIPC(hipMalloc(&pr.res, 2 * sizeof(unsigned long long)));
   unsigned long long h[2] = {0, 0};
-  if (e == hipSuccess) e = hipMemsetAsync(res, 0, sizeof(h), st);
+  hipError_t e = hipMemsetAsync(pr.res, 0, sizeof(h), pr.st);
   if (e == hipSuccess) {
-    launch_lane_order_check(res, st, blocks);
-    e = hipMemcpyAsync(h, res, sizeof(h), hipMemcpyDeviceToHost, st);
+    launch_lane_order_check(pr.res, pr.st, blocks);
+    e = hipMemcpyAsync(h, pr.res, sizeof(h), hipMemcpyDeviceToHost, pr.st);
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (res) (void)hipFree(res);
-  (void)hipStreamDestroy(st);
+  if (e == hipSuccess) e = hipStreamSynchronize(pr.st);
   hip_check(e, "LDS lane-order check");
   *bad = h[0];
   *checked = h[1];
@@ -1488,9 +1532,12 @@ void count_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, uint32_t sou
   const int k = idx->k;
   if (L <= k) return;
   // the batch keeps its code words only to be eligible for bucket-id radix streams (<= 12 M
-  // windows); KMHG_COUNT_BID=0 (A/B) builds it with key streams
-  const char* cbe = std::getenv("KMHG_COUNT_BID");
-  std::unique_ptr<kmhg_index> B(build_device(d_seq, L, k, s, !(cbe && cbe[0] == '0')));
+  // windows): a larger batch builds on key streams without them (no code block
+  // allocated or written for a batch that is discarded after the merge); KMHG_COUNT_BID=0 (A/B)
+  // builds every batch with key streams
+  const char* cbe = test_build_knob("KMHG_COUNT_BID");
+  const bool codes = !(cbe && cbe[0] == '0') && bid_streams_for(L - k + 1);
+  std::unique_ptr<kmhg_index> B(build_device(d_seq, L, k, s, codes));
   Release rel{B.get(), s};
   finish_build(B.get());
   B->stream = s;
@@ -1709,7 +1756,8 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   HIPC(hipStreamSynchronize(s));
   const uint32_t span = (uint32_t)__atomic_load_n(&hr.meta->n_pairs, __ATOMIC_ACQUIRE);
   const uint32_t total = __atomic_load_n(&hr.meta->max_count, __ATOMIC_ACQUIRE);
-  const uint32_t cap = read_kmers_cap_span(span);
+  const char* rkc = test_build_knob("KMHG_RK_CAP");   // A/B knob: LDS bytes per stream (16: global)
+  const uint32_t cap = rkc ? (((uint32_t)std::atoi(rkc) + 15) & ~15u) : read_kmers_cap_span(span);
   (void)mean_len;
   if (!total) return;
   DBuf<uint64_t> keys(total, s);

@@ -233,10 +233,10 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s, const BoundsFuse* bf = nullptr,
-                       bool aos = false);
+                       bool aos = false, bool aos_in = true);
 // Packed key streams (aos): position builds on key streams carry each window as ONE 12-B
-// element {key lo, key hi, pos} (kin / kout hold n + PTILE of them; pin / pout unused), so a
-// tile's digit run is one contiguous write.
+// element {key lo, key hi, pos} (kout holds n + PTILE of them; pout unused), so a tile's digit
+// run is one contiguous write; aos_in: the input is packed too (else kin / pin arrays).
 // Bucket-id streams (position builds that keep the sequence's code words): V_hist0 stores
 // every window's bucket id (`bids`, Nw u32, ~0 = not indexed), the radix passes carry (bucket
 // id u32, pos u32) and the last pass writes positions only (bout = nullptr); the bucket kernel

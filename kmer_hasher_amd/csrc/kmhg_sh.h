@@ -28,8 +28,6 @@ void launch_rk_span(const int64_t* off, uint32_t n_reads, uint32_t* span, hipStr
 // LDS bytes per staged stream: the measured span, capped (a workgroup whose reads do not fit
 // walks them from global memory)
 inline uint32_t read_kmers_cap_span(uint32_t span) {
-  if (const char* e = std::getenv("KMHG_RK_CAP"))   // A/B knob: LDS bytes per stream (16: global)
-    return ((uint32_t)std::atoi(e) + 15) & ~15u;
   uint32_t c = span < 1024 ? 1024 : span;
   if (c > 28672) c = 28672;
   return (c + 15) & ~15u;

@@ -119,7 +119,7 @@ class DeviceIndex:
             _lib.check(_lib.lib().kmhg_query_run_device(self._h, C.c_void_p(seq.data_ptr()),
                                                         seq.numel(), k, _stream_ptr(stream),
                                                         C.byref(q), C.byref(h)))
-        return DeviceQuery(q.value, h.value)
+        return DeviceQuery(q.value, h.value, seq.device)
 
     def query_range(self, seq: torch.Tensor, k: int, w0: int, w1: int, stream=None) -> "DeviceQuery":
         """Windows [w0, w1) of `seq` (the multi-GPU shard unit, see dist.py)."""
@@ -130,7 +130,7 @@ class DeviceIndex:
             _lib.check(_lib.lib().kmhg_query_run_device_range(
                 self._h, C.c_void_p(seq.data_ptr()), seq.numel(), k, w0, w1, _stream_ptr(stream),
                 C.byref(q), C.byref(h)))
-        return DeviceQuery(q.value, h.value)
+        return DeviceQuery(q.value, h.value, seq.device)
 
     def positions(self, opt: int, stream=None) -> dict:
         """kmer.pos into device tensors: {'kmer': uint8 (U, k+1), 'pos': int32 (N, 2),
@@ -227,9 +227,13 @@ class DevicePart(DeviceIndex):
 
 
 class DeviceQuery:
-    def __init__(self, handle: int, n_rows: int):
+    def __init__(self, handle: int, n_rows: int, device: torch.device | None = None):
         self._h = C.c_void_p(handle)
         self.n_rows = n_rows
+        # the device the query ran on (the query sequence's): rows_view of an empty result lands
+        # there too, like a non-empty one
+        self.device = device if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
 
     def copy_to(self, dst: torch.Tensor, stream=None) -> torch.Tensor:
         """Copy the (H, 2) int32 rows into `dst` (device, >= 2*H int32)."""
@@ -253,8 +257,7 @@ class DeviceQuery:
         (stream-ordered on the query's stream) when the last tensor using it is gone.  Used on
         the query's stream, as every result of the library is."""
         if not self.n_rows:
-            return torch.empty((0, 2), dtype=torch.int32,
-                               device=torch.device("cuda", torch.cuda.current_device()))
+            return torch.empty((0, 2), dtype=torch.int32, device=self.device)
         d = C.c_void_p()
         _lib.check(_lib.lib().kmhg_query_rows_device(self._h, C.byref(d)))
         return torch.as_tensor(_RowsBuffer(self, d.value))   # on the rows' own device

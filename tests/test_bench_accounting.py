@@ -62,3 +62,23 @@ def test_build_roofline_fields():
     assert r["frac_of_step"] == pytest.approx(B / 0.245e-3 / 1e9 / bench.HBM_PEAK_GBS, abs=1e-4)
     assert r["traffic"] == 3000 and r["traffic_step"] == 3000
     assert r["traffic_step_over_B"] == pytest.approx(3000 / B, abs=1e-3)
+
+
+def test_traffic_frac_prices_the_bytes_moved():
+    """traffic_frac = the PMC bytes of every kernel of the step over their summed device time /
+    peak (round 5): next to §8(d)'s frac, it tells work avoided from HBM efficiency.  The query
+    roofline carries no kernel_model (the diagonal path avoids most of the modelled bytes)."""
+    B = bench.survey_bytes("build", L=10_000_000, U=9_999_970, N=9_999_970)
+    big = {"k_v2_bucket_wg<false, true, false>": {"hbm_bytes_per_launch": 350_000_000}}
+    r = bench.roofline(B, "k_v2_bucket_wg", 0.11, 0.245, big, None, {"k_v2_bucket_wg": 1},
+                       device_ms=0.25)
+    assert r["traffic_frac"] == round(350e6 / 0.25e-3 / 1e9 / bench.HBM_PEAK_GBS, 4)
+    assert r["device_ms"] == pytest.approx(0.25)
+    assert "traffic_frac" not in bench.roofline(B, "k_v2_bucket_wg", 0.11, 0.245, PMC, None,
+                                                {"k_v2_bucket_wg": 1})
+    qper = {"k_query_probe": 0.035, "k_scan_tiles_u64": 0.006, "k_query_emit": 0.024}
+    qpmc = {k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"] * 100_000}
+            for k, v in PMC.items()}
+    q = bench.query_roofline(qper, 10_000_000, 9_999_970, 9_999_970, qpmc, step_ms=0.078)
+    assert "kernel_model" not in q
+    assert q["traffic_frac"] == round((500 + 1200 + 40 + 5) * 1e5 / 0.065e-3 / 1e9 / 8000, 4)

@@ -23,6 +23,23 @@ def test_library_loads_and_exports_header_symbols():
     assert set(declared) <= exported
 
 
+def test_product_library_reads_no_test_only_knob():
+    """Fault injection and the A/B-only switches exist only in libkmhgpu_test.so (built from the
+    same objects with the orchestrator compiled -DKMHG_TEST_BUILD): the product library does not
+    even hold their names; the test build exports the same C-ABI."""
+    import os
+    test_lib = os.path.join(os.path.dirname(_lib.LIB_PATH), "libkmhgpu_test.so")
+    prod = open(os.path.join(os.path.dirname(_lib.LIB_PATH), "libkmhgpu.so"), "rb").read()
+    test = open(test_lib, "rb").read()
+    for knob in (b"KMHG_TEST_DISORDER", b"KMHG_COUNT_BID", b"KMHG_RK_CAP", b"KMHG_D2H\0"):
+        assert knob not in prod, knob
+        assert knob in test, knob
+    out = subprocess.run(["nm", "-D", "--defined-only", test_lib], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert set(_lib.header_symbols()) <= exported
+
+
 def test_lib_is_gfx950_code_object():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob     # the .hip_fatbin holds a gfx950 object

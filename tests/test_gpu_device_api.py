@@ -69,6 +69,10 @@ def test_rows_view_owns_its_query(gpu):
     empty = DeviceIndex.build(t[:1000], 31)
     z = empty.query(torch.full((500,), ord("N"), dtype=torch.uint8, device=t.device), 31)
     assert z.n_rows == 0 and z.rows_view().shape == (0, 2)
+    assert z.device == t.device and z.rows_view().device == t.device   # empty rows: same device
+    # ... also when the current device is another one than the query's
+    with torch.cuda.device(t.device):
+        assert z.rows_view().device == t.device
 
 
 def test_image_export_import_roundtrip(gpu):

@@ -146,3 +146,70 @@ def test_owner_computes_build_and_broadcast_query(gpu, world, k, kq):
     assert (nk, npos, npair) == (oi.U, oi.N, oi.P)
     assert got == want
     assert phases == ["broadcast", "gather", "query"]
+
+
+def _nccl_worker(port, seq_bytes, k, kq, out_q):
+    """World size 1 over RCCL (backend "nccl"): every collective of the N > 1 path runs on the
+    real backend with device tensors -- the sequence broadcast (C1), the owner-computes part build
+    and its all-gather assembly, the index image broadcast, the sharded query's count all-gather
+    and row gather -- so an RCCL-only constraint surfaces on the one-GPU box, not first on the
+    driver's 8-GPU node."""
+    import torch
+    import torch.distributed as dist
+    from kmer_hasher_amd import dist as kd
+    from kmer_hasher_amd.device import DeviceIndex
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()).to(dev)
+        part, _ = kd.owner_build(seq, k, dev, src=0)
+        idx = kd.assemble_parts(part, dev)
+        part.free()
+        idx = kd.broadcast_index(idx, dev, src=0)
+        info = idx.info()
+        timings = {}
+        rows = kd.sharded_query(kd.HipQueryEngine(idx), seq, kq, dst=0, src=0, timings=timings)
+        torch.cuda.synchronize()
+        # the receiving side of an image broadcast: import the exported image
+        meta, bufs = idx.export_image()
+        torch.cuda.synchronize()
+        rep = DeviceIndex.import_image(meta.cpu(), bufs)
+        rows2 = kd.sharded_query(kd.HipQueryEngine(rep), seq, kq, dst=0)
+        torch.cuda.synchronize()
+        out_q.put(((info["n_kmers"], info["n_positions"], info["n_pairs"]),
+                   rows.cpu().numpy().reshape(-1).tolist(),
+                   rows2.cpu().numpy().reshape(-1).tolist(), sorted(timings),
+                   dist.get_backend(), str(rows.device)))
+        rep.free()
+        idx.free()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k,kq", [(31, 31), (21, 17)])
+def test_nccl_world1_owner_build_assemble_sharded_query(gpu, k, kq):
+    import torch.multiprocessing as mp
+    from kmer_hasher_amd import synth
+    from oracle import oracle as O
+    s = synth.add_n_runs(synth.repeat_rich(150_000, 9, n_gap_every=10_007), 0.004, 8)
+    s[-k - 2] = ord("N")
+    seq_bytes = s.tobytes()
+    oi = O.OracleIndex(seq_bytes, k)
+    want = oi.query(seq_bytes, kq).tolist()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), seq_bytes, k, kq, q))
+    p.start()
+    try:
+        (nk, npos, npair), got, got2, phases, backend, where = q.get(timeout=100)
+        p.join(60)
+        assert p.exitcode == 0
+    finally:
+        if p.is_alive():
+            p.kill()
+    assert backend == "nccl" and where == "cuda:0"
+    assert (nk, npos, npair) == (oi.U, oi.N, oi.P)
+    assert got == want and got2 == want
+    assert phases == ["broadcast", "gather", "query"]
