@@ -364,12 +364,7 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
 // latency (config 2: 14.5 us for 40 MB).  `in` holds n + PTILE elements (the passes' padded
 // streams), so whole-tile loads stay inside it.
 // MODE: 0 = u64 keys, 1 = u32 bucket ids, 2 = packed 12-B {key lo, key hi, pos} elements (the
-// position builds' key streams: 96 B = six 16-B loads per thread and tile).
-template <int MODE>
-__device__ __forceinline__ uint32_t word_of(const uint4* v, int i) {   // i: compile-time after unroll
-  const uint4 w = v[i >> 2];
-  return (i & 3) == 0 ? w.x : (i & 3) == 1 ? w.y : (i & 3) == 2 ? w.z : w.w;
-}
+// position builds' key streams).
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
@@ -388,11 +383,45 @@ k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, 
     for (uint32_t d = threadIdx.x; d < R; d += BLOCK) save_col0[d] = hist[(size_t)d * ntiles];
   for (uint32_t d = threadIdx.x; d < R; d += BLOCK) lh[d] = 0;
   constexpr bool BID = MODE == 1;
-  constexpr int NV = MODE == 1 ? 2 : MODE == 2 ? 6 : 4;   // 16-B loads per thread per tile
+  if constexpr (MODE == 2) {
+    // packed 12-B elements: thread t takes elements t + 256 j of the tile (j < 8), so every
+    // load instruction reads 768 contiguous bytes per wave (one element per lane, dwordx3); a
+    // thread's 96 consecutive bytes would spread each instruction over 48 lines
+    uint3 nx[8];
+    auto prefetch = [&](uint32_t tile) {
+      const uint3* src = reinterpret_cast<const uint3*>(in) + (uint64_t)tile * PTILE + threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) nx[j] = src[j * BLOCK];
+    };
+    prefetch(tile_at(0));
+    for (uint32_t it = 0; it < n_iter; ++it) {
+      const uint32_t tile = tile_at(it);
+      uint3 cur[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cur[j] = nx[j];
+      if (it + 1 < n_iter) prefetch(tile_at(it + 1));
+      __syncthreads();                                 // lh zeroed (previous tile written out)
+      const uint64_t e0 = (uint64_t)tile * PTILE + threadIdx.x;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (e0 + (uint64_t)j * BLOCK < n) {
+          const uint64_t key = ((uint64_t)cur[j].y << 32) | cur[j].x;
+          atomicAdd(&lh[digit_of_h(mix64(key), g, D)], 1u);
+        }
+      }
+      __syncthreads();
+      for (uint32_t d = threadIdx.x; d < R; d += BLOCK) {
+        hist[(size_t)d * ntiles + tile] = lh[d];
+        lh[d] = 0;
+      }
+    }
+    return;
+  }
+  constexpr int NV = MODE == 1 ? 2 : 4;                // 16-B loads per thread per tile
   uint4 nx[NV];
   auto prefetch = [&](uint32_t tile) {
     const uint4* src = reinterpret_cast<const uint4*>(in) +
-                       ((uint64_t)tile * PTILE + 8u * threadIdx.x) * (uint64_t)(NV * 2) / 16;
+                       ((uint64_t)tile * PTILE + 8u * threadIdx.x) / (BID ? 4 : 2);
 #pragma unroll
     for (int v = 0; v < NV; ++v) nx[v] = src[v];
   };
@@ -413,9 +442,6 @@ k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, 
           const uint4 w = cur[j >> 2];
           const uint32_t id = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
           dg = digit_of_b(id, D);
-        } else if (MODE == 2) {
-          const uint64_t key = ((uint64_t)word_of<MODE>(cur, 3 * j + 1) << 32) | word_of<MODE>(cur, 3 * j);
-          dg = digit_of_h(mix64(key), g, D);
         } else {
           const uint4 w = cur[j >> 1];
           const uint64_t key = (j & 1) ? (((uint64_t)w.w << 32) | w.z) : (((uint64_t)w.y << 32) | w.x);

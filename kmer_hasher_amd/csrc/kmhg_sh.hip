@@ -284,6 +284,8 @@ __device__ __forceinline__ void depth_write(const Slot* __restrict__ T, Geom g, 
                                             const int32_t* __restrict__ M, uint64_t key,
                                             int32_t* __restrict__ out, int64_t w) {
   uint32_t c = 0, aux = 0;
+  // (round 5, A/B in one run: four slots per round trip, table_find4, 0.385 -> 0.443 ms at
+  // config 2 -- profiles/r5g_ab_depth.log)
   const uint32_t slot = table_find(T, g, key, c, aux);
   int32_t* o = out + w * S;
   if (slot == NONE) {
