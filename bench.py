@@ -1364,7 +1364,9 @@ def bench_sharded_query(args, cfg, dev, world, rank):
         D.timing_select(None)
         D.timing_reset()
         D.DeviceIndex.build(ta, k).wait().free()
-        bper = {n: v[1] for n, v in D.timing_report().items() if v[0]}
+        _bt = D.timing_report()
+        bper = {n: v[1] for n, v in _bt.items() if v[0]}
+        blaunch = {n: v[0] for n, v in _bt.items() if v[0]}
         D.timing_enable(False)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -1383,17 +1385,16 @@ def bench_sharded_query(args, cfg, dev, world, rank):
                      "kernel_ms_sum": round(sum(bper.values()), 4),
                      "roofline": roofline(survey_bytes("build", L=L, U=binfo["n_kmers"],
                                                        N=binfo["n_positions"]),
-                                          bdom, bper[bdom], tb5 * 1e3, {}),
+                                          bdom, bper[bdom] / blaunch[bdom], tb5 * 1e3,
+                                          _load_pmc(5), None, blaunch,
+                                          device_ms=sum(bper.values())),
                      "build_path": {"build": binfo["build"], "fallback": binfo["fallback"]},
                      "note": "make.kmer.hash of A alone (500 Mbp, k=31), each build waited for "
                              "and freed; kernels_ms from HIP events of one build"}
     if rank == 0:
         per = {n: v[1] / v[0] for n, v in kt.items() if v[0]}
         launches = {n: v[0] / args.steps for n, v in kt.items() if v[0]}
-        dom = max(per, key=per.get)
         Nw_rank = (L - k + 1) // world
-        ab = algorithmic_bytes(dom, L // world, Nw_rank, 0, 0, H // world)
-        B_rank = survey_bytes("query", L=L // world, Nq=Nw_rank, H=H // world)
         cpu = cpu_query_baseline(*cpu_sample, k) if cpu_sample else None
         _emit({"metric": "seq.kmer.pos query Mbp/s (config 5, sharded)",
                "value": round(L / 1e6 * args.steps / t, 2), "unit": "Mbp/s", "n_gpus": world,
@@ -1410,8 +1411,8 @@ def bench_sharded_query(args, cfg, dev, world, rank):
                                         "row_gather": round(p_g * 1e3, 3),
                                         "note": "separate synchronized steps, max over ranks"},
                           "parallelism": f"shard{world}"},
-               "roofline": roofline(B_rank, dom, per[dom], t / args.steps * 1e3, _load_pmc(5),
-                                    ab, launches),
+               "roofline": query_roofline(per, L // world, Nw_rank, H // world, _load_pmc(5),
+                                          t / args.steps * 1e3, launches),
                "cpu_baseline": cpu,
                "index_build": build_rec,
                "kernels_ms": {n: round(v, 4) for n, v in per.items()}})

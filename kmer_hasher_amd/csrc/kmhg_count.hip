@@ -27,6 +27,7 @@
 // kmer.pos and seq.kmer.pos read a counts index with the position index's kernels -- the
 // reference's kmer_positions / sequence_kmer_positions equally read count vectors as positions.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 #include "kmhg_common.h"
 #include "kmhg_device.h"
 #include "kmhg_kernels.h"
@@ -366,6 +367,28 @@ void launch_rows_order(const uint32_t* F, int64_t n, uint64_t* status, uint32_t*
                        uint32_t* rorder, hipStream_t s) {
   const unsigned nt = (unsigned)(((uint64_t)n + TILE - 1) / TILE);
   hipLaunchKernelGGL(k_rows_order, dim3(nt), dim3(BLOCK), 0, s, F, n, status, ticket, rorder);
+}
+// The O(U) way to the same rorder (advisor round 4: F takes 4 B per character ever counted
+// into the pointer): the U (order key, row) pairs sorted by order key with rocPRIM's radix sort
+// (hipcub), over the key's `bits` low bits.  Rows are distinct and their order keys too, so the
+// result is the permutation k_rows_order compacts out of F.
+static __global__ void __launch_bounds__(BLOCK) k_iota_u32(uint32_t* __restrict__ a, uint32_t n) {
+  const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
+  if (r < n) a[r] = r;
+}
+size_t rows_sort_temp_bytes(uint32_t U, int bits) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint64_t*)nullptr,
+                                           (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)U, 0, bits);
+  return bytes;
+}
+void launch_rows_sort(const uint64_t* rord, uint32_t U, int bits, uint64_t* keys_out,
+                      uint32_t* rows_in, uint32_t* rorder, void* temp, size_t temp_bytes,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_iota_u32, dim3(grid_of(U)), dim3(BLOCK), 0, s, rows_in, U);
+  (void)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, rord, keys_out, rows_in, rorder,
+                                           (int)U, 0, bits, s);
 }
 void launch_rows_gather(const uint32_t* rorder, const uint64_t* ckeys, const int32_t* M,
                         uint32_t U, uint32_t S, uint64_t* okeys, int32_t* oM, hipStream_t s) {

@@ -34,7 +34,8 @@
 // build / query / counts path against the oracle (KMHG_BUILD, KMHG_BUILD_BID, KMHG_MAXR,
 // KMHG_FUSE_BOUNDS, KMHG_TEST_BALLOT, KMHG_QUERY_TAGS, KMHG_QUERY_DIAG, KMHG_DIAG_CODES,
 // KMHG_COUNT_TABLE, KMHG_COUNT_WALK, KMHG_CO_SPREAD, KMHG_CO_GLOBAL, KMHG_PART_COMPACT,
-// KMHG_SLICE_POISON, KMHG_TEST_REPLICA) choose between equivalent paths and change no result.
+// KMHG_ROW_ORDER_SORT, KMHG_SLICE_POISON, KMHG_TEST_REPLICA) choose between equivalent paths
+// and change no result.
 // Fault injection (KMHG_TEST_DISORDER) and the A/B-only switches (KMHG_D2H, KMHG_COUNT_BID,
 // KMHG_RK_CAP) exist only in the test build (-DKMHG_TEST_BUILD: libkmhgpu_test.so, make test):
 // the product library never reads them.
@@ -1638,6 +1639,27 @@ void ensure_row_order(kmhg_index* idx, hipStream_t s) {
   ReleaseGroup rg(s);
   const uint64_t U = idx->U;
   const int64_t n = idx->L;                       // every order key is < the characters counted
+  // F takes 4 B per character ever counted into the pointer (idx->L over all batches), which
+  // grows with the input, not with the rows: beyond 8 characters per row (many sources or
+  // batches of mostly known k-mers) the rows are ordered by a radix sort of their U order keys
+  // instead, O(U) scratch (advisor, round 4).  KMHG_ROW_ORDER_SORT=1 / 0 forces the sort / F
+  // (tests: both give the same order).
+  const char* rse = std::getenv("KMHG_ROW_ORDER_SORT");
+  const bool by_sort = rse ? rse[0] == '1' : (uint64_t)n > 8 * U;
+  if (by_sort) {
+    int bits = 1;
+    while (bits < 64 && (1ull << bits) < (uint64_t)n) ++bits;
+    const size_t tb = rows_sort_temp_bytes((uint32_t)U, bits);
+    DBuf<uint64_t> keys_out(U, s);
+    DBuf<uint32_t> rows_in(U, s);
+    DBuf<uint8_t> temp(std::max<size_t>(tb, 16), s);
+    idx->rorder.bind(s);
+    idx->rorder.reset(U);
+    LAUNCH("k_rows_sort", s, launch_rows_sort(idx->rord.p, (uint32_t)U, bits, keys_out.p,
+                                              rows_in.p, idx->rorder.p, temp.p, tb, s));
+    idx->order_ready = true;
+    return;
+  }
   DBuf<uint32_t> F((size_t)n, s);
   HIPC(hipMemsetAsync(F.p, 0xFF, (size_t)n * 4, s));
   LAUNCH("k_rows_place", s, launch_rows_place(idx->rord.p, (uint32_t)U, F.p, s));

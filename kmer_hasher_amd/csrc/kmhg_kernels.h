@@ -295,6 +295,12 @@ void launch_count_insert(const uint64_t* ckeys, uint32_t U, Slot* T, Geom g, uin
 void launch_rows_place(const uint64_t* rord, uint32_t U, uint32_t* F, hipStream_t s);
 void launch_rows_order(const uint32_t* F, int64_t n, uint64_t* status, uint32_t* ticket,
                        uint32_t* rorder, hipStream_t s);
+// rorder by a radix sort of the U (order key, row) pairs instead (O(U) scratch: keys_out U u64,
+// rows_in U u32, temp rows_sort_temp_bytes(U, bits)); bits covers every order key
+size_t rows_sort_temp_bytes(uint32_t U, int bits);
+void launch_rows_sort(const uint64_t* rord, uint32_t U, int bits, uint64_t* keys_out,
+                      uint32_t* rows_in, uint32_t* rorder, void* temp, size_t temp_bytes,
+                      hipStream_t s);
 void launch_rows_gather(const uint32_t* rorder, const uint64_t* ckeys, const int32_t* M,
                         uint32_t U, uint32_t S, uint64_t* okeys, int32_t* oM, hipStream_t s);
 // first batch into a new counts index / suffix hash: rows in slot order; `status` =

@@ -171,15 +171,19 @@ def test_gpu_counts_first_order_vs_oracle(gpu, cgold, monkeypatch, table):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", ["place", "sort"])
 @pytest.mark.parametrize("table", ["adopt", "rebuild"])
-def test_gpu_counts_readout_between_batches(gpu, cgold, monkeypatch, table):
+def test_gpu_counts_readout_between_batches(gpu, cgold, monkeypatch, table, order):
     """A batch's new rows are written in slot order with their insertion-order keys and sorted
     into first-insertion order only when a readout asks for rows (ensure_row_order).  A readout
     after every call -- rows sorted, then more appended unsorted and sorted again, the earlier
     rows' counts changed by later sources -- equals the oracle each time; golden cases plus
-    200 kbp batches that share half their sequence (known and new keys in one batch)."""
+    200 kbp batches that share half their sequence (known and new keys in one batch).  The
+    order comes from the order-key placement (F, 4 B per character counted) or from the radix
+    sort of the U order keys (O(U) scratch; the default beyond 8 characters per row)."""
     from kmer_hasher_amd import count_kmers, kmer_pos, synth
     monkeypatch.setenv("KMHG_COUNT_TABLE", table)
+    monkeypatch.setenv("KMHG_ROW_ORDER_SORT", "1" if order == "sort" else "0")
     base = synth.add_n_runs(synth.iid(300_000, 61), 0.001, 7).tobytes().decode("latin-1")
     big = {"name": "overlap", "k": 19, "source_n": 3,
            "calls": [(0, [base[:200_000]]), (1, [base[100_000:300_000], base[:5_000]]),
