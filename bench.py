@@ -61,7 +61,7 @@ CONFIGS = {
 PMC_PREFIX = {"k_v2_scatter_seq": ("k_v2_scatter<true", "k_v2_scatter<false, true"),
               "k_v2_scatter": ("k_v2_scatter<false, false",),
               "k_v2_hist0": ("k_v2_hist0p<", "k_v2_hist0("),
-              "k_v2_hist": ("k_v2_hist<",),
+              "k_v2_hist": ("k_v2_histp<", "k_v2_hist<"),
               "k_scan_u32": ("k_scan_lb_u32",),
               "k_v2_bounds": ("k_v2_bounds_lo", "k_v2_bounds"),
               "k_v2_bucket_wg": ("k_v2_bucket_wg<false",),

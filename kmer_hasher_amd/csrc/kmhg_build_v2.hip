@@ -364,12 +364,12 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
 // latency (config 2: 14.5 us for 40 MB).  `in` holds n + PTILE elements (the passes' padded
 // streams), so whole-tile loads stay inside it.
 // MODE: 0 = u64 keys, 1 = u32 bucket ids, 2 = packed 12-B {key lo, key hi, pos} elements (the
-// position builds' key streams).
+// position builds' key streams), 3 = packed 8-B elements (Pack8: the key is e >> sh).
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
            uint32_t* __restrict__ hist, uint32_t ntiles, uint64_t* __restrict__ scan_status,
-           uint32_t n_status, uint32_t* __restrict__ save_col0) {
+           uint32_t n_status, uint32_t* __restrict__ save_col0, int sh) {
   __shared__ uint32_t lh[V2_MAXR];
   for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n_status; i += gridDim.x * BLOCK)
     scan_status[i] = 0;
@@ -444,8 +444,8 @@ k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, 
           dg = digit_of_b(id, D);
         } else {
           const uint4 w = cur[j >> 1];
-          const uint64_t key = (j & 1) ? (((uint64_t)w.w << 32) | w.z) : (((uint64_t)w.y << 32) | w.x);
-          dg = digit_of_h(mix64(key), g, D);
+          const uint64_t e = (j & 1) ? (((uint64_t)w.w << 32) | w.z) : (((uint64_t)w.y << 32) | w.x);
+          dg = digit_of_h(mix64(MODE == 3 ? e >> sh : e), g, D);
         }
         atomicAdd(&lh[dg], 1u);
       }
@@ -599,7 +599,10 @@ __device__ __forceinline__ uint64_t block_excl_scan_n(uint64_t v, uint64_t* lds,
 // 3 = packed (key, pos) elements, 12 B each in kin / kout ({key lo, key hi, pos}; pin / pout
 // unused): a tile's digit run leaves as ONE contiguous piece instead of an 8 c-byte piece of
 // keys and a 4 c-byte piece of positions in two arrays; 4 = (key, pos) arrays in, packed out
-// (the last pass of a build whose earlier streams stay unpacked for their histogram passes).  Write-pattern probe
+// (the last pass of a build whose earlier streams stay unpacked for their histogram passes);
+// 6 = the first pass from the sequence writing packed 8-B elements (Pack8, small k), 7 = the
+// second pass reading them (each element's position restored from its segment, found in
+// pk.segb by its place in the stream) and writing packed 12-B elements.  Write-pattern probe
 // (tools/scatter_pattern.hip layout, profiles/r5a_scatter_layout.txt, 100 M elements): radix 313
 // 1.09 -> 0.87 ms, radix 79 0.72 -> 0.61 ms.
 // BALLOT: stable ranks from one ballot per digit bit instead of the count atomics' lane-ordered
@@ -611,10 +614,12 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, uint32_t ntiles,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad,
-             int skip_empty, BoundsFuse bf) {
+             int skip_empty, BoundsFuse bf, Pack8 pk) {
   constexpr bool BIDS = BM == 1 || BM == 2;      // bucket-id streams
-  constexpr bool AOS = BM == 3 || BM == 4;        // packed 12-B (key, pos) elements out
+  constexpr bool AOS = BM == 3 || BM == 4 || BM == 7;   // packed 12-B (key, pos) elements out
   constexpr bool AIN = BM == 3;                   // ... and in
+  constexpr bool P8OUT = BM == 6;                 // packed 8-B (key << sh | window) out
+  constexpr bool P8IN = BM == 7;                  // ... in
   using KT = typename std::conditional<BIDS, uint32_t, uint64_t>::type;
   using SL = ScatterLDS<KT>;
   static_assert(BM == 0 || !NOPOS, "bucket-id and packed streams carry positions");
@@ -650,7 +655,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
   if (bf.start)
     for (uint32_t lo = blockIdx.x; lo < bf.div; lo += gridDim.x)
       bounds_lo_body(lo, &S.wc[0][0], bf.kprev, *n_ptr, g, bf.Dlast, bf.div, hist, ntiles,
-                     bf.lo_start, bf.spread, bf.start, bf.bid, TB, bf.nlim);
+                     bf.lo_start, bf.spread, bf.start, bf.bid, TB, bf.nlim, bf.sh);
   // the next tile's inputs are in flight while this one is processed
   KT nkey[PER];
   uint32_t npos[PER];
@@ -670,6 +675,9 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
           const uint3 v = reinterpret_cast<const uint3*>(kin)[e];
           nkey[cc] = ((uint64_t)v.y << 32) | v.x;
           npos[cc] = v.z;
+        } else if (P8IN) {
+          nkey[cc] = kinT[e];                  // position restored from the segment table
+          npos[cc] = 0u;
         } else {
           nkey[cc] = kinT[e];
           npos[cc] = NOPOS ? 0u : pin[e];
@@ -687,7 +695,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
       reinterpret_cast<uint3*>(kout)[pad + threadIdx.x] = make_uint3(0u, 0u, 0u);
     } else {
       if (BM != 2) koutT[pad + threadIdx.x] = 0;
-      if (!NOPOS) pout[pad + threadIdx.x] = 0;
+      if (!NOPOS && !P8OUT) pout[pad + threadIdx.x] = 0;
     }
   }
   for (uint32_t it = 0; it < n_iter; ++it) {
@@ -722,8 +730,24 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         const uint64_t h = mix64(kk);
         const uint32_t bl = bucket_local(h, g);
         act[c] = act[c] && bl < g.nb;                        // a part build keeps its buckets
-        key[c] = BIDS ? (KT)bl : (KT)kk;
+        key[c] = BIDS ? (KT)bl
+                      : P8OUT ? (KT)((kk << pk.sh) | (e & ((1ull << pk.sh) - 1ull))) : (KT)kk;
         dg[c] = act[c] ? digit_of_b(bl, D) : 0;
+      } else if (P8IN) {
+        // key and window index from the packed element; the segment from the element's place
+        // in its pass-0 digit run (segb row of that digit: the largest s with segb[s] <= e)
+        act[c] = e < n;
+        const uint64_t kk = (uint64_t)key[c] >> pk.sh;
+        const uint64_t h = mix64(kk);
+        dg[c] = act[c] ? digit_of_h(h, g, D) : 0;
+        const uint32_t* row = pk.segb + (uint64_t)digit_of_h(h, g, pk.d0) * (pk.nseg + 1);
+        uint32_t lo = 0, hi = pk.nseg;                       // row[0] <= e < row[nseg]
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if ((uint64_t)row[mid] <= e) lo = mid; else hi = mid;
+        }
+        ps[c] = (uint32_t)((((uint64_t)lo << pk.sh) | ((uint64_t)key[c] & ((1ull << pk.sh) - 1ull))) + 1);
+        key[c] = (KT)kk;
       } else if (BIDS) {
         act[c] = e < n && !(KEYS0 && (uint32_t)key[c] == ~0u);
         dg[c] = act[c] ? digit_of_b((uint32_t)key[c], D) : 0;
@@ -826,7 +850,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         reinterpret_cast<uint3*>(kout)[dst] = make_uint3((uint32_t)kk, (uint32_t)(kk >> 32), S.spos[i]);
       } else {
         if (BM != 2) koutT[dst] = S.skey[i];
-        if (!NOPOS) pout[dst] = S.spos[i];
+        if (!NOPOS && !P8OUT) pout[dst] = S.spos[i];
       }
     }
   }
@@ -852,7 +876,7 @@ __device__ __forceinline__ void bounds_lo_body(uint32_t lo, uint32_t* cnt,
                                                const uint32_t* __restrict__ hist, uint32_t C,
                                                const uint32_t* __restrict__ lo_start,
                                                uint32_t spread, uint32_t* __restrict__ start,
-                                               int bid, int tb, uint32_t nlim) {
+                                               int bid, int tb, uint32_t nlim, int sh = 0) {
   const uint32_t R = Dlast.R;
   const uint32_t P = lo_start ? lo_start[lo] : 0u;
   for (uint32_t d = threadIdx.x; d < R; d += tb) cnt[d] = 0;
@@ -865,6 +889,8 @@ __device__ __forceinline__ void bounds_lo_body(uint32_t lo, uint32_t* cnt,
     } else if (bid == 2) {                 // packed (key, pos) elements
       const uint32_t* w = reinterpret_cast<const uint32_t*>(kprev) + 3 * (uint64_t)i;
       dg = digit_of(((uint64_t)w[1] << 32) | w[0], g, Dlast);
+    } else if (bid == 3) {                 // packed 8-B elements: key << sh | window
+      dg = digit_of(kprev[i] >> sh, g, Dlast);
     } else {
       dg = digit_of(kprev[i], g, Dlast);
     }
@@ -887,10 +913,24 @@ __global__ void __launch_bounds__(BLOCK)
 k_v2_bounds_lo(const uint64_t* __restrict__ kprev, const uint32_t* __restrict__ n_ptr, Geom g,
                Digit Dlast, uint32_t div, const uint32_t* __restrict__ hist, uint32_t C,
                const uint32_t* __restrict__ lo_start, uint32_t spread,
-               uint32_t* __restrict__ start, int bid, uint32_t nlim) {
+               uint32_t* __restrict__ start, int bid, uint32_t nlim, int sh) {
   __shared__ uint32_t cnt[V2_MAXR];
   bounds_lo_body(blockIdx.x, cnt, kprev, *n_ptr, g, Dlast, div, hist, C, lo_start, spread, start,
-                 bid, BLOCK, nlim);
+                 bid, BLOCK, nlim, sh);
+}
+
+// Pack8's segment table: segb[d * (nseg + 1) + s] = where segment s (tiles [s tps, (s + 1) tps))
+// of pass-0 digit d starts in pass 0's output -- the scanned histogram entry (d, s tps), or the
+// end of digit d's run past the last tile.
+__global__ void __launch_bounds__(BLOCK)
+k_seg_bounds(const uint32_t* __restrict__ hist, uint32_t ntiles, uint32_t R, uint32_t nseg,
+             uint32_t tps, const uint32_t* __restrict__ n_valid, uint32_t* __restrict__ segb) {
+  const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= R * (nseg + 1)) return;
+  const uint32_t d = i / (nseg + 1), sg = i % (nseg + 1);
+  const uint64_t t = (uint64_t)sg * tps;
+  segb[i] = t < ntiles ? hist[(size_t)d * ntiles + t]
+                       : (d + 1 < R ? hist[(size_t)(d + 1) * ntiles] : *n_valid);
 }
 
 // The radix passes are stable by the lane order of the LDS count atomics (V_scatter), so a
@@ -1421,22 +1461,28 @@ void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Dig
   static const unsigned cap = resident_blocks((const void*)k_v2_histp<1>);
   hipLaunchKernelGGL(k_v2_histp<1>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0, s,
                      reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ntiles,
-                     scan_status, n_status, save_col0);
+                     scan_status, n_status, save_col0, 0);
 }
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     uint32_t ntiles, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0, bool skip_empty,
-                    bool padded, bool aos) {
+                    bool padded, bool aos, int sh8) {
+  if (sh8) {                   // packed 8-B (key << sh | window) stream
+    static const unsigned cap = resident_blocks((const void*)k_v2_histp<3>);
+    hipLaunchKernelGGL(k_v2_histp<3>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0,
+                       s, keys, n_ptr, g, D, hist, ntiles, scan_status, n_status, save_col0, sh8);
+    return;
+  }
   if (aos) {                   // packed (key, pos) stream (padded by construction)
     static const unsigned cap = resident_blocks((const void*)k_v2_histp<2>);
     hipLaunchKernelGGL(k_v2_histp<2>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0,
-                       s, keys, n_ptr, g, D, hist, ntiles, scan_status, n_status, save_col0);
+                       s, keys, n_ptr, g, D, hist, ntiles, scan_status, n_status, save_col0, 0);
     return;
   }
   if (padded && !hll_rows && !skip_empty) {
     static const unsigned cap = resident_blocks((const void*)k_v2_histp<0>);
     hipLaunchKernelGGL(k_v2_histp<0>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0,
-                       s, keys, n_ptr, g, D, hist, ntiles, scan_status, n_status, save_col0);
+                       s, keys, n_ptr, g, D, hist, ntiles, scan_status, n_status, save_col0, 0);
     return;
   }
   if (hll_rows)
@@ -1451,10 +1497,16 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
                          uint32_t spread, uint32_t* start, uint32_t nlim, hipStream_t s,
-                         const uint32_t* bprev, bool aos) {
+                         const uint32_t* bprev, bool aos, int sh8) {
   hipLaunchKernelGGL(k_v2_bounds_lo, dim3(div), dim3(BLOCK), 0, s,
                      bprev ? reinterpret_cast<const uint64_t*>(bprev) : kprev, n_ptr, g, Dlast,
-                     div, hist, C, lo_start, spread, start, bprev ? 1 : aos ? 2 : 0, nlim);
+                     div, hist, C, lo_start, spread, start, bprev ? 1 : sh8 ? 3 : aos ? 2 : 0,
+                     nlim, sh8);
+}
+void launch_seg_bounds(const uint32_t* hist, uint32_t ntiles, uint32_t R, uint32_t nseg,
+                       uint32_t tps, const uint32_t* n_valid, uint32_t* segb, hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_bounds, dim3(grid_of((uint64_t)R * (nseg + 1), BLOCK)), dim3(BLOCK),
+                     0, s, hist, ntiles, R, nseg, tps, n_valid, segb);
 }
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s) {
@@ -1464,15 +1516,19 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
                      host_n);
 }
 static const BoundsFuse kNoFuse{nullptr, nullptr, nullptr, Digit{}, 0u, 1u, 0, 0u};
+static const Pack8 kNoPack{0, nullptr, 0u, Digit{}};
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
-                           uint32_t pad, hipStream_t s, bool aos) {
-  if (aos)
+                           uint32_t pad, hipStream_t s, bool aos, const Pack8* pk) {
+  if (pk && pk->sh)
+    KMHG_SCATTER_BM(true, false, false, 6, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist,
+                    ntiles, kout, nullptr, pad, 0, kNoFuse, *pk);
+  else if (aos)
     KMHG_SCATTER_BM(true, false, false, 3, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist,
-                    ntiles, kout, nullptr, pad, 0, kNoFuse);
+                    ntiles, kout, nullptr, pad, 0, kNoFuse, kNoPack);
   else
     KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
-                 kout, pout, pad, 0, kNoFuse);
+                 kout, pout, pad, 0, kNoFuse, kNoPack);
 }
 void launch_part_dense(const uint64_t* ck, const uint32_t* cp, const uint32_t* off,
                        uint32_t ntiles, const uint32_t* n_total, uint64_t* dk, uint32_t* dp,
@@ -1491,10 +1547,10 @@ void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
   if (bout)
     KMHG_SCATTER_BM(false, true, false, 1, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse);
+                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse, kNoPack);
   else
     KMHG_SCATTER_BM(false, true, false, 2, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse);
+                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse, kNoPack);
 }
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
@@ -1504,24 +1560,27 @@ void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint3
   const BoundsFuse f = bf ? *bf : kNoFuse;
   if (bout)
     KMHG_SCATTER_BM(false, false, false, 1, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0, f);
+                    g, D, hist, ntiles, ko, pout, pad, 0, f, kNoPack);
   else
     KMHG_SCATTER_BM(false, false, false, 2, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0, f);
+                    g, D, hist, ntiles, ko, pout, pad, 0, f, kNoPack);
 }
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                        uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf,
-                       bool aos, bool aos_in) {
-  if (aos && aos_in)
+                       bool aos, bool aos_in, const Pack8* pk) {
+  if (pk && pk->sh)            // packed 8-B elements in, packed 12-B out
+    KMHG_SCATTER_BM(false, false, false, 7, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr,
+                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, *pk);
+  else if (aos && aos_in)
     KMHG_SCATTER_BM(false, false, false, 3, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr,
-                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
+                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, kNoPack);
   else if (aos)
     KMHG_SCATTER_BM(false, false, false, 4, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin,
-                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
+                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, kNoPack);
   else
     KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,
-                 hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse);
+                 hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse, kNoPack);
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
                              Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
@@ -1529,16 +1588,16 @@ void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_
                              hipStream_t s) {
   if (nopos)
     KMHG_SCATTER(false, true, true, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr, n_ptr,
-                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0, kNoFuse);
+                 g, D, hist, ntiles, kout, nullptr, pad, skip_empty ? 1 : 0, kNoFuse, kNoPack);
   else
     KMHG_SCATTER(false, true, false, nullptr, (int64_t)0, 0, (int64_t)n_keys, kin, nullptr,
-                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0, kNoFuse);
+                 n_ptr, g, D, hist, ntiles, kout, pout, pad, skip_empty ? 1 : 0, kNoFuse, kNoPack);
 }
 void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g, Digit D,
                              const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t pad,
                              hipStream_t s, const BoundsFuse* bf) {
   KMHG_SCATTER(false, false, true, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr, n_ptr, g, D,
-               hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse);
+               hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, kNoPack);
 }
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,

@@ -34,8 +34,8 @@
 // build / query / counts path against the oracle (KMHG_BUILD, KMHG_BUILD_BID, KMHG_MAXR,
 // KMHG_FUSE_BOUNDS, KMHG_TEST_BALLOT, KMHG_QUERY_TAGS, KMHG_QUERY_DIAG, KMHG_DIAG_CODES,
 // KMHG_COUNT_TABLE, KMHG_COUNT_WALK, KMHG_CO_SPREAD, KMHG_CO_GLOBAL, KMHG_PART_COMPACT,
-// KMHG_ROW_ORDER_SORT, KMHG_SLICE_POISON, KMHG_TEST_REPLICA) choose between equivalent paths
-// and change no result.
+// KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_SLICE_POISON, KMHG_TEST_REPLICA) choose between
+// equivalent paths and change no result.
 // Fault injection (KMHG_TEST_DISORDER) and the A/B-only switches (KMHG_D2H, KMHG_COUNT_BID,
 // KMHG_RK_CAP) exist only in the test build (-DKMHG_TEST_BUILD: libkmhgpu_test.so, make test):
 // the product library never reads them.
@@ -922,8 +922,19 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // in one run (profiles/r5b_ab_aos_config3.log, r5c_ab_aos_config5.log).
   constexpr uint32_t AOS_MIN_RADIX = 160;
   auto packed = [&](int p) { return aos && (p + 1 == (int)passes || R >= AOS_MIN_RADIX); };
+  // Pack8 (two-pass builds of small k: 2k <= 52): the first pass writes 8-B elements, key << sh
+  // | the window's index inside its segment of 2^sh windows (sh = 64 - 2k), and the second pass
+  // restores the position from the element's place in the stream (k_seg_bounds' table).  The
+  // first stream's writes and the histogram pass's reads shrink from 12 to 8 B per window.
+  // KMHG_PACK8=0 keeps the 12-B first stream (A/B, tests).
+  const int sh8 = 64 - 2 * k;
+  const uint64_t seg8 = sh8 >= 12 && sh8 < 64 ? (1ull << sh8) : 0;
+  const uint32_t nseg8 = seg8 ? (uint32_t)(((uint64_t)Nw + seg8 - 1) / seg8) : 0;
+  const char* p8e = std::getenv("KMHG_PACK8");
+  const bool pack8 = aos && passes == 2 && n_parts < 2 && seg8 && nseg8 <= 256 &&
+                     !(p8e && p8e[0] == '0');
   bool any_unpacked = !aos;
-  for (int p = -1; p + 1 < (int)passes; ++p) any_unpacked |= !packed(p);
+  for (int p = -1; p + 1 < (int)passes; ++p) any_unpacked |= !packed(p) && !(pack8 && p == 0);
   const uint64_t kwords = bid ? 1 : aos ? ((uint64_t)(Nw + PTILE) * 3 + 1) / 2 : (uint64_t)(Nw + PTILE);
   DBuf<uint64_t> kA(kwords, s), kB(kwords, s);   // + pad
   // (Removed in round 4 after measurement, DESIGN.md §5: radix passes writing whole 128-B lines
@@ -942,6 +953,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const uint32_t pad = (uint32_t)Nw;
   DBuf<uint32_t> hist(nhist, s);
   DBuf<uint32_t> start((uint64_t)nb + 1, s);
+  DBuf<uint32_t> segb(pack8 ? (uint64_t)R * (nseg8 + 1) : 1, s);
+  const Pack8 pk8{pack8 ? sh8 : 0, segb.p, nseg8, make_digit(1, R)};
   // scratch (zeroed in-kernel by V_hist0 / V_hist, no memset): [n_valid][meta][scan status]
   const size_t off_meta = 64, off_status = 128;
   const uint32_t n_status = scan_tiles + 1;               // look-back words + ticket
@@ -1003,14 +1016,20 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       LAUNCH("k_scan_u32", s, launch_scan_u32(tcnt.p, ntiles, status, n_valid, s));
     } else {
       LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
-      if (bid)
+      if (bid) {
         LAUNCH("k_v2_scatter_seq", s,
                launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ntiles,
                                       passes == 1 ? nullptr : bA.p, pA.p, pad, s));
-      else
+      } else {
         LAUNCH("k_v2_scatter_seq", s,
                launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
-                                     pA.p, pad, s, packed(0)));
+                                     pA.p, pad, s, packed(0), pack8 ? &pk8 : nullptr));
+        // the segment table, before pass 1's histogram overwrites pass 0's
+        if (pack8)
+          LAUNCH("k_seg_bounds", s,
+                 launch_seg_bounds(hist.p, ntiles, R, nseg8, (uint32_t)(seg8 / PTILE), n_valid,
+                                   segb.p, s));
+      }
       div = R;
     }
   }
@@ -1055,10 +1074,13 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const bool last = p + 1 == passes;
     const uint32_t* lin = p == 1 ? lo_save.p : ((p - 1) % 2 ? lvA.p : lvB.p);
     uint32_t* lout = last ? start.p : (p % 2 ? lvA.p : lvB.p);
-    return BoundsFuse{reinterpret_cast<const uint64_t*>(kprev), lin, lout,
-                      make_digit((uint32_t)dv, R), (uint32_t)dv, spread,
-                      is_bid ? 1 : packed((int)p - 1) ? 2 : 0,
-                      last ? g.nb : (uint32_t)(dv * R)};
+    const bool p8 = pack8 && p == 1;                    // the input is the packed 8-B stream
+    BoundsFuse f{reinterpret_cast<const uint64_t*>(kprev), lin, lout,
+                 make_digit((uint32_t)dv, R), (uint32_t)dv, spread,
+                 is_bid ? 1 : p8 ? 3 : packed((int)p - 1) ? 2 : 0,
+                 last ? g.nb : (uint32_t)(dv * R)};
+    f.sh = p8 ? sh8 : 0;
+    return f;
   };
   auto fused = [&](uint32_t p) { return p >= 1 && fuse_on && !(co_auto && p + 1 == passes); };
   auto launch_level = [&](const BoundsFuse& f) {
@@ -1066,7 +1088,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const uint32_t* bp = f.bid ? reinterpret_cast<const uint32_t*>(f.kprev) : nullptr;
     LAUNCH("k_v2_bounds", s, launch_v2_bounds_lo(kp, n_valid, g, f.Dlast, f.div, hp, C,
                                                  f.lo_start, f.spread, f.start, f.nlim, s, bp,
-                                                 f.bid == 2));
+                                                 f.bid == 2, f.bid == 3 ? f.sh : 0));
   };
   for (uint32_t p = 1; bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
@@ -1094,7 +1116,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
            launch_v2_hist(src, n_valid, g, Dp, hp, C, status, nst, s,
                           hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
                           p == 1 ? save1 : nullptr, keys0 && skip_empty,
-                          /*padded=*/!keys0, !keys0 && packed((int)p - 1)));
+                          /*padded=*/!keys0, !keys0 && packed((int)p - 1),
+                          pack8 && p == 1 ? sh8 : 0));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hp, nh, status, n_valid, s));
     if (hll) {   // after the scan: the estimate travels with the valid key count
       LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ntiles, hll_regs.p,
@@ -1115,7 +1138,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
       else
         LAUNCH("k_v2_scatter", s,
                launch_v2_scatter(kin, pin, n_valid, g, Dp, hp, C, kout, pout, pad, s,
-                                 fused(p) ? &lv : nullptr, packed((int)p), packed((int)p - 1)));
+                                 fused(p) ? &lv : nullptr, packed((int)p), packed((int)p - 1),
+                                 pack8 && p == 1 ? &pk8 : nullptr));
       if (p >= 1 && !fused(p) && !last) launch_level(lv);
     }
     std::swap(kin, kout);

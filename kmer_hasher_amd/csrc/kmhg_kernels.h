@@ -188,7 +188,7 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
                     uint32_t ntiles, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows = nullptr, uint32_t* hll_regs = nullptr,
                     uint32_t* save_col0 = nullptr, bool skip_empty = false,
-                    bool padded = false, bool aos = false);
+                    bool padded = false, bool aos = false, int sh8 = 0);
 // one level of the bucket starts from the histograms (the unfused form of BoundsFuse): one
 // workgroup per lo value (div of them); kprev = pass p's input keys, lo_start = S_(p-1) (pass 0's
 // column 0 saved by launch_v2_hist's save_col0 for p = 1; nullptr for one pass); start[c / spread]
@@ -197,7 +197,10 @@ void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D
 void launch_v2_bounds_lo(const uint64_t* kprev, const uint32_t* n_ptr, Geom g, Digit Dlast,
                          uint32_t div, const uint32_t* hist, uint32_t C, const uint32_t* lo_start,
                          uint32_t spread, uint32_t* start, uint32_t nlim, hipStream_t s,
-                         const uint32_t* bprev = nullptr, bool aos = false);
+                         const uint32_t* bprev = nullptr, bool aos = false, int sh8 = 0);
+// segb (Pack8) from pass 0's scanned histogram: R x (nseg + 1) entries, tps = tiles per segment
+void launch_seg_bounds(const uint32_t* hist, uint32_t ntiles, uint32_t R, uint32_t nseg,
+                       uint32_t tps, const uint32_t* n_valid, uint32_t* segb, hipStream_t s);
 // also copies *n_valid (launch it after the pass's scan) to *host_n
 void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs, double* host_est,
                    const uint32_t* n_valid, uint64_t* host_n, hipStream_t s);
@@ -207,19 +210,33 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
 // is read only by the next level or the bucket kernel, so the pass's workgroups each compute
 // the starts of a few lower-digit values before their tiles (no launch, no key pass).
 // start == nullptr: not fused.
+// Packed 8-B elements of a small-k key stream (the first pass of a two-pass build with 2k <= 53):
+// the high 2k bits hold the key, the low sh = 64 - 2k bits the window's index inside its segment
+// of 2^sh windows.  The segment comes back from the element's place in the stream: pass 0 writes
+// digit d's elements tile by tile, so segment s of digit d starts at the scanned histogram entry
+// of (d, s * 2^sh / PTILE) -- segb[d * (nseg + 1) + s], nseg + 1 entries per digit.
+struct Pack8 {
+  int sh;                      // 0: no packed stream
+  const uint32_t* segb;
+  uint32_t nseg;
+  Digit d0;                    // pass 0's digit
+};
 struct BoundsFuse {
   const uint64_t* kprev;       // the pass's input (keys, or bucket ids with bid = 1)
   const uint32_t* lo_start;    // S_(p-1): starts of the input's combined lower digits
   uint32_t* start;             // S_p
   Digit Dlast;                 // the pass's own digit
   uint32_t div, spread;        // div = R^p lower-digit values
-  int bid;                     // 0 u64 keys, 1 u32 bucket ids, 2 packed 12-B (key, pos) elements
+  int bid;                     // 0 u64 keys, 1 u32 bucket ids, 2 packed 12-B (key, pos) elements,
+                               // 3 packed 8-B (key << sh | window) elements
   uint32_t nlim;               // entries of S_p: nb for the last pass, R^(p+1) before
+  int sh = 0;                  // bid 3: the element's key is e >> sh
 };
 // the sequence must be 16-B aligned (the engine copies an unaligned input)
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
-                           uint32_t pad, hipStream_t s, bool aos = false);
+                           uint32_t pad, hipStream_t s, bool aos = false,
+                           const Pack8* pk = nullptr);
 // first pass over a caller's key stream of n_keys keys (>= 1): positions are e + 1; nopos:
 // keys only (count-only builds), pout unused; skip_empty: EMPTY_KEY entries are not keys (padded
 // read k-mer streams, k <= 31)
@@ -233,7 +250,7 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s, const BoundsFuse* bf = nullptr,
-                       bool aos = false, bool aos_in = true);
+                       bool aos = false, bool aos_in = true, const Pack8* pk = nullptr);
 // Packed key streams (aos): position builds on key streams carry each window as ONE 12-B
 // element {key lo, key hi, pos} (kout holds n + PTILE of them; pout unused), so a tile's digit
 // run is one contiguous write; aos_in: the input is packed too (else kin / pin arrays).

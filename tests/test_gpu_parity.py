@@ -423,3 +423,23 @@ def test_query_diagonal_edges_vs_oracle(gpu, monkeypatch, codes):
     ptr = make(s, 31)
     assert np.array_equal(sqk(ptr, s, 31).reshape(-1), oi.query(s, 31))
     ptr.free()
+
+
+@pytest.mark.parametrize("k", [17, 21, 24, 26])
+@pytest.mark.parametrize("pack8", ["1", "0"])
+def test_pack8_two_pass_vs_oracle(gpu, monkeypatch, k, pack8):
+    """Two-pass key-stream builds of small k write the first stream as 8-B elements (key << sh |
+    the window's index inside its segment of 2^sh windows, sh = 64 - 2k) and restore each
+    position in the second pass from the element's place in the stream (k_seg_bounds' table of
+    where each segment of each pass-0 digit starts).  k = 26 has segments of 4,096 windows, so
+    700 K windows span 171 segments; k = 24 eleven; k <= 21 one.  KMHG_MAXR=40 forces two passes,
+    KMHG_BUILD_BID=0 key streams; KMHG_PACK8=0 the 12-B first stream.  Against the oracle: N-runs
+    and lower case (i.i.d.), and repeat-rich input with pairs."""
+    from kmer_hasher_amd import synth
+    monkeypatch.setenv("KMHG_MAXR", "40")
+    monkeypatch.setenv("KMHG_BUILD_BID", "0")
+    monkeypatch.setenv("KMHG_PACK8", pack8)
+    s = synth.add_n_runs(synth.iid(700_000, 70 + k), 0.002, 9).tobytes().decode("latin-1")
+    _check_against_oracle(s, k, qks=[k, min(k + 4, 31)], pairs=False)
+    rr = synth.repeat_rich(400_000, 90 + k, n_gap_every=70_001).tobytes().decode("latin-1")
+    _check_against_oracle(rr, k, qks=[k], pairs=True)
