@@ -998,9 +998,6 @@ struct Words3 {                                // three consecutive code words, 
 };
 // AOS: the stream is packed 12-B (key, pos) elements in `keys` (`pos` unused).
 template <bool COUNT_ONLY, bool CK, bool BALLOT, bool AOS = false>
-#ifndef KMHG_BUCKET_WGS
-#define KMHG_BUCKET_WGS 8      // workgroups per CU the compact LDS table allows (1,536 slots)
-#endif
 __global__ void __launch_bounds__(BLOCK, BALLOT ? 4 : KMHG_BUCKET_WGS)
 k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,

@@ -34,8 +34,8 @@
 // build / query / counts path against the oracle (KMHG_BUILD, KMHG_BUILD_BID, KMHG_MAXR,
 // KMHG_FUSE_BOUNDS, KMHG_TEST_BALLOT, KMHG_QUERY_TAGS, KMHG_QUERY_DIAG, KMHG_DIAG_CODES,
 // KMHG_COUNT_TABLE, KMHG_COUNT_WALK, KMHG_CO_SPREAD, KMHG_CO_GLOBAL, KMHG_PART_COMPACT,
-// KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_SLICE_POISON, KMHG_TEST_REPLICA) choose between
-// equivalent paths and change no result.
+// KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_NB_ROUND, KMHG_SLICE_POISON, KMHG_TEST_REPLICA) choose
+// between equivalent paths and change no result.
 // Fault injection (KMHG_TEST_DISORDER) and the A/B-only switches (KMHG_D2H, KMHG_COUNT_BID,
 // KMHG_RK_CAP) exist only in the test build (-DKMHG_TEST_BUILD: libkmhgpu_test.so, make test):
 // the product library never reads them.
@@ -866,9 +866,27 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const bool co_auto = count_only && co_spread == 0;
   int64_t bw_g = V2_BW_WG;
   if (count_only && !co_auto) bw_g *= std::max(1, std::min(8, co_spread));
-  const uint32_t nb_g =
+  uint32_t nb_g =
       co_auto ? (uint32_t)(12 * std::max<int64_t>(1, (Nw + 12 * V2_BW_WG - 1) / (12 * V2_BW_WG)))
               : (uint32_t)std::max<int64_t>(1, (Nw + bw_g - 1) / bw_g);
+  // Whole rounds of the bucket kernel: its workgroups take about equally long, so 4.77 rounds of
+  // the device's resident workgroups (config 2: 9,766 buckets on 256 CUs x 8) cost 5; rounding
+  // the bucket count up to whole rounds gives each bucket fewer windows instead (position builds
+  // of 2-16 rounds).  KMHG_NB_ROUND=0 keeps ceil(windows / 1,024) (A/B, tests).
+  if (!from_keys && !count_only && n_parts == 0) {
+    const char* nre = std::getenv("KMHG_NB_ROUND");
+    if (!(nre && nre[0] == '0')) {
+      static const uint32_t wave_wg = [] {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+          cus = 0;
+        return (uint32_t)std::max(cus, 0) * (uint32_t)KMHG_BUCKET_WGS;
+      }();
+      if (wave_wg && nb_g > wave_wg && nb_g <= 16 * wave_wg)
+        nb_g = (nb_g + wave_wg - 1) / wave_wg * wave_wg;
+    }
+  }
   uint32_t R = 0;
   uint32_t nb = nb_g;
   uint32_t passes = plan(nb_g, R);

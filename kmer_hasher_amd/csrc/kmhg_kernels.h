@@ -15,6 +15,9 @@ constexpr uint32_t LARGE_MIN = 64;     // keys with >= this many positions sort 
 #ifndef KMHG_CAPW
 #define KMHG_CAPW 1536
 #endif
+#ifndef KMHG_BUCKET_WGS
+#define KMHG_BUCKET_WGS 8      // workgroups per CU the compact LDS table allows (1,536 slots)
+#endif
 constexpr uint32_t V2_BW_WG = KMHG_BW_WG;
 constexpr uint32_t V2_CAPW = KMHG_CAPW;  // slots per group bucket (LDS sub-table of one workgroup)
 constexpr uint32_t V2_SLOT_BITS_WG = V2_CAPW >= 2048 ? 12 : 11;
