@@ -872,8 +872,9 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // Whole rounds of the bucket kernel: its workgroups take about equally long, so 4.77 rounds of
   // the device's resident workgroups (config 2: 9,766 buckets on 256 CUs x 8) cost 5; rounding
   // the bucket count up to whole rounds gives each bucket fewer windows instead (position builds
-  // of 2-16 rounds).  KMHG_NB_ROUND=0 keeps ceil(windows / 1,024) (A/B, tests).
-  if (!from_keys && !count_only && n_parts == 0) {
+  // of 2-16 rounds; the parts of an owner-computes build split the same rounded table, so they
+  // still assemble into the single-device table).  KMHG_NB_ROUND=0 keeps ceil(windows / 1,024).
+  if (!from_keys && !count_only) {
     const char* nre = std::getenv("KMHG_NB_ROUND");
     if (!(nre && nre[0] == '0')) {
       static const uint32_t wave_wg = [] {
