@@ -460,6 +460,18 @@ def cpu_reads_baseline(fq: bytes, seq_bytes: bytes, k: int, depth_bp: int = 2_00
         return na, dict(na)
 
 
+_JSON_OUT = sys.stdout        # the result line's stream (main() keeps the process's real stdout)
+
+
+def _claim_stdout() -> None:
+    """Stdout carries the one JSON line and nothing else: from here on, what anything else prints
+    there (RCCL's version banner at process-group init, runtime notices) goes to stderr."""
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -485,6 +497,7 @@ def main():
     ap.add_argument("--only-large", action="store_true",
                     help="run the out-of-cache record alone (profiling), printed as its own line")
     args = ap.parse_args()
+    _claim_stdout()
     # the side legs (query, counts, reads, depth) run for at least 50 timed calls: 20 calls of a
     # 0.1-0.5 ms leg are a few ms of wall time, where one host hiccup shows as a 2x swing
     leg_steps = max(args.steps, 50)
@@ -934,7 +947,7 @@ def main():
         for leg in ("query", "counts", "reads", "depth"):
             if leg in out:
                 out[leg]["steps"] = leg_steps
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=_JSON_OUT, flush=True)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
@@ -1042,7 +1055,7 @@ def bench_sharded_build(args, k, L, dev, world, rank, seed):
 
 
 def _emit(out):
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=_JSON_OUT, flush=True)
 
 
 LARGE_L, LARGE_K = 500_000_000, 31

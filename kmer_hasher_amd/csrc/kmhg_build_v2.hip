@@ -642,7 +642,16 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
   // thread t owns digits [DPT t, DPT t + DPT)
   const uint32_t G = gridDim.x;
   const uint32_t n_iter = (ntiles - blockIdx.x + G - 1) / G;
+  // Each XCD walks its tile range from the END: the histogram pass before this one read the
+  // same input ascending, so the tail it read last is still in the Infinity Cache when this
+  // pass starts (-DKMHG_NO_REVERSE: ascending, A/B)
+#ifndef KMHG_NO_REVERSE
+  auto tile_at = [&](uint32_t i) -> uint32_t {
+    return xcd_remap(blockIdx.x + (n_iter - 1 - i) * G, ntiles);
+  };
+#else
   auto tile_at = [&](uint32_t i) -> uint32_t { return xcd_remap(blockIdx.x + i * G, ntiles); };
+#endif
   uint32_t ngb[DPT];
   auto load_bases = [&](uint32_t tv) {     // unconditional (clamped) loads: static count
 #pragma unroll
@@ -993,6 +1002,11 @@ __device__ __forceinline__ int lds_find_g(const GroupTableC& W, uint64_t key) {
 // BALLOT: repeated keys' windows ranked by ballots instead of the cursor atomic's lane order.
 // Every key must hash to this bucket: a stream entry that does not (an unstable pass moving
 // another bucket's window in) is reported like an LDS overflow.
+#ifndef KMHG_NO_NT_TABLE
+constexpr bool NT_TABLE = true;                // (-DKMHG_NO_NT_TABLE: plain stores, A/B)
+#else
+constexpr bool NT_TABLE = false;
+#endif
 struct Words3 {                                // three consecutive code words, 4-B aligned
   uint32_t a, b, c;
 };
@@ -1043,7 +1057,11 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
 #pragma unroll
       for (int c = 0; c < PER; ++c) {
         const uint32_t i = elem(i0, c);
+#ifdef KMHG_EXP_NTLOAD
+        ps[c] = i < s1 ? __builtin_nontemporal_load(pos + i) : 1u;
+#else
         ps[c] = i < s1 ? pos[i] : 1u;               // 1-based window start
+#endif
         if (!one_batch) disorder |= stream_out_of_order(pos, i, s0, s1, ps[c]);
       }
 #pragma unroll
@@ -1283,7 +1301,15 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     if (j < V2_CAPW) {
       const uint64_t kk = W.key[j];
       const uint32_t aux = COUNT_ONLY ? 0u : (W.val[j] & ~VAL_MULTI);
-      *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), cnt[q], aux);
+      if (CK && NT_TABLE) {
+        // code-word keys: the table streams past the L2 (nontemporal), which keeps the code
+        // words every bucket gathers from resident there
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 sv = {(uint32_t)kk, (uint32_t)(kk >> 32), cnt[q], aux};
+        __builtin_nontemporal_store(sv, reinterpret_cast<u32x4*>(&Tb[j]));
+      } else {
+        *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), cnt[q], aux);
+      }
     }
   }
 #endif

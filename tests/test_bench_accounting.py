@@ -82,3 +82,17 @@ def test_traffic_frac_prices_the_bytes_moved():
     q = bench.query_roofline(qper, 10_000_000, 9_999_970, 9_999_970, qpmc, step_ms=0.078)
     assert "kernel_model" not in q
     assert q["traffic_frac"] == round((500 + 1200 + 40 + 5) * 1e5 / 0.065e-3 / 1e9 / 8000, 4)
+
+
+def test_stdout_carries_only_the_result_line():
+    """After _claim_stdout, output printed by anything else (RCCL prints its version banner to
+    stdout at process-group init) lands on stderr; the result line alone on stdout."""
+    import subprocess
+    code = ("import os, sys, json; sys.path.insert(0, %r); import bench; bench._claim_stdout(); "
+            "print('banner'); os.write(1, b'native banner\\n'); "
+            "print(json.dumps({'value': 1}), file=bench._JSON_OUT, flush=True)"
+            % os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.splitlines() == ['{"value": 1}']
+    assert "banner" in r.stderr and "native banner" in r.stderr
