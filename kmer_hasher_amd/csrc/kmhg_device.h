@@ -354,7 +354,22 @@ __device__ __forceinline__ uint32_t table_insert(Slot* __restrict__ T, Geom g, u
   }
 }
 
+// One 16-B slot as a probe reads it.  NT: a nontemporal load, for tables far beyond the
+// Infinity Cache, whose random slot lines would otherwise evict what the probe reuses (the code
+// words, the slot tags) for lines it reads once (launch_query_probe).
+template <bool NT = false>
+__device__ __forceinline__ uint4 ld_slot(const Slot* p) {
+  if constexpr (NT) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+
 // Read-only probe: returns the slot or NONE; count/aux from the same 16-B slot load.
+template <bool NT = false>
 __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom g, uint64_t key,
                                                uint32_t& count, uint32_t& aux) {
   if (key == EMPTY_KEY) {
@@ -368,7 +383,7 @@ __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom 
   uint32_t j = local_home(h, g.capb);
   for (;;) {
     const uint64_t i = b0 + j;
-    uint4 v = *reinterpret_cast<const uint4*>(&T[i]);
+    uint4 v = ld_slot<NT>(&T[i]);
     uint64_t cur = ((uint64_t)v.y << 32) | v.x;
     if (cur == key) { count = v.z; aux = v.w; return (uint32_t)i; }
     if (cur == EMPTY_KEY) { count = 0; aux = 0; return NONE; }
@@ -380,9 +395,10 @@ __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom 
 // occupied slots to an empty one: at load 0.67 ~5 slots, one 64-B span instead of 5 dependent
 // loads).  Used where misses dominate (the diagonal query path sends only anchors, unpredicted
 // windows and misses here).
+template <bool NT = false>
 __device__ __forceinline__ uint32_t table_find4(const Slot* __restrict__ T, Geom g, uint64_t key,
                                                 uint32_t& count, uint32_t& aux) {
-  if (key == EMPTY_KEY) return table_find(T, g, key, count, aux);
+  if (key == EMPTY_KEY) return table_find<NT>(T, g, key, count, aux);
   const uint64_t h = mix64(key);
   const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
   uint32_t j = local_home(h, g.capb);
@@ -392,7 +408,7 @@ __device__ __forceinline__ uint32_t table_find4(const Slot* __restrict__ T, Geom
     for (int q = 0; q < 4; ++q) {
       uint32_t jq = j + q;
       if (jq >= g.capb) jq -= g.capb;
-      v[q] = *reinterpret_cast<const uint4*>(&T[b0 + jq]);
+      v[q] = ld_slot<NT>(&T[b0 + jq]);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -427,11 +443,12 @@ __device__ __forceinline__ uint32_t zero_bytes8(uint64_t v) {
 // table_find through the tags: a miss reads the 16 tags of its home's aligned group (one 16-B
 // load from an array 1/16 the table's size) and usually stops at an empty tag without touching
 // the table; the table is read only at slots whose tag equals the key's.  Needs g.capb % 16 == 0.
+template <bool NT = false>
 __device__ __forceinline__ uint32_t table_find_tag(const Slot* __restrict__ T,
                                                    const uint8_t* __restrict__ TG, Geom g,
                                                    uint64_t key, uint32_t& count, uint32_t& aux) {
   count = 0; aux = 0;
-  if (key == EMPTY_KEY) return table_find(T, g, key, count, aux);
+  if (key == EMPTY_KEY) return table_find<NT>(T, g, key, count, aux);
   const uint64_t h = mix64(key);
   const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
   const uint32_t j = local_home(h, g.capb);
@@ -451,7 +468,7 @@ __device__ __forceinline__ uint32_t table_find_tag(const Slot* __restrict__ T,
       const uint32_t q = __ffs(cand) - 1;
       cand &= cand - 1;
       const uint64_t i = b0 + grp + q;
-      const uint4 sv = *reinterpret_cast<const uint4*>(&T[i]);
+      const uint4 sv = ld_slot<NT>(&T[i]);
       if ((((uint64_t)sv.y << 32) | sv.x) == key) { count = sv.z; aux = sv.w; return (uint32_t)i; }
     }
     if (zm) return NONE;

@@ -415,7 +415,7 @@ struct DiagAnchors {
 
 // Anchor probes of a staged tile (threads < DG_ANCHORS) and the last-predicting-anchor scan;
 // called by every thread of the block (two barriers inside).
-template <class ST>
+template <bool NT, class ST>
 __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_start, int64_t w1,
                                              int64_t L, int kq, const Slot* __restrict__ T,
                                              Geom g, DiagAnchors& A) {
@@ -431,12 +431,12 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
     // windows verify against its diagonal anyway.  A self dot plot probes every 512th window, a
     // cross query keeps every 256th where the tile head needs it.
     const bool primary = (threadIdx.x & 1) == 0;
-    if (kv && primary) table_find(T, g, key, count, aux);
+    if (kv && primary) table_find<NT>(T, g, key, count, aux);
     const uint64_t pm = __ballot(is_anchor && primary && count == 1);
     // (and only in a tile where some even anchor predicts: with none, the tile is unrelated to
     // the index and its windows probe the table whatever the odd anchors find)
     const bool second = kv && !primary && pm != 0 && (pm & lanemask_lt()) == 0;
-    if (second) table_find(T, g, key, count, aux);
+    if (second) table_find<NT>(T, g, key, count, aux);
     const uint64_t probed = __ballot(is_anchor && (primary || second));
     if (threadIdx.x == 0) A.probed = probed;
     if (is_anchor) {
@@ -465,7 +465,7 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
 // 0, so every lane issues a static number of loads), then resolved; windows whose prediction
 // fails probe through the slot tags (TG) or the table.
 // `out(w, s, count, aux)` receives every window of the tile, s = t_start + w (s >= w1: none).
-template <class ST, class Out>
+template <bool NT, class ST, class Out>
 __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_start, int64_t w0,
                                              int64_t w1, int64_t L, int kq,
                                              const Slot* __restrict__ T, Geom g, DiagIdx X,
@@ -506,12 +506,12 @@ __device__ __forceinline__ void diag_resolve(const ST& st, int o0, int64_t t_sta
       }
       if (!hit) {
         count = 0; aux = 0;
-        if (TG) table_find_tag(T, TG, g, key, count, aux);   // mostly misses here
+        if (TG) table_find_tag<NT>(T, TG, g, key, count, aux);   // mostly misses here
         else
 #ifndef KMHG_NO_FIND4
-          table_find4(T, g, key, count, aux);
+          table_find4<NT>(T, g, key, count, aux);
 #else
-          table_find(T, g, key, count, aux);
+          table_find<NT>(T, g, key, count, aux);
 #endif
       }
     }
@@ -531,7 +531,7 @@ struct DiagProbeLDS {
   uint64_t key[TILE];            // unresolved windows' keys
   uint8_t todo[TILE];            // 1: window w needs a table probe
 };
-template <class ST>
+template <bool NT, class ST>
 __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t t_start,
                                                   int64_t w0r, int64_t w1, int64_t L, int kq,
                                                   const Slot* __restrict__ T, Geom g, DiagIdx X,
@@ -604,8 +604,8 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
     if (P.todo[w]) {
       const int64_t s = t_start + w;
       uint32_t count = 0, aux = 0;
-      if (TG) table_find_tag(T, TG, g, P.key[w], count, aux);
-      else table_find4(T, g, P.key[w], count, aux);
+      if (TG) table_find_tag<NT>(T, TG, g, P.key[w], count, aux);
+      else table_find4<NT>(T, g, P.key[w], count, aux);
       put_qrec(qrec, qmulti, s - w0r, count, aux);
       rows += count;
     }
@@ -624,7 +624,7 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
 #else
 #define PROBE_BOUNDS __launch_bounds__(BLOCK)
 #endif
-template <bool DIAG>
+template <bool DIAG, bool NT>
 __global__ void PROBE_BOUNDS
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint32_t* __restrict__ qrec, uint2* __restrict__ qmulti, int64_t w0,
@@ -646,20 +646,20 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   const int o0 = (int)(t_start - base);
   stage_tile(seq, L, base, st, aligned != 0);
   __syncthreads();
-  if (DIAG) diag_anchors(st, o0, t_start, w1, L, kq, T, g, A);
+  if (DIAG) diag_anchors<NT>(st, o0, t_start, w1, L, kq, T, g, A);
   uint64_t rows = 0;
 #ifndef KMHG_PROBE_UNROLL
 #define KMHG_PROBE_UNROLL 2
 #endif
   if (DIAG) {
 #ifndef KMHG_PROBE_STRIDED
-    rows = diag_resolve8(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A, qrec, qmulti, PL);
+    rows = diag_resolve8<NT>(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A, qrec, qmulti, PL);
     uint64_t tot8;
     block_excl_scan(rows, sh, tot8);
     if (threadIdx.x == 0) tile_rows[tile] = tot8;
     return;
 #endif
-    diag_resolve(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
+    diag_resolve<NT>(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
                  [&](int w, int64_t s, uint32_t count, uint32_t aux) {
                    if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
                    rows += count;
@@ -679,7 +679,7 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
-    if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find(T, g, key, count, aux);
+    if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find<NT>(T, g, key, count, aux);
     // {count, position} for a key seen once, {count, first index} otherwise
     if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
     rows += count;
@@ -1236,19 +1236,32 @@ void launch_inline_singles(Slot* T, uint64_t nslots, const int32_t* positions, h
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(k_inline_singles, dim3(g), dim3(BLOCK), 0, s, T, nslots, positions);
 }
+#ifndef KMHG_NT_PROBE_MB
+#define KMHG_NT_PROBE_MB 4096
+#endif
+constexpr uint64_t NT_PROBE_BYTES = (uint64_t)KMHG_NT_PROBE_MB << 20;
 void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Geom g,
                         uint32_t* qrec, uint2* qmulti, int64_t w0, int64_t w1, bool aligned,
                         uint64_t* tile_rows,
                         hipStream_t s, DiagIdx X, const uint8_t* TG, uint32_t* ecount) {
   uint32_t nt = grid_for(w1 - w0, TILE);
   if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
-  if (X.code)
-    hipLaunchKernelGGL(k_query_probe<true>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti,
-                       w0, w1, aligned ? 1 : 0, tile_rows, X, TG, ecount);
-  else
-    hipLaunchKernelGGL(k_query_probe<false>, dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g, qrec, qmulti,
-                       w0, w1, aligned ? 1 : 0, tile_rows, DiagIdx{nullptr, nullptr, 0}, nullptr,
-                       ecount);
+  // nontemporal slot reads for a table of more than NT_PROBE_BYTES.  A/B in one run
+  // (profiles/r5n_ab_ntslot_*): the 12-GB table of the 500 Mbp record 5.40 -> 5.20 ms per
+  // query, config 3's 2.4 GB +-0, config 2's 0.24 GB -4 % (its table lines are reused)
+  const bool ntl = (uint64_t)g.nb * g.capb * sizeof(Slot) > NT_PROBE_BYTES;
+  if (X.code) {
+    if (ntl)
+      hipLaunchKernelGGL((k_query_probe<true, true>), dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g,
+                         qrec, qmulti, w0, w1, aligned ? 1 : 0, tile_rows, X, TG, ecount);
+    else
+      hipLaunchKernelGGL((k_query_probe<true, false>), dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g,
+                         qrec, qmulti, w0, w1, aligned ? 1 : 0, tile_rows, X, TG, ecount);
+  } else {
+    hipLaunchKernelGGL((k_query_probe<false, false>), dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g,
+                       qrec, qmulti, w0, w1, aligned ? 1 : 0, tile_rows,
+                       DiagIdx{nullptr, nullptr, 0}, nullptr, ecount);
+  }
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
