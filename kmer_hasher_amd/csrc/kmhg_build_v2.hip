@@ -1187,7 +1187,44 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
   // contiguous runs of 6 slots ran 0.104 ms against 0.096 for the kernel)
   constexpr uint32_t SPT = (V2_CAPW + 1 + TB - 1) / TB;
   uint32_t cnt[SPT];
-  uint32_t cs = 0, occ = 0, mx = 0;
+  uint32_t cs = 0;
+#ifndef KMHG_NO_LEAN_COUNTS
+  // The bucket's distinct keys by ballots (no cross-lane shuffles: each __shfl_xor is an LDS
+  // permute, in a kernel bound by its LDS instructions); the count maximum and the pairs only
+  // when some key is repeated, which the i.i.d. buckets of a large build almost never have.
+  uint32_t occ_w = 0;                      // wave-uniform
+  bool multi = false;
+#pragma unroll
+  for (uint32_t q = 0; q < SPT; ++q) {
+    const uint32_t j = q * TB + threadIdx.x;
+    const uint32_t c = j <= V2_CAPW ? W.val[j] : 0u;
+    cnt[q] = c;
+    cs += c;
+    multi |= c > 1;
+    occ_w += (uint32_t)__popcll(__ballot(c != 0));
+  }
+  if (lane == 0) red[0][wave] = occ_w;
+  const bool has_multi = __syncthreads_or(multi);
+  if (has_multi) {                         // block-uniform
+    uint32_t mx = 0;
+    uint64_t pairs = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < SPT; ++q) {
+      mx = max(mx, cnt[q]);
+      pairs += (uint64_t)cnt[q] * (cnt[q] - (cnt[q] ? 1u : 0u)) / 2;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+      pairs += __shfl_xor(pairs, d);
+      mx = max(mx, (uint32_t)__shfl_xor(mx, d));
+    }
+    if (lane == 0) {
+      red[1][wave] = mx;
+      sh[NW + wave] = pairs;               // sh[NW..2NW): the block scan below uses sh[0..NW)
+    }
+    __syncthreads();
+  }
+#else
+  uint32_t occ = 0, mx = 0;
   uint64_t pairs = 0;
 #pragma unroll
   for (uint32_t q = 0; q < SPT; ++q) {
@@ -1210,6 +1247,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     sh[NW + wave] = pairs;                 // sh[NW..2NW): the block scan below uses sh[0..NW)
   }
   const bool has_multi = __syncthreads_or(mx > 1);
+#endif
   if (chk && edge[EW * NW]) {                // stream out of order at a wave / row boundary
     if (threadIdx.x == 0) atomicOr(&meta->overflow, 1u);
     return;
@@ -1234,10 +1272,18 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
     st.max_count = 0;
     st.n_pairs = 0;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      st.n_kmers += red[0][w];
-      st.max_count = max(st.max_count, red[1][w]);
-      st.n_pairs += sh[NW + w];
+    for (int w = 0; w < NW; ++w) st.n_kmers += red[0][w];
+#ifndef KMHG_NO_LEAN_COUNTS
+    if (!has_multi) {
+      st.max_count = st.n_kmers ? 1u : 0u;
+    } else
+#endif
+    {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        st.max_count = max(st.max_count, red[1][w]);
+        st.n_pairs += sh[NW + w];
+      }
     }
     bstats[b] = st;
   }
