@@ -587,6 +587,25 @@ __device__ __forceinline__ uint64_t block_excl_scan_n(uint64_t v, uint64_t* lds,
   return off + inc - v;
 }
 
+// The same for u32 values whose block total fits 32 bits, the wave scans by DPP (no LDS permutes).
+template <int NWV>
+__device__ __forceinline__ uint32_t block_excl_scan_n32(uint32_t v, uint64_t* lds, uint64_t& total) {
+  const int wid = threadIdx.x >> 6;
+  const uint32_t inc = wave_incl_scan_u32(v);
+  if (lane_id() == 63) lds[wid] = inc;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) {
+    const uint64_t x = lds[w];
+    if (w < wid) off += x;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return (uint32_t)off + inc - v;
+}
+
 // KEYS0: the first pass over a caller's key stream (a table rebuilt from keys): `kin` holds
 // exactly n keys (loads clamped, no pad) and positions are implicit (e + 1), so the stream is
 // neither copied nor paired with an iota array first.  NOPOS: keys only (count-only builds:
@@ -796,7 +815,11 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
       own += sum;
     }
     uint64_t tile_n;
+#ifndef KMHG_NO_DPP_SCAN
+    uint32_t run = block_excl_scan_n32<NWV>((uint32_t)own, sh, tile_n);   // own <= PTILE
+#else
     uint32_t run = (uint32_t)block_excl_scan_n<NWV>(own, sh, tile_n);
+#endif
 #pragma unroll
     for (int q = 0; q < DPT; ++q) {
       const uint32_t d = threadIdx.x * DPT + q;

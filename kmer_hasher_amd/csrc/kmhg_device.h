@@ -16,13 +16,48 @@ __device__ __forceinline__ void st_relaxed(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Inclusive wave scan (64 lanes).
+// DPP move of a u64 (both halves by the same lane pattern); lanes without a source, or in a row
+// the row mask leaves out, read 0
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROWS, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROWS, 0xf, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Inclusive wave scan (64 lanes, every lane active): row shifts by 1, 2, 4, 8 inside each
+// 16-lane row, then row broadcasts of lanes 15 and 31 -- VALU moves, where a __shfl_up chain is
+// six dependent LDS permutes (ds_bpermute) per 32-bit half.
+#ifndef KMHG_SHFL_SCAN
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+  v += dpp_u64<0x111, 0xf>(v);             // row_shr:1
+  v += dpp_u64<0x112, 0xf>(v);             // row_shr:2
+  v += dpp_u64<0x114, 0xf>(v);             // row_shr:4
+  v += dpp_u64<0x118, 0xf>(v);             // row_shr:8
+  v += dpp_u64<0x142, 0xa>(v);             // row_bcast:15 into rows 1 and 3
+  v += dpp_u64<0x143, 0xc>(v);             // row_bcast:31 into rows 2 and 3
+  return v;
+}
+#else
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     uint64_t t = __shfl_up(v, d);
     if (lane_id() >= d) v += t;
   }
+  return v;
+}
+#endif
+
+// Inclusive wave scan of u32 values by DPP row shifts and row broadcasts: six VALU adds, no LDS
+// permute (a __shfl_up is a ds_bpermute, an LDS round trip per step).  All 64 lanes must call it.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);   // row_bcast:31
   return v;
 }
 
