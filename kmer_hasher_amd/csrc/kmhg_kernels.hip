@@ -444,12 +444,13 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
       A.info[threadIdx.x] = make_uint2(count, aux);
     }
     int32_t v = count == 1 ? (int32_t)threadIdx.x : -1;   // max-scan over the anchor indices
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int32_t u = __shfl_up(v, d);
-      if (lane >= d) v = max(v, u);
-    }
+    // by DPP (identity -1 for lanes without a source): VALU moves, not LDS permutes
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
     if (is_anchor) A.last[threadIdx.x] = v;
   }
   __syncthreads();
