@@ -130,7 +130,7 @@ __device__ __forceinline__ void tile_compact(const bool (&flag)[J], uint64_t (&r
   if (wave == 0) {                       // lanes 0 .. J*NW-1 own one (j, wave) count each
     const uint64_t c = lane < J * NW ? cw[lane] : 0;
     const uint64_t inc = wave_incl_scan(c);
-    const uint64_t tot = __shfl(inc, 63);
+    const uint64_t tot = lane63(inc);
     const uint64_t x = lookback_excl(status, tile, tot);
     if (lane < J * NW) cw[lane] = x + inc - c;
   }

@@ -49,6 +49,15 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
 }
 #endif
 
+// lane 63's value in every lane (a scalar read, not an LDS permute)
+__device__ __forceinline__ uint64_t lane63(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+// the sum over the wave's 64 lanes, in every lane
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) { return lane63(wave_incl_scan(v)); }
+
 // Inclusive wave scan of u32 values by DPP row shifts and row broadcasts: six VALU adds, no LDS
 // permute (a __shfl_up is a ds_bpermute, an LDS round trip per step).  All 64 lanes must call it.
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
@@ -153,10 +162,7 @@ __device__ inline uint64_t lookback_excl(uint64_t* status, uint32_t tile, uint64
     int first2 = m2 ? __ffsll((unsigned long long)m2) - 1 : 64;
     uint64_t need = first2 == 64 ? ~0ull : ((2ull << first2) - 1ull);   // lanes 0..first2
     if (m0 & need) { __builtin_amdgcn_s_sleep(1); continue; }
-    uint64_t v = (lane <= first2) ? (w & LB_MASK) : 0ull;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    excl += v;
+    excl += wave_sum((lane <= first2) ? (w & LB_MASK) : 0ull);
     if (first2 < 64) break;
     base -= 64;
   }

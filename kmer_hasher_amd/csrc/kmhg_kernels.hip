@@ -930,8 +930,7 @@ k_read_order(const uint2* __restrict__ F, int64_t L, const Slot* __restrict__ T,
     const uint64_t cm = own ? wm[lane] : 0, cp = own ? wp[lane] : 0;
     const uint64_t ik = wave_incl_scan(ck), ir = wave_incl_scan(cr);
     const uint64_t im = wave_incl_scan(cm), ip = wave_incl_scan(cp);
-    const uint64_t tk_ = __shfl(ik, 63), tr = __shfl(ir, 63), tm = __shfl(im, 63),
-                   tp = __shfl(ip, 63);
+    const uint64_t tk_ = lane63(ik), tr = lane63(ir), tm = lane63(im), tp = lane63(ip);
     const uint64_t agga = (tk_ << 31) | tr;
     const uint64_t xa = lookback_excl(st_a, tile, agga);
     const uint64_t xb = lookback_excl(st_b, tile, tm);
