@@ -1392,6 +1392,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
 // V_stats: reduce the per-bucket partials (grid-stride, one atomic per workgroup; meta was
 // zeroed by V_hist0).  The last workgroup to finish copies the totals into `host_meta`, a
 // pinned host record, so the host reads them without a copy launch.
+constexpr int STATS_PER = 8;
 __global__ void __launch_bounds__(BLOCK)
 k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __restrict__ n_valid,
            BuildMeta* __restrict__ meta, BuildMeta* __restrict__ host_meta) {
@@ -1399,17 +1400,26 @@ k_v2_stats(const BucketStats* __restrict__ bs, uint32_t nb, const uint32_t* __re
   __shared__ uint32_t sm[4];
   uint64_t u = 0, p = 0;
   uint32_t m = 0;
-  for (uint32_t b = blockIdx.x * BLOCK + threadIdx.x; b < nb; b += gridDim.x * BLOCK) {
-    const BucketStats x = bs[b];
-    u += x.n_kmers;
-    p += x.n_pairs;
-    m = max(m, x.max_count);
+  // STATS_PER buckets per thread and trip, their loads all in flight before any is summed (a
+  // plain grid-stride loop waits out one load latency per bucket)
+  const uint32_t stride = gridDim.x * BLOCK;
+  for (uint32_t b0 = blockIdx.x * BLOCK + threadIdx.x; b0 < nb; b0 += stride * STATS_PER) {
+    BucketStats x[STATS_PER];
+#pragma unroll
+    for (int q = 0; q < STATS_PER; ++q) {
+      const uint32_t b = b0 + q * stride;
+      x[q] = b < nb ? bs[b] : BucketStats{0u, 0u, 0ull};
+    }
+#pragma unroll
+    for (int q = 0; q < STATS_PER; ++q) {
+      u += x[q].n_kmers;
+      p += x[q].n_pairs;
+      m = max(m, x[q].max_count);
+    }
   }
-  for (int d = 32; d >= 1; d >>= 1) {
-    u += __shfl_xor(u, d);
-    p += __shfl_xor(p, d);
-    m = max(m, (uint32_t)__shfl_xor(m, d));
-  }
+  u = wave_sum(u);
+  p = wave_sum(p);
+  m = (uint32_t)lane63(wave_incl_max(m));
   const int w = threadIdx.x >> 6;
   if (lane_id() == 0) { su[w] = u; sp[w] = p; sm[w] = m; }
   __syncthreads();
@@ -1780,7 +1790,10 @@ void launch_v2_test_disorder(uint32_t* pos, uint32_t* start, const uint32_t* n_p
 }
 void launch_v2_stats(const BucketStats* bstats, uint32_t nb, const uint32_t* n_valid,
                      BuildMeta* meta, BuildMeta* host_meta, hipStream_t s) {
-  unsigned gr = grid_of(nb, BLOCK * 8);
+  // one bucket per thread up to 64 workgroups (config 2: 40), then STATS_PER per trip
+  // (measured: 5 workgroups of 8 buckets per thread 6.1 us at config 2, 40 of one 4.8; 256
+  // workgroups at config 3 16 us against 9 -- their device atomics and arrival tickets)
+  unsigned gr = grid_of(nb, BLOCK);
   if (gr > 64) gr = 64;
   hipLaunchKernelGGL(k_v2_stats, dim3(gr), dim3(BLOCK), 0, s, bstats, nb, n_valid, meta, host_meta);
 }
