@@ -1550,9 +1550,20 @@ void launch_v2_hist0(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, D
 // scan (three launches of reduce-then-scan before), config 2's 0.5 M 7.7 -> 7.0 us.
 void launch_scan_u32(uint32_t* a, uint64_t n, uint64_t* status, uint32_t* total, hipStream_t s) {
   const uint32_t nt = grid_of(n, TILE);
+  // entries per thread by length (round 5, `profiles/r5n_scan_width_build_only.txt`): config 2's
+  // 0.5 M entries 16 per thread (7.3 -> 6.1 us per scan against 32), config 3's 15 M 64 per
+  // thread (59 -> 51 us): a short array wants more workgroups, a long one a shorter look-back
   if (nt > 64) {
-    const uint32_t nt32 = grid_of(n, BLOCK * 32);
-    hipLaunchKernelGGL(k_scan_lb_u32<32>, dim3(nt32), dim3(BLOCK), 0, s, a, n, status, nt32, total);
+    if (n < (1ull << 21)) {
+      const uint32_t t16 = grid_of(n, BLOCK * 16);
+      hipLaunchKernelGGL(k_scan_lb_u32<16>, dim3(t16), dim3(BLOCK), 0, s, a, n, status, t16, total);
+    } else if (n < (1ull << 23)) {
+      const uint32_t t32 = grid_of(n, BLOCK * 32);
+      hipLaunchKernelGGL(k_scan_lb_u32<32>, dim3(t32), dim3(BLOCK), 0, s, a, n, status, t32, total);
+    } else {
+      const uint32_t t64 = grid_of(n, BLOCK * 64);
+      hipLaunchKernelGGL(k_scan_lb_u32<64>, dim3(t64), dim3(BLOCK), 0, s, a, n, status, t64, total);
+    }
   } else {
     hipLaunchKernelGGL(k_scan_lb_u32<WPT>, dim3(nt), dim3(BLOCK), 0, s, a, n, status, nt, total);
   }
