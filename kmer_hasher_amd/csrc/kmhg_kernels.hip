@@ -690,9 +690,10 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   if (threadIdx.x == 0) tile_rows[tile] = tot;
 }
 
-// Exclusive scan of n per-tile u64 totals in one workgroup (n = tiles, at most ~1M).
+// Exclusive scan of n per-tile u64 totals in one workgroup, any n (the fallback beyond
+// SCAN1_MAX: serial loads per thread, a Hillis-Steele pass over 1024 partials).
 __global__ void __launch_bounds__(1024)
-k_scan_tiles_u64(uint64_t* __restrict__ a, uint32_t n, uint64_t* __restrict__ total) {
+k_scan_tiles_u64_any(uint64_t* __restrict__ a, uint32_t n, uint64_t* __restrict__ total) {
   __shared__ uint64_t part[1024];
   const uint32_t per = (n + 1023) / 1024;
   const uint32_t i0 = threadIdx.x * per, i1 = min(n, i0 + per);
@@ -700,7 +701,7 @@ k_scan_tiles_u64(uint64_t* __restrict__ a, uint32_t n, uint64_t* __restrict__ to
   for (uint32_t i = i0; i < i1; ++i) s += a[i];
   part[threadIdx.x] = s;
   __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {      // Hillis-Steele over 1024 partials
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
     uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
     __syncthreads();
     part[threadIdx.x] += v;
@@ -709,6 +710,44 @@ k_scan_tiles_u64(uint64_t* __restrict__ a, uint32_t n, uint64_t* __restrict__ to
   uint64_t run = part[threadIdx.x] - s;
   for (uint32_t i = i0; i < i1; ++i) { uint64_t x = a[i]; a[i] = run; run += x; }
   if (threadIdx.x == 1023) *total = part[1023];
+}
+
+// Exclusive scan of n <= SCAN1_MAX per-tile u64 totals in one workgroup.
+__global__ void __launch_bounds__(1024)
+k_scan_tiles_u64(uint64_t* __restrict__ a, uint32_t n, uint64_t* __restrict__ total) {
+  // thread t owns entries [t per, t per + per), per <= SCAN1_MAX / 1024, all loaded at once; the
+  // wave scans by DPP, the 16 wave totals by one more wave scan (was: a serial load loop and a
+  // Hillis-Steele pass over 1024 partials, 20 barriers)
+  constexpr int MAXPER = (int)(SCAN1_MAX / 1024);
+  __shared__ uint64_t wtot[16];
+  const uint32_t per = (n + 1023) / 1024;
+  const uint32_t i0 = threadIdx.x * per;
+  uint64_t v[MAXPER];
+  uint64_t s = 0;
+#pragma unroll
+  for (int j = 0; j < MAXPER; ++j) {
+    v[j] = ((uint32_t)j < per && i0 + j < n) ? a[i0 + j] : 0ull;
+    s += v[j];
+  }
+  const int wave = threadIdx.x >> 6;
+  const uint64_t inc = wave_incl_scan(s);
+  if (lane_id() == 63) wtot[wave] = inc;
+  __syncthreads();
+  if (wave == 0) {
+    const uint64_t w = lane_id() < 16 ? wtot[lane_id()] : 0ull;
+    const uint64_t wi = wave_incl_scan(w);
+    if (lane_id() < 16) wtot[lane_id()] = wi - w;       // exclusive wave offsets
+    if (lane_id() == 15) *total = wi;
+  }
+  __syncthreads();
+  uint64_t run = wtot[wave] + inc - s;
+#pragma unroll
+  for (int j = 0; j < MAXPER; ++j) {
+    if ((uint32_t)j < per && i0 + j < n) {
+      a[i0 + j] = run;
+      run += v[j];
+    }
+  }
 }
 
 // Long u64 scans (many query tiles, e.g. 244K for a 500 Mbp query): reduce-then-scan over
@@ -1264,7 +1303,10 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
   }
 }
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
+  if (n <= SCAN1_MAX)
+    hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);
+  else
+    hipLaunchKernelGGL(k_scan_tiles_u64_any, dim3(1), dim3(1024), 0, s, a, n, total);
 }
 void launch_scan_u64(uint64_t* a, uint64_t n, uint64_t* total, uint64_t* scratch, hipStream_t s) {
   if (n <= SCAN1_MAX) {
