@@ -364,7 +364,8 @@ k_v2_hist(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr,
 // latency (config 2: 14.5 us for 40 MB).  `in` holds n + PTILE elements (the passes' padded
 // streams), so whole-tile loads stay inside it.
 // MODE: 0 = u64 keys, 1 = u32 bucket ids, 2 = packed 12-B {key lo, key hi, pos} elements (the
-// position builds' key streams), 3 = packed 8-B elements (Pack8: the key is e >> sh).
+// position builds' key streams), 3 = packed 8-B elements (Pack8: the key is e >> sh), 4 = the
+// previous pass's digit stream (u16 digits, DS in V_scatter), 5 = the same in u8 digits.
 template <int MODE>
 __global__ void __launch_bounds__(BLOCK)
 k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
@@ -417,11 +418,17 @@ k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, 
     }
     return;
   }
-  constexpr int NV = MODE == 1 ? 2 : 4;                // 16-B loads per thread per tile
+  constexpr bool DIG = MODE == 4, DIG8 = MODE == 5;
+  constexpr int NV = DIG || DIG8 ? 1 : MODE == 1 ? 2 : 4;   // 16-B loads per thread per tile
   uint4 nx[NV];
   auto prefetch = [&](uint32_t tile) {
+    if constexpr (DIG8) {                              // 8 u8 digits: one 8-B load
+      const uint2 v = reinterpret_cast<const uint2*>(in)[(uint64_t)tile * (PTILE / 8) + threadIdx.x];
+      nx[0] = make_uint4(v.x, v.y, 0u, 0u);
+      return;
+    }
     const uint4* src = reinterpret_cast<const uint4*>(in) +
-                       ((uint64_t)tile * PTILE + 8u * threadIdx.x) / (BID ? 4 : 2);
+                       ((uint64_t)tile * PTILE + 8u * threadIdx.x) / (DIG ? 8 : BID ? 4 : 2);
 #pragma unroll
     for (int v = 0; v < NV; ++v) nx[v] = src[v];
   };
@@ -438,7 +445,14 @@ k_v2_histp(const uint64_t* __restrict__ in, const uint32_t* __restrict__ n_ptr, 
     for (int j = 0; j < 8; ++j) {
       if (e0 + j < n) {
         uint32_t dg;
-        if (BID) {
+        if (DIG8) {
+          const uint32_t wj = (j >> 2) == 0 ? cur[0].x : cur[0].y;
+          dg = (wj >> (8 * (j & 3))) & 0xFFu;
+        } else if (DIG) {
+          const uint4 w = cur[0];
+          const uint32_t wj = (j >> 1) == 0 ? w.x : (j >> 1) == 1 ? w.y : (j >> 1) == 2 ? w.z : w.w;
+          dg = (j & 1) ? wj >> 16 : wj & 0xFFFFu;
+        } else if (BID) {
           const uint4 w = cur[j >> 2];
           const uint32_t id = (j & 3) == 0 ? w.x : (j & 3) == 1 ? w.y : (j & 3) == 2 ? w.z : w.w;
           dg = digit_of_b(id, D);
@@ -626,14 +640,17 @@ __device__ __forceinline__ uint32_t block_excl_scan_n32(uint32_t v, uint64_t* ld
 // 1.09 -> 0.87 ms, radix 79 0.72 -> 0.61 ms.
 // BALLOT: stable ranks from one ballot per digit bit instead of the count atomics' lane-ordered
 // returns -- chosen at run time where the device self-check finds that order violated.
-template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false, int BM = 0, bool BALLOT = false>
+// DS (digit stream): the pass also writes every element's digit of the NEXT pass (u16, at the
+// element's place in the output), which that pass's histogram reads instead of the keys.
+template <bool FROM_SEQ, bool KEYS0 = false, bool NOPOS = false, int BM = 0, bool BALLOT = false,
+          bool DS = false>
 __global__ void __launch_bounds__(SC_NWV * 64)
 k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
              const uint64_t* __restrict__ kin, const uint32_t* __restrict__ pin,
              const uint32_t* __restrict__ n_ptr, Geom g, Digit D,
              const uint32_t* __restrict__ hist, uint32_t ntiles,
              uint64_t* __restrict__ kout, uint32_t* __restrict__ pout, uint32_t pad,
-             int skip_empty, BoundsFuse bf, Pack8 pk) {
+             int skip_empty, BoundsFuse bf, Pack8 pk, DigitOut dso) {
   constexpr bool BIDS = BM == 1 || BM == 2;      // bucket-id streams
   constexpr bool AOS = BM == 3 || BM == 4 || BM == 7;   // packed 12-B (key, pos) elements out
   constexpr bool AIN = BM == 3;                   // ... and in
@@ -641,6 +658,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
   constexpr bool P8IN = BM == 7;                  // ... in
   using KT = typename std::conditional<BIDS, uint32_t, uint64_t>::type;
   using SL = ScatterLDS<KT>;
+  static_assert(!DS || !BIDS, "digit streams follow key streams");
   static_assert(BM == 0 || !NOPOS, "bucket-id and packed streams carry positions");
   static_assert(!(AOS && KEYS0), "packed streams start from the sequence");
   // KEYS0 with BM: the first pass over V_hist0's per-window bucket ids (~0: not indexed)
@@ -725,6 +743,10 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
       if (BM != 2) koutT[pad + threadIdx.x] = 0;
       if (!NOPOS && !P8OUT) pout[pad + threadIdx.x] = 0;
     }
+    if constexpr (DS) {
+      if (dso.out8) dso.out8[pad + threadIdx.x] = 0;
+      else dso.out[pad + threadIdx.x] = 0;
+    }
   }
   for (uint32_t it = 0; it < n_iter; ++it) {
     const uint32_t tile = tile_at(it);
@@ -781,7 +803,8 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
         dg[c] = act[c] ? digit_of_b((uint32_t)key[c], D) : 0;
       } else {
         act[c] = e < n && !(KEYS0 && skip_empty && key[c] == EMPTY_KEY);
-        dg[c] = act[c] ? digit_of_h(mix64((uint64_t)key[c]), g, D) : 0;
+        const uint64_t hk = mix64((uint64_t)key[c]);
+        dg[c] = act[c] ? digit_of_h(hk, g, D) : 0;
       }
     }
     if (!BALLOT) {
@@ -883,6 +906,12 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
       } else {
         if (BM != 2) koutT[dst] = S.skey[i];
         if (!NOPOS && !P8OUT) pout[dst] = S.spos[i];
+      }
+      if constexpr (DS) {       // the next pass's digit, from the staged key (no more LDS)
+        const uint64_t kk = P8OUT ? (uint64_t)S.skey[i] >> pk.sh : (uint64_t)S.skey[i];
+        const uint32_t dnx = digit_of(kk, g, dso.Dn);
+        if (dso.out8) dso.out8[dst] = (uint8_t)dnx;
+        else dso.out[dst] = (uint16_t)dnx;
       }
     }
   }
@@ -1503,19 +1532,26 @@ static inline unsigned grid_of(uint64_t n, unsigned per) {
 // kernels.  KMHG_TEST_BALLOT=1 (tests) forces them.
 bool ballot_ranks();
 
-#define KMHG_SCATTER_BM(FS, K0, NP, BM, ...)                                                  \
+#define KMHG_SCATTER_X(FS, K0, NP, BM, DSF, DSO, ...)                                         \
   do {                                                                                       \
     if (ballot_ranks()) {                                                                    \
-      static const unsigned cap_ = resident_blocks((const void*)k_v2_scatter<FS, K0, NP, BM, true>, \
-                                                   SC_NWV * 64);                             \
-      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, BM, true>), dim3(std::min(ntiles, cap_)),  \
-                         dim3(SC_NWV * 64), 0, s, __VA_ARGS__);                              \
+      static const unsigned cap_ =                                                           \
+          resident_blocks((const void*)k_v2_scatter<FS, K0, NP, BM, true, DSF>, SC_NWV * 64); \
+      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, BM, true, DSF>), dim3(std::min(ntiles, cap_)), \
+                         dim3(SC_NWV * 64), 0, s, __VA_ARGS__, DSO);                         \
     } else {                                                                                 \
-      static const unsigned cap_ = resident_blocks((const void*)k_v2_scatter<FS, K0, NP, BM, false>, \
-                                                   SC_NWV * 64);                             \
-      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, BM, false>), dim3(std::min(ntiles, cap_)), \
-                         dim3(SC_NWV * 64), 0, s, __VA_ARGS__);                              \
+      static const unsigned cap_ =                                                           \
+          resident_blocks((const void*)k_v2_scatter<FS, K0, NP, BM, false, DSF>, SC_NWV * 64); \
+      hipLaunchKernelGGL((k_v2_scatter<FS, K0, NP, BM, false, DSF>), dim3(std::min(ntiles, cap_)), \
+                         dim3(SC_NWV * 64), 0, s, __VA_ARGS__, DSO);                         \
     }                                                                                        \
+  } while (0)
+#define KMHG_SCATTER_BM(FS, K0, NP, BM, ...) KMHG_SCATTER_X(FS, K0, NP, BM, false, kNoDigits, __VA_ARGS__)
+// the same pass also writing the next pass's digits (dso)
+#define KMHG_SCATTER_BMD(FS, K0, NP, BM, DSO, ...)                                            \
+  do {                                                                                       \
+    if (DSO.out || DSO.out8) KMHG_SCATTER_X(FS, K0, NP, BM, true, DSO, __VA_ARGS__);                      \
+    else KMHG_SCATTER_X(FS, K0, NP, BM, false, kNoDigits, __VA_ARGS__);                       \
   } while (0)
 #define KMHG_SCATTER(FS, K0, NP, ...) KMHG_SCATTER_BM(FS, K0, NP, 0, __VA_ARGS__)
 
@@ -1576,6 +1612,21 @@ void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Dig
                      reinterpret_cast<const uint64_t*>(bids), n_ptr, g, D, hist, ntiles,
                      scan_status, n_status, save_col0, 0);
 }
+void launch_v2_hist_digits(const void* digits, bool u8, const uint32_t* n_ptr, Geom g, Digit D,
+                           uint32_t* hist, uint32_t ntiles, uint64_t* scan_status,
+                           uint32_t n_status, hipStream_t s, uint32_t* save_col0) {
+  if (u8) {
+    static const unsigned cap = resident_blocks((const void*)k_v2_histp<5>);
+    hipLaunchKernelGGL(k_v2_histp<5>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0, s,
+                       reinterpret_cast<const uint64_t*>(digits), n_ptr, g, D, hist, ntiles,
+                       scan_status, n_status, save_col0, 0);
+    return;
+  }
+  static const unsigned cap = resident_blocks((const void*)k_v2_histp<4>);
+  hipLaunchKernelGGL(k_v2_histp<4>, dim3(std::min<unsigned>(ntiles, cap)), dim3(BLOCK), 0, s,
+                     reinterpret_cast<const uint64_t*>(digits), n_ptr, g, D, hist, ntiles,
+                     scan_status, n_status, save_col0, 0);
+}
 void launch_v2_hist(const uint64_t* keys, const uint32_t* n_ptr, Geom g, Digit D, uint32_t* hist,
                     uint32_t ntiles, uint64_t* scan_status, uint32_t n_status, hipStream_t s,
                     uint32_t* hll_rows, uint32_t* hll_regs, uint32_t* save_col0, bool skip_empty,
@@ -1632,16 +1683,18 @@ static const BoundsFuse kNoFuse{nullptr, nullptr, nullptr, Digit{}, 0u, 1u, 0, 0
 static const Pack8 kNoPack{0, nullptr, 0u, Digit{}};
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
-                           uint32_t pad, hipStream_t s, bool aos, const Pack8* pk) {
+                           uint32_t pad, hipStream_t s, bool aos, const Pack8* pk,
+                           const DigitOut* ds) {
+  const DigitOut dso = ds ? *ds : kNoDigits;
   if (pk && pk->sh)
-    KMHG_SCATTER_BM(true, false, false, 6, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist,
-                    ntiles, kout, nullptr, pad, 0, kNoFuse, *pk);
+    KMHG_SCATTER_BMD(true, false, false, 6, dso, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D,
+                     hist, ntiles, kout, nullptr, pad, 0, kNoFuse, *pk);
   else if (aos)
-    KMHG_SCATTER_BM(true, false, false, 3, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist,
-                    ntiles, kout, nullptr, pad, 0, kNoFuse, kNoPack);
+    KMHG_SCATTER_BMD(true, false, false, 3, dso, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D,
+                     hist, ntiles, kout, nullptr, pad, 0, kNoFuse, kNoPack);
   else
-    KMHG_SCATTER(true, false, false, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D, hist, ntiles,
-                 kout, pout, pad, 0, kNoFuse, kNoPack);
+    KMHG_SCATTER_BMD(true, false, false, 0, dso, seq, L, k, Nw, nullptr, nullptr, nullptr, g, D,
+                     hist, ntiles, kout, pout, pad, 0, kNoFuse, kNoPack);
 }
 void launch_part_dense(const uint64_t* ck, const uint32_t* cp, const uint32_t* off,
                        uint32_t ntiles, const uint32_t* n_total, uint64_t* dk, uint32_t* dp,
@@ -1681,19 +1734,22 @@ void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint3
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,
                        uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf,
-                       bool aos, bool aos_in, const Pack8* pk) {
-  if (pk && pk->sh)            // packed 8-B elements in, packed 12-B out
+                       bool aos, bool aos_in, const Pack8* pk, const DigitOut* ds) {
+  const DigitOut dso = ds ? *ds : kNoDigits;
+  if (pk && pk->sh)            // packed 8-B elements in, packed 12-B out (a last pass)
     KMHG_SCATTER_BM(false, false, false, 7, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr,
                     n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, *pk);
   else if (aos && aos_in)
-    KMHG_SCATTER_BM(false, false, false, 3, nullptr, (int64_t)0, 0, (int64_t)0, kin, nullptr,
-                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, kNoPack);
+    KMHG_SCATTER_BMD(false, false, false, 3, dso, nullptr, (int64_t)0, 0, (int64_t)0, kin,
+                     nullptr, n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0,
+                     bf ? *bf : kNoFuse, kNoPack);
   else if (aos)
-    KMHG_SCATTER_BM(false, false, false, 4, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin,
-                    n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse, kNoPack);
+    KMHG_SCATTER_BMD(false, false, false, 4, dso, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin,
+                     n_ptr, g, D, hist, ntiles, kout, nullptr, pad, 0, bf ? *bf : kNoFuse,
+                     kNoPack);
   else
-    KMHG_SCATTER(false, false, false, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin, n_ptr, g, D,
-                 hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse, kNoPack);
+    KMHG_SCATTER_BMD(false, false, false, 0, dso, nullptr, (int64_t)0, 0, (int64_t)0, kin, pin,
+                     n_ptr, g, D, hist, ntiles, kout, pout, pad, 0, bf ? *bf : kNoFuse, kNoPack);
 }
 void launch_v2_scatter_keys0(const uint64_t* kin, uint64_t n_keys, const uint32_t* n_ptr, Geom g,
                              Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout,

@@ -940,7 +940,23 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // passes, radix 79) 18.2 -> 18.6 ms (histograms 1.9 -> 2.8 ms, scatters 11.2 -> 10.3), A/B
   // in one run (profiles/r5b_ab_aos_config3.log, r5c_ab_aos_config5.log).
   constexpr uint32_t AOS_MIN_RADIX = 160;
-  auto packed = [&](int p) { return aos && (p + 1 == (int)passes || R >= AOS_MIN_RADIX); };
+  // Digit streams (DS): each pass before the last also writes every output element's digit of
+  // the next pass (u8 up to radix 256, else u16), and that pass's histogram reads 1-2 B per
+  // element instead of the keys -- which also takes away the reason to leave the middle streams
+  // unpacked.  The digit writes are short scattered runs (PTILE / R elements per tile and
+  // digit), so they pay only at a low radix.  Measured (A/B in one run, profiles/r5y_ab_ds_*):
+  // the 500 Mbp build (3 passes, radix 79) 18.37 -> 16.82 ms with u8 digits (17.75 with u16;
+  // histograms 1.93 -> 0.48 ms); config 3 (2 passes, radix 313, u16) 2.81 -> 2.93 ms (histogram
+  // -0.11 ms, first scatter +0.22).  Sequence builds with positions on key streams below
+  // AOS_MIN_RADIX; KMHG_DIGIT_STREAM=0 / 1 forces off / on, KMHG_DS_U8=0 u16 digits.
+  const char* dse = std::getenv("KMHG_DIGIT_STREAM");
+  const bool ds_on = !bid && !from_keys && !count_only && passes >= 2 &&
+                     (dse && dse[0] ? dse[0] == '1' : R < AOS_MIN_RADIX);
+  const char* dpe = std::getenv("KMHG_DS_PACK");
+  const bool ds_pack = ds_on && !(dpe && dpe[0] == '0');
+  auto packed = [&](int p) {
+    return aos && (p + 1 == (int)passes || R >= AOS_MIN_RADIX || ds_pack);
+  };
   // Pack8 (two-pass builds of small k: 2k <= 52): the first pass writes 8-B elements, key << sh
   // | the window's index inside its segment of 2^sh windows (sh = 64 - 2k), and the second pass
   // restores the position from the element's place in the stream (k_seg_bounds' table).  The
@@ -973,6 +989,14 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   DBuf<uint32_t> hist(nhist, s);
   DBuf<uint32_t> start((uint64_t)nb + 1, s);
   DBuf<uint32_t> segb(pack8 ? (uint64_t)R * (nseg8 + 1) : 1, s);
+  // one digit buffer: pass p's histogram has read it before pass p rewrites it for pass p + 1
+  // u8 digits at a radix <= 256 (KMHG_DS_U8=0: u16, A/B)
+  const char* d8e = std::getenv("KMHG_DS_U8");
+  const bool ds8 = ds_on && R <= 256 && !(d8e && d8e[0] == '0');
+  DBuf<uint16_t> dsb(ds_on ? ((uint64_t)Nw + PTILE + 8) / (ds8 ? 2 : 1) + 8 : 1, s);
+  uint8_t* ds8p = ds8 ? reinterpret_cast<uint8_t*>(dsb.p) : nullptr;
+  uint16_t* ds16p = ds8 ? nullptr : dsb.p;
+  bool ds_ready = false;                                  // dsb holds the next pass's digits
   const Pack8 pk8{pack8 ? sh8 : 0, segb.p, nseg8, make_digit(1, R)};
   // scratch (zeroed in-kernel by V_hist0 / V_hist, no memset): [n_valid][meta][scan status]
   const size_t off_meta = 64, off_status = 128;
@@ -1040,9 +1064,12 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
                launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ntiles,
                                       passes == 1 ? nullptr : bA.p, pA.p, pad, s));
       } else {
+        const DigitOut ds0{ds16p, make_digit(R, R), ds8p};
         LAUNCH("k_v2_scatter_seq", s,
                launch_v2_scatter_seq(d_seq, L, k, Nw, g, make_digit(1, R), hist.p, ntiles, kA.p,
-                                     pA.p, pad, s, packed(0), pack8 ? &pk8 : nullptr));
+                                     pA.p, pad, s, packed(0), pack8 ? &pk8 : nullptr,
+                                     ds_on ? &ds0 : nullptr));
+        ds_ready = ds_on;
         // the segment table, before pass 1's histogram overwrites pass 0's
         if (pack8)
           LAUNCH("k_seg_bounds", s,
@@ -1131,12 +1158,17 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     const bool last = p + 1 == passes;
     const uint64_t* src = keys0 ? d_keys : kin;
     const bool hll = co_auto && p == 0;
-    LAUNCH("k_v2_hist", s,
-           launch_v2_hist(src, n_valid, g, Dp, hp, C, status, nst, s,
-                          hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
-                          p == 1 ? save1 : nullptr, keys0 && skip_empty,
-                          /*padded=*/!keys0, !keys0 && packed((int)p - 1),
-                          pack8 && p == 1 ? sh8 : 0));
+    if (ds_ready)
+      LAUNCH("k_v2_hist", s,
+             launch_v2_hist_digits(dsb.p, ds8, n_valid, g, Dp, hp, C, status, nst, s,
+                                   p == 1 ? save1 : nullptr));
+    else
+      LAUNCH("k_v2_hist", s,
+             launch_v2_hist(src, n_valid, g, Dp, hp, C, status, nst, s,
+                            hll ? hll_rows.p : nullptr, hll ? hll_regs.p : nullptr,
+                            p == 1 ? save1 : nullptr, keys0 && skip_empty,
+                            /*padded=*/!keys0, !keys0 && packed((int)p - 1),
+                            pack8 && p == 1 ? sh8 : 0));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hp, nh, status, n_valid, s));
     if (hll) {   // after the scan: the estimate travels with the valid key count
       LAUNCH("k_v2_hll", s, launch_v2_hll(hll_rows.p, ntiles, hll_regs.p,
@@ -1154,11 +1186,15 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
         LAUNCH("k_v2_scatter", s,
                launch_v2_scatter_nopos(kin, n_valid, g, Dp, hp, C, kout, pad, s,
                                        fused(p) ? &lv : nullptr));
-      else
+      else {
+        const DigitOut dsn{ds16p, make_digit(div * R, R), ds8p};
         LAUNCH("k_v2_scatter", s,
                launch_v2_scatter(kin, pin, n_valid, g, Dp, hp, C, kout, pout, pad, s,
                                  fused(p) ? &lv : nullptr, packed((int)p), packed((int)p - 1),
-                                 pack8 && p == 1 ? &pk8 : nullptr));
+                                 pack8 && p == 1 ? &pk8 : nullptr,
+                                 ds_on && !last ? &dsn : nullptr));
+      }
+      ds_ready = ds_on && !last;
       if (p >= 1 && !fused(p) && !last) launch_level(lv);
     }
     std::swap(kin, kout);

@@ -213,6 +213,18 @@ void launch_v2_hll(const uint32_t* hll_rows, uint32_t n_rows, uint32_t* hll_regs
 // is read only by the next level or the bucket kernel, so the pass's workgroups each compute
 // the starts of a few lower-digit values before their tiles (no launch, no key pass).
 // start == nullptr: not fused.
+// A radix pass's digit stream (DS): out[i] = the next pass's digit of output element i (u16,
+// or u8 in out8 for a radix <= 256; n + PTILE entries), which the next pass's histogram reads
+// (launch_v2_hist_digits) instead of the keys: 1-2 B per element instead of 8 or 12.
+struct DigitOut {
+  uint16_t* out;
+  Digit Dn;
+  uint8_t* out8 = nullptr;
+};
+constexpr DigitOut kNoDigits{nullptr, Digit{}, nullptr};
+void launch_v2_hist_digits(const void* digits, bool u8, const uint32_t* n_ptr, Geom g, Digit D,
+                           uint32_t* hist, uint32_t ntiles, uint64_t* scan_status,
+                           uint32_t n_status, hipStream_t s, uint32_t* save_col0 = nullptr);
 // Packed 8-B elements of a small-k key stream (the first pass of a two-pass build with 2k <= 53):
 // the high 2k bits hold the key, the low sh = 64 - 2k bits the window's index inside its segment
 // of 2^sh windows.  The segment comes back from the element's place in the stream: pass 0 writes
@@ -239,7 +251,7 @@ struct BoundsFuse {
 void launch_v2_scatter_seq(const uint8_t* seq, int64_t L, int k, int64_t Nw, Geom g, Digit D,
                            const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                            uint32_t pad, hipStream_t s, bool aos = false,
-                           const Pack8* pk = nullptr);
+                           const Pack8* pk = nullptr, const DigitOut* ds = nullptr);
 // first pass over a caller's key stream of n_keys keys (>= 1): positions are e + 1; nopos:
 // keys only (count-only builds), pout unused; skip_empty: EMPTY_KEY entries are not keys (padded
 // read k-mer streams, k <= 31)
@@ -253,7 +265,8 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
 void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t* n_ptr, Geom g,
                        Digit D, const uint32_t* hist, uint32_t ntiles, uint64_t* kout, uint32_t* pout,
                        uint32_t pad, hipStream_t s, const BoundsFuse* bf = nullptr,
-                       bool aos = false, bool aos_in = true, const Pack8* pk = nullptr);
+                       bool aos = false, bool aos_in = true, const Pack8* pk = nullptr,
+                       const DigitOut* ds = nullptr);
 // Packed key streams (aos): position builds on key streams carry each window as ONE 12-B
 // element {key lo, key hi, pos} (kout holds n + PTILE of them; pout unused), so a tile's digit
 // run is one contiguous write; aos_in: the input is packed too (else kin / pin arrays).

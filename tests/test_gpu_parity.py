@@ -262,7 +262,7 @@ def test_stream_disorder_falls_back(gpu):
     assert r.stdout.count("ok ") == 6, r.stdout
 
 
-@pytest.mark.parametrize("stream", ["bid", "keys", "keys-levels"])
+@pytest.mark.parametrize("stream", ["bid", "keys", "keys-levels", "keys-digits"])
 @pytest.mark.parametrize("ranks", ["lane", "ballot"])
 @pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
 def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, ranks, stream):
@@ -273,12 +273,15 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, ranks, stream):
     lower-digit value; a zero-width tile at a tile boundary), each level inside its pass's
     scatter, or launched on its own (keys-levels: KMHG_FUSE_BOUNDS=0).  Position builds carry
     bucket ids through the passes and cut the keys from the code words (default up to 12 M
-    windows); KMHG_BUILD_BID=0 carries the keys.  Ranks by the LDS atomics' lane order and by
-    ballots (KMHG_TEST_BALLOT=1)."""
+    windows); KMHG_BUILD_BID=0 carries the keys.  Key streams below radix 160 carry digit
+    streams by default (each pass writes the next pass's digits, which its histogram reads):
+    keys-levels turns them off (KMHG_DIGIT_STREAM=0), keys-digits forces them at every radix.
+    Ranks by the LDS atomics' lane order and by ballots (KMHG_TEST_BALLOT=1)."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_MAXR", maxr)
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
     monkeypatch.setenv("KMHG_FUSE_BOUNDS", "0" if stream == "keys-levels" else "1")
+    monkeypatch.setenv("KMHG_DIGIT_STREAM", {"keys-levels": "0", "keys-digits": "1"}.get(stream, ""))
     monkeypatch.setenv("KMHG_TEST_BALLOT", "1" if ranks == "ballot" else "0")
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
     _check_against_oracle(s, 31, pairs=False)
