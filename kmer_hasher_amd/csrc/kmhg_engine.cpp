@@ -34,7 +34,8 @@
 // build / query / counts path against the oracle (KMHG_BUILD, KMHG_BUILD_BID, KMHG_MAXR,
 // KMHG_FUSE_BOUNDS, KMHG_TEST_BALLOT, KMHG_QUERY_TAGS, KMHG_QUERY_DIAG, KMHG_DIAG_CODES,
 // KMHG_COUNT_TABLE, KMHG_COUNT_WALK, KMHG_CO_SPREAD, KMHG_CO_GLOBAL, KMHG_PART_COMPACT,
-// KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_NB_ROUND, KMHG_SLICE_POISON, KMHG_TEST_REPLICA) choose
+// KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_NB_ROUND, KMHG_SLICE_POISON, KMHG_TEST_REPLICA,
+// KMHG_DIGIT_STREAM, KMHG_DS_U8, KMHG_DS_PACK) choose
 // between equivalent paths and change no result.
 // Fault injection (KMHG_TEST_DISORDER) and the A/B-only switches (KMHG_D2H, KMHG_COUNT_BID,
 // KMHG_RK_CAP) exist only in the test build (-DKMHG_TEST_BUILD: libkmhgpu_test.so, make test):
@@ -843,7 +844,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // elements per digit run: beyond ~300 digits the runs get too short for coalesced writes and
   // an extra pass is cheaper.
   uint32_t maxr = V2_MAXR_IL;
-  if (const char* e = std::getenv("KMHG_MAXR"))   // testing knob: force more radix passes
+  const char* e = std::getenv("KMHG_MAXR");   // testing knob: force more radix passes
+  if (e && e[0])
     maxr = std::max<uint32_t>(2u, std::min<uint32_t>(maxr, (uint32_t)std::atoi(e)));
   auto plan = [&](uint32_t nbk, uint32_t& R) {
     for (uint32_t passes = 1; passes <= 4; ++passes) {
