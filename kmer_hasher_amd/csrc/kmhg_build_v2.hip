@@ -658,7 +658,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
   constexpr bool P8IN = BM == 7;                  // ... in
   using KT = typename std::conditional<BIDS, uint32_t, uint64_t>::type;
   using SL = ScatterLDS<KT>;
-  static_assert(!DS || !BIDS, "digit streams follow key streams");
+  static_assert(!DS || BM != 2, "the last bucket-id pass has no next pass");
   static_assert(BM == 0 || !NOPOS, "bucket-id and packed streams carry positions");
   static_assert(!(AOS && KEYS0), "packed streams start from the sequence");
   // KEYS0 with BM: the first pass over V_hist0's per-window bucket ids (~0: not indexed)
@@ -909,7 +909,7 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
       }
       if constexpr (DS) {       // the next pass's digit, from the staged key (no more LDS)
         const uint64_t kk = P8OUT ? (uint64_t)S.skey[i] >> pk.sh : (uint64_t)S.skey[i];
-        const uint32_t dnx = digit_of(kk, g, dso.Dn);
+        const uint32_t dnx = BIDS ? digit_of_b((uint32_t)kk, dso.Dn) : digit_of(kk, g, dso.Dn);
         if (dso.out8) dso.out8[dst] = (uint8_t)dnx;
         else dso.out[dst] = (uint16_t)dnx;
       }
@@ -1708,25 +1708,28 @@ void launch_part_dense(const uint64_t* ck, const uint32_t* cp, const uint32_t* o
 }
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
                             const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
-                            uint32_t pad, hipStream_t s) {
+                            uint32_t pad, hipStream_t s, const DigitOut* ds) {
   const uint64_t* ki = reinterpret_cast<const uint64_t*>(bids);
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
+  const DigitOut dso = ds ? *ds : kNoDigits;
   if (bout)
-    KMHG_SCATTER_BM(false, true, false, 1, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
-                    D, hist, ntiles, ko, pout, pad, 0, kNoFuse, kNoPack);
+    KMHG_SCATTER_BMD(false, true, false, 1, dso, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr,
+                     g, D, hist, ntiles, ko, pout, pad, 0, kNoFuse, kNoPack);
   else
     KMHG_SCATTER_BM(false, true, false, 2, nullptr, (int64_t)0, 0, Nw, ki, nullptr, nullptr, g,
                     D, hist, ntiles, ko, pout, pad, 0, kNoFuse, kNoPack);
 }
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
-                           uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf) {
+                           uint32_t* pout, uint32_t pad, hipStream_t s, const BoundsFuse* bf,
+                           const DigitOut* ds) {
   const uint64_t* ki = reinterpret_cast<const uint64_t*>(bin);
   uint64_t* ko = reinterpret_cast<uint64_t*>(bout);
   const BoundsFuse f = bf ? *bf : kNoFuse;
+  const DigitOut dso = ds ? *ds : kNoDigits;
   if (bout)
-    KMHG_SCATTER_BM(false, false, false, 1, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
-                    g, D, hist, ntiles, ko, pout, pad, 0, f, kNoPack);
+    KMHG_SCATTER_BMD(false, false, false, 1, dso, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin,
+                     n_ptr, g, D, hist, ntiles, ko, pout, pad, 0, f, kNoPack);
   else
     KMHG_SCATTER_BM(false, false, false, 2, nullptr, (int64_t)0, 0, (int64_t)0, ki, pin, n_ptr,
                     g, D, hist, ntiles, ko, pout, pad, 0, f, kNoPack);

@@ -951,11 +951,18 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // histograms 1.93 -> 0.48 ms); config 3 (2 passes, radix 313, u16) 2.81 -> 2.93 ms (histogram
   // -0.11 ms, first scatter +0.22).  Sequence builds with positions on key streams below
   // AOS_MIN_RADIX; KMHG_DIGIT_STREAM=0 / 1 forces off / on, KMHG_DS_U8=0 u16 digits.
+  // Bucket-id streams (u32 ids, in-cache sizes) can carry them too, but it is a wash: config 2
+  // histogram 10.2 -> 6.7 us, first scatter +3-6 us, build 0.2076-0.2092 ms either way
+  // (profiles/r5y_ab_ds_bid_config2.log).  KMHG_DS_BID=1 (or KMHG_DIGIT_STREAM=1) turns them on.
   const char* dse = std::getenv("KMHG_DIGIT_STREAM");
-  const bool ds_on = !bid && !from_keys && !count_only && passes >= 2 &&
-                     (dse && dse[0] ? dse[0] == '1' : R < AOS_MIN_RADIX);
+  const char* dbe = std::getenv("KMHG_DS_BID");
+  const bool ds_keys = !bid && !from_keys && !count_only && passes >= 2 &&
+                       (dse && dse[0] ? dse[0] == '1' : R < AOS_MIN_RADIX);
+  const bool ds_bids = bid && passes >= 2 &&
+                       (dse && dse[0] ? dse[0] == '1' : R <= 256 && dbe && dbe[0] == '1');
+  const bool ds_on = ds_keys || ds_bids;
   const char* dpe = std::getenv("KMHG_DS_PACK");
-  const bool ds_pack = ds_on && !(dpe && dpe[0] == '0');
+  const bool ds_pack = ds_keys && !(dpe && dpe[0] == '0');
   auto packed = [&](int p) {
     return aos && (p + 1 == (int)passes || R >= AOS_MIN_RADIX || ds_pack);
   };
@@ -1062,9 +1069,12 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     } else {
       LAUNCH("k_scan_u32", s, launch_scan_u32(hist.p, nhist, status, n_valid, s));
       if (bid) {
+        const DigitOut ds0{ds16p, make_digit(R, R), ds8p};
         LAUNCH("k_v2_scatter_seq", s,
                launch_v2_scatter_bid0(bB.p, Nw, g, make_digit(1, R), hist.p, ntiles,
-                                      passes == 1 ? nullptr : bA.p, pA.p, pad, s));
+                                      passes == 1 ? nullptr : bA.p, pA.p, pad, s,
+                                      ds_on ? &ds0 : nullptr));
+        ds_ready = ds_on;
       } else {
         const DigitOut ds0{ds16p, make_digit(R, R), ds8p};
         LAUNCH("k_v2_scatter_seq", s,
@@ -1141,14 +1151,22 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   for (uint32_t p = 1; bid && p < passes; ++p) {
     const Digit Dp = make_digit(div, R);
     const bool last = p + 1 == passes;
-    LAUNCH("k_v2_hist", s,
-           launch_v2_hist_bid(bin, n_valid, g, Dp, hp, C, status, nst, s,
-                              p == 1 ? save1 : nullptr));
+    if (ds_ready)
+      LAUNCH("k_v2_hist", s,
+             launch_v2_hist_digits(dsb.p, ds8, n_valid, g, Dp, hp, C, status, nst, s,
+                                   p == 1 ? save1 : nullptr));
+    else
+      LAUNCH("k_v2_hist", s,
+             launch_v2_hist_bid(bin, n_valid, g, Dp, hp, C, status, nst, s,
+                                p == 1 ? save1 : nullptr));
     LAUNCH("k_scan_u32", s, launch_scan_u32(hp, nh, status, n_valid, s));
     const BoundsFuse lv = level_of(p, bin, true, 1u);
+    const DigitOut dsn{ds16p, make_digit(div * R, R), ds8p};
     LAUNCH("k_v2_scatter", s,
            launch_v2_scatter_bid(bin, pin, n_valid, g, Dp, hp, C, last ? nullptr : bout,
-                                 pout, pad, s, fused(p) ? &lv : nullptr));
+                                 pout, pad, s, fused(p) ? &lv : nullptr,
+                                 ds_on && !last ? &dsn : nullptr));
+    ds_ready = ds_on && !last;
     if (!fused(p) && !last) launch_level(lv);
     std::swap(bin, bout);
     std::swap(pin, pout);

@@ -276,11 +276,11 @@ void launch_v2_scatter(const uint64_t* kin, const uint32_t* pin, const uint32_t*
 // cuts the keys from the code words.  Histograms without hashing.
 void launch_v2_scatter_bid0(const uint32_t* bids, int64_t Nw, Geom g, Digit D,
                             const uint32_t* hist, uint32_t ntiles, uint32_t* bout, uint32_t* pout,
-                            uint32_t pad, hipStream_t s);
+                            uint32_t pad, hipStream_t s, const DigitOut* ds = nullptr);
 void launch_v2_scatter_bid(const uint32_t* bin, const uint32_t* pin, const uint32_t* n_ptr,
                            Geom g, Digit D, const uint32_t* hist, uint32_t ntiles, uint32_t* bout,
                            uint32_t* pout, uint32_t pad, hipStream_t s,
-                           const BoundsFuse* bf = nullptr);
+                           const BoundsFuse* bf = nullptr, const DigitOut* ds = nullptr);
 void launch_v2_hist_bid(const uint32_t* bids, const uint32_t* n_ptr, Geom g, Digit D,
                         uint32_t* hist, uint32_t ntiles, uint64_t* scan_status, uint32_t n_status,
                         hipStream_t s, uint32_t* save_col0 = nullptr);

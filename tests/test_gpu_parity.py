@@ -275,13 +275,16 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, ranks, stream):
     bucket ids through the passes and cut the keys from the code words (default up to 12 M
     windows); KMHG_BUILD_BID=0 carries the keys.  Key streams below radix 160 carry digit
     streams by default (each pass writes the next pass's digits, which its histogram reads):
-    keys-levels turns them off (KMHG_DIGIT_STREAM=0), keys-digits forces them at every radix.
+    keys-levels turns them off (KMHG_DIGIT_STREAM=0), keys-digits forces them at every radix,
+    bid with lane ranks forces them on bucket-id streams (off by default there).
     Ranks by the LDS atomics' lane order and by ballots (KMHG_TEST_BALLOT=1)."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_MAXR", maxr)
     monkeypatch.setenv("KMHG_BUILD_BID", "1" if stream == "bid" else "0")
     monkeypatch.setenv("KMHG_FUSE_BOUNDS", "0" if stream == "keys-levels" else "1")
-    monkeypatch.setenv("KMHG_DIGIT_STREAM", {"keys-levels": "0", "keys-digits": "1"}.get(stream, ""))
+    # (bucket-id streams: digit streams forced on with lane ranks, the default off with ballots)
+    ds = {"keys-levels": "0", "keys-digits": "1", "bid": "1" if ranks == "lane" else ""}
+    monkeypatch.setenv("KMHG_DIGIT_STREAM", ds.get(stream, ""))
     monkeypatch.setenv("KMHG_TEST_BALLOT", "1" if ranks == "ballot" else "0")
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
     _check_against_oracle(s, 31, pairs=False)
