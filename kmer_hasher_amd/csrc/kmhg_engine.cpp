@@ -942,30 +942,6 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // passes, radix 79) 18.2 -> 18.6 ms (histograms 1.9 -> 2.8 ms, scatters 11.2 -> 10.3), A/B
   // in one run (profiles/r5b_ab_aos_config3.log, r5c_ab_aos_config5.log).
   constexpr uint32_t AOS_MIN_RADIX = 160;
-  // Digit streams (DS): each pass before the last also writes every output element's digit of
-  // the next pass (u8 up to radix 256, else u16), and that pass's histogram reads 1-2 B per
-  // element instead of the keys -- which also takes away the reason to leave the middle streams
-  // unpacked.  The digit writes are short scattered runs (PTILE / R elements per tile and
-  // digit), so they pay only at a low radix.  Measured (A/B in one run, profiles/r5y_ab_ds_*):
-  // the 500 Mbp build (3 passes, radix 79) 18.37 -> 16.82 ms with u8 digits (17.75 with u16;
-  // histograms 1.93 -> 0.48 ms); config 3 (2 passes, radix 313, u16) 2.81 -> 2.93 ms (histogram
-  // -0.11 ms, first scatter +0.22).  Sequence builds with positions on key streams below
-  // AOS_MIN_RADIX; KMHG_DIGIT_STREAM=0 / 1 forces off / on, KMHG_DS_U8=0 u16 digits.
-  // Bucket-id streams (u32 ids, in-cache sizes) can carry them too, but it is a wash: config 2
-  // histogram 10.2 -> 6.7 us, first scatter +3-6 us, build 0.2076-0.2092 ms either way
-  // (profiles/r5y_ab_ds_bid_config2.log).  KMHG_DS_BID=1 (or KMHG_DIGIT_STREAM=1) turns them on.
-  const char* dse = std::getenv("KMHG_DIGIT_STREAM");
-  const char* dbe = std::getenv("KMHG_DS_BID");
-  const bool ds_keys = !bid && !from_keys && !count_only && passes >= 2 &&
-                       (dse && dse[0] ? dse[0] == '1' : R < AOS_MIN_RADIX);
-  const bool ds_bids = bid && passes >= 2 &&
-                       (dse && dse[0] ? dse[0] == '1' : R <= 256 && dbe && dbe[0] == '1');
-  const bool ds_on = ds_keys || ds_bids;
-  const char* dpe = std::getenv("KMHG_DS_PACK");
-  const bool ds_pack = ds_keys && !(dpe && dpe[0] == '0');
-  auto packed = [&](int p) {
-    return aos && (p + 1 == (int)passes || R >= AOS_MIN_RADIX || ds_pack);
-  };
   // Pack8 (two-pass builds of small k: 2k <= 52): the first pass writes 8-B elements, key << sh
   // | the window's index inside its segment of 2^sh windows (sh = 64 - 2k), and the second pass
   // restores the position from the element's place in the stream (k_seg_bounds' table).  The
@@ -977,6 +953,40 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const char* p8e = std::getenv("KMHG_PACK8");
   const bool pack8 = aos && passes == 2 && n_parts < 2 && seg8 && nseg8 <= 256 &&
                      !(p8e && p8e[0] == '0');
+  // Digit streams (DS): each pass before the last also writes every output element's digit of
+  // the next pass (u8 up to radix 256, else u16), and that pass's histogram reads 1-2 B per
+  // element instead of the keys -- which also takes away the reason to leave the middle streams
+  // unpacked.  The digit writes are short scattered runs (PTILE / R elements per tile and
+  // digit); they pay once the streams outgrow the Infinity Cache, and u16 digits only well
+  // beyond it.  Measured (A/B in one run, profiles/r5y_ab_ds_*, r5y_ds_sizes_build_only.txt,
+  // k = 31 unless noted):
+  //   u8 (radix <= 256): 500 Mbp (3 passes, radix 79) 18.37 -> 16.82 ms (u16 17.75;
+  //     histograms 1.93 -> 0.48 ms); 60 Mbp 1.773 -> 1.744; 40 Mbp 1.115 -> 1.093; 30 Mbp
+  //     0.815 -> 0.804; but 20 Mbp 0.536 -> 0.549 and 16 Mbp 0.433 -> 0.446 (in cache);
+  //   u16: 200 Mbp (radix 448) 6.85 -> 6.23 ms; but 100 Mbp (radix 317) 3.127 -> 3.149, and
+  //     config 3 (k = 21, Pack8 first stream) 2.81 -> 2.93 (histogram -0.11, first scatter
+  //     +0.22 ms).
+  // Sequence builds with positions on key streams without Pack8, from DS_MIN_WINDOWS windows
+  // (u8) / DS16_MIN_WINDOWS (u16); KMHG_DIGIT_STREAM=0 / 1 forces off / on, KMHG_DS_U8=0 u16
+  // digits.
+  // Bucket-id streams (u32 ids, in-cache sizes) can carry them too, but it is a wash: config 2
+  // histogram 10.2 -> 6.7 us, first scatter +3-6 us, build 0.2076-0.2092 ms either way
+  // (profiles/r5y_ab_ds_bid_config2.log).  KMHG_DS_BID=1 (or KMHG_DIGIT_STREAM=1) turns them on.
+  constexpr int64_t DS_MIN_WINDOWS = 25'000'000, DS16_MIN_WINDOWS = 150'000'000;
+  const char* dse = std::getenv("KMHG_DIGIT_STREAM");
+  const char* dbe = std::getenv("KMHG_DS_BID");
+  const bool ds_keys = !bid && !from_keys && !count_only && passes >= 2 &&
+                       (dse && dse[0] ? dse[0] == '1'
+                                      : !pack8 && Nw >= (R <= 256 ? DS_MIN_WINDOWS
+                                                                  : DS16_MIN_WINDOWS));
+  const bool ds_bids = bid && passes >= 2 &&
+                       (dse && dse[0] ? dse[0] == '1' : R <= 256 && dbe && dbe[0] == '1');
+  const bool ds_on = ds_keys || ds_bids;
+  const char* dpe = std::getenv("KMHG_DS_PACK");
+  const bool ds_pack = ds_keys && !(dpe && dpe[0] == '0');
+  auto packed = [&](int p) {
+    return aos && (p + 1 == (int)passes || R >= AOS_MIN_RADIX || ds_pack);
+  };
   bool any_unpacked = !aos;
   for (int p = -1; p + 1 < (int)passes; ++p) any_unpacked |= !packed(p) && !(pack8 && p == 0);
   const uint64_t kwords = bid ? 1 : aos ? ((uint64_t)(Nw + PTILE) * 3 + 1) / 2 : (uint64_t)(Nw + PTILE);
