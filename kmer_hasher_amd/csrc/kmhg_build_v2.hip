@@ -910,6 +910,8 @@ k_v2_scatter(const uint8_t* __restrict__ seq, int64_t L, int k, int64_t Nw,
       if constexpr (DS) {       // the next pass's digit, from the staged key (no more LDS)
         const uint64_t kk = P8OUT ? (uint64_t)S.skey[i] >> pk.sh : (uint64_t)S.skey[i];
         const uint32_t dnx = BIDS ? digit_of_b((uint32_t)kk, dso.Dn) : digit_of(kk, g, dso.Dn);
+        // (plain stores: the partial lines merge in the XCD's L2; nontemporal digit stores cost
+        // the 500 Mbp build 16.86 -> 19.04 ms, profiles/r5y_variants_large_build_only.txt)
         if (dso.out8) dso.out8[dst] = (uint8_t)dnx;
         else dso.out[dst] = (uint16_t)dnx;
       }
