@@ -975,10 +975,12 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   constexpr int64_t DS_MIN_WINDOWS = 25'000'000, DS16_MIN_WINDOWS = 150'000'000;
   const char* dse = std::getenv("KMHG_DIGIT_STREAM");
   const char* dbe = std::getenv("KMHG_DS_BID");
+  // (a part build's later streams hold ~1/n_parts of the windows)
+  const int64_t ds_windows = n_parts >= 2 ? Nw / n_parts : Nw;
   const bool ds_keys = !bid && !from_keys && !count_only && passes >= 2 &&
                        (dse && dse[0] ? dse[0] == '1'
-                                      : !pack8 && Nw >= (R <= 256 ? DS_MIN_WINDOWS
-                                                                  : DS16_MIN_WINDOWS));
+                                      : !pack8 && ds_windows >= (R <= 256 ? DS_MIN_WINDOWS
+                                                                          : DS16_MIN_WINDOWS));
   const bool ds_bids = bid && passes >= 2 &&
                        (dse && dse[0] ? dse[0] == '1' : R <= 256 && dbe && dbe[0] == '1');
   const bool ds_on = ds_keys || ds_bids;
