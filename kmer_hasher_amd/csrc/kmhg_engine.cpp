@@ -957,30 +957,28 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // the next pass (u8 up to radix 256, else u16), and that pass's histogram reads 1-2 B per
   // element instead of the keys -- which also takes away the reason to leave the middle streams
   // unpacked.  The digit writes are short scattered runs (PTILE / R elements per tile and
-  // digit); they pay once the streams outgrow the Infinity Cache, and u16 digits only well
-  // beyond it.  Measured (A/B in one run, profiles/r5y_ab_ds_*, r5y_ds_sizes_build_only.txt,
-  // k = 31 unless noted):
-  //   u8 (radix <= 256): 500 Mbp (3 passes, radix 79) 18.37 -> 16.82 ms (u16 17.75;
-  //     histograms 1.93 -> 0.48 ms); 60 Mbp 1.773 -> 1.744; 40 Mbp 1.115 -> 1.093; 30 Mbp
-  //     0.815 -> 0.804; but 20 Mbp 0.536 -> 0.549 and 16 Mbp 0.433 -> 0.446 (in cache);
-  //   u16: 200 Mbp (radix 448) 6.85 -> 6.23 ms; but 100 Mbp (radix 317) 3.127 -> 3.149, and
-  //     config 3 (k = 21, Pack8 first stream) 2.81 -> 2.93 (histogram -0.11, first scatter
-  //     +0.22 ms).
-  // Sequence builds with positions on key streams without Pack8, from DS_MIN_WINDOWS windows
-  // (u8) / DS16_MIN_WINDOWS (u16); KMHG_DIGIT_STREAM=0 / 1 forces off / on, KMHG_DS_U8=0 u16
-  // digits.
+  // digit); u8 digits pay once the streams outgrow the Infinity Cache, u16 digits (radix
+  // 257-320: two-pass builds of ~66-100 M windows) did not.  Measured (A/B in one run,
+  // profiles/r5y_ab_ds_*, r5y_ds_sizes_build_only.txt, k = 31 unless noted):
+  //   u8: 500 Mbp (3 passes, radix 79) 18.37 -> 16.82 ms (u16 17.75; histograms 1.93 -> 0.48
+  //     ms); 200 Mbp (3 passes, radix 59) 6.85 -> 6.23; 60 Mbp 1.773 -> 1.744; 40 Mbp
+  //     1.115 -> 1.093; 30 Mbp 0.815 -> 0.804; but 20 Mbp 0.536 -> 0.549 and 16 Mbp
+  //     0.433 -> 0.446 (in cache);
+  //   u16: 100 Mbp (radix 317) 3.127 -> 3.149 ms; config 3 (k = 21, Pack8 first stream)
+  //     2.81 -> 2.93 (histogram -0.11, first scatter +0.22 ms).
+  // Sequence builds with positions on key streams without Pack8, radix <= 256, from
+  // DS_MIN_WINDOWS windows; KMHG_DIGIT_STREAM=0 / 1 forces off / on, KMHG_DS_U8=0 u16 digits.
   // Bucket-id streams (u32 ids, in-cache sizes) can carry them too, but it is a wash: config 2
   // histogram 10.2 -> 6.7 us, first scatter +3-6 us, build 0.2076-0.2092 ms either way
   // (profiles/r5y_ab_ds_bid_config2.log).  KMHG_DS_BID=1 (or KMHG_DIGIT_STREAM=1) turns them on.
-  constexpr int64_t DS_MIN_WINDOWS = 25'000'000, DS16_MIN_WINDOWS = 150'000'000;
+  constexpr int64_t DS_MIN_WINDOWS = 25'000'000;
   const char* dse = std::getenv("KMHG_DIGIT_STREAM");
   const char* dbe = std::getenv("KMHG_DS_BID");
   // (a part build's later streams hold ~1/n_parts of the windows)
   const int64_t ds_windows = n_parts >= 2 ? Nw / n_parts : Nw;
   const bool ds_keys = !bid && !from_keys && !count_only && passes >= 2 &&
                        (dse && dse[0] ? dse[0] == '1'
-                                      : !pack8 && ds_windows >= (R <= 256 ? DS_MIN_WINDOWS
-                                                                          : DS16_MIN_WINDOWS));
+                                      : !pack8 && R <= 256 && ds_windows >= DS_MIN_WINDOWS);
   const bool ds_bids = bid && passes >= 2 &&
                        (dse && dse[0] ? dse[0] == '1' : R <= 256 && dbe && dbe[0] == '1');
   const bool ds_on = ds_keys || ds_bids;
