@@ -13,13 +13,16 @@ seq.kmer.pos self-query of the same sequence is timed the same way and reported 
 sampled from it (packed in HBM) and `depth` seq.kmer.depth.sh of it against that suffix hash
 (SURVEY.md §8 f next-4), each with the reference's own core timed beside it.
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): value is the owner-computes build of
-ONE sequence of N x L bases (the reference's reader-pool partition,
-src/kmer_reader.c:28-39): rank 0 holds it and broadcasts it once, every rank builds the k-mers of
-its bucket range (kmhg_build_device_part), no data-path collective inside a step -> weak
-scaling; value = N x L Mbp divided by the max-over-ranks time per step.  The broadcast and the
-assembly of the whole index on every rank are timed beside it; every rank indexing its own L-base
-sequence (replicas) is reported as a side record.
+N > 1: one rank per GPU.  Launched by torch.distributed.run (WORLD_SIZE must equal --gpus), or
+as `python bench.py --gpus N`, which starts the N ranks itself (spawn_ranks) before touching the
+GPU.  value = N independent make.kmer.hash builds, every rank indexing its own L-base sequence
+(`parallelism: replicas{N}`, no data-path collective, weak scaling): N x L Mbp over the
+max-over-ranks time per step.  Two side records carry the sharded paths of SURVEY.md §8e:
+`sharded_query` -- north_star's seq.kmer.pos of config 5 (index(A) built on rank 0 and broadcast
+once, B's slices scattered from rank 0, range queries, rows gathered to rank 0; phases, and the
+rows delivered into a node-shared host matrix as `to_host`) -- and `sharded_build`, the
+owner-computes build of ONE N x L sequence (src/kmer_reader.c:28-39's partition) with the
+assembly that makes it queryable.
 
 `roofline` prices the dominant build kernel from per-kernel HIP events recorded on the stream
 the kernels run on; `traffic` comes from profiles/pmc_<config>.json (rocprofv3 --pmc passes made
@@ -472,6 +475,57 @@ def _claim_stdout() -> None:
     os.dup2(2, 1)
 
 
+def check_world(gpus: int, world_env: str | None) -> None:
+    """A launcher's WORLD_SIZE must equal --gpus: n_gpus in the line is the ranks that ran."""
+    if world_env is not None and int(world_env) != gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world_env} but --gpus {gpus}: launch one rank per "
+                         "GPU (--nproc-per-node N) with --gpus N")
+
+
+def rank_command(gpus: int, argv: list[str], port: int) -> list[str]:
+    """The torch.distributed.run command that starts `gpus` ranks of this script (one process
+    per GPU, rendezvous on 127.0.0.1) with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(gpus: int, argv: list[str] | None = None) -> int:
+    """Run the N ranks as a child process group and return its exit status.  The parent has not
+    initialised the GPU (no torch import), so nothing here replaces a process that holds it; the
+    ranks' stdout is this process's stdout (rank 0 prints the one JSON line)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    sys.stdout.flush()
+    return subprocess.call(rank_command(gpus, sys.argv[1:] if argv is None else argv, port),
+                           env=env)
+
+
+def launch_check(args) -> None:
+    """--launch-check: the rank launch and world check alone (tests/test_bench_launch.py), over
+    gloo on the CPU: every rank joins the group and asserts its size, rank 0 prints one line."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, "
+                             f"--gpus {args.gpus}")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        world = int(t.item())
+    if int(os.environ.get("RANK", "0")) == 0:
+        _emit({"metric": "launch-check", "n_gpus": world, "pid_parent": os.getppid()})
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -496,8 +550,19 @@ def main():
                     help="skip the out-of-cache side record (500 Mbp build + cross query)")
     ap.add_argument("--only-large", action="store_true",
                     help="run the out-of-cache record alone (profiling), printed as its own line")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="CPU test of the rank launch: gloo process group, no GPU, one line")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N ranks here, before this
+        # process touches the GPU (it never does: it only waits for its child)
+        raise SystemExit(spawn_ranks(args.gpus))
+    check_world(args.gpus, os.environ.get("WORLD_SIZE"))
     _claim_stdout()
+    if args.launch_check:
+        return launch_check(args)
     # the side legs (query, counts, reads, depth) run for at least 50 timed calls: 20 calls of a
     # 0.1-0.5 ms leg are a few ms of wall time, where one host hiccup shows as a 2x swing
     leg_steps = max(args.steps, 50)
@@ -521,6 +586,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench: process group has {dist.get_world_size()} ranks, "
+                             f"--gpus {args.gpus}")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -564,6 +632,7 @@ def main():
             check_build(info)
         return info
 
+    progress("build steps")
     # ---------------- build: W untimed warmups, 2 steps with events around every kernel (find the
     # dominant one), then exactly K timed steps with events around the dominant kernel only, so
     # the per-kernel events add no dead time to the rest of the timed region
@@ -607,6 +676,7 @@ def main():
     if distributed:
         sharded = bench_sharded_build(args, k, L, dev, world, rank, seed)
 
+    progress("self query")
     # ---------------- query: self seq.kmer.pos against one resident index.  The first query of an
     # index also derives the diagonal path's unique-window bits and slot tags (k_diag_valid /
     # k_diag_prep, kept with the index): timed on its own as first_call_ms.
@@ -680,6 +750,7 @@ def main():
     torch.cuda.synchronize()
     t_free = time.perf_counter() - t0
 
+    progress("counts / reads / depth legs")
     # ---------------- count.kmers (SURVEY.md §8 f next-4) of the same sequence: one call per step
     # into a new counts pointer (k, source 0 of 2)
     cper, t_count, cU, cslots, t_order, order_k = {}, 0.0, 0, 0, 0.0, {}
@@ -782,6 +853,13 @@ def main():
                       device=dev)
     if distributed:
         dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+    progress("sharded records")
+    # north_star's sharded seq.kmer.pos (config 5: index broadcast once, B scattered, range
+    # queries, rows gathered) on every N > 1 line; at N = 1 `large.query` is its one-GPU point
+    sq = None
+    if distributed and not args.profile and not args.no_large:
+        sq, _ = sharded_query_record(args, dev, world, rank, max(1, min(args.steps, 10)))
+    progress("out-of-cache record")
     # the out-of-cache side record (one GPU only: the driver's N = 1 line; the 8-GPU scaling runs
     # skip it)
     large = None
@@ -929,6 +1007,8 @@ def main():
             # the owner-computes build of one genome as a side record: its part
             # step, and the rate at which the parts become an index every rank can query
             out["sharded_build"] = sharded
+        if sq:
+            out["sharded_query"] = sq
         if large:
             out["large"] = large
         if not args.profile:
@@ -1058,6 +1138,16 @@ def _emit(out):
     print(json.dumps(out), file=_JSON_OUT, flush=True)
 
 
+_T_START = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One progress line on stderr (rank-tagged): long phases of a run stay visibly alive."""
+    r = os.environ.get("RANK", "0")
+    print(f"[bench r{r} +{time.perf_counter() - _T_START:.1f}s] {msg}", file=sys.stderr,
+          flush=True)
+
+
 LARGE_L, LARGE_K = 500_000_000, 31
 
 
@@ -1142,13 +1232,31 @@ def bench_large(args, dev) -> dict:
         idx.query(tb, k, stream).free()
     torch.cuda.synchronize()
     tq_ms = (time.perf_counter() - t0) / steps * 1e3
+    # the same query with its rows copied into a pinned host matrix (what an R session receives;
+    # the N = 1 point of sharded_query.to_host)
+    hostm = torch.empty((H, 2), dtype=torch.int32, pin_memory=True)
+    n_host = max(1, min(steps, 5))
+    for i in range(n_host + 1):
+        if i == 1:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        q = idx.query(tb, k, stream)
+        hostm.copy_(q.rows_view())
+        q.free()
+    torch.cuda.synchronize()
+    th_ms = (time.perf_counter() - t0) / n_host * 1e3
+    del hostm
     idx.free()
     Nw = L - k + 1
     query_rec = {
         "value": round(L / 1e6 / (tq_ms * 1e-3), 2), "unit": "Mbp/s", "ms_per_step": round(tq_ms, 4),
         "steps": steps, "rows": H, "first_query_ms": round(t_first * 1e3, 3),
         "kernels_ms_per_step": {n: round(v, 5) for n, v in qper.items()},
-        "roofline": query_roofline(qper, L, Nw, H, pmc, tq_ms, qlaunch)}
+        "roofline": query_roofline(qper, L, Nw, H, pmc, tq_ms, qlaunch),
+        "to_host": {"value": round(L / 1e6 / (th_ms * 1e-3), 2), "unit": "Mbp/s",
+                    "ms_per_step": round(th_ms, 3), "steps": n_host,
+                    "note": "the query with its rows copied D2H into a pinned host matrix (one "
+                            "GPU, one PCIe link): the N = 1 point of sharded_query.to_host"}}
     ref = _whole_size_config5()
     return {"workload": "configs[4] on one GPU: synthetic A = 500 Mbp iid ACGT (splitmix64 seed "
                         "4), B = A + 1% SNV + 20 inversions/translocations + N-runs (seed 5), "
@@ -1277,40 +1385,44 @@ def cpu_readout_baseline(seq_bytes: bytes, k: int, opt: int) -> dict:
                 "sample": f"unavailable: {e}"}
 
 
-def bench_sharded_query(args, cfg, dev, world, rank):
-    """Config 5: B (500 Mbp) queried against index(A); B's windows sharded over the ranks.
+def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: bool = False):
+    """config 5's seq.kmer.pos sharded over the ranks (BASELINE.json north_star):
+    B (500 Mbp) queried against index(A) (500 Mbp iid, k = 31), the reference loop
+    src/kmer_pos.c:110-136 behind src/kmer_hash.c:1151-1172.
 
-    The index is built on rank 0 and its image broadcast once (timed, outside the steps).  A
-    step is one seq.kmer.pos of B as the R session issues it: B sits on rank 0, is broadcast to
-    every rank (C1), each rank queries its window range with the HIP engine, and the rows are
-    gathered to rank 0 in rank order (= the reference's row order).  The phases are timed
-    separately (synchronized on each rank, max over ranks)."""
+    index(A) is built on rank 0 and its image (table + positions + code block) broadcast once
+    (timed, outside the steps).  A step is one seq.kmer.pos of B as the R session issues it: B
+    sits on rank 0; C1 scatters to every rank the slice of B its window range reads; each rank
+    runs the HIP range query; the rows are gathered into ONE device buffer on rank 0 in rank
+    order (= the reference's row order; `value`).  `to_host` times the same step with the rows
+    delivered instead into one host matrix shared by the node's ranks, each rank copying its own
+    rows over its own PCIe link (dist.deliver_rows_host), and `c1_broadcast` the C1 phase as a
+    broadcast of the whole B.  Phases are timed in separate synchronized steps, max over ranks.
+    Returns rank 0's record (None elsewhere) and the kernel times of the timed steps."""
     import torch
     import torch.distributed as dist
     from kmer_hasher_amd import device as D
     from kmer_hasher_amd import dist as kd
     from kmer_hasher_amd import synth
-    L, k = cfg["L"], cfg["k"]
-    A = synth.iid(L, 4)
-    B = synth.derived(A, 5) if rank == 0 else None
-    cpu_sample = None
-    if rank == 0 and not args.no_cpu and not args.profile:
-        cpu_sample = (A[:CONFIG5_CPU_BP].tobytes(), B[:CONFIG5_CPU_BP].tobytes())
-    tb = torch.from_numpy(B).to(dev) if rank == 0 else None
-    t_build = 0.0
+    L, k = LARGE_L, LARGE_K
+    tb, index, t_build = None, None, 0.0
     if rank == 0:
+        A = synth.iid(L, 4)
+        tb = torch.from_numpy(synth.derived(A, 5)).to(dev)
         ta = torch.from_numpy(A).to(dev)
+        del A
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         index = D.DeviceIndex.build(ta, k)
         index.wait()
         t_build = time.perf_counter() - t0
         del ta
-    else:
-        index = None
-    del A, B
     t_bcast = 0.0
-    if world > 1:
+    # every collective of the path runs whenever a process group exists (the RCCL world-1
+    # rehearsal, `--dist`, included); without one (`--config 5` at N = 1) the step is the plain
+    # query
+    use_pg = dist.is_available() and dist.is_initialized()
+    if use_pg:
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -1320,58 +1432,149 @@ def bench_sharded_query(args, cfg, dev, world, rank):
         t_bcast = time.perf_counter() - t0
     info = index.info()
     eng = kd.HipQueryEngine(index)
+    # the scatter's receive buffer (non-root ranks), reused across steps
+    seq_buf = torch.empty(L + 16, dtype=torch.uint8, device=dev) if rank else None
+    sink = kd.HostRowSink(0) if use_pg else None
+    host1 = None                                  # no process group: a pinned host matrix
 
-    def step(timings=None):
-        if world > 1:
-            return kd.sharded_query(eng, tb, k, dst=0, src=0, timings=timings)
+    def step(timings=None, to_host=False, c1="scatter"):
+        nonlocal host1
+        if use_pg:
+            return kd.sharded_query(eng, tb, k, dst=0, src=0, timings=timings, c1=c1,
+                                    sink=sink if to_host else None, seq_buf=seq_buf)
         t0 = time.perf_counter()
         r = eng.query_range(tb, k, 0, tb.numel() - k + 1)
         if timings is not None:
             torch.cuda.synchronize()
-            timings["query"] = timings.get("query", 0.0) + time.perf_counter() - t0
+        t1 = time.perf_counter()
+        if to_host:
+            if host1 is None or host1.shape[0] < r.shape[0]:
+                host1 = torch.empty((r.shape[0], 2), dtype=torch.int32, pin_memory=True)
+            host1[:r.shape[0]].copy_(r)
+            r = host1[:r.shape[0]]
+        if timings is not None:
+            t2 = time.perf_counter()
+            for n_, dt in (("broadcast", 0.0), ("query", t1 - t0), ("gather", t2 - t1)):
+                timings[n_] = timings.get(n_, 0.0) + dt
         return r
 
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    rows = step()                      # first query: the index's diagonal-path preparation
-    torch.cuda.synchronize()
-    t_first = time.perf_counter() - t0
-    del rows
-    for _ in range(args.warmup):
-        rows = step()
+    def timed(n, **kw):
+        if use_pg:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        H = 0
+        for _ in range(n):
+            rows = step(**kw)
+            H = rows.shape[0] if rows is not None else 0
+            del rows
+        if use_pg:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, H
+
+    def phases(n=2, **kw):
+        ph = {}
+        for _ in range(n):
+            rows = step(ph, **kw)
+            del rows
+        return [ph.get(p, 0.0) / n for p in ("broadcast", "query", "gather")]
+
+    progress(f"sharded query: index built {t_build:.3f} s, broadcast {t_bcast:.3f} s")
+    try:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rows = step()                  # first query: the index's diagonal-path preparation
+        torch.cuda.synchronize()
+        t_first = time.perf_counter() - t0
         del rows
-    # per-phase times in separate (synchronized) steps, then the timed steps without syncs
-    phases = {}
-    for _ in range(2):
-        rows = step(phases)
+        for _ in range(max(1, min(args.warmup, 3))):
+            rows = step()
+            del rows
+        ph_dev = phases()
+        if timing_kernels:
+            D.timing_enable(True)
+            D.timing_reset()
+        t_dev, H = timed(steps)
+        kt = D.timing_report() if timing_kernels else {}
+        if timing_kernels:
+            D.timing_enable(False)
+        progress("sharded query: rows to the host matrix")
+        # rows into the host matrix (what an R session receives): first delivery (the shared
+        # buffer's creation and registration) untimed
+        rows = step(to_host=True)
         del rows
-    D.timing_enable(True)
-    D.timing_reset()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    H = 0
-    for _ in range(args.steps):
-        rows = step()
-        H = rows.shape[0] if rows is not None else 0
-        del rows
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t = time.perf_counter() - t0
-    kt = D.timing_report()
-    D.timing_enable(False)
-    tt = torch.tensor([t] + [phases.get(p, 0.0) / 2 for p in ("broadcast", "query", "gather")],
-                      dtype=torch.float64, device=dev)
-    if world > 1:
+        ph_host = phases(to_host=True)
+        t_host, H_host = timed(max(1, min(steps, 5)), to_host=True)
+        n_host = max(1, min(steps, 5))
+        ph_bc = phases(c1="broadcast") if use_pg else [0.0, 0.0, 0.0]
+    finally:
+        if sink is not None:
+            sink.close()
+    vals = [t_dev, t_host] + ph_dev + ph_host + ph_bc
+    tt = torch.tensor(vals, dtype=torch.float64, device=dev)
+    if use_pg:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    t, p_b, p_q, p_g = tt.tolist()
+    t_dev, t_host, *ph = tt.tolist()
+    ph_dev, ph_host, ph_bc = ph[0:3], ph[3:6], ph[6:9]
+    index.free()
+    if rank != 0:
+        return None, kt
+    assert H_host == H, (H_host, H)
+
+    def ms(x):
+        return round(x * 1e3, 3)
+
+    rec = {"value": round(L / 1e6 * steps / t_dev, 2), "unit": "Mbp/s",
+           "ms_per_step": round(t_dev / steps * 1e3, 3), "steps": steps, "n_gpus": world,
+           "scaling": "strong", "seq_len": L, "k": k, "rows": H,
+           "distinct_kmers": info["n_kmers"],
+           "index_build_s": round(t_build, 4), "index_broadcast_s": round(t_bcast, 4),
+           "first_query_ms": ms(t_first),
+           "phases_ms": {"query_scatter": ms(ph_dev[0]), "range_query": ms(ph_dev[1]),
+                         "row_gather": ms(ph_dev[2]),
+                         "note": "separate synchronized steps, max over ranks"},
+           "to_host": {"value": round(L / 1e6 * n_host / t_host, 2), "unit": "Mbp/s",
+                       "ms_per_step": round(t_host / n_host * 1e3, 3), "steps": n_host,
+                       "phases_ms": {"query_scatter": ms(ph_host[0]),
+                                     "range_query": ms(ph_host[1]),
+                                     "rows_to_host": ms(ph_host[2])},
+                       "note": "the same step with the rows delivered into one host matrix "
+                               "(the R matrix's data): every rank copies its own rows D2H "
+                               "into a node-shared, HIP-registered buffer at its row offset "
+                               "(dist.deliver_rows_host); at n_gpus 1 the one GPU's rows into "
+                               "a pinned host matrix"},
+           "c1_broadcast_ms": ms(ph_bc[0]) if use_pg else None,
+           "c1_broadcast_note": "C1 as a broadcast of the whole B (one separate step), against "
+                                "query_scatter's slices",
+           "backend": dist.get_backend() if use_pg else None,
+           "note": "index(A) built on rank 0, its image broadcast once (index_broadcast_s); a "
+                   "step scatters B's slices from rank 0, runs every rank's window range on "
+                   "the HIP engine and gathers the rows into one device buffer on rank 0 in "
+                   "rank order (the reference's row order)"}
+    return rec, kt
+
+
+def bench_sharded_query(args, cfg, dev, world, rank):
+    """Config 5 as its own line (`--config 5`): sharded_query_record's step is the headline,
+    with the roofline of the per-rank range query, the reference on a bounded prefix beside it
+    and the 500 Mbp index build (rank 0) as a side record."""
+    import torch
+    from kmer_hasher_amd import device as D
+    from kmer_hasher_amd import synth
+    L, k = cfg["L"], cfg["k"]
+    rec, kt = sharded_query_record(args, dev, world, rank, args.steps, timing_kernels=True)
     # the 500 Mbp index build itself (make.kmer.hash of A), rank 0: per-kernel times of one
     # build, then BUILD5_STEPS timed builds (each waited for and freed)
     build_rec = None
+    cpu_sample = None
     if rank == 0 and not args.profile:
-        ta = torch.from_numpy(synth.iid(L, 4)).to(dev)
+        A = synth.iid(L, 4)
+        if not args.no_cpu:
+            cpu_sample = (A[:CONFIG5_CPU_BP].tobytes(),
+                          synth.derived(A, 5)[:CONFIG5_CPU_BP].tobytes())
+        ta = torch.from_numpy(A).to(dev)
+        del A
         D.DeviceIndex.build(ta, k).wait().free()
         D.timing_enable(True)
         D.timing_select(None)
@@ -1408,28 +1611,23 @@ def bench_sharded_query(args, cfg, dev, world, rank):
         per = {n: v[1] / v[0] for n, v in kt.items() if v[0]}
         launches = {n: v[0] / args.steps for n, v in kt.items() if v[0]}
         Nw_rank = (L - k + 1) // world
+        H = rec["rows"]
         cpu = cpu_query_baseline(*cpu_sample, k) if cpu_sample else None
+        cfg_rec = {kk: rec[kk] for kk in ("rows", "distinct_kmers", "index_build_s",
+                                          "index_broadcast_s", "first_query_ms", "phases_ms")}
         _emit({"metric": "seq.kmer.pos query Mbp/s (config 5, sharded)",
-               "value": round(L / 1e6 * args.steps / t, 2), "unit": "Mbp/s", "n_gpus": world,
+               "value": rec["value"], "unit": "Mbp/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(t / args.steps * 1e3, 3), "higher_is_better": True,
+               "ms_per_step": rec["ms_per_step"], "higher_is_better": True,
                "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-               "config": {"workload": cfg["workload"], "seq_len": L, "k": k, "rows": H,
-                          "distinct_kmers": info["n_kmers"],
-                          "index_build_s": round(t_build, 4),
-                          "index_broadcast_s": round(t_bcast, 4),
-                          "first_query_ms": round(t_first * 1e3, 3),
-                          "phases_ms": {"query_broadcast": round(p_b * 1e3, 3),
-                                        "range_query": round(p_q * 1e3, 3),
-                                        "row_gather": round(p_g * 1e3, 3),
-                                        "note": "separate synchronized steps, max over ranks"},
+               "config": {"workload": cfg["workload"], "seq_len": L, "k": k, **cfg_rec,
                           "parallelism": f"shard{world}"},
                "roofline": query_roofline(per, L // world, Nw_rank, H // world, _load_pmc(5),
-                                          t / args.steps * 1e3, launches),
+                                          rec["ms_per_step"], launches),
+               "to_host": rec["to_host"], "c1_broadcast_ms": rec["c1_broadcast_ms"],
                "cpu_baseline": cpu,
                "index_build": build_rec,
                "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
-    index.free()
 
 
 # config 5's CPU baseline: the reference on a prefix of A and of B (the whole 500 Mbp index needs

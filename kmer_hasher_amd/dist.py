@@ -66,16 +66,34 @@ def gather_rows(local: torch.Tensor, dst: int = 0, group=None) -> torch.Tensor |
         for c in counts:
             offs.append(offs[-1] + c)
         out[offs[rank]:offs[rank + 1]] = local
-        ops = [dist.P2POp(dist.irecv, out[offs[r]:offs[r + 1]], r, group=group)
-               for r in range(world) if r != dst and counts[r]]
-        for w in (dist.batch_isend_irecv(ops) if ops else []):
-            w.wait()
+        p2p([("recv", out[offs[r]:offs[r + 1]], r) for r in range(world)
+             if r != dst and counts[r]], group)
         return out
     if counts[rank]:
-        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), dst,
-                                                    group=group)]):
-            w.wait()
+        p2p([("send", local.contiguous(), dst)], group)
     return None
+
+
+def p2p(ops: list, group=None) -> None:
+    """One batch of point-to-point transfers, ("send" | "recv", tensor, group rank) each, waited
+    for.  gloo moves device tensors in its collectives but not point to point: there (the
+    one-GPU rehearsals) device tensors are staged through host copies."""
+    if not ops:
+        return
+    stage = dist.get_backend(group) == "gloo"
+    batch, post = [], []
+    for kind, t, peer in ops:
+        if stage and t.is_cuda:
+            h = t.cpu() if kind == "send" else torch.empty(t.shape, dtype=t.dtype)
+            if kind == "recv":
+                post.append((t, h))
+            t = h
+        batch.append(dist.P2POp(dist.isend if kind == "send" else dist.irecv, t,
+                                _global(peer, group), group=group))
+    for w in dist.batch_isend_irecv(batch):
+        w.wait()
+    for t, h in post:
+        t.copy_(h)
 
 
 def broadcast_sequence(seq: torch.Tensor | None, src: int, device: torch.device,
@@ -92,33 +110,186 @@ def broadcast_sequence(seq: torch.Tensor | None, src: int, device: torch.device,
     return out
 
 
+def slice_bounds(n_chars: int, k: int, w0: int, w1: int) -> tuple[int, int]:
+    """The chars [a, b) a range query of windows [w0, w1) reads: the window rule needs chars
+    [w0 - 1, w1 + k - 1) (src/kmer_pos.c:121-134: the N before a window, the end-drop test); the
+    probe's aligned tile loads and halo read a few more around them, which feed only windows
+    outside the range (the same bounds as the one-process multi-device split,
+    kmhg_engine.cpp query_multi_device)."""
+    if w1 <= w0:
+        return 0, 0
+    return max(0, (w0 & ~15) - 64), min(n_chars, w1 + k + 64)
+
+
+def scatter_sequence(seq: torch.Tensor | None, k: int, src: int, device: torch.device,
+                     group=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """C1 as a scatter: rank `src` holds the query; every other rank receives only the chars its
+    window range reads (slice_bounds), in place in a full-length buffer, so the range query
+    addresses the sequence by its absolute positions.  (N - 1)/N of L leaves the root, one slice
+    per link, instead of the whole L on every link (broadcast_sequence).  `out`: a buffer of at
+    least L + 16 bytes to reuse across calls.  Chars outside the slice are undefined (on CPU
+    they read 'A': the gloo tests' oracle engine reads the whole buffer)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n = torch.zeros(1, dtype=torch.int64, device=device)
+    if rank == src:
+        n[0] = seq.numel()
+    dist.broadcast(n, src, group=group)
+    L = int(n.item())
+    ranges = shard_ranges(max(0, L - k + 1), world)
+    if rank == src:
+        ops = []
+        for r in range(world):
+            a, b = slice_bounds(L, k, *ranges[r])
+            if r != src and b > a:
+                ops.append(("send", seq[a:b], r))
+        p2p(ops, group)
+        return seq
+    if out is None or out.numel() < L + 16 or out.device != device:
+        out = torch.empty(L + 16, dtype=torch.uint8, device=device)
+        if device.type == "cpu":
+            out.fill_(ord("A"))
+    a, b = slice_bounds(L, k, *ranges[rank])
+    if b > a:
+        p2p([("recv", out[a:b], src)], group)
+    return out[:L]
+
+
+def _global(r: int, group) -> int:
+    """P2POp peers are global ranks."""
+    return r if group is None else dist.get_global_rank(group, r)
+
+
+class HostRowSink:
+    """ONE host matrix shared by the ranks of a node (POSIX shared memory), into which every
+    rank copies its own rows D2H at its row offset: each GPU uses its own PCIe link, and no row
+    crosses xGMI ("Where the rows go").  The buffer is grown, never shrunk, and
+    registered with the HIP runtime (hipHostRegister) so the copies are direct DMA; reuse one
+    sink across queries.  close() on every rank releases it (the owner unlinks the segment)."""
+
+    def __init__(self, owner: int = 0, group=None):
+        self.owner, self.group = owner, group
+        self.rank = dist.get_rank(group)
+        self.cap = 0
+        self.gen = 0
+        self.shm = None
+        self.t = None
+        self.registered = None
+        self.token = None
+
+    def _name(self) -> str:
+        return f"kmhg_rows_{self.token}_{self.gen}"
+
+    def _release(self):
+        if self.registered is not None:
+            torch.cuda.cudart().cudaHostUnregister(self.registered)
+            self.registered = None
+        self.t = None
+        if self.shm is not None:
+            self.shm.close()
+            if self.rank == self.owner:
+                self.shm.unlink()
+            self.shm = None
+
+    def ensure(self, rows: int, device: torch.device):
+        """A buffer of at least `rows` rows on every rank (collective: same `rows` everywhere)."""
+        from multiprocessing import shared_memory
+        if self.token is None:
+            import os
+            tok = torch.tensor([os.getpid() if self.rank == self.owner else 0], dtype=torch.int64,
+                               device=device)
+            dist.broadcast(tok, _global(self.owner, self.group), group=self.group)
+            self.token = int(tok.item())
+        if rows <= self.cap and self.t is not None:
+            return
+        dist.barrier(group=self.group)             # nobody still writes the old buffer
+        self._release()
+        self.gen += 1
+        nbytes = max(8, rows * 8)
+        if self.rank == self.owner:
+            self.shm = shared_memory.SharedMemory(name=self._name(), create=True, size=nbytes)
+        dist.barrier(group=self.group)
+        if self.rank != self.owner:
+            self.shm = shared_memory.SharedMemory(name=self._name())
+            # only the owner unlinks: keep Python's resource tracker from unlinking the
+            # segment again when this process exits (it registers every attachment)
+            from multiprocessing import resource_tracker
+            try:
+                resource_tracker.unregister(self.shm._name, "shared_memory")
+            except Exception:
+                pass
+        self.t = torch.frombuffer(self.shm.buf, dtype=torch.int32, count=nbytes // 4)
+        if device.type == "cuda":
+            ptr = self.t.data_ptr()
+            if int(torch.cuda.cudart().cudaHostRegister(ptr, nbytes, 0)) == 0:
+                self.registered = ptr
+        self.cap = nbytes // 8
+
+    def close(self):
+        self._release()
+        self.cap = 0
+
+
+def deliver_rows_host(local: torch.Tensor, sink: HostRowSink, group=None):
+    """Every rank's (h_r, 2) int32 rows into the sink's shared host matrix, rank r's at row
+    offset h_0 + ... + h_{r-1} (= the reference's row order), each rank copying its own rows
+    D2H.  Returns the (H, 2) matrix (a view of the shared buffer) on the sink's owner, else
+    None.  The matrix is valid until the next delivery into the same sink."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = local.device
+    cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(counts, cnt, group=group)
+    counts = [int(c.item()) for c in counts]
+    H = sum(counts)
+    sink.ensure(H, dev)
+    off = sum(counts[:rank])
+    if counts[rank]:
+        sink.t[2 * off:2 * (off + counts[rank])].view(-1, 2).copy_(local)
+    dist.barrier(group=group)                       # every rank's copy has landed
+    if rank == sink.owner:
+        return sink.t[:2 * H].view(-1, 2)
+    return None
+
+
 def sharded_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, group=None,
-                  src: int | None = None, timings: dict | None = None):
+                  src: int | None = None, timings: dict | None = None, c1: str = "scatter",
+                  sink: HostRowSink | None = None, seq_buf: torch.Tensor | None = None):
     """seq.kmer.pos with the query windows split across ranks; rows gathered on `dst`.
 
     src=None: every rank already holds the whole query.  src=r: only rank r holds it (the R
-    session's query string arrives on one process) and it is broadcast first (C1).  `timings`
-    (optional) receives the seconds of each phase as seen by this rank: 'broadcast', 'query'
-    (the HIP range query) and 'gather'."""
+    session's query string arrives on one process): c1="scatter" sends each rank the slice its
+    windows read (scatter_sequence), c1="broadcast" the whole sequence (broadcast_sequence).
+    sink=None: rows gathered into one device buffer on `dst` (gather_rows, over xGMI); a
+    HostRowSink: every rank copies its rows into the shared host matrix (deliver_rows_host).
+    `seq_buf`: scatter receive buffer to reuse.  `timings` (optional) receives the seconds of
+    each phase as seen by this rank: 'broadcast' (C1), 'query' (the HIP range query) and
+    'gather'."""
     import time
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    dev = seq.device if seq is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+        else torch.device("cpu"))
 
     def mark():
-        if timings is not None and seq is not None and seq.is_cuda:
-            torch.cuda.synchronize(seq.device)
+        if timings is not None and dev.type == "cuda":
+            torch.cuda.synchronize(dev)
         return time.perf_counter()
 
     t0 = mark()
     if src is not None:
-        dev = seq.device if seq is not None else torch.device("cuda", torch.cuda.current_device())
-        seq = broadcast_sequence(seq, src, dev, group)
+        if c1 == "scatter":
+            seq = scatter_sequence(seq, k, src, dev, group, out=seq_buf)
+        else:
+            seq = broadcast_sequence(seq, src, dev, group)
     t1 = mark()
     n_windows = max(0, seq.numel() - k + 1)
     w0, w1 = shard_ranges(n_windows, world)[rank]
     local = engine.query_range(seq, k, w0, w1)
     t2 = mark()
-    rows = gather_rows(local, dst, group)
+    rows = gather_rows(local, dst, group) if sink is None else deliver_rows_host(local, sink, group)
     t3 = mark()
     if timings is not None:
         for name, dt in (("broadcast", t1 - t0), ("query", t2 - t1), ("gather", t3 - t2)):

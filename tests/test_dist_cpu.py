@@ -79,6 +79,77 @@ def test_sharded_query_matches_unsharded(world, k_index, kq):
     assert got == want
 
 
+def _c1_worker(rank, world, port, seq_bytes, k_index, kq, c1, host, out_q):
+    """The R session's query on rank 0 only: C1 by scatter (each rank receives the slice its
+    windows read) or broadcast, rows gathered on rank 0's device or delivered by every rank into
+    the shared host matrix; twice through one sink / one receive buffer (reuse)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sink = kd.HostRowSink(0) if host else None
+    try:
+        eng = OracleEngine(seq_bytes, k_index)
+        seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()) if rank == 0 else None
+        buf = torch.full((len(seq_bytes) + 16,), ord("A"), dtype=torch.uint8) if rank else None
+        got = []
+        for _ in range(2):
+            ph = {}
+            rows = kd.sharded_query(eng, seq, kq, dst=0, src=0, c1=c1, sink=sink, seq_buf=buf,
+                                    timings=ph)
+            assert set(ph) == {"broadcast", "query", "gather"}
+            if rank == 0:
+                got.append(rows.numpy().reshape(-1).tolist())
+            else:
+                assert rows is None
+        if rank == 0:
+            out_q.put(got)
+    finally:
+        if sink is not None:
+            sink.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,c1,host", [(2, "scatter", False), (2, "scatter", True),
+                                           (3, "scatter", True), (3, "broadcast", True)])
+def test_sharded_query_scatter_and_host_rows(world, c1, host):
+    """C1 as a scatter of slices and rows delivered into one shared host matrix reproduce the
+    unsharded reference rows exactly, including an N right at a shard edge and the end-drop
+    rule; the shared-memory segment is gone afterwards."""
+    from oracle import oracle as O
+    k = 21
+    s = synth.add_n_runs(synth.iid(40_000, 77), 0.01, 9)
+    n_w = len(s) - k + 1
+    for a, _ in kd.shard_ranges(n_w, world)[1:]:
+        s[a - 1] = ord("N")            # the char before a shard's first window
+        s[a + k - 1] = ord("N")        # the last char of a shard's first window
+    s[-k - 1] = ord("N")
+    seq_bytes = s.tobytes()
+    want = O.OracleIndex(seq_bytes, k).query(seq_bytes, k).tolist()
+    before = set(os.listdir("/dev/shm"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c1_worker, args=(r, world, port, seq_bytes, k, k, c1, host, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert got[0] == want and got[1] == want
+    assert not [f for f in set(os.listdir("/dev/shm")) - before if f.startswith("kmhg_rows")]
+
+
+def test_slice_bounds_cover_window_rule():
+    """A range's slice holds the char before its first window and the last char of its last
+    window (the window rule's reads), clipped to the sequence."""
+    for L, k, w0, w1 in [(1000, 31, 0, 500), (1000, 31, 500, 970), (10**6, 21, 123_457, 654_321)]:
+        a, b = kd.slice_bounds(L, k, w0, w1)
+        assert a <= max(0, w0 - 1) and b >= min(L, w1 + k - 1)
+        assert 0 <= a and b <= L
+    assert kd.slice_bounds(100, 5, 7, 7) == (0, 0)
+
+
 def test_shard_ranges():
     assert kd.shard_ranges(10, 3) == [(0, 4), (4, 7), (7, 10)]
     assert kd.shard_ranges(0, 2) == [(0, 0), (0, 0)]

@@ -213,3 +213,79 @@ def test_nccl_world1_owner_build_assemble_sharded_query(gpu, k, kq):
     assert (nk, npos, npair) == (oi.U, oi.N, oi.P)
     assert got == want and got2 == want
     assert phases == ["broadcast", "gather", "query"]
+
+
+def _scatter_worker(rank, world, port, seq_bytes, k, backend, out_q):
+    """The R session's query on rank 0 only (config 5's step): C1 scatters each rank the slice
+    its windows read (dist.scatter_sequence, into a reused buffer), every rank runs the HIP range
+    query, and the rows are gathered into rank 0's device buffer, then delivered into the
+    node-shared host matrix (dist.HostRowSink, hipHostRegister'ed)."""
+    import torch
+    import torch.distributed as dist
+    from kmer_hasher_amd import dist as kd
+    from kmer_hasher_amd.device import DeviceIndex
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    sink = kd.HostRowSink(0)
+    try:
+        seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()).to(dev) \
+            if rank == 0 else None
+        built = DeviceIndex.build(seq, k) if rank == 0 else None
+        idx = kd.broadcast_index(built, dev, src=0)
+        eng = kd.HipQueryEngine(idx)
+        buf = torch.empty(len(seq_bytes) + 16, dtype=torch.uint8, device=dev) if rank else None
+        res = []
+        for to_host in (False, True, True):
+            rows = kd.sharded_query(eng, seq, k, dst=0, src=0, c1="scatter",
+                                    sink=sink if to_host else None, seq_buf=buf)
+            torch.cuda.synchronize()
+            if rank == 0:
+                res.append((str(rows.device), rows.cpu().numpy().reshape(-1).tolist()))
+        if rank == 0:
+            out_q.put((res, sink.registered is not None))
+        dist.barrier()
+        idx.free()
+    finally:
+        sink.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k,backend", [(2, 31, "gloo"), (3, 21, "gloo"), (1, 31, "nccl")])
+def test_scatter_query_rows_to_device_and_host(gpu, world, k, backend):
+    import torch.multiprocessing as mp
+    from kmer_hasher_amd import synth
+    from kmer_hasher_amd import dist as kd
+    from oracle import oracle as O
+    s = synth.add_n_runs(synth.repeat_rich(130_000, 4, n_gap_every=8_009), 0.004, 5)
+    n_w = len(s) - k + 1
+    for a, _ in kd.shard_ranges(n_w, world)[1:]:
+        s[a - 1] = ord("N")              # an N just before a shard's first window
+    s[-k - 2] = ord("N")
+    seq_bytes = s.tobytes()
+    want = O.OracleIndex(seq_bytes, k).query(seq_bytes, k).tolist()
+    before = set(os.listdir("/dev/shm"))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, seq_bytes, k, backend, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res, registered = q.get(timeout=100)
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert [r[0] for r in res] == ["cuda:0", "cpu", "cpu"]
+    assert all(r[1] == want for r in res)
+    assert registered                   # the host matrix is DMA-registered
+    assert not [f for f in set(os.listdir("/dev/shm")) - before if f.startswith("kmhg_rows")]
