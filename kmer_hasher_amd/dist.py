@@ -3,11 +3,13 @@
 
   * the index is built once (rank 0) and its device image is broadcast to every rank
     (two ncclBroadcast calls: the hash table and the positions);
-  * the query's windows are split into `world` contiguous ranges; each rank runs the HIP query
-    on its range of the (replicated) query sequence -- validity at a range edge is decided on
-    the full sequence, so no halo logic leaks into the result;
+  * the query's windows are split into `world` contiguous ranges; the query, held by one rank,
+    is scattered (each rank receives the chars its range reads, at their absolute positions) or
+    broadcast; each rank runs the HIP query on its range -- validity at a range edge is decided
+    from the same chars as on the full sequence, so no halo logic leaks into the result;
   * per-rank row counts are all-gathered (8 B each) and the rows are gathered to the root with
-    point-to-point send/recv (RCCL has no gatherv); concatenation in rank order is exactly the
+    point-to-point send/recv (RCCL has no gatherv), or every rank copies its rows into one
+    node-shared host matrix (HostRowSink); concatenation in rank order is exactly the
     reference's row order (window end ascending, then index position ascending).
 
 The collective layer is engine-agnostic: anything with ``query_range(seq, k, w0, w1) -> (h, 2)
