@@ -88,10 +88,9 @@ BID_MAX_WINDOWS = 12 << 20   # kmhg_engine.cpp build_device_v2: bucket-id stream
 
 
 def bid_streams(Nw: int) -> bool:
-    """Whether a position build of Nw windows runs bucket-id radix streams (the engine's rule,
-    KMHG_BUILD_BID=0/1 forcing it)."""
-    e = os.environ.get("KMHG_BUILD_BID")
-    return e.startswith("1") if e else Nw <= BID_MAX_WINDOWS
+    """Whether a position build of Nw windows runs bucket-id radix streams (the engine's rule;
+    only the test build lets KMHG_BUILD_BID force it)."""
+    return Nw <= BID_MAX_WINDOWS
 
 
 def algorithmic_bytes(kernel: str, L: int, Nw: int, U: int, N: int, H: int = 0) -> int | None:

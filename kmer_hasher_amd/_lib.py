@@ -108,28 +108,62 @@ def header_symbols() -> list[str]:
     return sorted(set(re.findall(r"\b(kmhg_[a-z_]+)\s*\(", txt)))
 
 
+def _load(path: str):
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    # Load after torch (if present) so both share one HIP runtime (soname libamdhip64.so.7).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = C.CDLL(path)
+    for name, (res, args) in _PROTOS.items():
+        if os.environ.get("KMHG_LIB_VARIANT") and not hasattr(L, name):
+            continue              # an older A/B build may predate an entry point
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
 def lib():
     """Load libkmhgpu.so (raises if absent: the HIP path is the only path)."""
     global _LIB
     if _LIB is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(
-                f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
-                "(hipcc --offload-arch=gfx950); there is no CPU fallback")
-        # Load after torch (if present) so both share one HIP runtime (soname libamdhip64.so.7).
-        try:
-            import torch  # noqa: F401
-        except Exception:
-            pass
-        L = C.CDLL(LIB_PATH)
-        for name, (res, args) in _PROTOS.items():
-            if os.environ.get("KMHG_LIB_VARIANT") and not hasattr(L, name):
-                continue              # an older A/B build may predate an entry point
-            f = getattr(L, name)
-            f.restype = res
-            f.argtypes = args
-        _LIB = L
+        _LIB = _load(LIB_PATH)
     return _LIB
+
+
+TEST_LIB_PATH = os.path.join(_HERE, "libkmhgpu_test.so")
+_TEST_LIB = None
+
+
+class using_test_build:
+    """Context in which every entry point goes to libkmhgpu_test.so: the same kernels, with the
+    host orchestrator compiled -DKMHG_TEST_BUILD, the only build that reads the path selectors
+    and fault injection (kmhg_engine.cpp "Environment knobs").  For the GPU tests that force a
+    path; every handle made inside must be freed inside (the two libraries keep separate
+    pools)."""
+
+    def __enter__(self):
+        global _LIB, _TEST_LIB
+        lib()
+        if _TEST_LIB is None:
+            _TEST_LIB = _load(TEST_LIB_PATH)
+        self.prev, _LIB = _LIB, _TEST_LIB
+        return _TEST_LIB
+
+    def __exit__(self, *exc):
+        global _LIB
+        import gc
+        gc.collect()                   # handles of the test build die with it
+        try:
+            _TEST_LIB.kmhg_pool_trim()
+        finally:
+            _LIB = self.prev
+        return False
 
 
 def check(rc: int) -> None:

@@ -376,19 +376,19 @@ static __global__ void __launch_bounds__(BLOCK) k_iota_u32(uint32_t* __restrict_
   const uint32_t r = blockIdx.x * BLOCK + threadIdx.x;
   if (r < n) a[r] = r;
 }
-size_t rows_sort_temp_bytes(uint32_t U, int bits) {
-  size_t bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint64_t*)nullptr,
-                                           (uint64_t*)nullptr, (const uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (int)U, 0, bits);
-  return bytes;
+hipError_t rows_sort_temp_bytes(uint32_t U, int bits, size_t* bytes) {
+  *bytes = 0;
+  return hipcub::DeviceRadixSort::SortPairs(nullptr, *bytes, (const uint64_t*)nullptr,
+                                            (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                                            (uint32_t*)nullptr, (int)U, 0, bits);
 }
-void launch_rows_sort(const uint64_t* rord, uint32_t U, int bits, uint64_t* keys_out,
-                      uint32_t* rows_in, uint32_t* rorder, void* temp, size_t temp_bytes,
-                      hipStream_t s) {
+hipError_t launch_rows_sort(const uint64_t* rord, uint32_t U, int bits, uint64_t* keys_out,
+                            uint32_t* rows_in, uint32_t* rorder, void* temp, size_t temp_bytes,
+                            hipStream_t s) {
   hipLaunchKernelGGL(k_iota_u32, dim3(grid_of(U)), dim3(BLOCK), 0, s, rows_in, U);
-  (void)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, rord, keys_out, rows_in, rorder,
-                                           (int)U, 0, bits, s);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  return hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, rord, keys_out, rows_in, rorder,
+                                            (int)U, 0, bits, s);
 }
 void launch_rows_gather(const uint32_t* rorder, const uint64_t* ckeys, const int32_t* M,
                         uint32_t U, uint32_t S, uint64_t* okeys, int32_t* oM, hipStream_t s) {

@@ -29,17 +29,17 @@
 #include "kmhg_khash.h"
 #include "kmhg_sh.h"
 
-// Environment knobs.  Product: KMHG_TIMING (per-kernel events), KMHG_DEVICES (multi-device
-// query), KMHG_ROW_ORDER, KMHG_D2H_THREADS.  Path selectors the GPU suite uses to force each
+// Environment knobs.  The product library reads four: KMHG_TIMING (per-kernel events),
+// KMHG_DEVICES (multi-device query), KMHG_ROW_ORDER and KMHG_D2H_THREADS.  Everything else exists
+// only in the test build (-DKMHG_TEST_BUILD: libkmhgpu_test.so, which the GPU suite loads for the
+// tests that force a path, tests/conftest.py `test_lib`): the path selectors that force each
 // build / query / counts path against the oracle (KMHG_BUILD, KMHG_BUILD_BID, KMHG_MAXR,
 // KMHG_FUSE_BOUNDS, KMHG_TEST_BALLOT, KMHG_QUERY_TAGS, KMHG_QUERY_DIAG, KMHG_DIAG_CODES,
 // KMHG_COUNT_TABLE, KMHG_COUNT_WALK, KMHG_CO_SPREAD, KMHG_CO_GLOBAL, KMHG_PART_COMPACT,
 // KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_NB_ROUND, KMHG_SLICE_POISON, KMHG_TEST_REPLICA,
-// KMHG_DIGIT_STREAM, KMHG_DS_U8, KMHG_DS_PACK) choose
-// between equivalent paths and change no result.
-// Fault injection (KMHG_TEST_DISORDER) and the A/B-only switches (KMHG_D2H, KMHG_COUNT_BID,
-// KMHG_RK_CAP) exist only in the test build (-DKMHG_TEST_BUILD: libkmhgpu_test.so, make test):
-// the product library never reads them.
+// KMHG_DIGIT_STREAM, KMHG_DS_BID, KMHG_DS_U8, KMHG_DS_PACK), which choose between equivalent
+// paths and change no result; fault injection (KMHG_TEST_DISORDER); and the A/B-only switches
+// (KMHG_D2H, KMHG_COUNT_BID, KMHG_RK_CAP).
 namespace kmhg {
 inline const char* test_build_knob(const char* name) {
 #ifdef KMHG_TEST_BUILD
@@ -781,8 +781,25 @@ kmhg_index* build_device_v1(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 // (build_device_v2); KMHG_BUILD_BID=0 / 1 forces key / bucket-id streams.
 constexpr int64_t BID_MAX_WINDOWS = 12 << 20;
 bool bid_streams_for(int64_t Nw) {
-  const char* bide = std::getenv("KMHG_BUILD_BID");
+  const char* bide = test_build_knob("KMHG_BUILD_BID");
   return bide ? bide[0] == '1' : Nw <= BID_MAX_WINDOWS;
+}
+
+// One round of the bucket kernel on the current device: its CUs x the workgroups one CU holds
+// (cached per device; 0 if the device cannot be queried).
+uint32_t bucket_round_of_current_device() {
+  static std::atomic<uint32_t> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+  if (dev < 64) {
+    if (uint32_t v = cache[dev].load(std::memory_order_relaxed)) return v;
+  }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 0;
+  const uint32_t v = (uint32_t)std::max(cus, 0) * (uint32_t)KMHG_BUCKET_WGS;
+  if (dev < 64) cache[dev].store(v, std::memory_order_relaxed);
+  return v;
 }
 
 constexpr double CO_FILL = 0.6;                  // target mean occupancy of a count-only bucket
@@ -791,7 +808,7 @@ constexpr double CO_FILL = 0.6;                  // target mean occupancy of a c
 // ~`distinct` distinct ones: mean distinct keys per bucket ~CO_FILL x V2_CAPW, at most 4x.
 // KMHG_CO_SPREAD (tests) forces one, rounded down to a divisor of 12 (build_device_v2).
 int co_spread_for(double distinct, uint64_t total) {
-  if (const char* e = std::getenv("KMHG_CO_SPREAD")) {
+  if (const char* e = test_build_knob("KMHG_CO_SPREAD")) {
     int f = std::max(1, std::min(12, std::atoi(e)));
     while (12 % f) --f;
     return f;
@@ -844,7 +861,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // elements per digit run: beyond ~300 digits the runs get too short for coalesced writes and
   // an extra pass is cheaper.
   uint32_t maxr = V2_MAXR_IL;
-  const char* e = std::getenv("KMHG_MAXR");   // testing knob: force more radix passes
+  const char* e = test_build_knob("KMHG_MAXR");   // testing knob: force more radix passes
   if (e && e[0])
     maxr = std::max<uint32_t>(2u, std::min<uint32_t>(maxr, (uint32_t)std::atoi(e)));
   auto plan = [&](uint32_t nbk, uint32_t& R) {
@@ -875,19 +892,18 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // the device's resident workgroups (config 2: 9,766 buckets on 256 CUs x 8) cost 5; rounding
   // the bucket count up to whole rounds gives each bucket fewer windows instead (position builds
   // of 2-16 rounds; the parts of an owner-computes build split the same rounded table, so they
-  // still assemble into the single-device table).  KMHG_NB_ROUND=0 keeps ceil(windows / 1,024).
+  // still assemble into the single-device table).  Only when the extra buckets are few (at most
+  // an eighth more: a build just past a round boundary would otherwise nearly double its table
+  // and halve its load).  The round is the building device's own (CUs x workgroups per CU).
+  // KMHG_NB_ROUND=0 (test build) keeps ceil(windows / 1,024).
   if (!from_keys && !count_only) {
-    const char* nre = std::getenv("KMHG_NB_ROUND");
+    const char* nre = test_build_knob("KMHG_NB_ROUND");
     if (!(nre && nre[0] == '0')) {
-      static const uint32_t wave_wg = [] {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-          cus = 0;
-        return (uint32_t)std::max(cus, 0) * (uint32_t)KMHG_BUCKET_WGS;
-      }();
-      if (wave_wg && nb_g > wave_wg && nb_g <= 16 * wave_wg)
-        nb_g = (nb_g + wave_wg - 1) / wave_wg * wave_wg;
+      const uint32_t wave_wg = bucket_round_of_current_device();
+      if (wave_wg && nb_g > wave_wg && nb_g <= 16 * wave_wg) {
+        const uint32_t rounded = (nb_g + wave_wg - 1) / wave_wg * wave_wg;
+        if (rounded - nb_g <= nb_g / 8) nb_g = rounded;
+      }
     }
   }
   uint32_t R = 0;
@@ -950,7 +966,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const int sh8 = 64 - 2 * k;
   const uint64_t seg8 = sh8 >= 12 && sh8 < 64 ? (1ull << sh8) : 0;
   const uint32_t nseg8 = seg8 ? (uint32_t)(((uint64_t)Nw + seg8 - 1) / seg8) : 0;
-  const char* p8e = std::getenv("KMHG_PACK8");
+  const char* p8e = test_build_knob("KMHG_PACK8");
   const bool pack8 = aos && passes == 2 && n_parts < 2 && seg8 && nseg8 <= 256 &&
                      !(p8e && p8e[0] == '0');
   // Digit streams (DS): each pass before the last also writes every output element's digit of
@@ -972,8 +988,8 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // histogram 10.2 -> 6.7 us, first scatter +3-6 us, build 0.2076-0.2092 ms either way
   // (profiles/r5y_ab_ds_bid_config2.log).  KMHG_DS_BID=1 (or KMHG_DIGIT_STREAM=1) turns them on.
   constexpr int64_t DS_MIN_WINDOWS = 25'000'000;
-  const char* dse = std::getenv("KMHG_DIGIT_STREAM");
-  const char* dbe = std::getenv("KMHG_DS_BID");
+  const char* dse = test_build_knob("KMHG_DIGIT_STREAM");
+  const char* dbe = test_build_knob("KMHG_DS_BID");
   // (a part build's later streams hold ~1/n_parts of the windows)
   const int64_t ds_windows = n_parts >= 2 ? Nw / n_parts : Nw;
   const bool ds_keys = !bid && !from_keys && !count_only && passes >= 2 &&
@@ -982,7 +998,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   const bool ds_bids = bid && passes >= 2 &&
                        (dse && dse[0] ? dse[0] == '1' : R <= 256 && dbe && dbe[0] == '1');
   const bool ds_on = ds_keys || ds_bids;
-  const char* dpe = std::getenv("KMHG_DS_PACK");
+  const char* dpe = test_build_knob("KMHG_DS_PACK");
   const bool ds_pack = ds_keys && !(dpe && dpe[0] == '0');
   auto packed = [&](int p) {
     return aos && (p + 1 == (int)passes || R >= AOS_MIN_RADIX || ds_pack);
@@ -1010,7 +1026,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   DBuf<uint32_t> segb(pack8 ? (uint64_t)R * (nseg8 + 1) : 1, s);
   // one digit buffer: pass p's histogram has read it before pass p rewrites it for pass p + 1
   // u8 digits at a radix <= 256 (KMHG_DS_U8=0: u16, A/B)
-  const char* d8e = std::getenv("KMHG_DS_U8");
+  const char* d8e = test_build_knob("KMHG_DS_U8");
   const bool ds8 = ds_on && R <= 256 && !(d8e && d8e[0] == '0');
   DBuf<uint16_t> dsb(ds_on ? ((uint64_t)Nw + PTILE + 8) / (ds8 ? 2 : 1) + 8 : 1, s);
   uint8_t* ds8p = ds8 ? reinterpret_cast<uint8_t*>(dsb.p) : nullptr;
@@ -1055,7 +1071,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // parts on (one-GPU rehearsal, tools/part_step.py, per-rank step of 10 Mbp per part: 2 parts
   // 0.397 -> 0.467 ms, 4 parts 0.504 -> 0.495, 8 parts 0.749 -> 0.581).  KMHG_PART_COMPACT=0 / 1
   // forces the first pass over every window / the compaction (tests).
-  const char* pce = std::getenv("KMHG_PART_COMPACT");
+  const char* pce = test_build_knob("KMHG_PART_COMPACT");
   const bool partc = !from_keys && n_parts >= 2 && !bid && codes &&
                      (pce ? pce[0] == '1' : n_parts >= 4);
   DBuf<uint32_t> tcnt(partc ? ntiles : 1, s);
@@ -1134,7 +1150,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // each level of the bucket starts rides in its pass (BoundsFuse), except the last one of a
   // count-only build whose spread is chosen after the passes (co_auto); KMHG_FUSE_BOUNDS=0
   // (A/B) launches every level on its own
-  const char* fbe = std::getenv("KMHG_FUSE_BOUNDS");
+  const char* fbe = test_build_knob("KMHG_FUSE_BOUNDS");
   const bool fuse_on = !(fbe && fbe[0] == '0');
   auto level_of = [&](uint32_t p, const void* kprev, bool is_bid, uint32_t spread) {
     uint64_t dv = 1;                                    // R^p lower-digit values
@@ -1287,7 +1303,7 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
 
 // the tag filter of the diagonal query path (per call: tests switch it)
 bool tags_on() {
-  const char* e = std::getenv("KMHG_QUERY_TAGS");
+  const char* e = test_build_knob("KMHG_QUERY_TAGS");
   return !(e && e[0] == '0');
 }
 
@@ -1323,7 +1339,7 @@ static void lane_order_run(int blocks, uint64_t* bad, uint64_t* checked) {
   *checked = h[1];
 }
 bool lane_ballot() {
-  if (const char* e = std::getenv("KMHG_TEST_BALLOT"))
+  if (const char* e = test_build_knob("KMHG_TEST_BALLOT"))
     if (e[0] == '1') return true;
   int dev = 0;
   HIPC(hipGetDevice(&dev));
@@ -1343,7 +1359,7 @@ bool lane_ballot() {
 }
 
 int build_version() {   // read per build so tests can exercise the fallback (KMHG_BUILD=v1)
-  const char* e = std::getenv("KMHG_BUILD");
+  const char* e = test_build_knob("KMHG_BUILD");
   return (e && std::string(e) == "v1") ? 1 : 2;
 }
 
@@ -1351,7 +1367,7 @@ int build_version() {   // read per build so tests can exercise the fallback (KM
 // codes: keep the sequence's code words for the diagonal query path (position indices; a
 // count.kmers batch index has no use for them)
 kmhg_index* build_device(const uint8_t* d_seq, int64_t L, int k, hipStream_t s, bool codes = true) {
-  if (const char* e = std::getenv("KMHG_DIAG_CODES"))   // tests / A/B: no code block
+  if (const char* e = test_build_knob("KMHG_DIAG_CODES"))   // tests / A/B: no code block
     if (e[0] == '0') codes = false;
   if (build_version() == 2)
     return build_device_v2(d_seq, L, k, s, nullptr, 0, false, 1, false, codes);
@@ -1420,7 +1436,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   uint64_t H = 0;
   // diagonal path (k_query_probe): a position index queried at its own k
   const int64_t nA = idx->L - idx->k + 1;
-  const char* de = std::getenv("KMHG_QUERY_DIAG");
+  const char* de = test_build_knob("KMHG_QUERY_DIAG");
   const bool diag_ok = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
                        idx->U > 0 && idx->dcodes.p;
   bool diag = diag_ok;
@@ -1580,7 +1596,7 @@ uint64_t adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint
   const int32_t* bpos = ord ? B->positions.p : nullptr;
   uint64_t* rord = ord ? idx->rord.p : nullptr;
   uint64_t n_new = Ub;
-  const char* we = std::getenv("KMHG_COUNT_WALK");   // "lb": the look-back walk (A/B, tests)
+  const char* we = test_build_knob("KMHG_COUNT_WALK");   // "lb": the look-back walk (A/B, tests)
   if (B->bstats_nb == B->geom.nb && B->geom.nb > 0 && !(we && std::string(we) == "lb")) {
     // bucket-aligned tiles, row offsets from the bucket statistics: no look-back chain
     const uint32_t nt = count_walk_b_tiles(B->geom.nb);
@@ -1631,7 +1647,7 @@ uint64_t adopt_first_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint
 // KMHG_COUNT_TABLE (tests): "adopt" adopts regardless of size, "rebuild" / "probe" never do.
 bool adoptable(const kmhg_index* idx, const kmhg_index* B) {
   if (idx->U != 0 || B->u_upper) return false;   // a table sized by a key stream: rebuild
-  if (const char* e = std::getenv("KMHG_COUNT_TABLE")) return std::string(e) == "adopt";
+  if (const char* e = test_build_knob("KMHG_COUNT_TABLE")) return std::string(e) == "adopt";
   return B->slots() <= 6 * B->U;
 }
 
@@ -1671,7 +1687,7 @@ void merge_batch(kmhg_index* idx, kmhg_index* B, uint32_t source, uint64_t base,
   const uint64_t U0 = idx->U;
   const bool ord = !idx->canonical;
   // KMHG_COUNT_TABLE (tests): "rebuild" / "probe" take the general merge even for the first batch
-  const char* ct = std::getenv("KMHG_COUNT_TABLE");
+  const char* ct = test_build_knob("KMHG_COUNT_TABLE");
   if (adoptable(idx, B)) {         // first batch into an empty suffix hash
     adopt_first_batch(idx, B, source, base, s);
     return;
@@ -1753,19 +1769,23 @@ void ensure_row_order(kmhg_index* idx, hipStream_t s) {
   // batches of mostly known k-mers) the rows are ordered by a radix sort of their U order keys
   // instead, O(U) scratch (advisor, round 4).  KMHG_ROW_ORDER_SORT=1 / 0 forces the sort / F
   // (tests: both give the same order).
-  const char* rse = std::getenv("KMHG_ROW_ORDER_SORT");
+  const char* rse = test_build_knob("KMHG_ROW_ORDER_SORT");
   const bool by_sort = rse ? rse[0] == '1' : (uint64_t)n > 8 * U;
   if (by_sort) {
     int bits = 1;
     while (bits < 64 && (1ull << bits) < (uint64_t)n) ++bits;
-    const size_t tb = rows_sort_temp_bytes((uint32_t)U, bits);
+    size_t tb = 0;
+    HIPC(rows_sort_temp_bytes((uint32_t)U, bits, &tb));
     DBuf<uint64_t> keys_out(U, s);
     DBuf<uint32_t> rows_in(U, s);
     DBuf<uint8_t> temp(std::max<size_t>(tb, 16), s);
     idx->rorder.bind(s);
     idx->rorder.reset(U);
-    LAUNCH("k_rows_sort", s, launch_rows_sort(idx->rord.p, (uint32_t)U, bits, keys_out.p,
-                                              rows_in.p, idx->rorder.p, temp.p, tb, s));
+    hipError_t sort_err = hipSuccess;
+    LAUNCH("k_rows_sort", s, sort_err = launch_rows_sort(idx->rord.p, (uint32_t)U, bits,
+                                                         keys_out.p, rows_in.p, idx->rorder.p,
+                                                         temp.p, tb, s));
+    HIPC(sort_err);                 // rorder is not valid unless the sort ran
     idx->order_ready = true;
     return;
   }
@@ -1900,7 +1920,7 @@ void sh_count_reads_device(kmhg_index* idx, const uint8_t* d_seq, const uint8_t*
   // coverage: spread 1/2/3/4 -> 22.6/26.8/28.5/27.6 Gbp/s).  The spread comes from THIS
   // batch's HLL estimate of its distinct keys (build_device_v2, co_spread = 0).
   // KMHG_CO_GLOBAL=1 (tests): straight to the global fallback below
-  const bool force_global = std::getenv("KMHG_CO_GLOBAL") != nullptr;
+  const bool force_global = test_build_knob("KMHG_CO_GLOBAL") != nullptr;
   std::unique_ptr<kmhg_index> B;
   bool ovf = true;
   int path = 1;
@@ -2304,10 +2324,10 @@ kmhg_query* query_multi_device(kmhg_index* idx, const char* seq, int64_t L, int 
   q->device = idx->device;
   std::vector<kmhg_query*> parts(G, nullptr);
   std::vector<Error> errs(G, Error{KMHG_OK, ""});
-  const bool poison = std::getenv("KMHG_SLICE_POISON") != nullptr;   // tests: garbage outside
+  const bool poison = test_build_knob("KMHG_SLICE_POISON") != nullptr;   // tests: garbage outside
   // tests: parts after the first on the index's own device use a same-device replica, so the
   // copy path runs on a one-GPU box too
-  const bool test_replica = std::getenv("KMHG_TEST_REPLICA") != nullptr;
+  const bool test_replica = test_build_knob("KMHG_TEST_REPLICA") != nullptr;
   auto run = [&](int i) {
     try {
       const int64_t w0 = Nw * i / G, w1 = Nw * (i + 1) / G;
@@ -2444,7 +2464,7 @@ int kmhg_build_device_part(const void* d_seq, size_t L, int k, int part, int n_p
     if (!d_seq || !out) fail(KMHG_EINVAL, "null argument");
     check_build_args(L, k);
     if (n_parts < 1 || part < 0 || part >= n_parts) fail(KMHG_EINVAL, "part out of range");
-    if (const char* e = std::getenv("KMHG_BUILD"))
+    if (const char* e = test_build_knob("KMHG_BUILD"))
       if (std::string(e) == "v1") fail(KMHG_EINVAL, "part builds need the partitioned build");
     hipStream_t s = (hipStream_t)stream;
     *out = build_device_v2((const uint8_t*)d_seq, (int64_t)L, k, s, nullptr, 0, false, 1, false,

@@ -225,8 +225,8 @@ constexpr DigitOut kNoDigits{nullptr, Digit{}, nullptr};
 void launch_v2_hist_digits(const void* digits, bool u8, const uint32_t* n_ptr, Geom g, Digit D,
                            uint32_t* hist, uint32_t ntiles, uint64_t* scan_status,
                            uint32_t n_status, hipStream_t s, uint32_t* save_col0 = nullptr);
-// Packed 8-B elements of a small-k key stream (the first pass of a two-pass build with 2k <= 53):
-// the high 2k bits hold the key, the low sh = 64 - 2k bits the window's index inside its segment
+// Packed 8-B elements of a small-k key stream (the first pass of a two-pass build with 2k <= 52,
+// i.e. k <= 26: the engine needs sh >= 12): the high 2k bits hold the key, the low sh = 64 - 2k bits the window's index inside its segment
 // of 2^sh windows.  The segment comes back from the element's place in the stream: pass 0 writes
 // digit d's elements tile by tile, so segment s of digit d starts at the scanned histogram entry
 // of (d, s * 2^sh / PTILE) -- segb[d * (nseg + 1) + s], nseg + 1 entries per digit.
@@ -330,8 +330,8 @@ void launch_rows_order(const uint32_t* F, int64_t n, uint64_t* status, uint32_t*
                        uint32_t* rorder, hipStream_t s);
 // rorder by a radix sort of the U (order key, row) pairs instead (O(U) scratch: keys_out U u64,
 // rows_in U u32, temp rows_sort_temp_bytes(U, bits)); bits covers every order key
-size_t rows_sort_temp_bytes(uint32_t U, int bits);
-void launch_rows_sort(const uint64_t* rord, uint32_t U, int bits, uint64_t* keys_out,
+hipError_t rows_sort_temp_bytes(uint32_t U, int bits, size_t* bytes);
+hipError_t launch_rows_sort(const uint64_t* rord, uint32_t U, int bits, uint64_t* keys_out,
                       uint32_t* rows_in, uint32_t* rorder, void* temp, size_t temp_bytes,
                       hipStream_t s);
 void launch_rows_gather(const uint32_t* rorder, const uint64_t* ckeys, const int32_t* M,

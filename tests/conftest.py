@@ -38,3 +38,12 @@ def gpu():
     from kmer_hasher_amd import _lib
     _lib.lib()
     return torch
+
+
+@pytest.fixture
+def test_lib(gpu):
+    """The test build of the library (libkmhgpu_test.so) for one test: the only build that reads
+    the path selectors (KMHG_BUILD, KMHG_MAXR, ...), so tests that force a path request this."""
+    from kmer_hasher_amd import _lib
+    with _lib.using_test_build() as L:
+        yield L

@@ -40,6 +40,20 @@ def test_product_library_reads_no_test_only_knob():
     assert set(_lib.header_symbols()) <= exported
 
 
+def test_product_library_reads_only_four_knobs():
+    """No environment variable can switch the product library's build or query path (VERDICT
+    round 5, item 7): the only KMHG_ names it holds are its four product knobs; the path
+    selectors live in the test build."""
+    import re
+    prod = open(_lib.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"KMHG_[A-Z0-9_]+", prod))
+    assert names == {b"KMHG_TIMING", b"KMHG_DEVICES", b"KMHG_ROW_ORDER", b"KMHG_D2H_THREADS"}, names
+    test = open(_lib.TEST_LIB_PATH, "rb").read()
+    for knob in (b"KMHG_BUILD", b"KMHG_MAXR", b"KMHG_PACK8", b"KMHG_NB_ROUND", b"KMHG_DS_U8",
+                 b"KMHG_QUERY_DIAG", b"KMHG_COUNT_TABLE", b"KMHG_SLICE_POISON"):
+        assert knob in test, knob
+
+
 def test_lib_is_gfx950_code_object():
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in blob     # the .hip_fatbin holds a gfx950 object

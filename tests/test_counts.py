@@ -149,7 +149,7 @@ def test_gpu_counts_golden_khash_order(gpu, cgold):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("table", ["adopt", "adopt-lb", "rebuild", "probe"])
-def test_gpu_counts_first_order_vs_oracle(gpu, cgold, monkeypatch, table):
+def test_gpu_counts_first_order_vs_oracle(gpu, cgold, test_lib, monkeypatch, table):
     """Every way of making the counts table: the first batch's own table adopted (the default
     for a new pointer; its rows from bucket-aligned tiles offset by the bucket statistics, or by
     the look-back walk, adopt-lb: KMHG_COUNT_WALK=lb), the partitioned build over the key list
@@ -173,7 +173,7 @@ def test_gpu_counts_first_order_vs_oracle(gpu, cgold, monkeypatch, table):
 @pytest.mark.gpu
 @pytest.mark.parametrize("order", ["place", "sort"])
 @pytest.mark.parametrize("table", ["adopt", "rebuild"])
-def test_gpu_counts_readout_between_batches(gpu, cgold, monkeypatch, table, order):
+def test_gpu_counts_readout_between_batches(gpu, cgold, test_lib, monkeypatch, table, order):
     """A batch's new rows are written in slot order with their insertion-order keys and sorted
     into first-insertion order only when a readout asks for rows (ensure_row_order).  A readout
     after every call -- rows sorted, then more appended unsorted and sorted again, the earlier

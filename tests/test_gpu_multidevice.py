@@ -26,7 +26,7 @@ def _devices_list(torch, reps):
 
 @pytest.mark.parametrize("replica", ["copy", "home"])
 @pytest.mark.parametrize("reps", [2, 3, 8])
-def test_kmhg_devices_query_matches_oracle(gpu, monkeypatch, reps, replica):
+def test_kmhg_devices_query_matches_oracle(gpu, test_lib, monkeypatch, reps, replica):
     from kmer_hasher_amd import make_kmer_hash, seq_kmer_pos, synth
     monkeypatch.setenv("KMHG_DEVICES", _devices_list(gpu, reps))
     if replica == "copy":
@@ -54,7 +54,7 @@ def test_kmhg_devices_query_matches_oracle(gpu, monkeypatch, reps, replica):
     ptr.free()
 
 
-def test_kmhg_devices_device_readers(gpu, monkeypatch):
+def test_kmhg_devices_device_readers(gpu, test_lib, monkeypatch):
     """A multi-device query's rows read on the device: kmhg_query_rows_device (gathered once on
     the index's device) and kmhg_query_copy_device (peer copies of the parts)."""
     import torch

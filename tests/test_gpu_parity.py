@@ -143,7 +143,7 @@ def test_determinism(gpu):
 # check was removed in round 4 to keep the suite under three minutes.)
 
 
-def test_fallback_build_v1_matches_oracle(gpu, monkeypatch):
+def test_fallback_build_v1_matches_oracle(gpu, test_lib, monkeypatch):
     """The global-atomic build (used when a bucket's LDS sub-table overflows) on its own."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_BUILD", "v1")
@@ -186,7 +186,7 @@ def test_khash_row_order_is_byte_identical_to_reference(gpu, golden, testfa):
 
 @pytest.mark.parametrize("ranks", ["lane", "ballot"])
 @pytest.mark.parametrize("stream", ["bid", "keys"])
-def test_bucket_kernels_vs_oracle(gpu, monkeypatch, stream, ranks):
+def test_bucket_kernels_vs_oracle(gpu, test_lib, monkeypatch, stream, ranks):
     """The group bucket kernel (one workgroup per 1024-window bucket) on every size class:
     repeated keys spanning waves, buckets beyond one batch (tandem repeats), N-runs -- with the
     radix passes and the bucket kernel ranking by the LDS atomics' lane order (the default on a
@@ -219,7 +219,7 @@ def test_lds_atomic_lane_order(gpu):
     assert bad.value == 0, (bad.value, chk.value)
 
 
-def test_build_kind_reported(gpu, monkeypatch):
+def test_build_kind_reported(gpu, test_lib, monkeypatch):
     """kmhg_info.build names the kernels that built the index: partitioned with lane-order
     ranks on a device that passes the self-check, ballot ranks when forced (KMHG_TEST_BALLOT=1,
     what a device failing the check runs), the global-atomic build for KMHG_BUILD=v1."""
@@ -265,7 +265,7 @@ def test_stream_disorder_falls_back(gpu):
 @pytest.mark.parametrize("stream", ["bid", "keys", "keys-levels", "keys-digits"])
 @pytest.mark.parametrize("ranks", ["lane", "ballot"])
 @pytest.mark.parametrize("maxr", ["6", "12", "40", "640"])
-def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, ranks, stream):
+def test_multi_pass_partition_vs_oracle(gpu, test_lib, monkeypatch, maxr, ranks, stream):
     """More radix passes than the input needs (KMHG_MAXR caps the radix): 1-4 passes with N-runs
     and repeat-rich input (700 K windows: maxr 6 -> 4 passes, 12 -> 3, 40 and 640 -> 2; the tiny
     inputs 1).  Bucket starts come from the radix histograms level by level (V_bounds_lo: pass p
@@ -297,7 +297,7 @@ def test_multi_pass_partition_vs_oracle(gpu, monkeypatch, maxr, ranks, stream):
 
 
 @pytest.mark.parametrize("path", ["default", "nodiag", "notags"])
-def test_query_paths_vs_oracle(gpu, monkeypatch, path):
+def test_query_paths_vs_oracle(gpu, test_lib, monkeypatch, path):
     """seq.kmer.pos through the probe / scan / emit kernels (the emit's redo into an exact buffer
     when a query has more rows than the guessed capacity), with the diagonal path off
     (KMHG_QUERY_DIAG=0) and the slot tags off (KMHG_QUERY_TAGS=0): ragged sizes around the
@@ -342,7 +342,7 @@ def test_query_paths_vs_oracle(gpu, monkeypatch, path):
 
 
 @pytest.mark.parametrize("tags", ["1", "0"])
-def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags):
+def test_query_diagonal_path_vs_oracle(gpu, test_lib, monkeypatch, tags):
     """The diagonal path of k_query_probe (anchors every 64th window; later windows follow the
     last anchor with a unique hit and take {count 1, aux = predicted position} only when the
     index window there is unique and its key, read from the index's own code words, equals
@@ -396,7 +396,7 @@ def test_query_diagonal_path_vs_oracle(gpu, monkeypatch, tags):
 
 
 @pytest.mark.parametrize("codes", ["1", "0"])
-def test_query_diagonal_edges_vs_oracle(gpu, monkeypatch, codes):
+def test_query_diagonal_edges_vs_oracle(gpu, test_lib, monkeypatch, codes):
     """Edges of the diagonal path's verification against the index's own code words and unique-
     window bits: the reference's end-drop rule (a final N-free run of exactly k chars is not
     indexed, so a query window with that key must probe and miss even when an anchor predicts
@@ -433,7 +433,7 @@ def test_query_diagonal_edges_vs_oracle(gpu, monkeypatch, codes):
 
 @pytest.mark.parametrize("k", [17, 21, 24, 26])
 @pytest.mark.parametrize("pack8", ["1", "0"])
-def test_pack8_two_pass_vs_oracle(gpu, monkeypatch, k, pack8):
+def test_pack8_two_pass_vs_oracle(gpu, test_lib, monkeypatch, k, pack8):
     """Two-pass key-stream builds of small k write the first stream as 8-B elements (key << sh |
     the window's index inside its segment of 2^sh windows, sh = 64 - 2k) and restore each
     position in the second pass from the element's place in the stream (k_seg_bounds' table of
@@ -449,3 +449,20 @@ def test_pack8_two_pass_vs_oracle(gpu, monkeypatch, k, pack8):
     _check_against_oracle(s, k, qks=[k, min(k + 4, 31)], pairs=False)
     rr = synth.repeat_rich(400_000, 90 + k, n_gap_every=70_001).tobytes().decode("latin-1")
     _check_against_oracle(rr, k, qks=[k], pairs=True)
+
+
+def test_product_library_ignores_path_selectors(gpu, monkeypatch):
+    """A path selector in the environment of an R session does not reach the product library:
+    KMHG_BUILD=v1 / KMHG_TEST_BALLOT=1 leave its build partitioned with lane-order ranks (the test
+    build honours them, test_build_kind_reported)."""
+    import torch
+    from kmer_hasher_amd import _lib, synth
+    from kmer_hasher_amd.device import DeviceIndex
+    assert _lib.lib() is not _lib._TEST_LIB
+    seq = torch.from_numpy(synth.iid(50_000, 5)).cuda()
+    monkeypatch.setenv("KMHG_BUILD", "v1")
+    monkeypatch.setenv("KMHG_TEST_BALLOT", "1")
+    idx = DeviceIndex.build(seq, 31)
+    info = idx.info()
+    idx.free()
+    assert (info["build"], info["fallback"]) == (_lib.KMHG_BUILD_PARTITIONED, 0), info

@@ -54,7 +54,7 @@ def _slot_sets(table, positions, capb):
 
 @pytest.mark.parametrize("stream", ["bid", "keys", "keys-first-pass"])
 @pytest.mark.parametrize("n_parts", [1, 2, 3, 5, 8])
-def test_parts_reassemble_to_the_single_build(gpu, monkeypatch, n_parts, stream):
+def test_parts_reassemble_to_the_single_build(gpu, test_lib, monkeypatch, n_parts, stream):
     """`stream`: bucket-id streams (the default up to 12 M windows), key streams whose parts
     compact their own windows in the first histogram pass and run every radix pass over those
     alone (the default beyond), and key streams with the older first pass over every window

@@ -34,7 +34,7 @@ def _sorted_table(ptr):
 
 @pytest.mark.parametrize("table", ["adopt", "adopt-lb", "rebuild"])
 @pytest.mark.parametrize("case", GOLD["cases"], ids=lambda c: c["name"])
-def test_sh_golden(gpu, case, inputs, monkeypatch, table):
+def test_sh_golden(gpu, case, inputs, test_lib, monkeypatch, table):
     """`table`: the first batch's table adopted as the suffix hash (default; rows from
     bucket-aligned tiles, or from the look-back walk with adopt-lb: KMHG_COUNT_WALK=lb) or
     rebuilt from the key list (KMHG_COUNT_TABLE=rebuild, the path of every later batch)."""
@@ -225,7 +225,7 @@ def _count_packed(torch, seq, qual, k, mq, ptr=None, source=0, S=1):
 @pytest.mark.parametrize("table", ["adopt", "rebuild"])
 @pytest.mark.parametrize("env,want_path", [({}, 1), ({"KMHG_CO_SPREAD": "8"}, 2),
                                            ({"KMHG_CO_GLOBAL": "1"}, 3)])
-def test_sh_count_only_build_paths(gpu, monkeypatch, env, want_path, table):
+def test_sh_count_only_build_paths(gpu, test_lib, monkeypatch, env, want_path, table):
     """Every path of the count-only batch build, forced, against the oracle: the spread chosen
     from the batch's own HLL estimate (1), a spread too wide for low-coverage reads (distinct /
     stream ~ 0.9: KMHG_CO_SPREAD=8 overflows a sub-table -> the batch is rebuilt at spread 1)
