@@ -1065,14 +1065,21 @@ struct Words3 {                                // three consecutive code words, 
   uint32_t a, b, c;
 };
 // AOS: the stream is packed 12-B (key, pos) elements in `keys` (`pos` unused).
-template <bool COUNT_ONLY, bool CK, bool BALLOT, bool AOS = false>
+// TAGS (position builds beyond the cache, round 6): the diagonal query path's preparation comes
+// with the build -- each slot's tag byte TG[slot] (0 empty, else slot_tag of its key's hash: the
+// same bytes V_diag_prep would write), and for every window of a repeated key its bit in `rep`
+// (u32 word (pos - 1) / 32, zeroed before the launch), so the first query runs V_diag_valid
+// alone (uniq = indexed windows AND NOT rep).
+template <bool COUNT_ONLY, bool CK, bool BALLOT, bool AOS = false, bool TAGS = false>
 __global__ void __launch_bounds__(BLOCK, BALLOT ? 4 : KMHG_BUCKET_WGS)
 k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ pos,
                const uint32_t* __restrict__ start, Geom g, Slot* __restrict__ T,
                int32_t* __restrict__ positions, BucketStats* __restrict__ bstats,
                BuildMeta* __restrict__ meta, const uint32_t* __restrict__ code, int k,
-               const uint32_t* __restrict__ n_ptr, uint32_t nw) {
+               const uint32_t* __restrict__ n_ptr, uint32_t nw, uint8_t* __restrict__ TG,
+               uint32_t* __restrict__ rep) {
   static_assert(!(CK && COUNT_ONLY), "code-word keys belong to position builds");
+  static_assert(!(TAGS && (CK || COUNT_ONLY)), "build-time tags: key-stream position builds");
   static_assert(!(AOS && (CK || COUNT_ONLY)), "packed streams carry keys and positions");
   static_assert(V2_CAPW % BLOCK == 0, "the side slot V2_CAPW is slot q = V2_CAPW / TB of thread 0");
   constexpr int TB = BLOCK;
@@ -1369,6 +1376,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
             if (multi) {
               const uint32_t at = atomicAdd(&W.val[slot[c]], 1u) & ~VAL_MULTI;
               positions[at] = (int32_t)ps[c];
+              if (TAGS) atomicOr(&rep[(ps[c] - 1u) >> 5], 1u << ((ps[c] - 1u) & 31u));
             }
           } else if (__ballot(multi)) {
             const uint64_t m = match_bits((uint32_t)slot[c], V2_SLOT_BITS_WG, multi);
@@ -1376,6 +1384,7 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
             if (multi && leader == lane) W.val[slot[c]] = v + (uint32_t)__popcll(m);
             const uint32_t cur = (uint32_t)__shfl((int)v, leader) & ~VAL_MULTI;
             if (multi) positions[cur + (uint32_t)__popcll(m & lanemask_lt())] = (int32_t)ps[c];
+            if (TAGS && multi) atomicOr(&rep[(ps[c] - 1u) >> 5], 1u << ((ps[c] - 1u) & 31u));
           }
         }
         __syncthreads();
@@ -1410,6 +1419,8 @@ k_v2_bucket_wg(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ p
       } else {
         *reinterpret_cast<uint4*>(&Tb[j]) = make_uint4((uint32_t)kk, (uint32_t)(kk >> 32), cnt[q], aux);
       }
+      if (TAGS)      // one byte per slot: 64 consecutive bytes per wave and row q
+        TG[(uint64_t)b * V2_CAPW + j] = kk == EMPTY_KEY ? (uint8_t)0 : slot_tag(mix64(kk));
     }
   }
 #endif
@@ -1776,29 +1787,27 @@ void launch_v2_scatter_nopos(const uint64_t* kin, const uint32_t* n_ptr, Geom g,
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, const uint32_t* n_ptr, uint32_t nw,
-                         const uint32_t* code, int k, bool aos) {
+                         const uint32_t* code, int k, bool aos, uint8_t* TG, uint32_t* rep) {
   const bool ballot = ballot_ranks();
-  if (aos && !ballot)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, false, false, true>), dim3(g.nb), dim3(BLOCK), 0, s,
-                       keys, pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
+  const bool tags = TG != nullptr && !count_only && !code;
+  const dim3 gr(g.nb), bl(BLOCK);
+#define KMHG_BUCKET(CO, CKK, BAL, AO, TG_)                                                     \
+  hipLaunchKernelGGL((k_v2_bucket_wg<CO, CKK, BAL, AO, TG_>), gr, bl, 0, s, keys, pos, start, g, \
+                     T, positions, bstats, meta, CKK ? code : nullptr, CKK ? k : 0, n_ptr, nw,   \
+                     TG, rep)
+  if (aos && tags)
+    { if (ballot) KMHG_BUCKET(false, false, true, true, true); else KMHG_BUCKET(false, false, false, true, true); }
   else if (aos)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, false, true, true>), dim3(g.nb), dim3(BLOCK), 0, s,
-                       keys, pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
+    { if (ballot) KMHG_BUCKET(false, false, true, true, false); else KMHG_BUCKET(false, false, false, true, false); }
   else if (count_only)              // no positions: nothing is ranked
-    hipLaunchKernelGGL((k_v2_bucket_wg<true, false, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
-  else if (code && !ballot)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, true, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, code, k, n_ptr, nw);
+    KMHG_BUCKET(true, false, false, false, false);
   else if (code)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, true, true>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, code, k, n_ptr, nw);
-  else if (!ballot)
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, false, false>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
+    { if (ballot) KMHG_BUCKET(false, true, true, false, false); else KMHG_BUCKET(false, true, false, false, false); }
+  else if (tags)
+    { if (ballot) KMHG_BUCKET(false, false, true, false, true); else KMHG_BUCKET(false, false, false, false, true); }
   else
-    hipLaunchKernelGGL((k_v2_bucket_wg<false, false, true>), dim3(g.nb), dim3(BLOCK), 0, s, keys,
-                       pos, start, g, T, positions, bstats, meta, nullptr, 0, n_ptr, nw);
+    { if (ballot) KMHG_BUCKET(false, false, true, false, false); else KMHG_BUCKET(false, false, false, false, false); }
+#undef KMHG_BUCKET
 }
 // The hardware property the radix passes' ranks rest on, checked on the device itself
 // (tools/lds_order.hip is the stand-alone probe): the lanes of one returning LDS add that hit

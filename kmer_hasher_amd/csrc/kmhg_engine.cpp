@@ -664,6 +664,9 @@ struct kmhg_index {
   std::map<int, kmhg_index*> replicas;
   std::mutex rep_mu;
   bool ps_failed = false;                 // guarded by ps_mu
+  // the build wrote ptag and the repeated keys' window bits (build_device_v2, build-time tags):
+  // the first diagonal query derives uniq alone (V_diag_valid)
+  bool tags_built = false;
   std::mutex ps_mu;
   DiagBlock diag_block_of() const { return diag_block(dcodes.p, L - k + 1); }
   DiagIdx diag_view() const {
@@ -1282,10 +1285,40 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
     if (!no_pos && td[0] >= '1' && td[0] <= '3')
       launch_v2_test_disorder(aos ? reinterpret_cast<uint32_t*>(kin) + 2 : pin, start.p, n_valid,
                               td[0] - '0', s, aos ? 3u : 1u);
+  // Build-time tags (round 6): a position build beyond the cache (key
+  // streams, Nw > BID_MAX_WINDOWS) writes the diagonal query path's slot tags and repeated-key
+  // bits itself, so the first seq.kmer.pos of a new index does not pay V_diag_prep (2.6 ms at
+  // 500 Mbp, +70 % on the query).  In cache (config 2) the build is the headline and the
+  // preparation stays with the first query (round-3 A/B: tags in the build +1-1.5 % there).
+  // KMHG_BUILD_TAGS=0 / 1 (test build) forces either.
+  uint8_t* tg = nullptr;
+  uint32_t* rep = nullptr;
+  {
+    const char* bte = test_build_knob("KMHG_BUILD_TAGS");
+    const bool want = codes && !bid && !from_keys && !count_only && n_parts == 0 &&
+                      (bte ? bte[0] == '1' : Nw > BID_MAX_WINDOWS);
+    if (want) {
+      try {
+        idx->ptag.reset(idx->slots() + 32);    // + the 32-B span the last probe group reads
+        idx->ptag.bind(s);
+        tg = idx->ptag.p;
+        rep = db.uniq;
+        HIPC(hipMemsetAsync(rep, 0, diag_uniq_words(Nw) * 4, s));
+        // the side slot's tag (its key is the empty sentinel: 0) and the tail
+        HIPC(hipMemsetAsync(tg + idx->slots() - 1, 0, 33, s));
+      } catch (const Error& e) {               // no room for the tags: the first query makes them
+        if (e.code != KMHG_ENOMEM) throw;
+        (void)hipGetLastError();
+        tg = nullptr;
+        rep = nullptr;
+      }
+    }
+  }
   LAUNCH("k_v2_bucket_wg", s,
          launch_v2_bucket_wg(kin, pin, start.p, gb, idx->table.p, idx->positions.p, idx->bstats.p,
                              meta, no_pos, s, n_valid, (uint32_t)Nw, bid ? db.code : nullptr, k,
-                             aos));
+                             aos, tg, rep));
+  idx->tags_built = tg != nullptr;
   LAUNCH("k_v2_stats", s, launch_v2_stats(idx->bstats.p, gb.nb, n_valid, meta, idx->rec.meta, s));
   idx->bstats_nb = gb.nb;
   HIPC(hipEventRecord(idx->rec.ev, s));
@@ -1391,6 +1424,7 @@ void finish_build(kmhg_index* idx) {
     if (idx->is_part) fail(KMHG_EOVERFLOW, "a bucket of a part build overflowed its LDS table");
     std::unique_ptr<kmhg_index> v1(build_device_v1(src, idx->L, idx->k, idx->stream));
     idx->build_kind = KMHG_BUILD_GLOBAL;
+    idx->tags_built = false;                     // the tags were the partitioned table's
     idx->bstats_nb = 0;                          // one global bucket: no per-bucket statistics
     idx->fallback = 1;                      // reported by kmhg_index_info (bench.py fails on it)
     idx->geom = v1->geom;
@@ -1443,14 +1477,22 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   if (diag && !idx->ps_ready.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> lk(idx->ps_mu);
     if (!idx->ps_ready.load(std::memory_order_relaxed) && !idx->ps_failed) {
-      try {
-        idx->ptag.reset(idx->slots() + 32);    // + the 32-B span the last probe group reads
-      } catch (const Error& e) {               // no room for the tags: table probes only
-        if (e.code != KMHG_ENOMEM) throw;
-        idx->ps_failed = true;
-        (void)hipGetLastError();
+      if (!idx->tags_built) {
+        try {
+          idx->ptag.reset(idx->slots() + 32);  // + the 32-B span the last probe group reads
+        } catch (const Error& e) {             // no room for the tags: table probes only
+          if (e.code != KMHG_ENOMEM) throw;
+          idx->ps_failed = true;
+          (void)hipGetLastError();
+        }
       }
-      if (!idx->ps_failed) {
+      if (idx->tags_built) {                   // the build wrote the tags and repeat bits
+        idx->dcodes.bind(s);
+        const DiagBlock db = idx->diag_block_of();
+        LAUNCH("k_diag_valid", s, launch_diag_valid(db.nbit, idx->L, idx->k, db.uniq, true, s));
+        HIPC(hipStreamSynchronize(s));
+        idx->ps_ready.store(true, std::memory_order_release);
+      } else if (!idx->ps_failed) {
         idx->ptag.bind(s);
         idx->dcodes.bind(s);
         const DiagBlock db = idx->diag_block_of();

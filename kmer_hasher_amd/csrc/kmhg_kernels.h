@@ -101,7 +101,9 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
 void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, const Slot* T,
                       uint64_t nslots, const int32_t* positions, uint8_t* TG, hipStream_t s);
 // An index whose build already wrote the slot tags and set the repeated keys' window bits in
-// the uniq words (V_bucket_wg): uniq = the indexed windows AND NOT those bits
+// the uniq words (V_bucket_wg, TAGS): uniq = the indexed windows AND NOT those bits
+void launch_diag_valid(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, bool multi_in,
+                       hipStream_t s);
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
 // exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
 // reduce-then-scan with `scratch` = scan_u64_scratch(n) u64
@@ -293,7 +295,11 @@ struct BucketStats {           // per-bucket partials of the build statistics
 void launch_v2_bucket_wg(const uint64_t* keys, const uint32_t* pos, const uint32_t* start, Geom g,
                          Slot* T, int32_t* positions, BucketStats* bstats, BuildMeta* meta,
                          bool count_only, hipStream_t s, const uint32_t* n_ptr, uint32_t nw,
-                         const uint32_t* code = nullptr, int k = 0, bool aos = false);
+                         const uint32_t* code = nullptr, int k = 0, bool aos = false,
+                         uint8_t* TG = nullptr, uint32_t* rep = nullptr);
+// TG / rep (key-stream position builds): the build also writes the diagonal path's slot tags and
+// sets the repeated keys' window bits in rep (zeroed by the caller); the first query then runs
+// launch_diag_valid(..., multi_in = true) instead of launch_diag_prep
 // ballot_ranks(): the current device fails the LDS lane-order self-check (or KMHG_TEST_BALLOT):
 // the radix passes and the bucket kernel then rank with ballots (kmhg_engine.cpp)
 bool ballot_ranks();

@@ -346,6 +346,13 @@ k_diag_prep(const Slot* __restrict__ T, uint64_t nslots, const int32_t* __restri
   }
 }
 
+void launch_diag_valid(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, bool multi_in,
+                       hipStream_t s) {
+  const uint64_t nw = diag_uniq_words(L - k + 1);
+  hipLaunchKernelGGL(k_diag_valid, dim3((unsigned)((nw + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                     nbit, L, k, uniq, nw, multi_in ? 1 : 0);
+}
+
 void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, const Slot* T,
                       uint64_t nslots, const int32_t* positions, uint8_t* TG, hipStream_t s) {
   const uint64_t nw = diag_uniq_words(L - k + 1);

@@ -286,6 +286,9 @@ def test_multi_pass_partition_vs_oracle(gpu, test_lib, monkeypatch, maxr, ranks,
     ds = {"keys-levels": "0", "keys-digits": "1", "bid": "1" if ranks == "lane" else ""}
     monkeypatch.setenv("KMHG_DIGIT_STREAM", ds.get(stream, ""))
     monkeypatch.setenv("KMHG_TEST_BALLOT", "1" if ranks == "ballot" else "0")
+    # key streams: the build writes the diagonal path's tags and repeat bits (what builds beyond
+    # 12 M windows do), in every bucket-kernel variant (packed / plain stream, lane / ballot)
+    monkeypatch.setenv("KMHG_BUILD_TAGS", "0" if stream == "bid" else "1")
     s = synth.add_n_runs(synth.iid(700_000, 41), 0.002, 9).tobytes().decode("latin-1")
     _check_against_oracle(s, 31, pairs=False)
     rr = synth.repeat_rich(300_000, 42, n_gap_every=100_000).tobytes().decode("latin-1")
@@ -341,8 +344,9 @@ def test_query_paths_vs_oracle(gpu, test_lib, monkeypatch, path):
     ptr.free()
 
 
+@pytest.mark.parametrize("prep", ["query", "build"])
 @pytest.mark.parametrize("tags", ["1", "0"])
-def test_query_diagonal_path_vs_oracle(gpu, test_lib, monkeypatch, tags):
+def test_query_diagonal_path_vs_oracle(gpu, test_lib, monkeypatch, tags, prep):
     """The diagonal path of k_query_probe (anchors every 64th window; later windows follow the
     last anchor with a unique hit and take {count 1, aux = predicted position} only when the
     index window there is unique and its key, read from the index's own code words, equals
@@ -352,10 +356,17 @@ def test_query_diagonal_path_vs_oracle(gpu, test_lib, monkeypatch, tags):
     input (multi-hit anchors predict nothing; keys with > 16 positions have their windows'
     unique bits cleared by a whole wave), shards of the window range that start inside a
     diagonal, and a query k different from the index k (path off).  The slot tags and the
-    repeated keys' window bits are built by the index's first diagonal query (V_diag_prep)."""
+    repeated keys' window bits are built by the index's first diagonal query (V_diag_prep), or
+    (prep = build, key streams) by the build's bucket kernel, the first query deriving the
+    unique bits alone (V_diag_valid)."""
     import torch
     from kmer_hasher_amd import device as D, synth
     monkeypatch.setenv("KMHG_QUERY_TAGS", tags)
+    if prep == "build":
+        monkeypatch.setenv("KMHG_BUILD_BID", "0")
+        monkeypatch.setenv("KMHG_BUILD_TAGS", "1")
+    else:
+        monkeypatch.setenv("KMHG_BUILD_TAGS", "0")
     make, kpos, sqk = _api()
     A = synth.add_n_runs(synth.iid(300_000, 61), 0.0005, 62, max_run=40)
     B = synth.derived(A, 63)
@@ -395,8 +406,9 @@ def test_query_diagonal_path_vs_oracle(gpu, test_lib, monkeypatch, tags):
     idx.free()
 
 
+@pytest.mark.parametrize("prep", ["query", "build"])
 @pytest.mark.parametrize("codes", ["1", "0"])
-def test_query_diagonal_edges_vs_oracle(gpu, test_lib, monkeypatch, codes):
+def test_query_diagonal_edges_vs_oracle(gpu, test_lib, monkeypatch, codes, prep):
     """Edges of the diagonal path's verification against the index's own code words and unique-
     window bits: the reference's end-drop rule (a final N-free run of exactly k chars is not
     indexed, so a query window with that key must probe and miss even when an anchor predicts
@@ -405,6 +417,9 @@ def test_query_diagonal_edges_vs_oracle(gpu, test_lib, monkeypatch, codes):
     in the index, and an index built without the code block (KMHG_DIAG_CODES=0: table probes)."""
     from kmer_hasher_amd import synth
     monkeypatch.setenv("KMHG_DIAG_CODES", codes)
+    if prep == "build":                  # the build writes the tags and repeat bits
+        monkeypatch.setenv("KMHG_BUILD_BID", "0")
+        monkeypatch.setenv("KMHG_BUILD_TAGS", "1")
     make, kpos, sqk = _api()
     rng = np.random.default_rng(91)
 
@@ -466,3 +481,36 @@ def test_product_library_ignores_path_selectors(gpu, monkeypatch):
     info = idx.info()
     idx.free()
     assert (info["build"], info["fallback"]) == (_lib.KMHG_BUILD_PARTITIONED, 0), info
+
+
+@pytest.mark.parametrize("force", ["", "1", "0"])
+def test_first_query_preparation_kernels(gpu, test_lib, monkeypatch, force):
+    """Which kernel prepares the diagonal path at an index's first query: V_diag_valid alone when
+    the build wrote the tags (builds beyond 12 M windows, or KMHG_BUILD_TAGS=1 on key streams),
+    V_diag_valid + V_diag_prep otherwise; later queries run neither; rows equal either way."""
+    import torch
+    from kmer_hasher_amd import device as D, synth
+    monkeypatch.setenv("KMHG_BUILD_BID", "0")
+    if force:
+        monkeypatch.setenv("KMHG_BUILD_TAGS", force)
+    A = synth.add_n_runs(synth.repeat_rich(400_000, 71, n_gap_every=90_000), 0.001, 72)
+    dA = torch.from_numpy(A).cuda()
+    dB = torch.from_numpy(synth.derived(A, 73)).cuda()
+    idx = D.DeviceIndex.build(dA, 31)
+    idx.wait()
+    D.timing_enable(True)
+    D.timing_reset()
+    first = idx.query(dB, 31).rows().cpu().numpy()
+    k1 = {n for n, v in D.timing_report().items() if v[0]}
+    D.timing_reset()
+    again = idx.query(dB, 31).rows().cpu().numpy()
+    k2 = {n for n, v in D.timing_report().items() if v[0]}
+    D.timing_enable(False)
+    idx.free()
+    built = force == "1"            # (default at 400 K windows: the first query prepares)
+    assert ("k_diag_prep" in k1) != built, k1
+    assert "k_diag_valid" in k1 or "k_diag_prep" in k1, k1
+    assert not ({"k_diag_prep", "k_diag_valid"} & k2), k2
+    assert np.array_equal(first, again)
+    oi = O.OracleIndex(A.tobytes().decode("latin-1"), 31)
+    assert np.array_equal(first.reshape(-1), oi.query(dB.cpu().numpy().tobytes().decode("latin-1"), 31))
