@@ -1207,7 +1207,6 @@ def bench_large(args, dev) -> dict:
     # ---- B's cross query against index(A)
     idx = D.DeviceIndex.build(ta, k, stream)
     idx.info()
-    del ta
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     q = idx.query(tb, k, stream)
@@ -1246,10 +1245,65 @@ def bench_large(args, dev) -> dict:
     th_ms = (time.perf_counter() - t0) / n_host * 1e3
     del hostm
     idx.free()
+    # the first query of a second index, once the process's pools hold query-sized blocks: what
+    # every later make.kmer.hash + seq.kmer.pos pair of an R session pays (the diagonal path's
+    # preparation: V_diag_valid after a build that wrote the tags), with its kernels
+    idx = D.DeviceIndex.build(ta, k, stream)
+    idx.info()
+    del ta
+    torch.cuda.synchronize()
+    D.timing_enable(True)
+    D.timing_reset()
+    t0 = time.perf_counter()
+    idx.query(tb, k, stream).free()
+    torch.cuda.synchronize()
+    t_first2 = time.perf_counter() - t0
+    fk = {n: round(v[1], 4) for n, v in D.timing_report().items() if v[0]}
+    D.timing_enable(False)
+    # the general lookup beyond the cache: index(A) queried by an independent i.i.d. 500 Mbp
+    # sequence (seed 6), so every window misses and probes the 12 GB table through its slot
+    # tags (the reference's kh_get per window, src/kmer_pos.c:55-60, 126-132)
+    del tb
+    tc = torch.from_numpy(synth.iid(L, 6)).to(dev)
+    idx.query(tc, k, stream).free()
+    D.timing_enable(True)
+    D.timing_reset()
+    for _ in range(2):
+        idx.query(tc, k, stream).free()
+    ut = D.timing_report()
+    D.timing_enable(False)
+    uper = {n: v[1] / 2 for n, v in ut.items() if v[0]}
+    ulaunch = {n: v[0] / 2 for n, v in ut.items() if v[0]}
+    n_u = max(1, min(steps, 10))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_u):
+        q = idx.query(tc, k, stream)
+        H_u = q.n_rows
+        q.free()
+    torch.cuda.synchronize()
+    tu_ms = (time.perf_counter() - t0) / n_u * 1e3
+    del tc
+    idx.free()
     Nw = L - k + 1
+    unrel_rec = {
+        "value": round(L / 1e6 / (tu_ms * 1e-3), 2), "unit": "Mbp/s", "ms_per_step": round(tu_ms, 4),
+        "steps": n_u, "rows": H_u,
+        "kernels_ms_per_step": {n: round(v, 5) for n, v in uper.items()},
+        "roofline": query_roofline(uper, L, Nw, H_u, _load_pmc("largeunrel"), tu_ms, ulaunch),
+        "note": "index(A) queried by an independent i.i.d. 500 Mbp sequence (splitmix64 seed 6): "
+                "every window misses and probes the 12 GB table through its slot tags (one random "
+                "16-B tag group per window, the table only at a matching tag); PMC from "
+                "profiles/pmc_configlargeunrel.json (tools/query_unrelated.py --L 500000000)"}
     query_rec = {
         "value": round(L / 1e6 / (tq_ms * 1e-3), 2), "unit": "Mbp/s", "ms_per_step": round(tq_ms, 4),
         "steps": steps, "rows": H, "first_query_ms": round(t_first * 1e3, 3),
+        "first_query_new_index_ms": round(t_first2 * 1e3, 3),
+        "first_query_new_index_kernels_ms": fk,
+        "first_query_note": "first_query_ms: the first query of the process at this size (its "
+                            "query buffers' first allocation included); "
+                            "first_query_new_index_ms: the first query of a second index (the "
+                            "per-index preparation an R session's build-and-query pays)",
         "kernels_ms_per_step": {n: round(v, 5) for n, v in qper.items()},
         "roofline": query_roofline(qper, L, Nw, H, pmc, tq_ms, qlaunch),
         "to_host": {"value": round(L / 1e6 / (th_ms * 1e-3), 2), "unit": "Mbp/s",
@@ -1261,7 +1315,7 @@ def bench_large(args, dev) -> dict:
                         "4), B = A + 1% SNV + 20 inversions/translocations + N-runs (seed 5), "
                         "k=31; make.kmer.hash(A) and seq.kmer.pos(index(A), B), inputs resident "
                         "in HBM",
-            "seq_len": L, "k": k, "build": build_rec, "query": query_rec,
+            "seq_len": L, "k": k, "build": build_rec, "query": query_rec, "unrelated": unrel_rec,
             "generate_s": round(t_gen, 2),
             "cpu_baseline": {"value": ref["build_value"] if ref else None, "unit": "Mbp/s",
                              "cores": ref["cores"] if ref else 1, "kind": "reference",
@@ -1501,11 +1555,16 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
         progress("sharded query: rows to the host matrix")
         # rows into the host matrix (what an R session receives): first delivery (the shared
         # buffer's creation and registration) untimed
-        rows = step(to_host=True)
-        del rows
-        ph_host = phases(to_host=True)
-        t_host, H_host = timed(max(1, min(steps, 5)), to_host=True)
         n_host = max(1, min(steps, 5))
+        host_skip = None
+        try:
+            rows = step(to_host=True)
+            del rows
+            ph_host = phases(to_host=True)
+            t_host, H_host = timed(n_host, to_host=True)
+        except RuntimeError as e:     # no room for the shared host matrix (every rank raises)
+            host_skip = str(e)
+            ph_host, t_host, H_host = [0.0, 0.0, 0.0], 0.0, H
         ph_bc = phases(c1="broadcast") if use_pg else [0.0, 0.0, 0.0]
     finally:
         if sink is not None:
@@ -1533,7 +1592,8 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
            "phases_ms": {"query_scatter": ms(ph_dev[0]), "range_query": ms(ph_dev[1]),
                          "row_gather": ms(ph_dev[2]),
                          "note": "separate synchronized steps, max over ranks"},
-           "to_host": {"value": round(L / 1e6 * n_host / t_host, 2), "unit": "Mbp/s",
+           "to_host": {"skipped": host_skip} if host_skip else {
+                       "value": round(L / 1e6 * n_host / t_host, 2), "unit": "Mbp/s",
                        "ms_per_step": round(t_host / n_host * 1e3, 3), "steps": n_host,
                        "phases_ms": {"query_scatter": ms(ph_host[0]),
                                      "range_query": ms(ph_host[1]),

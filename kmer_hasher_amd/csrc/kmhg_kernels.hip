@@ -606,7 +606,10 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
       if (s0 + j < w1) qrec[s0 + j - w0r] = rec[j];
   }
   __syncthreads();             // phase 1's keys, flags and records (vmcnt drained) are in place
-#pragma unroll 2
+#ifndef KMHG_P2_UNROLL
+#define KMHG_P2_UNROLL 2
+#endif
+#pragma unroll KMHG_P2_UNROLL
   for (int j = 0; j < 8; ++j) {
     const int w = j * BLOCK + (int)threadIdx.x;
     if (P.todo[w]) {

@@ -204,10 +204,24 @@ class HostRowSink:
             self.token = int(tok.item())
         if rows <= self.cap and self.t is not None:
             return
+        nbytes = max(8, rows * 8)
+        # room in /dev/shm (a tmpfs: writing past its size would SIGBUS every rank), decided by
+        # the owner for every rank, before anything is created
+        import os
+        ok = torch.tensor([1], dtype=torch.int32, device=device)
+        if self.rank == self.owner:
+            try:
+                st = os.statvfs("/dev/shm")
+                free = st.f_bavail * st.f_frsize + (self.cap * 8 if self.t is not None else 0)
+                ok[0] = 1 if free >= nbytes + (64 << 20) else 0
+            except OSError:
+                ok[0] = 0
+        dist.broadcast(ok, _global(self.owner, self.group), group=self.group)
+        if not int(ok.item()):
+            raise RuntimeError(f"HostRowSink: /dev/shm has no room for {nbytes} bytes of rows")
         dist.barrier(group=self.group)             # nobody still writes the old buffer
         self._release()
         self.gen += 1
-        nbytes = max(8, rows * 8)
         if self.rank == self.owner:
             self.shm = shared_memory.SharedMemory(name=self._name(), create=True, size=nbytes)
         dist.barrier(group=self.group)

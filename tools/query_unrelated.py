@@ -22,9 +22,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--L", type=int, default=10_000_000)
 ap.add_argument("--k", type=int, default=31)
 ap.add_argument("--steps", type=int, default=10)
+ap.add_argument("--seed-index", type=int, default=None, help="default: 1 (4 at --L 500000000)")
+ap.add_argument("--seed-query", type=int, default=None, help="default: 101 (6 at --L 500000000)")
 a = ap.parse_args()
-seq = torch.from_numpy(synth.iid(a.L, 1)).cuda()
-other = torch.from_numpy(synth.iid(a.L, 101)).cuda()
+big = a.L == 500_000_000               # bench.py large.unrelated: A seed 4, query seed 6
+sa = a.seed_index if a.seed_index is not None else (4 if big else 1)
+sq = a.seed_query if a.seed_query is not None else (6 if big else 101)
+seq = torch.from_numpy(synth.iid(a.L, sa)).cuda()
+other = torch.from_numpy(synth.iid(a.L, sq)).cuda()
 idx = D.DeviceIndex.build(seq, a.k)
 idx.info()
 q = idx.query(other, a.k)
