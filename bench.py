@@ -270,7 +270,7 @@ def host_boundary(seq_bytes: bytes, k: int, calls: int = 10) -> dict:
     import numpy as np
     from kmer_hasher_amd import _lib
     L = _lib.lib()
-    t_run = t_fresh = t_warm = 0.0
+    t_run = t_fresh = t_warm = t_rel = 0.0
     warm = np.ones(2 * rows.shape[0], np.int32)
     for _ in range(calls):
         q, h = C.c_void_p(), C.c_int64()
@@ -287,7 +287,9 @@ def host_boundary(seq_bytes: bytes, k: int, calls: int = 10) -> dict:
         t_run += t1 - t0
         t_fresh += t2 - t1
         t_warm += t3 - t2
-        del fresh
+        t4 = time.perf_counter()
+        del fresh                         # the host returns the result's pages (munmap)
+        t_rel += time.perf_counter() - t4
     ptr.free()
     mbp = len(seq_bytes) / 1e6
     return {"build": {"value": round(mbp / t_b, 2), "unit": "Mbp/s", "ms": round(t_b * 1e3, 3)},
@@ -297,9 +299,14 @@ def host_boundary(seq_bytes: bytes, k: int, calls: int = 10) -> dict:
                                   "rows_to_fresh_array": round(t_fresh / calls * 1e3, 3),
                                   "rows_to_touched_array": round(t_warm / calls * 1e3, 3),
                                   "page_faults": round((t_fresh - t_warm) / calls * 1e3, 3),
+                                  "result_release": round(t_rel / calls * 1e3, 3),
                                   "note": "fresh = a new array whose pages the copy faults in "
                                           "(as R's allocMatrix); touched = the same copy into "
-                                          "resident pages (DMA + host copy only)"}},
+                                          "resident pages (DMA + host copy only); "
+                                          "result_release = freeing the previous call's 2 x H "
+                                          "int32 result (the host unmapping its pages: R's GC "
+                                          "pays the same for its matrix), part of `ms` because "
+                                          "each call's result replaces the last"}},
             "calls": calls,
             "note": "PCIe-inclusive: host sequence in (pageable), host rows out, synchronous "
                     "per call (the R API); not `value`"}
