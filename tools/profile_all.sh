@@ -19,4 +19,5 @@ else
   run ${P}p4 --config 4 --steps 3 --warmup 1 --profile --no-cpu
   run ${P}p5 --config 5 --steps 3 --warmup 1 --no-cpu
   run ${P}plarge --only-large --steps 3 --warmup 1
+  PROG=tools/query_unrelated.py run ${P}plargeunrel --L 500000000 --steps 10
 fi
