@@ -63,25 +63,30 @@ def gather_rows(local: torch.Tensor, dst: int = 0, group=None) -> torch.Tensor |
     dist.all_gather(counts, cnt, group=group)
     counts = [int(c.item()) for c in counts]
     if rank == dst:
+        if world == 1:
+            return local                     # the rows are already where they belong
         out = torch.empty((sum(counts), 2), dtype=torch.int32, device=dev)
         offs = [0]
         for c in counts:
             offs.append(offs[-1] + c)
+        # the peers' rows arrive (the backend's stream) while the root copies its own part
+        works = p2p([("recv", out[offs[r]:offs[r + 1]], r) for r in range(world)
+                     if r != dst and counts[r]], group, wait=False)
         out[offs[rank]:offs[rank + 1]] = local
-        p2p([("recv", out[offs[r]:offs[r + 1]], r) for r in range(world)
-             if r != dst and counts[r]], group)
+        p2p_wait(works)
         return out
     if counts[rank]:
         p2p([("send", local.contiguous(), dst)], group)
     return None
 
 
-def p2p(ops: list, group=None) -> None:
+def p2p(ops: list, group=None, wait: bool = True):
     """One batch of point-to-point transfers, ("send" | "recv", tensor, group rank) each, waited
-    for.  gloo moves device tensors in its collectives but not point to point: there (the
-    one-GPU rehearsals) device tensors are staged through host copies."""
+    for (wait=False: returned, for p2p_wait).  gloo moves device tensors in its collectives but
+    not point to point: there (the one-GPU rehearsals) device tensors are staged through host
+    copies."""
     if not ops:
-        return
+        return ([], [])
     stage = dist.get_backend(group) == "gloo"
     batch, post = [], []
     for kind, t, peer in ops:
@@ -92,7 +97,16 @@ def p2p(ops: list, group=None) -> None:
             t = h
         batch.append(dist.P2POp(dist.isend if kind == "send" else dist.irecv, t,
                                 _global(peer, group), group=group))
-    for w in dist.batch_isend_irecv(batch):
+    works = (dist.batch_isend_irecv(batch), post)
+    if wait:
+        p2p_wait(works)
+    return works
+
+
+def p2p_wait(works) -> None:
+    """Wait for a p2p(..., wait=False) batch (and land its host-staged receives)."""
+    reqs, post = works
+    for w in reqs:
         w.wait()
     for t, h in post:
         t.copy_(h)
