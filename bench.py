@@ -1610,6 +1610,8 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
                                "into a node-shared, HIP-registered buffer at its row offset "
                                "(dist.deliver_rows_host); at n_gpus 1 the one GPU's rows into "
                                "a pinned host matrix"},
+           "roofline": sharded_roofline(survey_bytes("query", L=L, Nq=L - k + 1, H=H),
+                                        t_dev / steps, ph_dev[1], world),
            "c1_broadcast_ms": ms(ph_bc[0]) if use_pg else None,
            "c1_broadcast_note": "C1 as a broadcast of the whole B (one separate step), against "
                                 "query_scatter's slices",
@@ -1619,6 +1621,23 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
                    "the HIP engine and gathers the rows into one device buffer on rank 0 in "
                    "rank order (the reference's row order)"}
     return rec, kt
+
+
+def sharded_roofline(B: int, step_s: float, query_s: float, world: int) -> dict:
+    """The sharded query against the node's HBM roofline: SURVEY.md §8(d)'s query bytes of the
+    whole job over the step (C1 + range queries + rows gathered) and over the range-query phase
+    alone, per GPU (the job's bytes / n_gpus), against one GPU's 8 TB/s."""
+    per_gpu = B / world
+    ach = per_gpu / step_s / 1e9 if step_s else None
+    achq = per_gpu / query_s / 1e9 if query_s else None
+    return {"bound": "hbm", "algorithmic_bytes": B, "bytes_per_gpu": int(per_gpu),
+            "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None,
+            "range_query_achieved": round(achq, 2) if achq else None,
+            "range_query_frac": round(achq / HBM_PEAK_GBS, 4) if achq else None,
+            "bytes_source": "SURVEY.md §8(d) query bytes (L_q + 12 N_q + 12 H) of the whole job, "
+                            "split evenly over the GPUs; frac over the whole step, "
+                            "range_query_frac over the range-query phase alone"}
 
 
 def bench_sharded_query(args, cfg, dev, world, rank):
