@@ -96,3 +96,16 @@ def test_stdout_carries_only_the_result_line():
     assert r.returncode == 0, r.stderr
     assert r.stdout.splitlines() == ['{"value": 1}']
     assert "banner" in r.stderr and "native banner" in r.stderr
+
+
+def test_sharded_roofline_splits_the_job_over_the_gpus():
+    """The sharded query's roofline: §8(d) query bytes of the whole job, an even share per GPU,
+    over the whole step and over the range-query phase."""
+    L, k, H = 500_000_000, 31, 376_104_028
+    B = bench.survey_bytes("query", L=L, Nq=L - k + 1, H=H)
+    r = bench.sharded_roofline(B, step_s=3.6e-3, query_s=0.65e-3, world=8)
+    assert r["algorithmic_bytes"] == B and r["bytes_per_gpu"] == B // 8
+    assert r["achieved"] == pytest.approx(B / 8 / 3.6e-3 / 1e9, rel=1e-4)
+    assert r["frac"] == pytest.approx(r["achieved"] / bench.HBM_PEAK_GBS, rel=1e-3)
+    assert r["range_query_frac"] > r["frac"]
+    assert bench.sharded_roofline(B, 0.0, 0.0, 1)["frac"] is None
