@@ -133,8 +133,31 @@ class DevicePool {
         live_[pd.p] = pd.key;
         return pd.p;
       }
+      // a large request with no block of its own size: the smallest idle cached block of at
+      // most 1.5x its size serves it (it keeps its own size class and returns to it).  A
+      // hipMalloc of GBs costs ~0.1 ms per GB: the first 500 Mbp query of a process reuses the
+      // build's freed 6 GB stream buffers for its records and rows (2 of its 3 GB-sized
+      // buffers) instead of allocating 10 GB.
+      static const bool best_fit = [] {           // KMHG_POOL_BESTFIT=0 (test build): off
+        const char* e = test_build_knob("KMHG_POOL_BESTFIT");
+        return !(e && e[0] == '0');
+      }();
+      if (best_fit && sz >= BEST_FIT_MIN) {
+        auto it = free_.lower_bound({dev, sz});
+        for (; it != free_.end() && it->first.first == dev && it->first.second <= sz + sz / 2;
+             ++it) {
+          if (it->second.empty()) continue;
+          void* p = it->second.back();
+          it->second.pop_back();
+          cached_ -= it->first.second;
+          live_[p] = it->first;
+          return p;
+        }
+      }
     }
     void* p = nullptr;
+    static const bool trace = test_build_knob("KMHG_POOL_TRACE") != nullptr;   // test build
+    if (trace) std::fprintf(stderr, "kmhg pool: hipMalloc %zu B on device %d\n", sz, dev);
     hipError_t e = hipMalloc(&p, sz);
     if (e == hipErrorOutOfMemory) {   // release the cache and retry once
       (void)hipGetLastError();
@@ -260,6 +283,7 @@ class DevicePool {
       }
     }
   }
+  static constexpr size_t BEST_FIT_MIN = (size_t)256 << 20;
   static size_t round(size_t b) {
     if (b <= (1u << 20)) {           // small: power of two >= 256 B
       size_t r = 256;
