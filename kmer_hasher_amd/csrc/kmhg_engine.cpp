@@ -121,8 +121,15 @@ class DevicePool {
         return p;
       }
       // a block of this size still in use by queued work: wait for it rather than grow the
-      // pool -- the back-pressure that bounds how far asynchronous builds run ahead
-      for (size_t i = 0; i < pending_.size(); ++i) {
+      // pool -- the back-pressure that bounds how far asynchronous builds run ahead.  Up to
+      // DEPTH blocks of a size class exist before a request waits.  (Depth 2, so that the host
+      // enqueues build i + 1 while build i runs, measured no faster at 10 / 100 / 500 Mbp:
+      // the gaps between a build's kernels are the device's, not the host's enqueue.)
+      static const size_t depth = [] {            // KMHG_POOL_DEPTH (test build): 1..8
+        const char* e = test_build_knob("KMHG_POOL_DEPTH");
+        return e ? (size_t)std::max(1, std::min(8, std::atoi(e))) : POOL_DEPTH;
+      }();
+      for (size_t i = 0; i < pending_.size() && count_[{dev, sz}] >= depth; ++i) {
         if (pending_[i].key != std::make_pair(dev, sz)) continue;
         Pending pd = pending_[i];
         pending_.erase(pending_.begin() + (long)i);
@@ -167,6 +174,7 @@ class DevicePool {
     hip_check(e, "hipMalloc");
     std::lock_guard<std::mutex> g(mu_);
     live_[p] = {dev, sz};
+    ++count_[{dev, sz}];
     return p;
   }
   // Stream-ordered release: the block returns to the free list once the work queued on
@@ -255,6 +263,7 @@ class DevicePool {
     for (auto& kv : free_) {
       (void)hipSetDevice(kv.first.first);
       for (void* p : kv.second) (void)hipFree(p);
+      count_[kv.first] -= std::min(count_[kv.first], kv.second.size());
       kv.second.clear();
     }
     (void)hipSetDevice(cur);
@@ -284,6 +293,7 @@ class DevicePool {
     }
   }
   static constexpr size_t BEST_FIT_MIN = (size_t)256 << 20;
+  static constexpr size_t POOL_DEPTH = 1;   // depth 2 measured: no gain
   static size_t round(size_t b) {
     if (b <= (1u << 20)) {           // small: power of two >= 256 B
       size_t r = 256;
@@ -295,6 +305,7 @@ class DevicePool {
   }
   std::mutex mu_;
   std::map<std::pair<int, size_t>, std::vector<void*>> free_;
+  std::map<std::pair<int, size_t>, size_t> count_;   // blocks of each size class (any state)
   std::map<void*, std::pair<int, size_t>> live_;
   std::vector<Pending> pending_;
   std::vector<hipEvent_t> events_;
