@@ -145,6 +145,23 @@ int kmhg_query_run_device(kmhg_index *idx, const void *d_seq, size_t L, int k, v
 int kmhg_query_run_device_range(kmhg_index *idx, const void *d_seq, size_t L, int k,
                                 int64_t w_begin, int64_t w_end, void *stream, kmhg_query **q,
                                 int64_t *n_rows);
+/* seq.kmer.pos over a PART of an owner-computes build (kmhg_build_device_part), without
+ * assembling the parts: every window of the query is hashed and only the windows whose k-mer
+ * this part owns are probed, so the rows are those windows' rows, in window order.  With one
+ * such query per part (one per rank), kmhg_merge_part_rows on the root interleaves them into
+ * exactly the unsharded seq.kmer.pos rows (src/kmer_pos.c:110-136 behind
+ * src/kmer_hash.c:1151-1172; the partition is the reference reader pool's,
+ * src/kmer_reader.c:28-39).  kmhg_query_tile_offsets writes the query's n_tiles + 1 per-tile row
+ * offsets (tiles of 2048 windows; [n_tiles] = n_rows) to device memory on `stream`. */
+int kmhg_query_run_device_part(kmhg_index *part, const void *d_seq, size_t L, int k,
+                               void *stream, kmhg_query **q, int64_t *n_rows);
+int kmhg_query_tile_offsets(kmhg_query *q, uint64_t *d_out, int64_t *n_tiles, void *stream);
+/* The root's merge: n_parts segments of (i, j) rows in device memory, part r's at
+ * d_rows + 2 * d_seg_base[r] int32, with its tile offsets at d_tile_off + r * (n_tiles + 1);
+ * writes the sum of their rows to d_out ordered by window end i, then j, on `stream`. */
+int kmhg_merge_part_rows(const void *d_rows, const uint64_t *d_seg_base,
+                         const uint64_t *d_tile_off, int n_parts, int64_t n_tiles, int k,
+                         int64_t w0, void *d_out, void *stream);
 int kmhg_query_fill(kmhg_query *q, int32_t *rows);               /* host, 2 * n_rows int32 */
 int kmhg_query_rows_device(kmhg_query *q, const int32_t **d_rows); /* owned by q */
 /* Device-to-device copy of the 2 x n_rows int32 rows into caller memory on `stream`. */

@@ -61,6 +61,11 @@ _PROTOS = {
     "kmhg_query_run_device": (C.c_int, [vp, vp, C.c_size_t, C.c_int, vp, C.POINTER(vp), i64p]),
     "kmhg_query_run_device_range": (C.c_int, [vp, vp, C.c_size_t, C.c_int, C.c_int64, C.c_int64,
                                               vp, C.POINTER(vp), i64p]),
+    "kmhg_query_run_device_part": (C.c_int, [vp, vp, C.c_size_t, C.c_int, vp, C.POINTER(vp),
+                                             i64p]),
+    "kmhg_query_tile_offsets": (C.c_int, [vp, vp, i64p, vp]),
+    "kmhg_merge_part_rows": (C.c_int, [vp, vp, vp, C.c_int, C.c_int64, C.c_int, C.c_int64, vp,
+                                       vp]),
     "kmhg_pairs_run": (C.c_int, [vp, vp, C.POINTER(vp), i64p]),
     "kmhg_pairs_run_device": (C.c_int, [vp, vp, vp, C.POINTER(vp), i64p]),
     "kmhg_query_fill": (C.c_int, [vp, vp]),

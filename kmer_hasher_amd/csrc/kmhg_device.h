@@ -420,8 +420,20 @@ __device__ __forceinline__ uint4 ld_slot(const Slot* p) {
   }
 }
 
-// Read-only probe: returns the slot or NONE; count/aux from the same 16-B slot load.
-template <bool NT = false>
+// A part of an owner-computes build (Geom.nbh != 0) holds buckets [b0, b0 + nb) of a table of
+// nbh buckets, indexed from 0: the part's own bucket of hash h, >= g.nb for another part's key.
+__device__ __forceinline__ uint32_t part_bucket(uint64_t h, const Geom& g) {
+  return bucket_of(h, g.nbh) - g.b0;
+}
+// whether this part owns `key` (the k = 32 sentinel key ~0 lives in the side slot of the part
+// that owns its hash's bucket)
+__device__ __forceinline__ bool part_owns(uint64_t key, const Geom& g) {
+  return part_bucket(mix64(key), g) < g.nb;
+}
+
+// Read-only probe: returns the slot or NONE; count/aux from the same 16-B slot load.  PART: T is
+// a part's table (the caller checked part_owns).
+template <bool NT = false, bool PART = false>
 __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom g, uint64_t key,
                                                uint32_t& count, uint32_t& aux) {
   if (key == EMPTY_KEY) {
@@ -431,7 +443,7 @@ __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom 
     return count ? (uint32_t)i : NONE;
   }
   const uint64_t h = mix64(key);
-  const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
+  const uint64_t b0 = (uint64_t)(PART ? part_bucket(h, g) : bucket_of(h, g.nb)) * g.capb;
   uint32_t j = local_home(h, g.capb);
   for (;;) {
     const uint64_t i = b0 + j;

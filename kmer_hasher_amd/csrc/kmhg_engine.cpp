@@ -729,6 +729,10 @@ struct kmhg_query {
   std::vector<kmhg_query*> parts;
   std::vector<int64_t> part_off;
   bool gathered = false;
+  // a query over a part of an owner-computes build (kmhg_query_run_device_part): the first row
+  // of each query tile (TILE windows from w0), for the root's merge of the parts' rows
+  DBuf<uint64_t> tile_off;
+  int64_t n_tiles = 0;
 };
 
 namespace {
@@ -1480,10 +1484,12 @@ void finish_build(kmhg_index* idx) {
 // Windows [w0, w1) of the query (default: all L - kq + 1).  Rows come out ordered by window
 // end, so shards of consecutive window ranges concatenate to the unsharded result.
 kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int kq, int64_t w0,
-                         int64_t w1, hipStream_t s) {
+                         int64_t w1, hipStream_t s, bool part_query = false) {
   ReleaseGroup rg(s);
   if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
-  if (idx->is_part) fail(KMHG_EINVAL, "a part index must be assembled before it is queried");
+  if (idx->is_part != part_query)
+    fail(KMHG_EINVAL, idx->is_part ? "a part index must be assembled before it is queried"
+                                   : "not a part of an owner-computes build");
   finish_build(idx);
   auto q = std::make_unique<kmhg_query>();
   q->device = idx->device;
@@ -1507,7 +1513,7 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   const int64_t nA = idx->L - idx->k + 1;
   const char* de = test_build_knob("KMHG_QUERY_DIAG");
   const bool diag_ok = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
-                       idx->U > 0 && idx->dcodes.p;
+                       idx->U > 0 && idx->dcodes.p && !part_query;
   bool diag = diag_ok;
   if (diag && !idx->ps_ready.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> lk(idx->ps_mu);
@@ -1563,6 +1569,11 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   HIPC(hipStreamSynchronize(s));
   H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
   q->H = (int64_t)H;
+  if (part_query) {              // the tile offsets stay with the query (the root's merge)
+    tiles.bind(s);
+    q->tile_off.swap_with(tiles);
+    q->n_tiles = nt;
+  }
   if (H <= cap) {
     rg.synced = true;                            // nothing queued behind the synchronize
     return q.release();
@@ -3175,6 +3186,49 @@ int kmhg_query_run_device_range(kmhg_index* idx, const void* d_seq, size_t L, in
     hipStream_t s = (hipStream_t)stream;   // caller stream; NULL = HIP null stream
     *q = query_device(idx, (const uint8_t*)d_seq, (int64_t)L, k, w_begin, w_end, s);
     if (n_rows) *n_rows = (*q)->H;
+  });
+}
+
+int kmhg_query_run_device_part(kmhg_index* part, const void* d_seq, size_t L, int k,
+                               void* stream, kmhg_query** q, int64_t* n_rows) {
+  return guarded([&] {
+    if (!part || !d_seq || !q) fail(KMHG_EINVAL, "null argument");
+    check_query_args(L, k);
+    DeviceGuard g(part->device);
+    *q = query_device(part, (const uint8_t*)d_seq, (int64_t)L, k, 0, (int64_t)L - k + 1,
+                      (hipStream_t)stream, true);
+    if (n_rows) *n_rows = (*q)->H;
+  });
+}
+
+int kmhg_query_tile_offsets(kmhg_query* q, uint64_t* d_out, int64_t* n_tiles, void* stream) {
+  return guarded([&] {
+    if (!q || !n_tiles) fail(KMHG_EINVAL, "null argument");
+    if (!q->tile_off.p && q->H) fail(KMHG_EINVAL, "not a part query");
+    *n_tiles = q->n_tiles;
+    if (!d_out) return;
+    DeviceGuard g(q->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (q->n_tiles)
+      HIPC(hipMemcpyAsync(d_out, q->tile_off.p, (size_t)q->n_tiles * 8, hipMemcpyDeviceToDevice, s));
+    const uint64_t h = (uint64_t)q->H;            // [n_tiles] = the part's row total
+    launch_fill_u64(d_out + q->n_tiles, h, s);
+  });
+}
+
+int kmhg_merge_part_rows(const void* d_rows, const uint64_t* d_seg_base, const uint64_t* d_tile_off,
+                         int n_parts, int64_t n_tiles, int k, int64_t w0, void* d_out,
+                         void* stream) {
+  return guarded([&] {
+    if (n_parts < 1 || n_tiles < 0 || k < 1 || k > 32) fail(KMHG_EINVAL, "bad merge arguments");
+    if (!n_tiles) return;
+    if (!d_rows || !d_seg_base || !d_tile_off || !d_out) fail(KMHG_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    LAUNCH("k_merge_part_rows", s,
+           launch_merge_part_rows(reinterpret_cast<const int2*>(d_rows), d_seg_base, d_tile_off,
+                                  (uint32_t)n_parts, (uint32_t)n_tiles, k, w0,
+                                  reinterpret_cast<int2*>(d_out), s));
+    HIPC(hipGetLastError());
   });
 }
 

@@ -105,6 +105,13 @@ void launch_diag_prep(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, co
 void launch_diag_valid(const uint16_t* nbit, int64_t L, int k, uint32_t* uniq, bool multi_in,
                        hipStream_t s);
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s);
+// the owner-routed query's merge (kmhg_merge_part_rows): n_parts rank segments of rows (rank r's
+// at rows + seg_base[r]) with their per-tile offsets tile_off[r * (nt + 1) + t] -> out, ordered
+// by window as the unsharded query (one workgroup per query tile of TILE windows from w0)
+void launch_merge_part_rows(const int2* rows, const uint64_t* seg_base, const uint64_t* tile_off,
+                            uint32_t n_parts, uint32_t nt, int kq, int64_t w0, int2* out,
+                            hipStream_t s);
+void launch_fill_u64(uint64_t* p, uint64_t v, hipStream_t s);
 // exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
 // reduce-then-scan with `scratch` = scan_u64_scratch(n) u64
 // (round 4: one workgroup up to 64 K / 256 K totals instead -- config 3 query 185 -> 162 Gbp/s,

@@ -635,7 +635,10 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
 #else
 #define PROBE_BOUNDS __launch_bounds__(BLOCK)
 #endif
-template <bool DIAG, bool NT>
+// PART (owner-routed query over a part of an owner-computes build): table probes only, and only
+// for the windows whose key this part owns; every other window records no hit here (its owner's
+// rank emits its rows).
+template <bool DIAG, bool NT, bool PART = false>
 __global__ void PROBE_BOUNDS
 k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __restrict__ T,
               Geom g, uint32_t* __restrict__ qrec, uint2* __restrict__ qmulti, int64_t w0,
@@ -690,7 +693,8 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
     const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
-    if (s < w1 && window_key(st, o0 + w, s, L, kq, key)) table_find<NT>(T, g, key, count, aux);
+    if (s < w1 && window_key(st, o0 + w, s, L, kq, key) && (!PART || part_owns(key, g)))
+      table_find<NT, PART>(T, g, key, count, aux);
     // {count, position} for a key seen once, {count, first index} otherwise
     if (s < w1) put_qrec(qrec, qmulti, s - w0, count, aux);
     rows += count;
@@ -1294,6 +1298,12 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
                         uint64_t* tile_rows,
                         hipStream_t s, DiagIdx X, const uint8_t* TG, uint32_t* ecount) {
   uint32_t nt = grid_for(w1 - w0, TILE);
+  if (g.nbh) {                                  // a part's table: owned windows, table probes
+    hipLaunchKernelGGL((k_query_probe<false, false, true>), dim3(nt), dim3(BLOCK), 0, s, seq, L,
+                       kq, T, g, qrec, qmulti, w0, w1, aligned ? 1 : 0, tile_rows,
+                       DiagIdx{nullptr, nullptr, 0}, nullptr, ecount);
+    return;
+  }
   if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
   // nontemporal slot reads for a table of more than NT_PROBE_BYTES.  A/B in one run
   // (profiles/r5n_ab_ntslot_*): the 12-GB table of the 500 Mbp record 5.40 -> 5.20 ms per
@@ -1312,6 +1322,80 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
                        DiagIdx{nullptr, nullptr, 0}, nullptr, ecount);
   }
 }
+// ---------------------------------------------------------------- owner-routed query merge
+// dist.owner_query: rank r queried every window against its part of an owner-computes build and
+// holds the rows of the windows whose k-mer it owns, in window order, with its tile offsets
+// tile_off[r * (nt + 1) + t] (exclusive, [nt] = its total).  A window's rows all come from one
+// rank (its key's owner), in j order; merged, query tile t's rows start at the sum over the
+// ranks of their offset of t and are ordered by window.  One workgroup per tile: count the rows
+// of every window of the tile in LDS (and where each window's run starts in its rank's
+// segment), scan the counts, then place every row at its window's start + its index in the run.
+// Two reads of the rows and one write: the merge moves 24 B per row.
+__global__ void __launch_bounds__(BLOCK)
+k_merge_part_rows(const int2* __restrict__ rows, const uint64_t* __restrict__ seg_base,
+                  const uint64_t* __restrict__ tile_off, uint32_t n_parts, uint32_t nt, int kq,
+                  int64_t w0, int2* __restrict__ out) {
+  __shared__ uint32_t cnt[TILE];
+  __shared__ uint32_t first[TILE];
+  __shared__ uint64_t sh[8];
+  const uint32_t t = blockIdx.x;
+  const int64_t wt = w0 + (int64_t)t * TILE;              // the tile's first window
+  for (uint32_t o = threadIdx.x; o < TILE; o += BLOCK) cnt[o] = 0;
+  uint64_t out0 = 0;
+  for (uint32_t r = 0; r < n_parts; ++r) out0 += tile_off[(uint64_t)r * (nt + 1) + t];
+  __syncthreads();
+  for (uint32_t r = 0; r < n_parts; ++r) {
+    const uint64_t a = tile_off[(uint64_t)r * (nt + 1) + t];
+    const uint64_t b = tile_off[(uint64_t)r * (nt + 1) + t + 1];
+    const int2* R = rows + seg_base[r];
+    for (uint64_t p = a + threadIdx.x; p < b; p += BLOCK) {
+      const int i = R[p].x;
+      const uint32_t o = (uint32_t)((int64_t)i - kq - wt);   // window start - tile start
+      atomicAdd(&cnt[o], 1u);
+      if (p == a || R[p - 1].x != i) first[o] = (uint32_t)(p - a);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of the TILE counts: 8 consecutive windows per thread
+  uint32_t c8[WPT], sum = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    c8[j] = cnt[threadIdx.x * WPT + j];
+    sum += c8[j];
+  }
+  uint64_t tot;
+  uint32_t run = (uint32_t)block_excl_scan((uint64_t)sum, sh, tot);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    cnt[threadIdx.x * WPT + j] = run;                      // now each window's first row
+    run += c8[j];
+  }
+  __syncthreads();
+  for (uint32_t r = 0; r < n_parts; ++r) {
+    const uint64_t a = tile_off[(uint64_t)r * (nt + 1) + t];
+    const uint64_t b = tile_off[(uint64_t)r * (nt + 1) + t + 1];
+    const int2* R = rows + seg_base[r];
+    for (uint64_t p = a + threadIdx.x; p < b; p += BLOCK) {
+      const int2 v = R[p];
+      const uint32_t o = (uint32_t)((int64_t)v.x - kq - wt);
+      out[out0 + cnt[o] + ((uint32_t)(p - a) - first[o])] = v;
+    }
+  }
+}
+
+__global__ void k_fill_u64(uint64_t* __restrict__ p, uint64_t v) { *p = v; }
+
+void launch_merge_part_rows(const int2* rows, const uint64_t* seg_base, const uint64_t* tile_off,
+                            uint32_t n_parts, uint32_t nt, int kq, int64_t w0, int2* out,
+                            hipStream_t s) {
+  hipLaunchKernelGGL(k_merge_part_rows, dim3(nt), dim3(BLOCK), 0, s, rows, seg_base, tile_off,
+                     n_parts, nt, kq, w0, out);
+}
+void launch_fill_u64(uint64_t* p, uint64_t v, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill_u64, dim3(1), dim3(1), 0, s, p, v);
+}
+
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   if (n <= SCAN1_MAX)
     hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);

@@ -226,6 +226,38 @@ class DevicePart(DeviceIndex):
                                                    p(positions), p(codes), _stream_ptr(stream)))
 
 
+    def query_part(self, seq: torch.Tensor, k: int, stream=None) -> "DeviceQuery":
+        """seq.kmer.pos of every window of `seq` against this part only
+        (kmhg_query_run_device_part): the rows of the windows whose k-mer the part owns, in
+        window order; merge_part_rows interleaves every part's rows."""
+        _check_seq(seq)
+        q = C.c_void_p()
+        h = C.c_int64()
+        with torch.cuda.device(seq.device):
+            _lib.check(_lib.lib().kmhg_query_run_device_part(
+                self._h, C.c_void_p(seq.data_ptr()), seq.numel(), k, _stream_ptr(stream),
+                C.byref(q), C.byref(h)))
+        return DeviceQuery(q.value, h.value, seq.device)
+
+
+def merge_part_rows(rows: torch.Tensor, seg_base: list[int], tile_off: torch.Tensor, k: int,
+                    w0: int = 0, stream=None) -> torch.Tensor:
+    """kmhg_merge_part_rows: `rows` (H, 2) int32 holds every part's rows (part r's from row
+    seg_base[r]), `tile_off` (n_parts, n_tiles + 1) uint64 their per-tile offsets; returns the
+    (H, 2) rows in the unsharded seq.kmer.pos order."""
+    dev = rows.device
+    n_parts, nt1 = tile_off.shape
+    out = torch.empty_like(rows)
+    base = torch.tensor(seg_base, dtype=torch.int64, device=dev)
+    toff = tile_off.to(device=dev, dtype=torch.int64).contiguous()
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().kmhg_merge_part_rows(
+            C.c_void_p(rows.data_ptr()), C.c_void_p(base.data_ptr()),
+            C.c_void_p(toff.data_ptr()), n_parts, nt1 - 1, k, w0, C.c_void_p(out.data_ptr()),
+            _stream_ptr(stream)))
+    return out
+
+
 class DeviceQuery:
     def __init__(self, handle: int, n_rows: int, device: torch.device | None = None):
         self._h = C.c_void_p(handle)
@@ -250,6 +282,16 @@ class DeviceQuery:
         if self.n_rows:
             self.copy_to(t)
         return t
+
+    def tile_offsets(self, stream=None) -> torch.Tensor:
+        """A part query's n_tiles + 1 per-tile row offsets (uint64 as int64, on its device)."""
+        n = C.c_int64()
+        _lib.check(_lib.lib().kmhg_query_tile_offsets(self._h, None, C.byref(n), None))
+        out = torch.empty(n.value + 1, dtype=torch.int64, device=self.device)
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.lib().kmhg_query_tile_offsets(self._h, C.c_void_p(out.data_ptr()),
+                                                          C.byref(n), _stream_ptr(stream)))
+        return out
 
     def rows_view(self) -> torch.Tensor:
         """The (H, 2) int32 rows where the emit kernel wrote them (kmhg_query_rows_device), as a

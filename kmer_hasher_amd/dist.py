@@ -454,3 +454,70 @@ def broadcast_index(index, device: torch.device, src: int = 0, group=None):
     meta, bufs = broadcast_buffers(None, None, src, device, group)
     torch.cuda.synchronize(device)
     return DeviceIndex.import_image(meta.cpu(), bufs)
+
+
+# ------------------------------------------------------- owner-routed query over resident parts
+class HipPartEngine:
+    """Adapter: this rank's DevicePart (libkmhgpu) as an owner-routed query engine."""
+
+    def __init__(self, part):
+        self.part = part
+
+    def query_part(self, seq: torch.Tensor, k: int):
+        """(rows of the windows this part owns, in window order; their n_tiles + 1 per-tile row
+        offsets) -- kmhg_query_run_device_part."""
+        q = self.part.query_part(seq, k)
+        return q.rows_view(), q.tile_offsets()
+
+    def merge(self, rows: torch.Tensor, seg_base: list[int], tile_off: torch.Tensor, k: int):
+        from .device import merge_part_rows
+        return merge_part_rows(rows, seg_base, tile_off, k)
+
+
+def owner_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, src: int | None = 0,
+                group=None, timings: dict | None = None):
+    """seq.kmer.pos against an index that stays split in its owner-computes parts, one per rank
+    (the reference's reader-pool partition src/kmer_reader.c:28-39): no assembly
+    and no index broadcast.  The query is broadcast (C1: every rank walks every window), each
+    rank probes only the windows whose k-mer it owns and emits their rows in window order with
+    its per-tile row offsets; the rows and offsets go to `dst`, whose merge
+    (kmhg_merge_part_rows) interleaves them by window into exactly the unsharded rows (a
+    window's rows all come from its key's owner).  Returns the (H, 2) rows on `dst`, None
+    elsewhere.  `timings` receives 'broadcast', 'query', 'gather' and 'merge' seconds."""
+    import time
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = seq.device if seq is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+        else torch.device("cpu"))
+
+    def mark():
+        if timings is not None and dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        return time.perf_counter()
+
+    t0 = mark()
+    if src is not None:
+        seq = broadcast_sequence(seq, src, dev, group)
+    t1 = mark()
+    local, toff = engine.query_part(seq, k)
+    t2 = mark()
+    toff = toff.to(torch.int64)
+    offs = [torch.empty_like(toff) for _ in range(world)]
+    dist.all_gather(offs, toff, group=group)
+    rows = gather_rows(local, dst, group)
+    t3 = mark()
+    out = None
+    if rank == dst:
+        if world == 1:
+            out = rows                        # one part owns every window: already in order
+        else:
+            totals = [int(o[-1].item()) for o in offs]
+            seg_base = [sum(totals[:r]) for r in range(world)]
+            out = engine.merge(rows, seg_base, torch.stack(offs), k)
+    t4 = mark()
+    if timings is not None:
+        for name, dt in (("broadcast", t1 - t0), ("query", t2 - t1), ("gather", t3 - t2),
+                         ("merge", t4 - t3)):
+            timings[name] = timings.get(name, 0.0) + dt
+    return out

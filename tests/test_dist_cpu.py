@@ -308,3 +308,77 @@ def test_assemble_parts_failure_reaches_every_rank(world, bad):
     for r in range(world):
         if r != bad:
             assert "another rank's part build failed" in res[r], res
+
+
+# ------------------------------------------------------------ owner-routed query (gloo, CPU)
+TILE = 2048
+
+
+class FakePartEngine:
+    """Rank r's part for the CPU test: the oracle's rows of the windows this rank "owns" (here a
+    hash of the window index: every window's rows on exactly one rank, as the real parts own a
+    window by its key), with their per-tile offsets (tiles of 2048 windows); the merge is a
+    stable sort by window end (the HIP merge is tested on the GPU)."""
+
+    def __init__(self, seq_bytes, k_index, rank, world):
+        from oracle import oracle as O
+        self.oi = O.OracleIndex(seq_bytes, k_index)
+        self.rank, self.world = rank, world
+
+    def query_part(self, seq, k):
+        rows = self.oi.query(seq.numpy().tobytes(), k).reshape(-1, 2)
+        i = rows[:, 0].astype(np.int64)
+        own = ((i * 2654435761) >> 7) % self.world == self.rank
+        mine = np.ascontiguousarray(rows[own])
+        nw = seq.numel() - k + 1
+        nt = (nw + TILE - 1) // TILE
+        tiles = (mine[:, 0].astype(np.int64) - k) // TILE
+        cnt = np.bincount(tiles, minlength=nt)[:nt]
+        off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+        return torch.from_numpy(mine), torch.from_numpy(off)
+
+    def merge(self, rows, seg_base, tile_off, k):
+        r = rows.numpy()
+        assert tile_off.shape[0] == self.world and seg_base[0] == 0
+        o = np.argsort(r[:, 0], kind="stable")
+        return torch.from_numpy(np.ascontiguousarray(r[o]))
+
+
+def _owner_worker(rank, world, port, seq_bytes, k, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = FakePartEngine(seq_bytes, k, rank, world)
+        seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()) if rank == 0 else None
+        ph = {}
+        rows = kd.owner_query(eng, seq, k, dst=0, src=0, timings=ph)
+        assert set(ph) == {"broadcast", "query", "gather", "merge"}
+        if rank == 0:
+            out_q.put(rows.numpy().reshape(-1).tolist())
+        else:
+            assert rows is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_owner_query_orchestration(world):
+    """owner_query: the query broadcast from rank 0, every rank's owned rows and tile offsets
+    gathered to rank 0 and merged back into the unsharded seq.kmer.pos rows."""
+    from oracle import oracle as O
+    k = 17
+    s = synth.add_n_runs(synth.repeat_rich(30_000, 6, n_gap_every=7_001), 0.01, 9)
+    seq_bytes = s.tobytes()
+    want = O.OracleIndex(seq_bytes, k).query(seq_bytes, k).tolist()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_worker, args=(r, world, port, seq_bytes, k, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert got == want

@@ -289,3 +289,70 @@ def test_scatter_query_rows_to_device_and_host(gpu, world, k, backend):
     assert all(r[1] == want for r in res)
     assert registered                   # the host matrix is DMA-registered
     assert not [f for f in set(os.listdir("/dev/shm")) - before if f.startswith("kmhg_rows")]
+
+
+def _owner_query_worker(rank, world, port, seq_bytes, k, kq, backend, out_q):
+    """Owner-computes build over `world` ranks sharing cuda:0 and the owner-routed query over the
+    resident parts (no assembly): the query broadcast from rank 0, every rank probing the
+    windows its part owns (kmhg_query_run_device_part), rows and tile offsets to rank 0, merged
+    there by kmhg_merge_part_rows."""
+    import torch
+    import torch.distributed as dist
+    from kmer_hasher_amd import dist as kd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()).to(dev) \
+            if rank == 0 else None
+        part, _ = kd.owner_build(seq, k, dev, src=0)
+        kd.part_info_all(part, dev)
+        eng = kd.HipPartEngine(part)
+        res = []
+        for q in (seq, seq):                 # twice: the second reuses the pools
+            ph = {}
+            rows = kd.owner_query(eng, q if rank == 0 else None, kq, dst=0, src=0, timings=ph)
+            torch.cuda.synchronize()
+            if rank == 0:
+                res.append(rows.cpu().numpy().reshape(-1).tolist())
+        if rank == 0:
+            out_q.put((res, sorted(ph)))
+        dist.barrier()
+        part.free()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k,kq,backend", [(2, 31, 31, "gloo"), (3, 21, 17, "gloo"),
+                                                (3, 31, 31, "gloo"), (1, 21, 21, "nccl")])
+def test_owner_routed_query_over_parts(gpu, world, k, kq, backend):
+    import torch.multiprocessing as mp
+    from kmer_hasher_amd import synth
+    from oracle import oracle as O
+    s = synth.add_n_runs(synth.repeat_rich(160_000, 12, n_gap_every=10_009), 0.004, 13)
+    s[-k - 2] = ord("N")
+    seq_bytes = s.tobytes()
+    want = O.OracleIndex(seq_bytes, k).query(seq_bytes, kq).tolist()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_query_worker,
+                         args=(r, world, port, seq_bytes, k, kq, backend, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res, phases = q.get(timeout=100)
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert len(want) > 0 and all(r == want for r in res)
+    assert phases == ["broadcast", "gather", "merge", "query"]

@@ -111,3 +111,37 @@ def test_part_index_refuses_queries(gpu):
     with pytest.raises(_lib.KmhgError, match="part out of range"):
         DeviceIndex.build_part(seq, 21, 2, 2)
     p.free()
+
+
+def test_merge_part_rows_interleaves_by_window(gpu):
+    """kmhg_merge_part_rows on hand-made parts: windows dealt to three parts (a window's rows on
+    one part, j ascending), ragged tiles (empty tiles, a window with 3,000 rows, a part with no
+    rows) -> the rows ordered by window, then by the part's order, as the unsharded query."""
+    import torch
+    from kmer_hasher_amd.device import merge_part_rows
+    rng = np.random.default_rng(5)
+    k, nw, T = 21, 3 * 2048 + 77, 2048
+    per_window = rng.integers(0, 3, size=nw)
+    per_window[100] = 3000                     # a heavy window
+    per_window[2048:4096] = 0                  # an empty tile
+    owner = rng.integers(0, 2, size=nw)        # part 2 owns nothing
+    rows = {0: [], 1: [], 2: []}
+    want = []
+    for s in range(nw):
+        for j in range(per_window[s]):
+            r = (s + k, int(rng.integers(1, 10**6)))
+            rows[owner[s]].append(r)
+            want.append(r)
+    nt = (nw + T - 1) // T
+    segs, offs, base = [], [], [0]
+    for p in range(3):
+        a = np.array(rows[p], np.int32).reshape(-1, 2)
+        tiles = (a[:, 0].astype(np.int64) - k) // T
+        cnt = np.bincount(tiles, minlength=nt)[:nt]
+        offs.append(np.concatenate([[0], np.cumsum(cnt)]))
+        segs.append(a)
+        base.append(base[-1] + a.shape[0])
+    allrows = torch.from_numpy(np.concatenate(segs)).cuda()
+    tile_off = torch.from_numpy(np.stack(offs).astype(np.int64)).cuda()
+    out = merge_part_rows(allrows, base[:3], tile_off, k).cpu().numpy()
+    assert out.tolist() == [list(r) for r in want]
