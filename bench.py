@@ -1465,24 +1465,28 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
     from kmer_hasher_amd import dist as kd
     from kmer_hasher_amd import synth
     L, k = LARGE_L, LARGE_K
-    tb, index, t_build = None, None, 0.0
+    tb, ta, index, t_build = None, None, None, 0.0
     if rank == 0:
         A = synth.iid(L, 4)
         tb = torch.from_numpy(synth.derived(A, 5)).to(dev)
         ta = torch.from_numpy(A).to(dev)
         del A
+        D.DeviceIndex.build(ta, k).wait().free()       # the pool's first allocations, untimed
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         index = D.DeviceIndex.build(ta, k)
         index.wait()
         t_build = time.perf_counter() - t0
-        del ta
     t_bcast = 0.0
     # every collective of the path runs whenever a process group exists (the RCCL world-1
     # rehearsal, `--dist`, included); without one (`--config 5` at N = 1) the step is the plain
     # query
     use_pg = dist.is_available() and dist.is_initialized()
     if use_pg:
+        # once untimed (the receivers' first allocations), then timed
+        rep = kd.broadcast_index(index, dev)
+        if rank:
+            rep.free()
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -1583,9 +1587,57 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
     t_dev, t_host, *ph = tt.tolist()
     ph_dev, ph_host, ph_bc = ph[0:3], ph[3:6], ph[6:9]
     index.free()
+    # ---- the owner-routed alternative (no index broadcast, no replica): A broadcast, every rank
+    # builds the k-mers it owns (dist.owner_build), B queried over the resident parts
+    # (dist.owner_query: B broadcast, owned windows probed, rows merged on rank 0)
+    own = None
+    if use_pg:
+        progress("sharded query: owner-routed parts")
+        part, _ = kd.owner_build(ta, k, dev, src=0)      # untimed: first allocations
+        kd.part_info_all(part, dev)
+        part.free()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        part, _ = kd.owner_build(ta, k, dev, src=0)
+        kd.part_info_all(part, dev)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t_obuild = time.perf_counter() - t0
+        oeng = kd.HipPartEngine(part)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rows = kd.owner_query(oeng, tb, k, dst=0, src=0)
+        torch.cuda.synchronize()
+        t_ofirst = time.perf_counter() - t0
+        H_own = rows.shape[0] if rows is not None else 0
+        del rows
+        oph = {}
+        for _ in range(2):
+            rows = kd.owner_query(oeng, tb, k, dst=0, src=0, timings=oph)
+            del rows
+        n_own = max(1, min(steps, 5))
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n_own):
+            rows = kd.owner_query(oeng, tb, k, dst=0, src=0)
+            del rows
+        dist.barrier()
+        torch.cuda.synchronize()
+        t_own = time.perf_counter() - t0
+        part.free()
+        to = torch.tensor([t_obuild, t_ofirst, t_own] +
+                          [oph.get(p, 0.0) / 2 for p in ("broadcast", "query", "gather", "merge")],
+                          dtype=torch.float64, device=dev)
+        dist.all_reduce(to, op=dist.ReduceOp.MAX)
+        own = to.tolist() + [H_own, n_own]
     if rank != 0:
         return None, kt
     assert H_host == H, (H_host, H)
+    if own is not None and int(own[7]) != H:
+        raise SystemExit(f"bench: the owner-routed query returned {int(own[7])} rows, the "
+                         f"replicated one {H}")
 
     def ms(x):
         return round(x * 1e3, 3)
@@ -1613,6 +1665,24 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
            "roofline": sharded_roofline(survey_bytes("query", L=L, Nq=L - k + 1, H=H),
                                         t_dev / steps, ph_dev[1], world),
            "c1_broadcast_ms": ms(ph_bc[0]) if use_pg else None,
+           "owner_routed": None if own is None else {
+               "value": round(L / 1e6 * own[8] / own[2], 2), "unit": "Mbp/s",
+               "ms_per_step": round(own[2] / own[8] * 1e3, 3), "steps": own[8],
+               "rows": own[7], "part_build_ms": ms(own[0]), "first_query_ms": ms(own[1]),
+               "phases_ms": {"query_broadcast": ms(own[3]), "part_query": ms(own[4]),
+                             "row_gather": ms(own[5]), "merge": ms(own[6])},
+               "build_and_query_once_ms": {
+                   "owner_routed": ms(own[0] + own[1]),
+                   "replicated": ms(t_build + t_bcast + t_first),
+                   "note": "make.kmer.hash(A) then one seq.kmer.pos(B), as an R session issues "
+                           "them: owner-computes parts (A broadcast, every rank builds the "
+                           "k-mers it owns) + one owner-routed query, against rank 0's build + "
+                           "the index image broadcast + the first sharded query"},
+               "note": "no assembly, no index broadcast: every rank holds its part (1/n_gpus "
+                       "of the index); a query step broadcasts B, every rank probes the "
+                       "windows whose k-mer it owns (kmhg_query_run_device_part), the rows and "
+                       "per-tile offsets go to rank 0, which interleaves them by window "
+                       "(kmhg_merge_part_rows)"},
            "c1_broadcast_note": "C1 as a broadcast of the whole B (one separate step), against "
                                 "query_scatter's slices",
            "backend": dist.get_backend() if use_pg else None,
