@@ -459,12 +459,12 @@ __device__ __forceinline__ uint32_t table_find(const Slot* __restrict__ T, Geom 
 // occupied slots to an empty one: at load 0.67 ~5 slots, one 64-B span instead of 5 dependent
 // loads).  Used where misses dominate (the diagonal query path sends only anchors, unpredicted
 // windows and misses here).
-template <bool NT = false>
+template <bool NT = false, bool PART = false>
 __device__ __forceinline__ uint32_t table_find4(const Slot* __restrict__ T, Geom g, uint64_t key,
                                                 uint32_t& count, uint32_t& aux) {
-  if (key == EMPTY_KEY) return table_find<NT>(T, g, key, count, aux);
+  if (key == EMPTY_KEY) return table_find<NT, PART>(T, g, key, count, aux);
   const uint64_t h = mix64(key);
-  const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
+  const uint64_t b0 = (uint64_t)(PART ? part_bucket(h, g) : bucket_of(h, g.nb)) * g.capb;
   uint32_t j = local_home(h, g.capb);
   for (;;) {
     uint4 v[4];
@@ -507,14 +507,15 @@ __device__ __forceinline__ uint32_t zero_bytes8(uint64_t v) {
 // table_find through the tags: a miss reads the 16 tags of its home's aligned group (one 16-B
 // load from an array 1/16 the table's size) and usually stops at an empty tag without touching
 // the table; the table is read only at slots whose tag equals the key's.  Needs g.capb % 16 == 0.
-template <bool NT = false>
+// PART: T and TG are a part's (the caller checked part_owns).
+template <bool NT = false, bool PART = false>
 __device__ __forceinline__ uint32_t table_find_tag(const Slot* __restrict__ T,
                                                    const uint8_t* __restrict__ TG, Geom g,
                                                    uint64_t key, uint32_t& count, uint32_t& aux) {
   count = 0; aux = 0;
-  if (key == EMPTY_KEY) return table_find<NT>(T, g, key, count, aux);
+  if (key == EMPTY_KEY) return table_find<NT, PART>(T, g, key, count, aux);
   const uint64_t h = mix64(key);
-  const uint64_t b0 = (uint64_t)bucket_of(h, g.nb) * g.capb;
+  const uint64_t b0 = (uint64_t)(PART ? part_bucket(h, g) : bucket_of(h, g.nb)) * g.capb;
   const uint32_t j = local_home(h, g.capb);
   const uint64_t tt = 0x0101010101010101ull * slot_tag(h);
   uint32_t grp = j & ~15u, off = j & 15u;

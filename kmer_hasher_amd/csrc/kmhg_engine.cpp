@@ -684,11 +684,12 @@ struct kmhg_index {
   // cleared and the slot tags built on the first eligible query (V_diag_prep)
   DBuf<uint64_t> dcodes;
   DBuf<uint8_t> ptag;             // one tag byte per table slot (0 = empty)
+  // part of an owner-computes build (kmhg_build_device_part): holds buckets
+  // [geom.b0, geom.b0 + geom.nb) of a table of geom.nbh buckets; exported for an assembly, or
+  // queried in place by the owner-routed query (kmhg_query_run_device_part)
+  bool is_part = false;
   // ps_ready: published (release) after the preparing query's synchronize; read (acquire) by
   // later queries, possibly on other threads, before they use ptag / the uniq bits
-  // part of an owner-computes build (kmhg_build_device_part): holds buckets
-  // [geom.b0, geom.b0 + geom.nb) of a table of geom.nbh buckets; exported, never queried
-  bool is_part = false;
   std::atomic<bool> ps_ready{false};
   // how the index was built (kmhg_info.build / .fallback): KMHG_BUILD_* and whether
   // finish_build() had to rebuild it with the global-atomic build
@@ -1329,12 +1330,14 @@ kmhg_index* build_device_v2(const uint8_t* d_seq, int64_t L, int k, hipStream_t 
   // bits itself, so the first seq.kmer.pos of a new index does not pay V_diag_prep (2.6 ms at
   // 500 Mbp, +70 % on the query).  In cache (config 2) the build is the headline and the
   // preparation stays with the first query (round-3 A/B: tags in the build +1-1.5 % there).
-  // KMHG_BUILD_TAGS=0 / 1 (test build) forces either.
+  // A part of an owner-computes build does the same for its own slots and keys (the owner-
+  // routed query runs the diagonal path on it).  KMHG_BUILD_TAGS=0 / 1 (test build) forces
+  // either on key streams.
   uint8_t* tg = nullptr;
   uint32_t* rep = nullptr;
   {
     const char* bte = test_build_knob("KMHG_BUILD_TAGS");
-    const bool want = codes && !bid && !from_keys && !count_only && n_parts == 0 &&
+    const bool want = codes && !bid && !from_keys && !count_only &&
                       (bte ? bte[0] == '1' : Nw > BID_MAX_WINDOWS);
     if (want) {
       try {
@@ -1512,8 +1515,10 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   // diagonal path (k_query_probe): a position index queried at its own k
   const int64_t nA = idx->L - idx->k + 1;
   const char* de = test_build_knob("KMHG_QUERY_DIAG");
+  // (a part query too: its anchors and verified windows count only where the part owns the key,
+  // and its tags and repeated-key bits come from its own table, k_query_probe<..., PART>)
   const bool diag_ok = !(de && de[0] == '0') && kq == idx->k && idx->sources == 0 && nA > 0 &&
-                       idx->U > 0 && idx->dcodes.p && !part_query;
+                       idx->U > 0 && idx->dcodes.p;
   bool diag = diag_ok;
   if (diag && !idx->ps_ready.load(std::memory_order_acquire)) {
     std::lock_guard<std::mutex> lk(idx->ps_mu);

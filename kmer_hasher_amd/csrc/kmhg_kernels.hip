@@ -421,8 +421,9 @@ struct DiagAnchors {
 };
 
 // Anchor probes of a staged tile (threads < DG_ANCHORS) and the last-predicting-anchor scan;
-// called by every thread of the block (two barriers inside).
-template <bool NT, class ST>
+// called by every thread of the block (two barriers inside).  PART: only the anchors whose key
+// the part owns probe (the others record no hit and predict nothing).
+template <bool NT, bool PART = false, class ST>
 __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_start, int64_t w1,
                                              int64_t L, int kq, const Slot* __restrict__ T,
                                              Geom g, DiagAnchors& A) {
@@ -432,18 +433,19 @@ __device__ __forceinline__ void diag_anchors(const ST& st, int o0, int64_t t_sta
     const int64_t s = t_start + w;
     uint64_t key = 0;
     uint32_t count = 0, aux = 0;
-    const bool kv = is_anchor && s < w1 && window_key(st, o0 + w, s, L, kq, key);
+    const bool kv = is_anchor && s < w1 && window_key(st, o0 + w, s, L, kq, key) &&
+                    (!PART || part_owns(key, g));
     // Adaptive anchors: the even ones are always probed; an odd one only while no even anchor
     // before it predicts (the tile's head after a miss), since behind a predicting anchor the
     // windows verify against its diagonal anyway.  A self dot plot probes every 512th window, a
     // cross query keeps every 256th where the tile head needs it.
     const bool primary = (threadIdx.x & 1) == 0;
-    if (kv && primary) table_find<NT>(T, g, key, count, aux);
+    if (kv && primary) table_find<NT, PART>(T, g, key, count, aux);
     const uint64_t pm = __ballot(is_anchor && primary && count == 1);
     // (and only in a tile where some even anchor predicts: with none, the tile is unrelated to
     // the index and its windows probe the table whatever the odd anchors find)
     const bool second = kv && !primary && pm != 0 && (pm & lanemask_lt()) == 0;
-    if (second) table_find<NT>(T, g, key, count, aux);
+    if (second) table_find<NT, PART>(T, g, key, count, aux);
     const uint64_t probed = __ballot(is_anchor && (primary || second));
     if (threadIdx.x == 0) A.probed = probed;
     if (is_anchor) {
@@ -539,7 +541,10 @@ struct DiagProbeLDS {
   uint64_t key[TILE];            // unresolved windows' keys
   uint8_t todo[TILE];            // 1: window w needs a table probe
 };
-template <bool NT, class ST>
+// PART (owner-routed query over a part): only the windows whose key the part owns can hit (the
+// code words and window bits are the whole index sequence's, the repeated-key bits the part's
+// own keys'); a verified window of another part's key records no hit and is not probed.
+template <bool NT, bool PART, class ST>
 __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t t_start,
                                                   int64_t w0r, int64_t w1, int64_t L, int kq,
                                                   const Slot* __restrict__ T, Geom g, DiagIdx X,
@@ -569,6 +574,7 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
     uint32_t count = 0, aux = 0;
     if (s < w1 && win.valid(j)) {
       const uint64_t key = win.key(j);
+      const bool own = !PART || part_owns(key, g);
       bool hit;
       if (j == 0 && w0 % DG_STRIDE == 0 && A.was_probed(w0 / DG_STRIDE)) {   // probed already
         const uint2 ai = A.info[w0 / DG_STRIDE];
@@ -578,13 +584,15 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
         const int sh = 2 * (ro + j);                       // <= 44
         const uint64_t top = sh ? (ih << sh) | (il >> (64 - sh)) : ih;
         const uint64_t ikey = top >> (64 - 2 * kq);
-        hit = pred && (int64_t)(p0 + j) < X.nA && ((ub >> (rb + j)) & 1ull) && ikey == key;
+        hit = own && pred && (int64_t)(p0 + j) < X.nA && ((ub >> (rb + j)) & 1ull) && ikey == key;
         count = 1; aux = (uint32_t)(p0 + 1 + j);
       }
       if (!hit) {
         count = 0; aux = 0;
-        P.key[w0 + j] = key;
-        todo |= 1u << (8 * (j & 3));
+        if (own) {
+          P.key[w0 + j] = key;
+          todo |= 1u << (8 * (j & 3));
+        }
       }
     }
     if (j == 3) {
@@ -615,8 +623,8 @@ __device__ __forceinline__ uint64_t diag_resolve8(const ST& st, int o0, int64_t 
     if (P.todo[w]) {
       const int64_t s = t_start + w;
       uint32_t count = 0, aux = 0;
-      if (TG) table_find_tag<NT>(T, TG, g, P.key[w], count, aux);
-      else table_find4<NT>(T, g, P.key[w], count, aux);
+      if (TG) table_find_tag<NT, PART>(T, TG, g, P.key[w], count, aux);
+      else table_find4<NT, PART>(T, g, P.key[w], count, aux);
       put_qrec(qrec, qmulti, s - w0r, count, aux);
       rows += count;
     }
@@ -660,18 +668,22 @@ k_query_probe(const uint8_t* __restrict__ seq, int64_t L, int kq, const Slot* __
   const int o0 = (int)(t_start - base);
   stage_tile(seq, L, base, st, aligned != 0);
   __syncthreads();
-  if (DIAG) diag_anchors<NT>(st, o0, t_start, w1, L, kq, T, g, A);
+  if (DIAG) diag_anchors<NT, PART>(st, o0, t_start, w1, L, kq, T, g, A);
   uint64_t rows = 0;
 #ifndef KMHG_PROBE_UNROLL
 #define KMHG_PROBE_UNROLL 2
 #endif
   if (DIAG) {
 #ifndef KMHG_PROBE_STRIDED
-    rows = diag_resolve8<NT>(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A, qrec, qmulti, PL);
+    rows = diag_resolve8<NT, PART>(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A, qrec, qmulti,
+                                   PL);
     uint64_t tot8;
     block_excl_scan(rows, sh, tot8);
     if (threadIdx.x == 0) tile_rows[tile] = tot8;
     return;
+#else
+    static_assert(!(PART && DIAG),
+                  "the strided diagonal variant (-DKMHG_PROBE_STRIDED) has no part form");
 #endif
     diag_resolve<NT>(st, o0, t_start, w0, w1, L, kq, T, g, X, TG, A,
                  [&](int w, int64_t s, uint32_t count, uint32_t aux) {
@@ -1298,17 +1310,24 @@ void launch_query_probe(const uint8_t* seq, int64_t L, int kq, const Slot* T, Ge
                         uint64_t* tile_rows,
                         hipStream_t s, DiagIdx X, const uint8_t* TG, uint32_t* ecount) {
   uint32_t nt = grid_for(w1 - w0, TILE);
-  if (g.nbh) {                                  // a part's table: owned windows, table probes
-    hipLaunchKernelGGL((k_query_probe<false, false, true>), dim3(nt), dim3(BLOCK), 0, s, seq, L,
-                       kq, T, g, qrec, qmulti, w0, w1, aligned ? 1 : 0, tile_rows,
-                       DiagIdx{nullptr, nullptr, 0}, nullptr, ecount);
-    return;
-  }
   if (g.capb % 16 != 0) TG = nullptr;           // the tag groups are aligned 16-slot spans
   // nontemporal slot reads for a table of more than NT_PROBE_BYTES.  A/B in one run
   // (profiles/r5n_ab_ntslot_*): the 12-GB table of the 500 Mbp record 5.40 -> 5.20 ms per
   // query, config 3's 2.4 GB +-0, config 2's 0.24 GB -4 % (its table lines are reused)
   const bool ntl = (uint64_t)g.nb * g.capb * sizeof(Slot) > NT_PROBE_BYTES;
+  if (g.nbh) {                                  // a part's table: the windows it owns
+    if (X.code && ntl)
+      hipLaunchKernelGGL((k_query_probe<true, true, true>), dim3(nt), dim3(BLOCK), 0, s, seq, L,
+                         kq, T, g, qrec, qmulti, w0, w1, aligned ? 1 : 0, tile_rows, X, TG, ecount);
+    else if (X.code)
+      hipLaunchKernelGGL((k_query_probe<true, false, true>), dim3(nt), dim3(BLOCK), 0, s, seq, L,
+                         kq, T, g, qrec, qmulti, w0, w1, aligned ? 1 : 0, tile_rows, X, TG, ecount);
+    else
+      hipLaunchKernelGGL((k_query_probe<false, false, true>), dim3(nt), dim3(BLOCK), 0, s, seq, L,
+                         kq, T, g, qrec, qmulti, w0, w1, aligned ? 1 : 0, tile_rows,
+                         DiagIdx{nullptr, nullptr, 0}, nullptr, ecount);
+    return;
+  }
   if (X.code) {
     if (ntl)
       hipLaunchKernelGGL((k_query_probe<true, true>), dim3(nt), dim3(BLOCK), 0, s, seq, L, kq, T, g,

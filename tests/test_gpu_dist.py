@@ -291,15 +291,20 @@ def test_scatter_query_rows_to_device_and_host(gpu, world, k, backend):
     assert not [f for f in set(os.listdir("/dev/shm")) - before if f.startswith("kmhg_rows")]
 
 
-def _owner_query_worker(rank, world, port, seq_bytes, k, kq, backend, out_q):
+def _owner_query_worker(rank, world, port, seq_bytes, k, kq, backend, out_q, qbytes=None,
+                        knobs=None):
     """Owner-computes build over `world` ranks sharing cuda:0 and the owner-routed query over the
-    resident parts (no assembly): the query broadcast from rank 0, every rank probing the
-    windows its part owns (kmhg_query_run_device_part), rows and tile offsets to rank 0, merged
-    there by kmhg_merge_part_rows."""
+    resident parts (no assembly): the query (`qbytes`, default the indexed sequence) broadcast
+    from rank 0, every rank probing the windows its part owns (kmhg_query_run_device_part: the
+    diagonal path where kq == k), rows and tile offsets to rank 0, merged there by
+    kmhg_merge_part_rows.  `knobs`: path selectors for the test build (libkmhgpu_test.so)."""
+    import contextlib
     import torch
     import torch.distributed as dist
+    from kmer_hasher_amd import _lib
     from kmer_hasher_amd import dist as kd
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(knobs or {})
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     if backend == "nccl":
@@ -307,41 +312,56 @@ def _owner_query_worker(rank, world, port, seq_bytes, k, kq, backend, out_q):
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()).to(dev) \
-            if rank == 0 else None
-        part, _ = kd.owner_build(seq, k, dev, src=0)
-        kd.part_info_all(part, dev)
-        eng = kd.HipPartEngine(part)
-        res = []
-        for q in (seq, seq):                 # twice: the second reuses the pools
-            ph = {}
-            rows = kd.owner_query(eng, q if rank == 0 else None, kq, dst=0, src=0, timings=ph)
-            torch.cuda.synchronize()
+        with (_lib.using_test_build() if knobs else contextlib.nullcontext()):
+            seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()).to(dev) \
+                if rank == 0 else None
+            qry = seq if qbytes is None or rank != 0 else \
+                torch.from_numpy(np.frombuffer(qbytes, np.uint8).copy()).to(dev)
+            part, _ = kd.owner_build(seq, k, dev, src=0)
+            kd.part_info_all(part, dev)
+            eng = kd.HipPartEngine(part)
+            res = []
+            for _ in range(2):               # twice: the second reuses the pools and the tags
+                ph = {}
+                rows = kd.owner_query(eng, qry if rank == 0 else None, kq, dst=0, src=0,
+                                      timings=ph)
+                torch.cuda.synchronize()
+                if rank == 0:
+                    res.append(rows.cpu().numpy().reshape(-1).tolist())
             if rank == 0:
-                res.append(rows.cpu().numpy().reshape(-1).tolist())
-        if rank == 0:
-            out_q.put((res, sorted(ph)))
-        dist.barrier()
-        part.free()
+                out_q.put((res, sorted(ph)))
+            dist.barrier()
+            part.free()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k,kq,backend", [(2, 31, 31, "gloo"), (3, 21, 17, "gloo"),
-                                                (3, 31, 31, "gloo"), (1, 21, 21, "nccl")])
-def test_owner_routed_query_over_parts(gpu, world, k, kq, backend):
+@pytest.mark.parametrize("world,k,kq,backend,query", [
+    (2, 31, 31, "gloo", "self"), (3, 21, 17, "gloo", "self"), (3, 31, 31, "gloo", "self"),
+    (1, 21, 21, "nccl", "self"), (3, 31, 31, "gloo", "related"), (2, 21, 21, "gloo", "nodiag"),
+    (3, 31, 31, "gloo", "buildtags")])
+def test_owner_routed_query_over_parts(gpu, world, k, kq, backend, query):
+    """Owner-routed rows equal the oracle's: self dot plots of a repeat-rich sequence (diagonal
+    path at kq == k, table probes at kq != k), a related query (config 5's shape: SNVs,
+    inversions / translocations and N-runs, so verifications fail and windows probe), the
+    table-probe path forced at kq == k, and the parts' slot tags and repeated-key bits written by
+    their builds (what parts beyond the cache do) instead of the first query."""
+    knobs = {"nodiag": {"KMHG_QUERY_DIAG": "0"},
+             "buildtags": {"KMHG_BUILD_TAGS": "1", "KMHG_BUILD_BID": "0"}}.get(query)
     import torch.multiprocessing as mp
     from kmer_hasher_amd import synth
     from oracle import oracle as O
     s = synth.add_n_runs(synth.repeat_rich(160_000, 12, n_gap_every=10_009), 0.004, 13)
     s[-k - 2] = ord("N")
     seq_bytes = s.tobytes()
-    want = O.OracleIndex(seq_bytes, k).query(seq_bytes, kq).tolist()
+    qbytes = synth.derived(s, 9, 0.01, 4).tobytes() if query in ("related", "buildtags") \
+        else None
+    want = O.OracleIndex(seq_bytes, k).query(qbytes or seq_bytes, kq).tolist()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_owner_query_worker,
-                         args=(r, world, port, seq_bytes, k, kq, backend, q))
+                         args=(r, world, port, seq_bytes, k, kq, backend, q, qbytes, knobs))
              for r in range(world)]
     for p in procs:
         p.start()
