@@ -7,6 +7,7 @@
 // Reference entry points each C function replaces are listed in include/kmhgpu.h.
 #include <atomic>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <climits>
@@ -37,9 +38,10 @@
 // KMHG_FUSE_BOUNDS, KMHG_TEST_BALLOT, KMHG_QUERY_TAGS, KMHG_QUERY_DIAG, KMHG_DIAG_CODES,
 // KMHG_COUNT_TABLE, KMHG_COUNT_WALK, KMHG_CO_SPREAD, KMHG_CO_GLOBAL, KMHG_PART_COMPACT,
 // KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_NB_ROUND, KMHG_SLICE_POISON, KMHG_TEST_REPLICA,
-// KMHG_DIGIT_STREAM, KMHG_DS_BID, KMHG_DS_U8, KMHG_DS_PACK), which choose between equivalent
-// paths and change no result; fault injection (KMHG_TEST_DISORDER); and the A/B-only switches
-// (KMHG_D2H, KMHG_COUNT_BID, KMHG_RK_CAP).
+// KMHG_DIGIT_STREAM, KMHG_DS_BID, KMHG_DS_U8, KMHG_DS_PACK, KMHG_BUILD_TAGS), which choose
+// between equivalent paths and change no result; fault injection (KMHG_TEST_DISORDER); and the
+// A/B-only switches (KMHG_D2H, KMHG_D2H_HUGE, KMHG_COUNT_BID, KMHG_RK_CAP, KMHG_POOL_DEPTH,
+// KMHG_POOL_BESTFIT, KMHG_POOL_TRACE).
 namespace kmhg {
 inline const char* test_build_knob(const char* name) {
 #ifdef KMHG_TEST_BUILD
@@ -556,12 +558,32 @@ static PinStage& pin_stage() {           // the device's two pinned D2H_CHUNK bu
   return stages[dev];
 }
 
+// A result matrix is usually fresh memory of the caller's allocator (R's allocMatrix: malloc,
+// 4-KB pages), so the copy below takes one page fault per 4 KB.  Asking for transparent huge
+// pages on the destination's whole 2-MB spans first (madvise(MADV_HUGEPAGE): a hint on the
+// mapping, no change to its contents or ownership) makes that one fault per 2 MB.  Measured on
+// the box (tools/host_thp_probe.py, profiles/r6r_thp.json, 10 M rows = 80 MB into a fresh
+// array): 7.49 ms with 4-KB pages, 2.82 ms with huge pages (numpy asks for them itself).
+// KMHG_D2H_HUGE=0 (test build) leaves the destination alone (A/B).
+constexpr size_t HUGE_SPAN = 2u << 20;
+static void hint_huge_pages(void* dst, size_t bytes) {
+  static const bool on = [] {
+    const char* e = test_build_knob("KMHG_D2H_HUGE");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || bytes < 2 * HUGE_SPAN) return;
+  const uintptr_t m = ~(uintptr_t)(HUGE_SPAN - 1), d = reinterpret_cast<uintptr_t>(dst);
+  const uintptr_t a = (d + HUGE_SPAN - 1) & m, b = (d + bytes) & m;
+  if (b > a) (void)madvise(reinterpret_cast<void*>(a), b - a, MADV_HUGEPAGE);   // a hint only
+}
+
 void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (!bytes) return;
   static const bool staged = [] {
     const char* e = test_build_knob("KMHG_D2H");      // A/B knob: "direct" = one hipMemcpy
     return !(e && std::string(e) == "direct");
   }();
+  hint_huge_pages(dst, bytes);
   if (!staged || bytes < D2H_STAGE_MIN) {
     HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
