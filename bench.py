@@ -1563,6 +1563,14 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
         kt = D.timing_report() if timing_kernels else {}
         if timing_kernels:
             D.timing_enable(False)
+        # the gather's wire format: rank 0's own range as diagonal runs (dist.HipRunCodec; the
+        # other ranks' rows travel the same way), untimed
+        w_r0 = kd.shard_ranges(L - k + 1, world)[0]
+        loc = eng.query_range(tb, k, *w_r0) if rank == 0 else None
+        runs0 = eng.codec.encode(loc) if loc is not None else None
+        runs_fmt = None if loc is None else {
+            "rows": int(loc.shape[0]), "runs": None if runs0 is None else int(runs0.shape[0])}
+        del loc, runs0
         progress("sharded query: rows to the host matrix")
         # rows into the host matrix (what an R session receives): first delivery (the shared
         # buffer's creation and registration) untimed
@@ -1664,6 +1672,12 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
                                "a pinned host matrix"},
            "roofline": sharded_roofline(survey_bytes("query", L=L, Nq=L - k + 1, H=H),
                                         t_dev / steps, ph_dev[1], world),
+           "gather_format": dict(runs_fmt, bytes_ratio=round(
+               8 * runs_fmt["rows"] / (12 * runs_fmt["runs"]), 1) if runs_fmt["runs"] else None,
+               note="the rows cross xGMI as diagonal runs (12 B per run of rows (i, j), (i + 1, "
+                    "j + 1), ...; dist.gather_rows + HipRunCodec: kmhg_rows_runs on the "
+                    "senders, kmhg_runs_expand on rank 0); counted on rank 0's own window "
+                    "range") if runs_fmt else None,
            "c1_broadcast_ms": ms(ph_bc[0]) if use_pg else None,
            "owner_routed": None if own is None else {
                "value": round(L / 1e6 * own[8] / own[2], 2), "unit": "Mbp/s",
@@ -1689,7 +1703,7 @@ def sharded_query_record(args, dev, world, rank, steps: int, timing_kernels: boo
            "note": "index(A) built on rank 0, its image broadcast once (index_broadcast_s); a "
                    "step scatters B's slices from rank 0, runs every rank's window range on "
                    "the HIP engine and gathers the rows into one device buffer on rank 0 in "
-                   "rank order (the reference's row order)"}
+                   "rank order (the reference's row order), sent as diagonal runs"}
     return rec, kt
 
 

@@ -162,6 +162,16 @@ int kmhg_query_tile_offsets(kmhg_query *q, uint64_t *d_out, int64_t *n_tiles, vo
 int kmhg_merge_part_rows(const void *d_rows, const uint64_t *d_seg_base,
                          const uint64_t *d_tile_off, int n_parts, int64_t n_tiles, int k,
                          int64_t w0, void *d_out, void *stream);
+/* The sharded query's row gather format (src/kmer_pos.c:110-136's rows, moved between ranks):
+ * n_rows (i, j) int32 rows in device memory as diagonal runs -- maximal stretches of rows
+ * (i, j), (i + 1, j + 1), ... -- each run 3 int32 {its first row's index, i, j}.
+ * kmhg_rows_runs counts the runs (*n_runs; it waits for `stream`) and writes them to d_runs when
+ * *n_runs <= cap_runs (else nothing: the caller sends rows); kmhg_runs_expand writes the n_rows
+ * rows back to d_rows on `stream`.  n_rows < 2^31. */
+int kmhg_rows_runs(const void *d_rows, int64_t n_rows, void *d_runs, int64_t cap_runs,
+                   int64_t *n_runs, void *stream);
+int kmhg_runs_expand(const void *d_runs, int64_t n_runs, int64_t n_rows, void *d_rows,
+                     void *stream);
 int kmhg_query_fill(kmhg_query *q, int32_t *rows);               /* host, 2 * n_rows int32 */
 int kmhg_query_rows_device(kmhg_query *q, const int32_t **d_rows); /* owned by q */
 /* Device-to-device copy of the 2 x n_rows int32 rows into caller memory on `stream`. */

@@ -3259,6 +3259,50 @@ int kmhg_merge_part_rows(const void* d_rows, const uint64_t* d_seg_base, const u
   });
 }
 
+int kmhg_rows_runs(const void* d_rows, int64_t n_rows, void* d_runs, int64_t cap_runs,
+                   int64_t* n_runs, void* stream) {
+  return guarded([&] {
+    if (n_rows < 0 || n_rows > INT32_MAX || !n_runs) fail(KMHG_EINVAL, "bad run arguments");
+    *n_runs = 0;
+    if (!n_rows) return;
+    if (!d_rows) fail(KMHG_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    ReleaseGroup rg(s);
+    const uint64_t nt = ((uint64_t)n_rows + TILE - 1) / TILE;
+    DBuf<uint64_t> tiles(nt + scan_u64_scratch(nt), s);
+    PinnedRec hrec = PinnedPool::get().take();
+    GiveBack give_back{hrec, s};
+    uint64_t* total = &hrec.meta->n_kmers;
+    const int2* rows = reinterpret_cast<const int2*>(d_rows);
+    LAUNCH("k_runs_count", s, launch_runs_count(rows, (uint64_t)n_rows, tiles.p, s));
+    LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tiles.p, nt, total, tiles.p + nt, s));
+    HIPC(hipStreamSynchronize(s));
+    const uint64_t n = __atomic_load_n(total, __ATOMIC_ACQUIRE);
+    *n_runs = (int64_t)n;
+    if (d_runs && (int64_t)n <= cap_runs)
+      LAUNCH("k_runs_emit", s, launch_runs_emit(rows, (uint64_t)n_rows, tiles.p,
+                                                static_cast<int32_t*>(d_runs), s));
+    HIPC(hipGetLastError());
+  });
+}
+
+int kmhg_runs_expand(const void* d_runs, int64_t n_runs, int64_t n_rows, void* d_rows,
+                     void* stream) {
+  return guarded([&] {
+    if (n_rows < 0 || n_rows > INT32_MAX || n_runs < 0 || n_runs > n_rows || (n_rows && !n_runs))
+      fail(KMHG_EINVAL, "bad run arguments");
+    if (!n_rows) return;
+    if (!d_runs || !d_rows) fail(KMHG_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    ReleaseGroup rg(s);
+    DBuf<uint32_t> cover(((uint64_t)n_rows + TILE - 1) / TILE, s);
+    LAUNCH("k_runs_expand", s,
+           launch_runs_expand(static_cast<const int32_t*>(d_runs), (uint64_t)n_runs,
+                              (uint64_t)n_rows, cover.p, static_cast<int2*>(d_rows), s));
+    HIPC(hipGetLastError());
+  });
+}
+
 int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
   return guarded([&] {
     if (!q) fail(KMHG_EINVAL, "null query");

@@ -112,6 +112,14 @@ void launch_merge_part_rows(const int2* rows, const uint64_t* seg_base, const ui
                             uint32_t n_parts, uint32_t nt, int kq, int64_t w0, int2* out,
                             hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t v, hipStream_t s);
+// diagonal runs of query rows (the sharded query's gather format, kmhg_rows_runs /
+// kmhg_runs_expand): run starts per TILE rows; the starts as {row, i, j} at the scanned tile
+// offsets; and back to rows (`cover`: one u32 per output tile, scratch)
+void launch_runs_count(const int2* rows, uint64_t n, uint64_t* tile_cnt, hipStream_t s);
+void launch_runs_emit(const int2* rows, uint64_t n, const uint64_t* tile_off, int32_t* runs,
+                      hipStream_t s);
+void launch_runs_expand(const int32_t* runs, uint64_t n_runs, uint64_t n, uint32_t* cover,
+                        int2* out, hipStream_t s);
 // exclusive u64 scan in place, *total <- sum: one workgroup up to SCAN1_MAX entries, else
 // reduce-then-scan with `scratch` = scan_u64_scratch(n) u64
 // (round 4: one workgroup up to 64 K / 256 K totals instead -- config 3 query 185 -> 162 Gbp/s,

@@ -1415,6 +1415,149 @@ void launch_fill_u64(uint64_t* p, uint64_t v, hipStream_t s) {
   hipLaunchKernelGGL(k_fill_u64, dim3(1), dim3(1), 0, s, p, v);
 }
 
+// ---------------------------------------------------------------- diagonal runs (row gather)
+// The sharded query's rows travel to the root as diagonal runs: a run is a maximal stretch of
+// consecutive rows (i, j), (i + 1, j + 1), ... -- a dot plot's diagonal -- sent as {its first
+// row's index in the rank's rows, i, j} (12 B) instead of 8 B per row.  Config 5 (B = A + 1 %
+// SNVs) has ~70 rows per run.  R_flag decides a row's start: row 0, or i / j not both one past
+// the previous row's.  Tiles of TILE rows, element e = j * BLOCK + t (lane-contiguous loads).
+__device__ __forceinline__ bool run_start(const int2* __restrict__ rows, uint64_t r) {
+  if (r == 0) return true;
+  const int2 v = rows[r], p = rows[r - 1];
+  return (uint32_t)v.x != (uint32_t)p.x + 1u || (uint32_t)v.y != (uint32_t)p.y + 1u;
+}
+
+// R_count: run starts per tile -> tile_cnt (scanned by launch_scan_u64 into tile offsets)
+__global__ void __launch_bounds__(BLOCK)
+k_runs_count(const int2* __restrict__ rows, uint64_t n, uint64_t* __restrict__ tile_cnt) {
+  __shared__ uint32_t wc[BLOCK / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const uint64_t r = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    c += (uint32_t)__popcll(__ballot(r < n && run_start(rows, r)));
+  }
+  if (lane_id() == 0) wc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) t += wc[w];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+// R_emit: every run start as {row index, i, j} at its tile's offset + its rank in the tile
+__global__ void __launch_bounds__(BLOCK)
+k_runs_emit(const int2* __restrict__ rows, uint64_t n, const uint64_t* __restrict__ tile_off,
+            int32_t* __restrict__ runs) {
+  __shared__ uint64_t cw[WPT * (BLOCK / 64) + 1];
+  const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+  bool st[WPT];
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const uint64_t r = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    st[j] = r < n && run_start(rows, r);
+  }
+  uint64_t rk[WPT];
+  tile_rank_at<WPT>(st, rk, cw, tile_off[blockIdx.x]);
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    if (st[j]) {
+      const uint64_t r = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+      const int2 v = rows[r];
+      int32_t* o = runs + 3 * rk[j];
+      o[0] = (int32_t)r;
+      o[1] = v.x;
+      o[2] = v.y;
+    }
+  }
+}
+
+// R_cover: for every output tile t, the run covering its first row t * TILE (the last run
+// starting at or before it): a binary search over the run starts, one thread per tile
+__global__ void __launch_bounds__(BLOCK)
+k_runs_cover(const int32_t* __restrict__ runs, uint64_t n_runs, uint32_t nt,
+             uint32_t* __restrict__ cover) {
+  const uint32_t t = blockIdx.x * BLOCK + threadIdx.x;
+  if (t >= nt) return;
+  const uint64_t row = (uint64_t)t * TILE;
+  uint64_t lo = 0, hi = n_runs;                 // runs[0] starts at row 0
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if ((uint64_t)(uint32_t)runs[3 * mid] <= row) lo = mid; else hi = mid;
+  }
+  cover[t] = (uint32_t)lo;
+}
+
+// R_expand: one workgroup per output tile [t0, t0 + TILE): the runs from the covering one on
+// (at most TILE + 1 reach into the tile) into LDS, a flag at every later run's first row, an
+// inclusive scan of the flags = each row's run (relative to the covering run), then every row
+// written as its run's {i, j} + its distance from the run's first row -- coalesced 8-B stores.
+__global__ void __launch_bounds__(BLOCK)
+k_runs_expand(const int32_t* __restrict__ runs, uint64_t n_runs, uint64_t n,
+              const uint32_t* __restrict__ cover, int2* __restrict__ out) {
+  __shared__ uint32_t rs[TILE + 1], ri[TILE + 1], rj[TILE + 1];
+  __shared__ uint16_t fl[TILE];
+  __shared__ uint64_t sh[8];
+  const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+  const uint64_t t1 = min(n, t0 + (uint64_t)TILE);
+  const uint64_t f = cover[blockIdx.x];
+  for (uint32_t x = threadIdx.x; x < TILE; x += BLOCK) fl[x] = 0;
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q <= TILE; q += BLOCK) {
+    const uint64_t g = f + q;
+    const uint64_t s0 = g < n_runs ? (uint64_t)(uint32_t)runs[3 * g] : n;
+    if (s0 < t1) {
+      rs[q] = (uint32_t)s0;
+      ri[q] = (uint32_t)runs[3 * g + 1];
+      rj[q] = (uint32_t)runs[3 * g + 2];
+      if (q > 0) fl[s0 - t0] = 1;             // q = 0 starts at or before t0
+    }
+  }
+  __syncthreads();
+  // inclusive scan of the flags: thread t owns rows [8 t, 8 t + 8) of the tile
+  uint32_t c[WPT], sum = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    sum += fl[threadIdx.x * WPT + j];
+    c[j] = sum;
+  }
+  uint64_t tot;
+  const uint32_t ex = (uint32_t)block_excl_scan((uint64_t)sum, sh, tot);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) fl[threadIdx.x * WPT + j] = (uint16_t)(ex + c[j]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const uint64_t r = t0 + (uint64_t)j * BLOCK + threadIdx.x;
+    if (r < t1) {
+      const uint32_t q = fl[r - t0];
+      const uint32_t d = (uint32_t)(r - rs[q]);
+      out[r] = make_int2((int32_t)(ri[q] + d), (int32_t)(rj[q] + d));
+    }
+  }
+}
+
+void launch_runs_count(const int2* rows, uint64_t n, uint64_t* tile_cnt, hipStream_t s) {
+  hipLaunchKernelGGL(k_runs_count, dim3((unsigned)((n + TILE - 1) / TILE)), dim3(BLOCK), 0, s,
+                     rows, n, tile_cnt);
+}
+void launch_runs_emit(const int2* rows, uint64_t n, const uint64_t* tile_off, int32_t* runs,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(k_runs_emit, dim3((unsigned)((n + TILE - 1) / TILE)), dim3(BLOCK), 0, s,
+                     rows, n, tile_off, runs);
+}
+void launch_runs_expand(const int32_t* runs, uint64_t n_runs, uint64_t n, uint32_t* cover,
+                        int2* out, hipStream_t s) {
+  const uint32_t nt = (uint32_t)((n + TILE - 1) / TILE);
+  hipLaunchKernelGGL(k_runs_cover, dim3((nt + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, runs,
+                     n_runs, nt, cover);
+  hipLaunchKernelGGL(k_runs_expand, dim3(nt), dim3(BLOCK), 0, s, runs, n_runs, n, cover, out);
+}
+
 void launch_scan_tiles_u64(uint64_t* a, uint32_t n, uint64_t* total, hipStream_t s) {
   if (n <= SCAN1_MAX)
     hipLaunchKernelGGL(k_scan_tiles_u64, dim3(1), dim3(1024), 0, s, a, n, total);

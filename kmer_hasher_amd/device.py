@@ -258,6 +258,46 @@ def merge_part_rows(rows: torch.Tensor, seg_base: list[int], tile_off: torch.Ten
     return out
 
 
+def rows_to_runs(rows: torch.Tensor, stream=None) -> torch.Tensor | None:
+    """kmhg_rows_runs: the (H, 2) int32 rows as diagonal runs, an (n_runs, 3) int32 tensor of
+    {first row index, i, j} -- or None when runs would not be smaller than the rows (12 B per
+    run against 8 B per row)."""
+    H = rows.shape[0]
+    if H == 0:
+        return None
+    dev = rows.device
+    rows = rows.contiguous()
+    n = C.c_int64()
+    cap = max(1, H // 16)                    # a dot plot's runs: tens of rows each
+    with torch.cuda.device(dev):
+        for _ in range(2):
+            runs = torch.empty((cap, 3), dtype=torch.int32, device=dev)
+            _lib.check(_lib.lib().kmhg_rows_runs(
+                C.c_void_p(rows.data_ptr()), H, C.c_void_p(runs.data_ptr()), cap, C.byref(n),
+                _stream_ptr(stream)))
+            if 3 * n.value >= 2 * H:
+                return None
+            if n.value <= cap:
+                return runs[:n.value]
+            cap = n.value
+    raise RuntimeError("kmhg_rows_runs: run count changed between calls")
+
+
+def runs_expand(runs: torch.Tensor, n_rows: int, out: torch.Tensor, stream=None) -> torch.Tensor:
+    """kmhg_runs_expand: (n_runs, 3) int32 runs back to their n_rows (i, j) rows in `out` (a
+    contiguous (n_rows, 2) int32 device tensor)."""
+    if n_rows == 0:
+        return out
+    if out.shape != (n_rows, 2) or out.dtype != torch.int32 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous (n_rows, 2) int32 tensor")
+    runs = runs.to(device=out.device, dtype=torch.int32).contiguous()
+    with torch.cuda.device(out.device):
+        _lib.check(_lib.lib().kmhg_runs_expand(
+            C.c_void_p(runs.data_ptr()), runs.shape[0], n_rows, C.c_void_p(out.data_ptr()),
+            _stream_ptr(stream)))
+    return out
+
+
 class DeviceQuery:
     def __init__(self, handle: int, n_rows: int, device: torch.device | None = None):
         self._h = C.c_void_p(handle)

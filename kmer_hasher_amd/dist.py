@@ -8,7 +8,8 @@
     broadcast; each rank runs the HIP query on its range -- validity at a range edge is decided
     from the same chars as on the full sequence, so no halo logic leaks into the result;
   * per-rank row counts are all-gathered (8 B each) and the rows are gathered to the root with
-    point-to-point send/recv (RCCL has no gatherv), or every rank copies its rows into one
+    point-to-point send/recv (RCCL has no gatherv) -- as diagonal runs, 12 B per run of rows
+    (i, j), (i + 1, j + 1), ..., expanded on the root -- or every rank copies its rows into one
     node-shared host matrix (HostRowSink); concatenation in rank order is exactly the
     reference's row order (window end ascending, then index position ascending).
 
@@ -53,15 +54,23 @@ def broadcast_buffers(meta: torch.Tensor | None, bufs: list[torch.Tensor] | None
     return m, bufs
 
 
-def gather_rows(local: torch.Tensor, dst: int = 0, group=None) -> torch.Tensor | None:
-    """Concatenate every rank's (h_r, 2) int32 rows on `dst` in rank order."""
+def gather_rows(local: torch.Tensor, dst: int = 0, group=None, codec=None) -> torch.Tensor | None:
+    """Concatenate every rank's (h_r, 2) int32 rows on `dst` in rank order.
+
+    codec: rows travel as diagonal runs where that is smaller ("Rows as diagonal
+    runs"): codec.encode(rows) -> an (n, 3) int32 runs tensor or None (send the rows), and
+    codec.decode(runs, h, out) on `dst` writes the h rows into `out`.  A dot plot's rows are
+    long diagonals (config 5: ~70 rows per 12-B run), so the link carries ~1/45 of the bytes."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = local.device
-    cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
-    counts = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(counts, cnt, group=group)
-    counts = [int(c.item()) for c in counts]
+    runs = codec.encode(local) if codec is not None and rank != dst and local.shape[0] else None
+    cnt = torch.tensor([local.shape[0], -1 if runs is None else runs.shape[0]], dtype=torch.int64,
+                       device=dev)
+    metas = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(metas, cnt, group=group)
+    counts = [int(m[0].item()) for m in metas]
+    n_runs = [int(m[1].item()) for m in metas]
     if rank == dst:
         if world == 1:
             return local                     # the rows are already where they belong
@@ -69,14 +78,18 @@ def gather_rows(local: torch.Tensor, dst: int = 0, group=None) -> torch.Tensor |
         offs = [0]
         for c in counts:
             offs.append(offs[-1] + c)
-        # the peers' rows arrive (the backend's stream) while the root copies its own part
-        works = p2p([("recv", out[offs[r]:offs[r + 1]], r) for r in range(world)
-                     if r != dst and counts[r]], group, wait=False)
+        # the peers' rows (or runs) arrive (the backend's stream) while the root copies its own
+        bufs = {r: torch.empty((n_runs[r], 3), dtype=torch.int32, device=dev)
+                for r in range(world) if r != dst and counts[r] and n_runs[r] >= 0}
+        works = p2p([("recv", bufs[r] if r in bufs else out[offs[r]:offs[r + 1]], r)
+                     for r in range(world) if r != dst and counts[r]], group, wait=False)
         out[offs[rank]:offs[rank + 1]] = local
         p2p_wait(works)
+        for r, b in bufs.items():
+            codec.decode(b, counts[r], out[offs[r]:offs[r + 1]])
         return out
     if counts[rank]:
-        p2p([("send", local.contiguous(), dst)], group)
+        p2p([("send", local.contiguous() if runs is None else runs, dst)], group)
     return None
 
 
@@ -291,8 +304,9 @@ def sharded_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, group=
     src=None: every rank already holds the whole query.  src=r: only rank r holds it (the R
     session's query string arrives on one process): c1="scatter" sends each rank the slice its
     windows read (scatter_sequence), c1="broadcast" the whole sequence (broadcast_sequence).
-    sink=None: rows gathered into one device buffer on `dst` (gather_rows, over xGMI); a
-    HostRowSink: every rank copies its rows into the shared host matrix (deliver_rows_host).
+    sink=None: rows gathered into one device buffer on `dst` (gather_rows, over xGMI; as
+    diagonal runs when the engine has a `codec`); a HostRowSink: every rank copies its rows into
+    the shared host matrix (deliver_rows_host).
     `seq_buf`: scatter receive buffer to reuse.  `timings` (optional) receives the seconds of
     each phase as seen by this rank: 'broadcast' (C1), 'query' (the HIP range query) and
     'gather'."""
@@ -319,7 +333,8 @@ def sharded_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, group=
     w0, w1 = shard_ranges(n_windows, world)[rank]
     local = engine.query_range(seq, k, w0, w1)
     t2 = mark()
-    rows = gather_rows(local, dst, group) if sink is None else deliver_rows_host(local, sink, group)
+    rows = gather_rows(local, dst, group, getattr(engine, "codec", None)) if sink is None \
+        else deliver_rows_host(local, sink, group)
     t3 = mark()
     if timings is not None:
         for name, dt in (("broadcast", t1 - t0), ("query", t2 - t1), ("gather", t3 - t2)):
@@ -430,8 +445,25 @@ def assemble_parts(part, device: torch.device, group=None, import_fn=None):
     return (import_fn or DeviceIndex.import_image)(meta, [table, positions, codes])
 
 
+class HipRunCodec:
+    """gather_rows' run codec on the GPU: kmhg_rows_runs / kmhg_runs_expand."""
+
+    @staticmethod
+    def encode(rows: torch.Tensor):
+        from .device import rows_to_runs
+        return rows_to_runs(rows)
+
+    @staticmethod
+    def decode(runs: torch.Tensor, n_rows: int, out: torch.Tensor):
+        from .device import runs_expand
+        runs_expand(runs, n_rows, out)
+
+
 class HipQueryEngine:
-    """Adapter: a DeviceIndex (libkmhgpu) as a sharded-query engine."""
+    """Adapter: a DeviceIndex (libkmhgpu) as a sharded-query engine; its rows travel to the
+    root as diagonal runs (HipRunCodec)."""
+
+    codec = HipRunCodec()
 
     def __init__(self, index):
         self.index = index

@@ -36,11 +36,14 @@ class OracleEngine:
         return torch.from_numpy(np.ascontiguousarray(rows[keep]))
 
 
-def _worker(rank, world, port, seq_bytes, k_index, kq, out_q):
+def _worker(rank, world, port, seq_bytes, k_index, kq, out_q, codec=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         eng = OracleEngine(seq_bytes, k_index)
+        if codec:                      # rows to the root as diagonal runs (dist.gather_rows)
+            import runs_ref
+            eng.codec = runs_ref.NumpyRunCodec()
         seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy())
         # image broadcast path (generic buffer broadcast) round-trips bytes exactly
         meta = torch.tensor([0] * 8 + [7, 3, 5, 11, 13], dtype=torch.int64) if rank == 0 else None
@@ -57,8 +60,10 @@ def _worker(rank, world, port, seq_bytes, k_index, kq, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k_index,kq", [(2, 15, 15), (2, 16, 12), (3, 31, 31)])
-def test_sharded_query_matches_unsharded(world, k_index, kq):
+@pytest.mark.parametrize("world,k_index,kq,codec", [(2, 15, 15, False), (2, 16, 12, False),
+                                                    (3, 31, 31, False), (2, 15, 15, True),
+                                                    (3, 31, 31, True)])
+def test_sharded_query_matches_unsharded(world, k_index, kq, codec):
     from oracle import oracle as O
     s = synth.add_n_runs(synth.repeat_rich(60_000, 5, n_gap_every=7_001), 0.01, 9)
     s[-k_index - 3] = ord("N")        # an end-drop case near the last shard's edge
@@ -67,7 +72,7 @@ def test_sharded_query_matches_unsharded(world, k_index, kq):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, seq_bytes, k_index, kq, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, seq_bytes, k_index, kq, q, codec))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -138,6 +143,70 @@ def test_sharded_query_scatter_and_host_rows(world, c1, host):
         assert p.exitcode == 0
     assert got[0] == want and got[1] == want
     assert not [f for f in set(os.listdir("/dev/shm")) - before if f.startswith("kmhg_rows")]
+
+
+def _run_cases():
+    rng = np.random.default_rng(5)
+    diag = np.stack([np.arange(100, 5100), np.arange(7, 5007)], 1)       # one long diagonal
+    cut = diag.copy()
+    cut[1000:] += [0, 3]                                                 # a shifted diagonal
+    rep = np.repeat(np.arange(50, 90), 3)                                # 3 hits per window
+    reps = np.stack([rep, np.tile([5, 900, 77_000], 40)], 1)
+    rnd = np.sort(rng.integers(1, 1 << 30, (3000, 2)), 0)
+    big = np.stack([np.arange(1 << 20), np.arange(1 << 20)], 1) + [31, 1]
+    big[::4097] += [0, 11]
+    return {"empty": np.zeros((0, 2)), "one": np.array([[40, 9]]), "diag": diag, "cut": cut,
+            "repeats": reps, "random": rnd, "tiles": big,
+            "wrap": np.array([[2**31 - 2, 5], [2**31 - 1, 6], [-2**31, 7]])}
+
+
+def test_run_codec_reference():
+    """The numpy run reference round-trips every shape of row set: one long diagonal, a shifted
+    one, multi-hit windows (runs of one row), sorted random rows, runs across 2048-row tiles, i
+    at the int32 edge."""
+    import runs_ref
+    for name, rows in _run_cases().items():
+        r = np.asarray(rows, np.int64).astype(np.uint32).view(np.int32).reshape(-1, 2)
+        runs = runs_ref.encode(r)
+        assert np.array_equal(runs_ref.decode(runs, r.shape[0]), r), name
+    assert runs_ref.encode(_run_cases()["diag"]).shape == (1, 3)
+    assert runs_ref.encode(_run_cases()["cut"]).shape == (2, 3)
+
+
+def _codec_gather_worker(rank, world, port, out_q):
+    """gather_rows with the run codec: every rank's rows of another shape (a diagonal, repeats
+    that do not compress, nothing), concatenated on rank 0 in rank order."""
+    import runs_ref
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cases = _run_cases()
+        mine = [cases["diag"], cases["repeats"], cases["empty"], cases["cut"]][rank]
+        local = torch.from_numpy(np.ascontiguousarray(mine, np.int32).reshape(-1, 2))
+        out = kd.gather_rows(local, 0, None, runs_ref.NumpyRunCodec())
+        if rank == 0:
+            out_q.put(out.numpy().tolist())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_gather_rows_with_run_codec(world):
+    cases = _run_cases()
+    parts = [cases["diag"], cases["repeats"], cases["empty"], cases["cut"]][:world]
+    want = np.concatenate([np.asarray(p, np.int32).reshape(-1, 2) for p in parts]).tolist()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_codec_gather_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert got == want
 
 
 def test_slice_bounds_cover_window_rule():

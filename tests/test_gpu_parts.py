@@ -145,3 +145,34 @@ def test_merge_part_rows_interleaves_by_window(gpu):
     tile_off = torch.from_numpy(np.stack(offs).astype(np.int64)).cuda()
     out = merge_part_rows(allrows, base[:3], tile_off, k).cpu().numpy()
     assert out.tolist() == [list(r) for r in want]
+
+
+def test_rows_runs_round_trip_vs_reference(gpu):
+    """kmhg_rows_runs / kmhg_runs_expand (the sharded query's gather format) against the numpy
+    reference, run for run: one long diagonal, a shifted one, multi-hit windows (which do not
+    compress: None), sorted random rows, runs across 2048-row tiles, i at the int32 edge, and
+    the rows of a real related-sequence query."""
+    import torch
+    import runs_ref
+    from test_dist_cpu import _run_cases
+    from kmer_hasher_amd import synth
+    from kmer_hasher_amd.device import DeviceIndex, rows_to_runs, runs_expand
+    cases = _run_cases()
+    a = synth.iid(300_000, 3)
+    b = synth.derived(a, 4, 0.01, 3)
+    idx = DeviceIndex.build(torch.from_numpy(a).cuda(), 21)
+    cases["query"] = idx.query(torch.from_numpy(b).cuda(), 21).rows().cpu().numpy()
+    idx.free()
+    for name, rows in cases.items():
+        r = np.asarray(rows, np.int64).astype(np.uint32).view(np.int32).reshape(-1, 2)
+        want = runs_ref.encode(r)
+        got = rows_to_runs(torch.from_numpy(np.ascontiguousarray(r)).cuda())
+        if 3 * want.shape[0] >= 2 * r.shape[0]:
+            assert got is None, name           # runs would not be smaller: the rows travel
+            got = torch.from_numpy(want).cuda()
+        else:
+            assert got is not None and np.array_equal(got.cpu().numpy(), want), name
+        out = torch.full((r.shape[0], 2), -7, dtype=torch.int32, device="cuda")
+        runs_expand(got, r.shape[0], out)
+        assert np.array_equal(out.cpu().numpy(), r), name
+    assert cases["query"].shape[0] > 100_000
