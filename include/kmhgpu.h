@@ -162,6 +162,16 @@ int kmhg_query_tile_offsets(kmhg_query *q, uint64_t *d_out, int64_t *n_tiles, vo
 int kmhg_merge_part_rows(const void *d_rows, const uint64_t *d_seg_base,
                          const uint64_t *d_tile_off, int n_parts, int64_t n_tiles, int k,
                          int64_t w0, void *d_out, void *stream);
+/* A device sequence as it crosses xGMI (C1 scatter / broadcast of the multi-GPU query and of
+ * the owner-computes build): what the reference reads of a char -- its 2-bit code (c >> 1) & 3
+ * and its N test, src/kmer_pos.c:81-83 -- as 16 chars per u32 code word and u16 N-flag word
+ * (ceil(L / 16) of each; 6 B per 16 chars).  kmhg_seq_unpack writes chars [a, b) back ("ACTG"
+ * by code, or 'N', which every entry point reads as the original) from the words held at
+ * d_code / d_nbit starting with word `word0` (<= a / 16), on `stream`. */
+int kmhg_seq_pack(const void *d_seq, int64_t L, uint32_t *d_code, uint16_t *d_nbit,
+                  void *stream);
+int kmhg_seq_unpack(const uint32_t *d_code, const uint16_t *d_nbit, int64_t word0, int64_t a,
+                    int64_t b, void *d_seq, void *stream);
 /* The sharded query's row gather format (src/kmer_pos.c:110-136's rows, moved between ranks):
  * n_rows (i, j) int32 rows in device memory as diagonal runs -- maximal stretches of rows
  * (i, j), (i + 1, j + 1), ... -- each run 3 int32 {its first row's index, i, j}.

@@ -3259,6 +3259,32 @@ int kmhg_merge_part_rows(const void* d_rows, const uint64_t* d_seg_base, const u
   });
 }
 
+int kmhg_seq_pack(const void* d_seq, int64_t L, uint32_t* d_code, uint16_t* d_nbit,
+                  void* stream) {
+  return guarded([&] {
+    if (L < 0) fail(KMHG_EINVAL, "bad sequence length");
+    if (!L) return;
+    if (!d_seq || !d_code || !d_nbit) fail(KMHG_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    LAUNCH("k_seq_pack", s, launch_seq_pack(static_cast<const uint8_t*>(d_seq), L, d_code,
+                                            d_nbit, s));
+    HIPC(hipGetLastError());
+  });
+}
+
+int kmhg_seq_unpack(const uint32_t* d_code, const uint16_t* d_nbit, int64_t word0, int64_t a,
+                    int64_t b, void* d_seq, void* stream) {
+  return guarded([&] {
+    if (a < 0 || b < a || word0 < 0 || word0 > a / 16) fail(KMHG_EINVAL, "bad unpack range");
+    if (b == a) return;
+    if (!d_code || !d_nbit || !d_seq) fail(KMHG_EINVAL, "null argument");
+    hipStream_t s = (hipStream_t)stream;
+    LAUNCH("k_seq_unpack", s, launch_seq_unpack(d_code, d_nbit, (uint64_t)word0, a, b,
+                                                static_cast<uint8_t*>(d_seq), s));
+    HIPC(hipGetLastError());
+  });
+}
+
 int kmhg_rows_runs(const void* d_rows, int64_t n_rows, void* d_runs, int64_t cap_runs,
                    int64_t* n_runs, void* stream) {
   return guarded([&] {

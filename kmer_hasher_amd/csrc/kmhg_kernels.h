@@ -112,6 +112,12 @@ void launch_merge_part_rows(const int2* rows, const uint64_t* seg_base, const ui
                             uint32_t n_parts, uint32_t nt, int kq, int64_t w0, int2* out,
                             hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t v, hipStream_t s);
+// a sequence as 2-bit codes + N flags, 16 chars per u32 / u16 word (kmhg_seq_pack /
+// kmhg_seq_unpack: C1 transfers); unpack writes chars [a, b) from the words held from w0 on
+void launch_seq_pack(const uint8_t* seq, int64_t L, uint32_t* code, uint16_t* nbit,
+                     hipStream_t s);
+void launch_seq_unpack(const uint32_t* code, const uint16_t* nbit, uint64_t w0, int64_t a,
+                       int64_t b, uint8_t* seq, hipStream_t s);
 // diagonal runs of query rows (the sharded query's gather format, kmhg_rows_runs /
 // kmhg_runs_expand): run starts per TILE rows; the starts as {row, i, j} at the scanned tile
 // offsets; and back to rows (`cover`: one u32 per output tile, scratch)

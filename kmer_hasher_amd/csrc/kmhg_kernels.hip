@@ -1541,6 +1541,78 @@ k_runs_expand(const int32_t* __restrict__ runs, uint64_t n_runs, uint64_t n,
   }
 }
 
+// ---------------------------------------------------------------- packed sequence (C1 transfers)
+// A sequence crosses xGMI (C1 scatter / broadcast, the owner-computes build's broadcast) as the
+// two things every kernel reads from a char -- its 2-bit code (c >> 1) & 3 and its N flag
+// ((c | 0x20) == 'n') -- 16 chars per u32 code word and u16 flag word, MSB first: 6 B per 16
+// chars instead of 16.  Unpacked, a char is "ACTG"[code] or 'N', which every kernel reads as the
+// original (lower case, IUPAC letters and the like map to the code they already had).
+__global__ void __launch_bounds__(BLOCK)
+k_seq_pack(const uint8_t* __restrict__ seq, int64_t L, uint32_t* __restrict__ code,
+           uint16_t* __restrict__ nbit, uint64_t words) {
+  const uint64_t w = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (w >= words) return;
+  const int64_t c0 = (int64_t)w * 16;
+  uint8_t ch[16];
+  if (c0 + 16 <= L && (reinterpret_cast<uintptr_t>(seq + c0) & 15) == 0) {
+    const uint4 v = *reinterpret_cast<const uint4*>(seq + c0);
+    const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ch[q] = (uint8_t)(x[q >> 2] >> (8 * (q & 3)));
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ch[q] = c0 + q < L ? seq[c0 + q] : (uint8_t)'A';
+  }
+  uint32_t cw = 0, nw = 0;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    cw |= (uint32_t)((ch[q] >> 1) & 3u) << (30 - 2 * q);
+    nw |= (uint32_t)((ch[q] | 0x20) == 'n') << (15 - q);
+  }
+  code[w] = cw;
+  nbit[w] = (uint16_t)nw;
+}
+
+// chars [a, b) of seq from the words [w0, ...) held at code / nbit (word w at index w - w0)
+__global__ void __launch_bounds__(BLOCK)
+k_seq_unpack(const uint32_t* __restrict__ code, const uint16_t* __restrict__ nbit, uint64_t w0,
+             int64_t a, int64_t b, uint8_t* __restrict__ seq) {
+  const uint64_t w = (uint64_t)(a >> 4) + (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int64_t c0 = (int64_t)w * 16;
+  if (c0 >= b) return;
+  const uint32_t cw = code[w - w0], nw = nbit[w - w0];
+  uint8_t ch[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const uint32_t c = (cw >> (30 - 2 * q)) & 3u;
+    ch[q] = ((nw >> (15 - q)) & 1u) ? (uint8_t)'N'
+                                     : (uint8_t)(c == 0 ? 'A' : c == 1 ? 'C' : c == 2 ? 'T' : 'G');
+  }
+  if (c0 >= a && c0 + 16 <= b && (reinterpret_cast<uintptr_t>(seq + c0) & 15) == 0) {
+    uint32_t x[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) x[q >> 2] |= (uint32_t)ch[q] << (8 * (q & 3));
+    *reinterpret_cast<uint4*>(seq + c0) = make_uint4(x[0], x[1], x[2], x[3]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (c0 + q >= a && c0 + q < b) seq[c0 + q] = ch[q];
+  }
+}
+
+void launch_seq_pack(const uint8_t* seq, int64_t L, uint32_t* code, uint16_t* nbit,
+                     hipStream_t s) {
+  const uint64_t words = ((uint64_t)L + 15) / 16;
+  hipLaunchKernelGGL(k_seq_pack, dim3((unsigned)((words + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s,
+                     seq, L, code, nbit, words);
+}
+void launch_seq_unpack(const uint32_t* code, const uint16_t* nbit, uint64_t w0, int64_t a,
+                       int64_t b, uint8_t* seq, hipStream_t s) {
+  const uint64_t words = (uint64_t)((b + 15) >> 4) - (uint64_t)(a >> 4);
+  hipLaunchKernelGGL(k_seq_unpack, dim3((unsigned)((words + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                     s, code, nbit, w0, a, b, seq);
+}
+
 void launch_runs_count(const int2* rows, uint64_t n, uint64_t* tile_cnt, hipStream_t s) {
   hipLaunchKernelGGL(k_runs_count, dim3((unsigned)((n + TILE - 1) / TILE)), dim3(BLOCK), 0, s,
                      rows, n, tile_cnt);

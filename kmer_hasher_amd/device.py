@@ -258,6 +258,36 @@ def merge_part_rows(rows: torch.Tensor, seg_base: list[int], tile_off: torch.Ten
     return out
 
 
+def seq_pack(seq: torch.Tensor, stream=None) -> tuple[torch.Tensor, torch.Tensor]:
+    """kmhg_seq_pack: a uint8 device sequence as (code u32 words, N-flag u16 words), 16 chars
+    each -- what crosses xGMI in place of the chars (6 B per 16)."""
+    _check_seq(seq)
+    words = (seq.numel() + 15) // 16
+    code = torch.empty(max(1, words), dtype=torch.int32, device=seq.device)
+    nbit = torch.empty(max(1, words), dtype=torch.int16, device=seq.device)
+    with torch.cuda.device(seq.device):
+        _lib.check(_lib.lib().kmhg_seq_pack(
+            C.c_void_p(seq.data_ptr()), seq.numel(), C.c_void_p(code.data_ptr()),
+            C.c_void_p(nbit.data_ptr()), _stream_ptr(stream)))
+    return code[:words], nbit[:words]
+
+
+def seq_unpack(code: torch.Tensor, nbit: torch.Tensor, word0: int, a: int, b: int,
+               out: torch.Tensor, stream=None) -> torch.Tensor:
+    """kmhg_seq_unpack: chars [a, b) of `out` (uint8, device) from words held from word0 on."""
+    if b <= a:
+        return out
+    if out.numel() < b or out.dtype != torch.uint8 or not out.is_cuda:
+        raise ValueError("out must be a uint8 CUDA tensor of at least b chars")
+    if code.numel() < (b + 15) // 16 - word0 or nbit.numel() < (b + 15) // 16 - word0:
+        raise ValueError("the packed words do not cover [a, b)")
+    with torch.cuda.device(out.device):
+        _lib.check(_lib.lib().kmhg_seq_unpack(
+            C.c_void_p(code.data_ptr()), C.c_void_p(nbit.data_ptr()), word0, a, b,
+            C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+    return out
+
+
 def rows_to_runs(rows: torch.Tensor, stream=None) -> torch.Tensor | None:
     """kmhg_rows_runs: the (H, 2) int32 rows as diagonal runs, an (n_runs, 3) int32 tensor of
     {first row index, i, j} -- or None when runs would not be smaller than the rows (12 B per

@@ -126,16 +126,34 @@ def p2p_wait(works) -> None:
 
 
 def broadcast_sequence(seq: torch.Tensor | None, src: int, device: torch.device,
-                       group=None) -> torch.Tensor:
+                       group=None, codec=None) -> torch.Tensor:
     """C1: the root's uint8 sequence on every rank (its length first, then one
-    broadcast of the bytes; over RCCL the root fans out on its xGMI links)."""
+    broadcast of the bytes; over RCCL the root fans out on its xGMI links).  codec: the bytes
+    travel packed (codec.pack -> (code words, N-flag words), 6 B per 16 chars; HipSeqCodec) and
+    are unpacked on arrival."""
     rank = dist.get_rank(group)
     n = torch.zeros(1, dtype=torch.int64, device=device)
     if rank == src:
         n[0] = seq.numel()
     dist.broadcast(n, src, group=group)
-    out = seq if rank == src else torch.empty(int(n.item()), dtype=torch.uint8, device=device)
-    dist.broadcast(out, src, group=group)
+    L = int(n.item())
+    if codec is None or L == 0 or dist.get_world_size(group) == 1:
+        out = seq if rank == src else torch.empty(L, dtype=torch.uint8, device=device)
+        if L:
+            dist.broadcast(out, src, group=group)
+        return out
+    words = (L + 15) // 16
+    if rank == src:
+        code, nbit = codec.pack(seq)
+    else:
+        code = torch.empty(words, dtype=torch.int32, device=device)
+        nbit = torch.empty(words, dtype=torch.int16, device=device)
+    dist.broadcast(code, src, group=group)
+    dist.broadcast(nbit.view(torch.uint8), src, group=group)   # (gloo broadcasts no int16)
+    if rank == src:
+        return seq
+    out = torch.empty(L, dtype=torch.uint8, device=device)
+    codec.unpack(code, nbit, 0, 0, L, out)
     return out
 
 
@@ -151,13 +169,14 @@ def slice_bounds(n_chars: int, k: int, w0: int, w1: int) -> tuple[int, int]:
 
 
 def scatter_sequence(seq: torch.Tensor | None, k: int, src: int, device: torch.device,
-                     group=None, out: torch.Tensor | None = None) -> torch.Tensor:
+                     group=None, out: torch.Tensor | None = None, codec=None) -> torch.Tensor:
     """C1 as a scatter: rank `src` holds the query; every other rank receives only the chars its
     window range reads (slice_bounds), in place in a full-length buffer, so the range query
     addresses the sequence by its absolute positions.  (N - 1)/N of L leaves the root, one slice
     per link, instead of the whole L on every link (broadcast_sequence).  `out`: a buffer of at
     least L + 16 bytes to reuse across calls.  Chars outside the slice are undefined (on CPU
-    they read 'A': the gloo tests' oracle engine reads the whole buffer)."""
+    they read 'A': the gloo tests' oracle engine reads the whole buffer).  codec: the slices
+    travel packed (the code and N-flag words covering them), unpacked into `out` on arrival."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n = torch.zeros(1, dtype=torch.int64, device=device)
@@ -168,10 +187,15 @@ def scatter_sequence(seq: torch.Tensor | None, k: int, src: int, device: torch.d
     ranges = shard_ranges(max(0, L - k + 1), world)
     if rank == src:
         ops = []
+        packed = codec.pack(seq) if codec is not None and L and world > 1 else None
         for r in range(world):
             a, b = slice_bounds(L, k, *ranges[r])
             if r != src and b > a:
-                ops.append(("send", seq[a:b], r))
+                if packed is None:
+                    ops.append(("send", seq[a:b], r))
+                else:
+                    wa, wb = a // 16, (b + 15) // 16
+                    ops += [("send", packed[0][wa:wb], r), ("send", packed[1][wa:wb], r)]
         p2p(ops, group)
         return seq
     if out is None or out.numel() < L + 16 or out.device != device:
@@ -180,7 +204,14 @@ def scatter_sequence(seq: torch.Tensor | None, k: int, src: int, device: torch.d
             out.fill_(ord("A"))
     a, b = slice_bounds(L, k, *ranges[rank])
     if b > a:
-        p2p([("recv", out[a:b], src)], group)
+        if codec is None:
+            p2p([("recv", out[a:b], src)], group)
+        else:
+            wa, wb = a // 16, (b + 15) // 16
+            code = torch.empty(wb - wa, dtype=torch.int32, device=device)
+            nbit = torch.empty(wb - wa, dtype=torch.int16, device=device)
+            p2p([("recv", code, src), ("recv", nbit, src)], group)
+            codec.unpack(code, nbit, wa, a, b, out)
     return out[:L]
 
 
@@ -323,11 +354,12 @@ def sharded_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, group=
         return time.perf_counter()
 
     t0 = mark()
+    sc = getattr(engine, "seq_codec", None)
     if src is not None:
         if c1 == "scatter":
-            seq = scatter_sequence(seq, k, src, dev, group, out=seq_buf)
+            seq = scatter_sequence(seq, k, src, dev, group, out=seq_buf, codec=sc)
         else:
-            seq = broadcast_sequence(seq, src, dev, group)
+            seq = broadcast_sequence(seq, src, dev, group, sc)
     t1 = mark()
     n_windows = max(0, seq.numel() - k + 1)
     w0, w1 = shard_ranges(n_windows, world)[rank]
@@ -363,17 +395,20 @@ def part_layout(infos: list[dict]) -> dict:
 
 
 def owner_build(seq: torch.Tensor | None, k: int, device: torch.device, src: int | None = 0,
-                group=None, stream=None):
+                group=None, stream=None, codec="auto"):
     """make.kmer.hash over G ranks, owner-computes (the reference's reader pool
     gives each thread the k-mers it owns, src/kmer_reader.c:28-39): the sequence is broadcast
-    from `src` (C1; src=None: every rank holds it already), every rank walks all windows and
-    builds only the k-mers of its bucket range (kmhg_build_device_part).  Returns this rank's
-    DevicePart; assemble_parts() makes the whole index on every rank."""
+    from `src` (C1; src=None: every rank holds it already; packed by HipSeqCodec on a GPU),
+    every rank walks all windows and builds only the k-mers of its bucket range
+    (kmhg_build_device_part).  Returns this rank's DevicePart and the sequence it built from;
+    assemble_parts() makes the whole index on every rank."""
     from .device import DeviceIndex
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    if codec == "auto":
+        codec = HipSeqCodec() if device.type == "cuda" else None
     if src is not None:
-        seq = broadcast_sequence(seq, src, device, group)
+        seq = broadcast_sequence(seq, src, device, group, codec)
     return DeviceIndex.build_part(seq, k, rank, world, stream), seq
 
 
@@ -445,6 +480,22 @@ def assemble_parts(part, device: torch.device, group=None, import_fn=None):
     return (import_fn or DeviceIndex.import_image)(meta, [table, positions, codes])
 
 
+class HipSeqCodec:
+    """C1's sequence codec on the GPU: kmhg_seq_pack / kmhg_seq_unpack (2-bit codes + N flags,
+    6 B per 16 chars on the wire)."""
+
+    @staticmethod
+    def pack(seq: torch.Tensor):
+        from .device import seq_pack
+        return seq_pack(seq)
+
+    @staticmethod
+    def unpack(code: torch.Tensor, nbit: torch.Tensor, word0: int, a: int, b: int,
+               out: torch.Tensor):
+        from .device import seq_unpack
+        seq_unpack(code, nbit, word0, a, b, out)
+
+
 class HipRunCodec:
     """gather_rows' run codec on the GPU: kmhg_rows_runs / kmhg_runs_expand."""
 
@@ -464,6 +515,7 @@ class HipQueryEngine:
     root as diagonal runs (HipRunCodec)."""
 
     codec = HipRunCodec()
+    seq_codec = HipSeqCodec()
 
     def __init__(self, index):
         self.index = index
@@ -491,6 +543,8 @@ def broadcast_index(index, device: torch.device, src: int = 0, group=None):
 # ------------------------------------------------------- owner-routed query over resident parts
 class HipPartEngine:
     """Adapter: this rank's DevicePart (libkmhgpu) as an owner-routed query engine."""
+
+    seq_codec = HipSeqCodec()
 
     def __init__(self, part):
         self.part = part
@@ -530,7 +584,7 @@ def owner_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, src: int
 
     t0 = mark()
     if src is not None:
-        seq = broadcast_sequence(seq, src, dev, group)
+        seq = broadcast_sequence(seq, src, dev, group, getattr(engine, "seq_codec", None))
     t1 = mark()
     local, toff = engine.query_part(seq, k)
     t2 = mark()

@@ -1,6 +1,10 @@
-"""Reference (numpy) of the row gather's diagonal-run format, for the tests: a run is a maximal
-stretch of consecutive rows (i, j), (i + 1, j + 1), ...; it travels as {its first row's index,
-i, j} (kmhg_rows_runs / kmhg_runs_expand, kmhg_kernels.hip R_count / R_emit / R_expand)."""
+"""Reference (numpy) of the multi-GPU wire formats, for the tests.
+
+Rows: a run is a maximal stretch of consecutive rows (i, j), (i + 1, j + 1), ...; it travels as
+{its first row's index, i, j} (kmhg_rows_runs / kmhg_runs_expand, kmhg_kernels.hip R_count /
+R_emit / R_expand).  Sequences: 16 chars per u32 word of 2-bit codes (c >> 1) & 3 and u16 word
+of N flags ((c | 0x20) == 'n'), MSB first; unpacked as "ACTG"[code] or 'N' (kmhg_seq_pack /
+kmhg_seq_unpack)."""
 import numpy as np
 import torch
 
@@ -40,3 +44,50 @@ class NumpyRunCodec:
     @staticmethod
     def decode(runs: torch.Tensor, n_rows: int, out: torch.Tensor):
         out.copy_(torch.from_numpy(decode(runs.numpy(), n_rows)))
+
+
+def seq_pack(seq: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """uint8 chars -> (int32 code words, int16 N-flag words), 16 chars each, MSB first; the
+    tail padded with 'A'."""
+    c = np.asarray(seq, np.uint8)
+    L = c.size
+    words = (L + 15) // 16
+    pad = np.full(words * 16, ord("A"), np.uint8)
+    pad[:L] = c
+    codes = ((pad >> 1) & 3).astype(np.uint64).reshape(-1, 16)
+    isn = ((pad | 0x20) == ord("n")).astype(np.uint64).reshape(-1, 16)
+    sh2 = np.uint64(30) - np.arange(16, dtype=np.uint64) * np.uint64(2)
+    sh1 = np.uint64(15) - np.arange(16, dtype=np.uint64)
+    code = (codes << sh2).sum(1).astype(np.uint32).view(np.int32)
+    nbit = (isn << sh1).sum(1).astype(np.uint16).view(np.int16)
+    return code, nbit
+
+
+def seq_unpack(code: np.ndarray, nbit: np.ndarray, word0: int, a: int, b: int,
+               out: np.ndarray) -> np.ndarray:
+    """chars [a, b) of `out` from the words held from word0 on."""
+    if b <= a:
+        return out
+    lut = np.frombuffer(b"ACTG", np.uint8)
+    pos = np.arange(a, b)
+    w = pos // 16 - word0
+    q = (pos % 16).astype(np.uint32)
+    cw = np.asarray(code).view(np.uint32)[w]
+    nw = np.asarray(nbit).view(np.uint16)[w].astype(np.uint32)
+    ch = lut[(cw >> (np.uint32(30) - 2 * q)) & 3]
+    out[a:b] = np.where((nw >> (np.uint32(15) - q)) & 1, np.uint8(ord("N")), ch)
+    return out
+
+
+class NumpySeqCodec:
+    """dist's sequence codec over CPU tensors (the gloo tests' stand-in for dist.HipSeqCodec)."""
+
+    @staticmethod
+    def pack(seq: torch.Tensor):
+        code, nbit = seq_pack(seq.numpy())
+        return torch.from_numpy(code), torch.from_numpy(nbit)
+
+    @staticmethod
+    def unpack(code: torch.Tensor, nbit: torch.Tensor, word0: int, a: int, b: int,
+               out: torch.Tensor):
+        seq_unpack(code.numpy(), nbit.numpy(), word0, a, b, out.numpy())

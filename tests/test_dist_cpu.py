@@ -84,15 +84,20 @@ def test_sharded_query_matches_unsharded(world, k_index, kq, codec):
     assert got == want
 
 
-def _c1_worker(rank, world, port, seq_bytes, k_index, kq, c1, host, out_q):
+def _c1_worker(rank, world, port, seq_bytes, k_index, kq, c1, host, out_q, codecs=False):
     """The R session's query on rank 0 only: C1 by scatter (each rank receives the slice its
     windows read) or broadcast, rows gathered on rank 0's device or delivered by every rank into
-    the shared host matrix; twice through one sink / one receive buffer (reuse)."""
+    the shared host matrix; twice through one sink / one receive buffer (reuse).  codecs: the
+    sequence travels packed and the rows as diagonal runs (the numpy wire-format references)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sink = kd.HostRowSink(0) if host else None
     try:
         eng = OracleEngine(seq_bytes, k_index)
+        if codecs:
+            import runs_ref
+            eng.codec = runs_ref.NumpyRunCodec()
+            eng.seq_codec = runs_ref.NumpySeqCodec()
         seq = torch.from_numpy(np.frombuffer(seq_bytes, np.uint8).copy()) if rank == 0 else None
         buf = torch.full((len(seq_bytes) + 16,), ord("A"), dtype=torch.uint8) if rank else None
         got = []
@@ -113,15 +118,20 @@ def _c1_worker(rank, world, port, seq_bytes, k_index, kq, c1, host, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,c1,host", [(2, "scatter", False), (2, "scatter", True),
-                                           (3, "scatter", True), (3, "broadcast", True)])
-def test_sharded_query_scatter_and_host_rows(world, c1, host):
+@pytest.mark.parametrize("world,c1,host,codecs", [
+    (2, "scatter", False, False), (2, "scatter", True, False), (3, "scatter", True, False),
+    (3, "broadcast", True, False), (2, "scatter", False, True), (3, "scatter", False, True),
+    (3, "broadcast", False, True)])
+def test_sharded_query_scatter_and_host_rows(world, c1, host, codecs):
     """C1 as a scatter of slices and rows delivered into one shared host matrix reproduce the
     unsharded reference rows exactly, including an N right at a shard edge and the end-drop
-    rule; the shared-memory segment is gone afterwards."""
+    rule; the shared-memory segment is gone afterwards.  With the wire codecs
+    (packed sequence, rows as runs) on a sequence with lower case and IUPAC letters."""
     from oracle import oracle as O
     k = 21
     s = synth.add_n_runs(synth.iid(40_000, 77), 0.01, 9)
+    if codecs:
+        s = synth.add_ambiguity(synth.add_lowercase(s, 0.1, 3), 0.01, 4)
     n_w = len(s) - k + 1
     for a, _ in kd.shard_ranges(n_w, world)[1:]:
         s[a - 1] = ord("N")            # the char before a shard's first window
@@ -133,7 +143,8 @@ def test_sharded_query_scatter_and_host_rows(world, c1, host):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_c1_worker, args=(r, world, port, seq_bytes, k, k, c1, host, q))
+    procs = [ctx.Process(target=_c1_worker,
+                         args=(r, world, port, seq_bytes, k, k, c1, host, q, codecs))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -158,6 +169,25 @@ def _run_cases():
     return {"empty": np.zeros((0, 2)), "one": np.array([[40, 9]]), "diag": diag, "cut": cut,
             "repeats": reps, "random": rnd, "tiles": big,
             "wrap": np.array([[2**31 - 2, 5], [2**31 - 1, 6], [-2**31, 7]])}
+
+
+def test_seq_codec_reference():
+    """The numpy sequence packing keeps what the reference reads of every char: the 2-bit code
+    and the N test (lower case, IUPAC letters, other bytes), for every slice [a, b)."""
+    import runs_ref
+    rng = np.random.default_rng(3)
+    s = rng.integers(0, 256, 1000).astype(np.uint8)
+    s[::7] = ord("N")
+    s[3::11] = ord("n")
+    code, nbit = runs_ref.seq_pack(s)
+    for a, b in [(0, 1000), (0, 1), (16, 999), (5, 37), (992, 1000), (500, 500)]:
+        out = np.zeros(1000, np.uint8)
+        w0 = a // 16
+        runs_ref.seq_unpack(code[w0:], nbit[w0:], w0, a, b, out)
+        got, orig = out[a:b], s[a:b]
+        isn = (orig | 0x20) == ord("n")
+        assert np.array_equal((got | 0x20) == ord("n"), isn)
+        assert np.array_equal(((got >> 1) & 3)[~isn], ((orig >> 1) & 3)[~isn])
 
 
 def test_run_codec_reference():

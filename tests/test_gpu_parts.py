@@ -176,3 +176,32 @@ def test_rows_runs_round_trip_vs_reference(gpu):
         runs_expand(got, r.shape[0], out)
         assert np.array_equal(out.cpu().numpy(), r), name
     assert cases["query"].shape[0] > 100_000
+
+
+def test_seq_pack_unpack_vs_reference(gpu):
+    """kmhg_seq_pack / kmhg_seq_unpack (C1's wire format) against the numpy reference, word for
+    word and char for char: arbitrary bytes, N / n, lower case, ragged lengths, slices [a, b)
+    with unaligned ends, an unaligned source pointer."""
+    import torch
+    import runs_ref
+    from kmer_hasher_amd.device import seq_pack, seq_unpack
+    rng = np.random.default_rng(9)
+    for L in (1, 15, 16, 17, 4096, 100_003):
+        s = rng.integers(0, 256, L + 1).astype(np.uint8)
+        s[::5] = ord("N")
+        s[2::13] = ord("n")
+        s[1::3] = np.frombuffer(b"acgtACGT", np.uint8)[rng.integers(0, 8, s[1::3].size)]
+        for off in (0, 1):                   # off = 1: the sequence starts 1 B past alignment
+            src = torch.from_numpy(s).cuda()[off:off + L]
+            code, nbit = seq_pack(src)
+            rc, rn = runs_ref.seq_pack(s[off:off + L])
+            assert np.array_equal(code.cpu().numpy(), rc), (L, off)
+            assert np.array_equal(nbit.cpu().numpy(), rn), (L, off)
+            for a, b in [(0, L), (min(16, L), L), (L // 3 // 16 * 16, L - L // 5), (L, L),
+                         (min(5, L), L)]:
+                w0 = a // 16
+                out = torch.full((L + 16,), 7, dtype=torch.uint8, device="cuda")
+                seq_unpack(code[w0:], nbit[w0:], w0, a, b, out)
+                want = np.full(L + 16, 7, np.uint8)
+                runs_ref.seq_unpack(rc[w0:], rn[w0:], w0, a, b, want)
+                assert np.array_equal(out.cpu().numpy(), want), (L, off, a, b)
