@@ -149,7 +149,7 @@ def broadcast_sequence(seq: torch.Tensor | None, src: int, device: torch.device,
         code = torch.empty(words, dtype=torch.int32, device=device)
         nbit = torch.empty(words, dtype=torch.int16, device=device)
     dist.broadcast(code, src, group=group)
-    dist.broadcast(nbit.view(torch.uint8), src, group=group)   # (gloo broadcasts no int16)
+    dist.broadcast(nbit.view(torch.uint8), src, group=group)   # (no int16 in gloo or RCCL)
     if rank == src:
         return seq
     out = torch.empty(L, dtype=torch.uint8, device=device)
@@ -194,8 +194,9 @@ def scatter_sequence(seq: torch.Tensor | None, k: int, src: int, device: torch.d
                 if packed is None:
                     ops.append(("send", seq[a:b], r))
                 else:
-                    wa, wb = a // 16, (b + 15) // 16
-                    ops += [("send", packed[0][wa:wb], r), ("send", packed[1][wa:wb], r)]
+                    wa, wb = a // 16, (b + 15) // 16     # (u16 words as bytes: no int16 in RCCL)
+                    ops += [("send", packed[0][wa:wb], r),
+                            ("send", packed[1][wa:wb].view(torch.uint8), r)]
         p2p(ops, group)
         return seq
     if out is None or out.numel() < L + 16 or out.device != device:
@@ -210,7 +211,7 @@ def scatter_sequence(seq: torch.Tensor | None, k: int, src: int, device: torch.d
             wa, wb = a // 16, (b + 15) // 16
             code = torch.empty(wb - wa, dtype=torch.int32, device=device)
             nbit = torch.empty(wb - wa, dtype=torch.int16, device=device)
-            p2p([("recv", code, src), ("recv", nbit, src)], group)
+            p2p([("recv", code, src), ("recv", nbit.view(torch.uint8), src)], group)
             codec.unpack(code, nbit, wa, a, b, out)
     return out[:L]
 
