@@ -1061,7 +1061,7 @@ def bench_sharded_build(args, k, L, dev, world, rank, seed):
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    seq_all = kd.broadcast_sequence(big, 0, dev)
+    seq_all = kd.broadcast_sequence(big, 0, dev, codec=kd.HipSeqCodec())   # packed, as C1
     torch.cuda.synchronize()
     t_bc = time.perf_counter() - t0
     for _ in range(max(1, args.warmup)):
