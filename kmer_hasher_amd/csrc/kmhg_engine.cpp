@@ -7,6 +7,7 @@
 // Reference entry points each C function replaces are listed in include/kmhgpu.h.
 #include <atomic>
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <sys/mman.h>
 
 #include <algorithm>
@@ -40,8 +41,8 @@
 // KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_NB_ROUND, KMHG_SLICE_POISON, KMHG_TEST_REPLICA,
 // KMHG_DIGIT_STREAM, KMHG_DS_BID, KMHG_DS_U8, KMHG_DS_PACK, KMHG_BUILD_TAGS), which choose
 // between equivalent paths and change no result; fault injection (KMHG_TEST_DISORDER); and the
-// A/B-only switches (KMHG_D2H, KMHG_D2H_HUGE, KMHG_COUNT_BID, KMHG_RK_CAP, KMHG_POOL_DEPTH,
-// KMHG_POOL_BESTFIT, KMHG_POOL_TRACE).
+// A/B-only switches (KMHG_D2H, KMHG_D2H_HUGE, KMHG_HOST_RUNS, KMHG_COUNT_BID, KMHG_RK_CAP,
+// KMHG_POOL_DEPTH, KMHG_POOL_BESTFIT, KMHG_POOL_TRACE).
 namespace kmhg {
 inline const char* test_build_knob(const char* name) {
 #ifdef KMHG_TEST_BUILD
@@ -624,6 +625,112 @@ void d2h_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
     host_copy_par(static_cast<char*>(dst) + off, pin[i & 1], n);
     if (i + 2 < nch) issue(i + 2);
   }
+}
+
+// Query rows into a host matrix (kmhg_query_fill, the R matrix of seq.kmer.pos).  A dot plot's
+// rows are diagonal runs -- (i, j), (i + 1, j + 1), ... (config 5: 133 rows per run) -- so from
+// RUNS_HOST_MIN rows on, the device writes the runs (R_count, scan, R_emit: the sharded
+// query's gather format), 12 B per run cross PCIe into a pinned buffer, and host threads
+// expand them into dst: the link carries ~1/90 of the bytes and the host's memory bandwidth
+// writes the rows.  Rows that do not shrink RUNS_HOST_GAIN-fold (multi-hit windows) take
+// d2h_host.  KMHG_HOST_RUNS=0 (test build): always d2h_host (A/B).
+constexpr uint64_t RUNS_HOST_MIN = 1u << 19;           // rows (4 MB)
+constexpr uint64_t RUNS_HOST_GAIN = 4;
+struct PinRuns {
+  std::mutex mu;
+  int32_t* p = nullptr;
+  size_t cap = 0;                                       // int32 words
+};
+static PinRuns& pin_runs() {                            // the device's pinned run buffer
+  static std::mutex map_mu;
+  static std::map<int, PinRuns> bufs;
+  int dev = 0;
+  HIPC(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(map_mu);
+  return bufs[dev];
+}
+
+// Host threads for the expansion: it is bound by the host's write bandwidth, which more threads
+// reach (box, 16 CPUs, config 5's 376 M rows: 4 threads 51 ms, 8 30 ms, 16 16.5 ms;
+// profiles/r6y_runs_probe*.json): every CPU this process may run on, at most 16.
+static int expand_threads() {
+  static const int n = [] {
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    const int c = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : 8;
+    return std::max(1, std::min(16, c));
+  }();
+  return n;
+}
+
+static void expand_runs_host(const int32_t* runs, uint64_t n, uint64_t H, int32_t* dst) {
+  const int T = expand_threads();
+  const uint64_t stripe = (((H + T - 1) / T) + 511) & ~(uint64_t)511;
+  auto work = [=](uint64_t r0, uint64_t r1) {
+    uint64_t lo = 0, hi = n;                            // the run covering r0
+    while (hi - lo > 1) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if ((uint64_t)(uint32_t)runs[3 * mid] <= r0) lo = mid; else hi = mid;
+    }
+    uint64_t r = r0;
+    for (uint64_t q = lo; r < r1; ++q) {
+      const uint64_t st = (uint32_t)runs[3 * q];
+      const uint32_t i0 = (uint32_t)runs[3 * q + 1], j0 = (uint32_t)runs[3 * q + 2];
+      const uint64_t e = std::min(r1, q + 1 < n ? (uint64_t)(uint32_t)runs[3 * q + 3] : H);
+      uint32_t* o = reinterpret_cast<uint32_t*>(dst) + 2 * r;
+      for (uint32_t d = (uint32_t)(r - st); r < e; ++r, ++d, o += 2) {
+        o[0] = i0 + d;
+        o[1] = j0 + d;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) {
+    const uint64_t a = std::min(H, t * stripe), b = std::min(H, a + stripe);
+    if (a < b) th.emplace_back(work, a, b);
+  }
+  work(0, std::min(H, stripe));
+  for (auto& x : th) x.join();
+}
+
+void rows_to_host(const int2* d_rows, uint64_t H, int32_t* dst, hipStream_t s) {
+  if (!H) return;
+  const char* hre = test_build_knob("KMHG_HOST_RUNS");    // (read per call: tests flip it)
+  const bool runs_on = !(hre && hre[0] == '0');
+  if (!runs_on || H < RUNS_HOST_MIN || H > INT32_MAX) {
+    d2h_host(dst, d_rows, H * 8, s);
+    return;
+  }
+  ReleaseGroup rg(s);
+  const uint64_t nt = (H + TILE - 1) / TILE;
+  DBuf<uint64_t> tiles(nt + scan_u64_scratch(nt), s);
+  PinnedRec hrec = PinnedPool::get().take();
+  GiveBack give_back{hrec, s};
+  uint64_t* total = &hrec.meta->n_kmers;
+  LAUNCH("k_runs_count", s, launch_runs_count(d_rows, H, tiles.p, s));
+  LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tiles.p, nt, total, tiles.p + nt, s));
+  HIPC(hipStreamSynchronize(s));
+  const uint64_t n = __atomic_load_n(total, __ATOMIC_ACQUIRE);
+  if (n * 12 * RUNS_HOST_GAIN > H * 8) {                // runs would not pay: the rows
+    d2h_host(dst, d_rows, H * 8, s);
+    return;
+  }
+  DBuf<int32_t> druns(3 * n, s);
+  LAUNCH("k_runs_emit", s, launch_runs_emit(d_rows, H, tiles.p, druns.p, s));
+  PinRuns& pr = pin_runs();
+  std::lock_guard<std::mutex> g(pr.mu);
+  if (pr.cap < 3 * n) {
+    if (pr.p) HIPC(hipHostFree(pr.p));                  // (no copy into it is in flight)
+    pr.p = nullptr;
+    pr.cap = 0;
+    const size_t cap = std::max<size_t>(3 * n, 3u << 20);
+    HIPC(hipHostMalloc(reinterpret_cast<void**>(&pr.p), cap * 4, hipHostMallocPortable));
+    pr.cap = cap;
+  }
+  HIPC(hipMemcpyAsync(pr.p, druns.p, 3 * n * 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  hint_huge_pages(dst, H * 8);
+  expand_runs_host(pr.p, n, H, dst);
 }
 
 // Pageable host -> device copy for the host-pointer entry points (the R string of make.kmer.hash
@@ -3341,7 +3448,7 @@ int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
           kmhg_query* p = q->parts[i];
           if (!p->H) return;
           DeviceGuard g(p->device);
-          d2h_host(rows + 2 * q->part_off[i], p->rows.p, (size_t)p->H * 8, lib_stream());
+          rows_to_host(p->rows.p, (uint64_t)p->H, rows + 2 * q->part_off[i], lib_stream());
         } catch (const Error& e) {
           errs[i] = e;
         }
@@ -3356,7 +3463,7 @@ int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
     }
     DeviceGuard g(q->device);
     hipStream_t s = lib_stream();
-    d2h_host(rows, q->rows.p, (size_t)q->H * 8, s);
+    rows_to_host(q->rows.p, (uint64_t)q->H, rows, s);
   });
 }
 

@@ -50,3 +50,28 @@ def test_query_rows_over_int_max_raise(gpu):
     with pytest.raises(KmerHashError, match="2\\^31-1 columns"):
         seq_kmer_pos(ptr, "A" * 46_343, 1)
     ptr.free()
+
+
+@pytest.mark.parametrize("case", ["self", "related", "repeats"])
+def test_query_rows_to_host_as_runs(gpu, test_lib, monkeypatch, case):
+    """seq.kmer.pos into a host matrix (kmhg_query_fill) from 512 K rows on: the rows cross PCIe
+    as diagonal runs and host threads expand them; results equal the oracle's with runs and with
+    the plain copy (KMHG_HOST_RUNS=0): a self dot plot (one run per stretch between repeats), a
+    related sequence (SNVs, rearrangements, N-runs), and repeat-rich rows that do not shrink
+    (the plain copy is taken).  Odd row counts split unevenly over the host threads."""
+    from kmer_hasher_amd import make_kmer_hash, seq_kmer_pos, synth
+    k = 21
+    if case == "repeats":
+        a = synth.repeat_rich(700_000, 12, n_gap_every=70_001)
+    else:
+        a = synth.add_n_runs(synth.iid(1_300_001, 8), 0.0005, 3)
+    b = synth.derived(a, 6, 0.01, 3) if case == "related" else a
+    A, B = a.tobytes().decode("latin-1"), b.tobytes().decode("latin-1")
+    want = O.OracleIndex(A, k).query(B, k)
+    assert want.size // 2 >= (1 << 19)
+    ptr = make_kmer_hash(A, k)
+    for runs in ("1", "0"):
+        monkeypatch.setenv("KMHG_HOST_RUNS", runs)
+        got = seq_kmer_pos(ptr, B, k)
+        assert np.array_equal(got.reshape(-1), want), runs
+    ptr.free()
