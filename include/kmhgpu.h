@@ -178,6 +178,10 @@ int kmhg_seq_unpack(const uint32_t *d_code, const uint16_t *d_nbit, int64_t word
  * kmhg_rows_runs counts the runs (*n_runs; it waits for `stream`) and writes them to d_runs when
  * *n_runs <= cap_runs (else nothing: the caller sends rows); kmhg_runs_expand writes the n_rows
  * rows back to d_rows on `stream`.  n_rows < 2^31. */
+/* n_rows (i, j) rows in device memory into host memory (2 * n_rows int32, e.g. an R matrix or
+ * one rank's slice of a node-shared matrix), as kmhg_query_fill copies a query's rows: from
+ * 512 K rows on as diagonal runs over PCIe, expanded by host threads.  Synchronous. */
+int kmhg_rows_to_host(const void *d_rows, int64_t n_rows, int32_t *rows, void *stream);
 int kmhg_rows_runs(const void *d_rows, int64_t n_rows, void *d_runs, int64_t cap_runs,
                    int64_t *n_runs, void *stream);
 int kmhg_runs_expand(const void *d_runs, int64_t n_runs, int64_t n_rows, void *d_rows,

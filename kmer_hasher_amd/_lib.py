@@ -67,6 +67,7 @@ _PROTOS = {
     "kmhg_seq_pack": (C.c_int, [vp, C.c_int64, vp, vp, vp]),
     "kmhg_seq_unpack": (C.c_int, [vp, vp, C.c_int64, C.c_int64, C.c_int64, vp, vp]),
     "kmhg_rows_runs": (C.c_int, [vp, C.c_int64, vp, C.c_int64, i64p, vp]),
+    "kmhg_rows_to_host": (C.c_int, [vp, C.c_int64, vp, vp]),
     "kmhg_runs_expand": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp]),
     "kmhg_merge_part_rows": (C.c_int, [vp, vp, vp, C.c_int, C.c_int64, C.c_int, C.c_int64, vp,
                                        vp]),

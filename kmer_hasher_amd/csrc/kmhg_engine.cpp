@@ -3419,6 +3419,15 @@ int kmhg_rows_runs(const void* d_rows, int64_t n_rows, void* d_runs, int64_t cap
   });
 }
 
+int kmhg_rows_to_host(const void* d_rows, int64_t n_rows, int32_t* rows, void* stream) {
+  return guarded([&] {
+    if (n_rows < 0) fail(KMHG_EINVAL, "bad row count");
+    if (!n_rows) return;
+    if (!d_rows || !rows) fail(KMHG_EINVAL, "null argument");
+    rows_to_host(static_cast<const int2*>(d_rows), (uint64_t)n_rows, rows, (hipStream_t)stream);
+  });
+}
+
 int kmhg_runs_expand(const void* d_runs, int64_t n_runs, int64_t n_rows, void* d_rows,
                      void* stream) {
   return guarded([&] {

@@ -288,6 +288,22 @@ def seq_unpack(code: torch.Tensor, nbit: torch.Tensor, word0: int, a: int, b: in
     return out
 
 
+def rows_to_host(rows: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:
+    """kmhg_rows_to_host: (H, 2) int32 device rows into `out`, a contiguous host (H, 2) int32
+    tensor (pinned or not), as kmhg_query_fill delivers a query: diagonal runs over PCIe,
+    expanded by host threads.  Synchronous."""
+    H = rows.shape[0]
+    if out.shape != (H, 2) or out.dtype != torch.int32 or out.is_cuda or not out.is_contiguous():
+        raise ValueError("out must be a contiguous host (H, 2) int32 tensor")
+    if H == 0:
+        return out
+    rows = rows.contiguous()
+    with torch.cuda.device(rows.device):
+        _lib.check(_lib.lib().kmhg_rows_to_host(C.c_void_p(rows.data_ptr()), H,
+                                                C.c_void_p(out.data_ptr()), _stream_ptr(stream)))
+    return out
+
+
 def rows_to_runs(rows: torch.Tensor, stream=None) -> torch.Tensor | None:
     """kmhg_rows_runs: the (H, 2) int32 rows as diagonal runs, an (n_runs, 3) int32 tensor of
     {first row index, i, j} -- or None when runs would not be smaller than the rows (12 B per

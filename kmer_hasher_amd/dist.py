@@ -305,11 +305,13 @@ class HostRowSink:
         self.cap = 0
 
 
-def deliver_rows_host(local: torch.Tensor, sink: HostRowSink, group=None):
+def deliver_rows_host(local: torch.Tensor, sink: HostRowSink, group=None, codec=None):
     """Every rank's (h_r, 2) int32 rows into the sink's shared host matrix, rank r's at row
     offset h_0 + ... + h_{r-1} (= the reference's row order), each rank copying its own rows
-    D2H.  Returns the (H, 2) matrix (a view of the shared buffer) on the sink's owner, else
-    None.  The matrix is valid until the next delivery into the same sink."""
+    D2H (codec.to_host when the codec has one: HipRunCodec sends them over PCIe as diagonal
+    runs, expanded by host threads).  Returns the (H, 2) matrix (a view of the shared buffer)
+    on the sink's owner, else None.  The matrix is valid until the next delivery into the same
+    sink."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = local.device
@@ -321,7 +323,11 @@ def deliver_rows_host(local: torch.Tensor, sink: HostRowSink, group=None):
     sink.ensure(H, dev)
     off = sum(counts[:rank])
     if counts[rank]:
-        sink.t[2 * off:2 * (off + counts[rank])].view(-1, 2).copy_(local)
+        dst = sink.t[2 * off:2 * (off + counts[rank])].view(-1, 2)
+        if codec is not None and hasattr(codec, "to_host") and local.is_cuda:
+            codec.to_host(local, dst)
+        else:
+            dst.copy_(local)
     dist.barrier(group=group)                       # every rank's copy has landed
     if rank == sink.owner:
         return sink.t[:2 * H].view(-1, 2)
@@ -366,8 +372,9 @@ def sharded_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, group=
     w0, w1 = shard_ranges(n_windows, world)[rank]
     local = engine.query_range(seq, k, w0, w1)
     t2 = mark()
-    rows = gather_rows(local, dst, group, getattr(engine, "codec", None)) if sink is None \
-        else deliver_rows_host(local, sink, group)
+    codec = getattr(engine, "codec", None)
+    rows = gather_rows(local, dst, group, codec) if sink is None \
+        else deliver_rows_host(local, sink, group, codec)
     t3 = mark()
     if timings is not None:
         for name, dt in (("broadcast", t1 - t0), ("query", t2 - t1), ("gather", t3 - t2)):
@@ -509,6 +516,11 @@ class HipRunCodec:
     def decode(runs: torch.Tensor, n_rows: int, out: torch.Tensor):
         from .device import runs_expand
         runs_expand(runs, n_rows, out)
+
+    @staticmethod
+    def to_host(rows: torch.Tensor, out: torch.Tensor):
+        from .device import rows_to_host
+        rows_to_host(rows, out)
 
 
 class HipQueryEngine:
