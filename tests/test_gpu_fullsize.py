@@ -68,12 +68,20 @@ def _check_positions(idx, r, opt):
 
 
 def _check_query(idx, seq, r, k):
+    """The rows on the device and, as an R session receives them, in a host matrix
+    (kmhg_query_fill: diagonal runs over PCIe, expanded by host threads)."""
+    import ctypes
+    import numpy as np
+    from kmer_hasher_amd import _lib
     q = idx.query(seq, k)
     want = r["query"][str(k)]
     assert q.n_rows == want["H"]
     rows = q.rows()
+    host = np.empty(2 * q.n_rows, np.int32)
+    _lib.check(_lib.lib().kmhg_query_fill(q._h, ctypes.c_void_p(host.ctypes.data)))
     q.free()
     assert _sha_dev(rows) == want["sha"]
+    assert hashlib.sha256(host.view(np.uint8)).hexdigest() == want["sha"]
 
 
 def test_config2_10mbp_k31_reference_digests(gpu, fullsize):
