@@ -41,8 +41,8 @@
 // KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_NB_ROUND, KMHG_SLICE_POISON, KMHG_TEST_REPLICA,
 // KMHG_DIGIT_STREAM, KMHG_DS_BID, KMHG_DS_U8, KMHG_DS_PACK, KMHG_BUILD_TAGS), which choose
 // between equivalent paths and change no result; fault injection (KMHG_TEST_DISORDER); and the
-// A/B-only switches (KMHG_D2H, KMHG_D2H_HUGE, KMHG_HOST_RUNS, KMHG_COUNT_BID, KMHG_RK_CAP,
-// KMHG_POOL_DEPTH, KMHG_POOL_BESTFIT, KMHG_POOL_TRACE).
+// A/B-only switches (KMHG_D2H, KMHG_D2H_HUGE, KMHG_HOST_RUNS, KMHG_HOST_PAIRS, KMHG_COUNT_BID,
+// KMHG_RK_CAP, KMHG_POOL_DEPTH, KMHG_POOL_BESTFIT, KMHG_POOL_TRACE).
 namespace kmhg {
 inline const char* test_build_knob(const char* name) {
 #ifdef KMHG_TEST_BUILD
@@ -3229,6 +3229,78 @@ int kmhg_positions_fill_device(kmhg_index* idx, uint32_t opt, char* d_kmers, int
   });
 }
 
+// kmer.pos's pair rows into a host matrix (the R API's readout).  A pair row is {key label,
+// position j, position q} for every j < q of a repeated key's list -- P rows from the lists'
+// ~N positions (config 4: 686 M rows, 8.2 GB, from 40 M positions) -- so from HOST_PAIRS_MIN
+// rows on, the lists and their keys' offsets cross PCIe (pkeys, pair_off, rinfo, positions:
+// ~0.4 GB at config 4) and host threads write the rows, each from its stripe's first pair on
+// (the pair t of a key with n positions: the largest j with j (2n - j - 1) / 2 <= t, as
+// V_read_pairs).  KMHG_HOST_PAIRS=0 (test build): the rows are made on the device and copied.
+constexpr uint64_t HOST_PAIRS_MIN = 1u << 22;           // rows (48 MB)
+static void expand_pairs_host(const uint32_t* pk, const uint64_t* po, uint64_t M, const uint2* ri,
+                              const int32_t* ps, uint64_t P, int32_t* out) {
+  const int T = expand_threads();
+  const uint64_t stripe = (P + T - 1) / T;
+  auto work = [=](uint64_t r0, uint64_t r1) {
+    uint64_t m = (uint64_t)(std::upper_bound(po, po + M, r0) - po) - 1;
+    uint64_t t = r0 - po[m], r = r0;
+    while (r < r1) {
+      const uint32_t c = pk[m];
+      const uint64_t n = ri[c].x;
+      const int32_t* lst = ps + (ri[c].y - n);
+      auto S = [n](uint64_t x) { return x * (2 * n - x - 1) / 2; };
+      uint64_t j = 0;
+      if (t) {
+        const double dn = 2.0 * (double)n - 1.0, disc = dn * dn - 8.0 * (double)t;
+        j = (uint64_t)std::max(0.0, (dn - std::sqrt(std::max(disc, 0.0))) * 0.5);
+        j = std::min<uint64_t>(j, n - 2);
+        while (j > 0 && S(j) > t) --j;
+        while (j + 1 <= n - 2 && S(j + 1) <= t) ++j;
+      }
+      uint64_t q = j + 1 + (t - S(j));
+      const int32_t lab = (int32_t)(c + 1);
+      for (; j + 1 < n && r < r1; ++j, q = j + 1) {
+        const int32_t pj = lst[j];
+        const uint64_t qe = std::min<uint64_t>(n, q + (r1 - r));
+        int32_t* o = out + 3 * r;
+        for (uint64_t x = q; x < qe; ++x, o += 3) {
+          o[0] = lab;
+          o[1] = pj;
+          o[2] = lst[x];
+        }
+        r += qe - q;
+      }
+      ++m;
+      t = 0;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < T; ++i) {
+    const uint64_t a = std::min(P, i * stripe), b = std::min(P, a + stripe);
+    if (a < b) th.emplace_back(work, a, b);
+  }
+  work(0, std::min(P, stripe));
+  for (auto& x : th) x.join();
+}
+
+static void pairs_to_host(kmhg_index* idx, int32_t* out, hipStream_t s) {
+  Canon& c = idx->canon;                     // prepare_readout ran (positions_device)
+  const uint64_t M = c.n_multi, U = idx->U, P = idx->P;
+  std::unique_ptr<uint32_t[]> pk(new uint32_t[M]);
+  std::unique_ptr<uint64_t[]> po(new uint64_t[M]);
+  std::unique_ptr<uint2[]> ri(new uint2[U]);
+  d2h_host(pk.get(), c.pkeys.p, M * 4, s);
+  d2h_host(po.get(), c.pair_off.p, M * 8, s);
+  d2h_host(ri.get(), c.rinfo.p, U * 8, s);
+  uint64_t n_lists = 0;                      // the list entries in use: [0, max end)
+  for (uint64_t m = 0; m < M; ++m) n_lists = std::max<uint64_t>(n_lists, ri[pk[m]].y);
+  if (n_lists > idx->positions.n) fail(KMHG_EDEVICE, "pair lists beyond the positions");
+  std::unique_ptr<int32_t[]> ps(new int32_t[std::max<uint64_t>(n_lists, 1)]);
+  d2h_host(ps.get(), idx->positions.p, n_lists * 4, s);
+  hint_huge_pages(out, P * 12);
+  expand_pairs_host(pk.get(), po.get(), M, ri.get(), ps.get(), P, out);
+}
+
 int kmhg_positions_fill(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos, int32_t* pairs,
                         int32_t* counts) {
   return guarded([&] {
@@ -3236,16 +3308,22 @@ int kmhg_positions_fill(kmhg_index* idx, uint32_t opt, char* kmers, int32_t* pos
     DeviceGuard g(idx->device);
     hipStream_t s = lib_stream();
     const size_t U = idx->U;
+    const char* hpe = test_build_knob("KMHG_HOST_PAIRS");
+    const bool host_pairs = (opt & KMHG_OPT_PAIRS) && pairs && idx->P >= HOST_PAIRS_MIN &&
+                            idx->sources == 0 && !(hpe && hpe[0] == '0');   // position indices
+    const uint32_t dopt = host_pairs ? opt & ~(uint32_t)KMHG_OPT_PAIRS : opt;
     DBuf<char> dk((opt & KMHG_OPT_KMER) ? U * (idx->k + 1) : 0, s);
     DBuf<int32_t> dp((opt & KMHG_OPT_POS) ? 2 * idx->N : 0, s);
-    DBuf<int32_t> dpp((opt & KMHG_OPT_PAIRS) ? 3 * idx->P : 0, s);
+    DBuf<int32_t> dpp((dopt & KMHG_OPT_PAIRS) ? 3 * idx->P : 0, s);
     DBuf<int32_t> dc((opt & KMHG_OPT_COUNT) ? U : 0, s);
-    positions_device(idx, opt, dk.p, dp.p, dpp.p, dc.p, s);
+    positions_device(idx, dopt, dk.p, dp.p, dpp.p, dc.p, s);
     if ((opt & KMHG_OPT_KMER) && U && kmers)
       d2h_host(kmers, dk.p, dk.bytes(), s);
     if ((opt & KMHG_OPT_POS) && idx->N && pos)
       d2h_host(pos, dp.p, dp.bytes(), s);
-    if ((opt & KMHG_OPT_PAIRS) && idx->P && pairs)
+    if (host_pairs)
+      pairs_to_host(idx, pairs, s);
+    else if ((opt & KMHG_OPT_PAIRS) && idx->P && pairs)
       d2h_host(pairs, dpp.p, dpp.bytes(), s);
     if ((opt & KMHG_OPT_COUNT) && U && counts)
       d2h_host(counts, dc.p, dc.bytes(), s);

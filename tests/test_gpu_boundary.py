@@ -75,3 +75,36 @@ def test_query_rows_to_host_as_runs(gpu, test_lib, monkeypatch, case):
         got = seq_kmer_pos(ptr, B, k)
         assert np.array_equal(got.reshape(-1), want), runs
     ptr.free()
+
+
+def test_pair_rows_to_host_generated(gpu, test_lib, monkeypatch):
+    """kmer.pos pair rows into a host matrix from 4 M rows on are written by host threads from
+    the keys' position lists (kmhg_positions_fill): identical to the device-made rows copied over
+    (KMHG_HOST_PAIRS=0) and to the oracle, for a 150-copy family, a 20-copy family and a 5 kb
+    poly-A run (one key with ~5,000 positions: 12 M pairs), with the stripes of the host threads
+    cutting through keys and through one key's rows."""
+    from kmer_hasher_amd import kmer_pos, make_kmer_hash, synth
+    rng = np.random.default_rng(17)
+    s = synth.iid(2_000_000, 21).copy()
+    fam = synth.iid(500, 22)
+    for at in rng.choice(np.arange(10_000, 1_900_000, 1_000), 150, replace=False):
+        s[at:at + 500] = fam
+    fam2 = synth.iid(3_000, 23)
+    for at in range(1_950_000, 1_950_000 + 20 * 3_001, 3_001)[:16]:
+        s[at:at + 3_000] = fam2
+    s[5_000:10_000] = ord("A")
+    A = s.tobytes().decode("latin-1")
+    oi = O.OracleIndex(A, 21)
+    want = oi.pair_rows()
+    assert want.size // 3 >= (1 << 22)
+    ptr = make_kmer_hash(A, 21)
+    got = {}
+    for hp in ("1", "0"):
+        monkeypatch.setenv("KMHG_HOST_PAIRS", hp)
+        res = kmer_pos(ptr, 2 + 4 + 8)
+        got[hp] = res["pair.pos"].reshape(-1)
+        assert np.array_equal(res["pos"].reshape(-1), oi.pos_rows())
+        assert np.array_equal(res["count"], oi.counts)
+    ptr.free()
+    assert np.array_equal(got["0"], want)
+    assert np.array_equal(got["1"], want)

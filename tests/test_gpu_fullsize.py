@@ -114,6 +114,16 @@ def test_config4_40mbp_pairs_reference_digests(gpu, fullsize):
     seq, idx = _build_khash(synth.config4(r["L"], 3), r["k"])
     _check_index(idx, r)
     _check_positions(idx, r, 2 | 4 | 8)
+    # the pair rows as an R session receives them (kmhg_positions_fill: written by host threads
+    # from the position lists)
+    import ctypes
+    import numpy as np
+    from kmer_hasher_amd import _lib
+    host = np.empty(3 * r["P"], np.int32)
+    _lib.check(_lib.lib().kmhg_positions_fill(idx.handle, 4, None, None,
+                                              ctypes.c_void_p(host.ctypes.data), None))
+    assert hashlib.sha256(host.view(np.uint8)).hexdigest() == r["raw_sha"]["pair.pos"]
+    del host
     idx.free()
 
 
