@@ -1383,6 +1383,25 @@ def bench_readout(args, cfg, dev, world, rank):
     t = time.perf_counter() - t0
     kt = D.timing_report()
     D.timing_enable(False)
+    # the same readout into fresh host matrices, as the R API's kmer.pos returns it
+    # (kmhg_positions_fill: pos rows and counts copied, pair rows written by host threads from
+    # the position lists); the matrices' release is not timed
+    host_ms = None
+    if not args.profile:
+        import ctypes as _C
+        import numpy as np
+        from kmer_hasher_amd import _lib
+        P_, N_, U_ = info["n_pairs"], info["n_positions"], info["n_kmers"]
+        th = []
+        for _ in range(3):
+            bufs = [np.empty(2 * N_, np.int32), np.empty(3 * P_, np.int32), np.empty(U_, np.int32)]
+            t0 = time.perf_counter()
+            _lib.check(_lib.lib().kmhg_positions_fill(
+                idx.handle, opt, None, *[_C.c_void_p(b.ctypes.data) if b.size else None
+                                         for b in bufs]))
+            th.append(time.perf_counter() - t0)
+            del bufs
+        host_ms = min(th) * 1e3
     tt = torch.tensor([t], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -1410,6 +1429,13 @@ def bench_readout(args, cfg, dev, world, rank):
                                                     if v[0] and n in ("k_read_first", "k_read_order")}},
                "roofline": roofline(B, dom, per[dom], t / args.steps * 1e3, pmc, ab, launches),
                "cpu_baseline": cpu,
+               "host": None if host_ms is None else {
+                   "ms": round(host_ms, 3), "value": round(P / (host_ms * 1e-3) / 1e9, 4),
+                   "unit": "G pair rows/s",
+                   "note": "kmer.pos(opt 14) into fresh host matrices (kmhg_positions_fill, the R "
+                           "API: pos rows and counts copied D2H, pair rows written by host "
+                           "threads from the position lists), best of 3; PCIe- and host-memory-"
+                           "inclusive, never `value`"},
                "kernels_ms": {n: round(v, 4) for n, v in per.items()}})
     idx.free()
 
