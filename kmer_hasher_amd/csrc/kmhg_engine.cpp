@@ -653,18 +653,23 @@ static PinRuns& pin_runs() {                            // the device's pinned r
 // Host threads for the expansion: it is bound by the host's write bandwidth, which more threads
 // reach (box, 16 CPUs, config 5's 376 M rows: 4 threads 51 ms, 8 30 ms, 16 16.5 ms;
 // profiles/r6y_runs_probe*.json): every CPU this process may run on, at most 16.
-static int expand_threads() {
+// (The host's later unmapping of the matrix grows with the threads that wrote it -- 80 MB: 2.5
+// ms written by one thread, 5.2 by 16, profiles/r6af_release_probe.json -- but giving each thread
+// 16 MB instead (5 threads at 80 MB) traded 0.85 ms of fill for 0.9 of release,
+// profiles/r6ag_release.json: every thread is used from 1 MB of output per thread on.)
+constexpr uint64_t EXPAND_MIN_BYTES = 1u << 20;
+static int expand_threads(uint64_t out_bytes) {
   static const int n = [] {
     cpu_set_t cs;
     CPU_ZERO(&cs);
     const int c = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : 8;
     return std::max(1, std::min(16, c));
   }();
-  return n;
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>(n, out_bytes / EXPAND_MIN_BYTES));
 }
 
 static void expand_runs_host(const int32_t* runs, uint64_t n, uint64_t H, int32_t* dst) {
-  const int T = expand_threads();
+  const int T = expand_threads(H * 8);
   const uint64_t stripe = (((H + T - 1) / T) + 511) & ~(uint64_t)511;
   auto work = [=](uint64_t r0, uint64_t r1) {
     uint64_t lo = 0, hi = n;                            // the run covering r0
@@ -3239,7 +3244,7 @@ int kmhg_positions_fill_device(kmhg_index* idx, uint32_t opt, char* d_kmers, int
 constexpr uint64_t HOST_PAIRS_MIN = 1u << 22;           // rows (48 MB)
 static void expand_pairs_host(const uint32_t* pk, const uint64_t* po, uint64_t M, const uint2* ri,
                               const int32_t* ps, uint64_t P, int32_t* out) {
-  const int T = expand_threads();
+  const int T = expand_threads(P * 12);
   const uint64_t stripe = (P + T - 1) / T;
   auto work = [=](uint64_t r0, uint64_t r1) {
     uint64_t m = (uint64_t)(std::upper_bound(po, po + M, r0) - po) - 1;
