@@ -1,10 +1,10 @@
 """kmer.pos(opt) into fresh host matrices (kmhg_positions_fill, the R API's readout) against the
 same readout into HBM (kmhg_positions_fill_device), config 4's repeat-rich 40 Mbp index (k = 31,
 686 M pair rows).  numpy's own huge-page hint is off (R's allocMatrix gives plain malloc
-memory).  `--no-host-pairs`: the test build with KMHG_HOST_PAIRS=0 (pair rows copied, A/B).
+memory).  Runs on the test build, which reads the A/B knobs from the environment;
+`--no-host-pairs`: KMHG_HOST_PAIRS=0 (pair rows copied).
     python tools/host_readout_probe.py [opt] [reps] [--no-host-pairs]"""
 import ctypes as C
-import contextlib
 import json
 import os
 import sys
@@ -31,7 +31,7 @@ def main():
     _set_madvise_hugepage(False)
     from kmer_hasher_amd import _lib, synth
     from kmer_hasher_amd.device import DeviceIndex
-    with (_lib.using_test_build() if plain else contextlib.nullcontext()) as _:
+    with _lib.using_test_build():               # (reads KMHG_HOST_PAIRS / KMHG_HOST_NT)
         L = _lib.lib()
         seq = torch.from_numpy(synth.config4(40_000_000, 3)).cuda()
         idx = DeviceIndex.build(seq, 31)
