@@ -1513,7 +1513,7 @@ k_runs_expand(const int32_t* __restrict__ runs, uint64_t n_runs, uint64_t n,
       rs[q] = (uint32_t)s0;
       ri[q] = (uint32_t)runs[3 * g + 1];
       rj[q] = (uint32_t)runs[3 * g + 2];
-      if (q > 0) fl[s0 - t0] = 1;             // q = 0 starts at or before t0
+      if (q > 0 && s0 > t0) fl[s0 - t0] = 1;  // q = 0 starts at or before t0 (runs ascend)
     }
   }
   __syncthreads();
