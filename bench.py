@@ -680,7 +680,8 @@ def main():
     # once, apart.  The replicas above (every rank its own L bases) become a side record.
     sharded = None
     if distributed:
-        sharded = bench_sharded_build(args, k, L, dev, world, rank, seed)
+        sharded = _side_record("sharded build", bench_sharded_build, args, k, L, dev, world,
+                               rank, seed)
 
     progress("self query")
     # ---------------- query: self seq.kmer.pos against one resident index.  The first query of an
@@ -864,7 +865,8 @@ def main():
     # queries, rows gathered) on every N > 1 line; at N = 1 `large.query` is its one-GPU point
     sq = None
     if distributed and not args.profile and not args.no_large:
-        sq, _ = sharded_query_record(args, dev, world, rank, max(1, min(args.steps, 10)))
+        sq = _side_record("sharded query", lambda *a: sharded_query_record(*a)[0], args, dev,
+                          world, rank, max(1, min(args.steps, 10)))
     progress("out-of-cache record")
     # the out-of-cache side record (one GPU only: the driver's N = 1 line; the 8-GPU scaling runs
     # skip it)
@@ -1037,6 +1039,20 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _side_record(name: str, fn, *a):
+    """An N > 1 side record whose failure must not cost the line its headline: an exception that
+    every rank raises alike (an API or argument error) is recorded as the record's `error` and
+    the ranks carry on; the headline `value` was measured before it."""
+    import torch.distributed as dist
+    try:
+        return fn(*a)
+    except Exception as e:                         # noqa: BLE001 -- reported in the line
+        progress(f"{name} failed: {type(e).__name__}: {e}")
+        if dist.is_initialized():
+            dist.barrier()
+        return {"error": f"{type(e).__name__}: {e}"[:500]}
 
 
 def check_build(info: dict) -> None:
