@@ -108,3 +108,26 @@ def test_pair_rows_to_host_generated(gpu, test_lib, monkeypatch):
     ptr.free()
     assert np.array_equal(got["0"], want)
     assert np.array_equal(got["1"], want)
+
+
+def test_large_host_string_ends_at_nul(gpu):
+    """kmhg_build / kmhg_query_run of a host string of >= 4 MB: the NUL scan runs beside the
+    copy of all L bytes, and the sequence still ends at its first NUL (a C string)."""
+    import ctypes as C
+    from kmer_hasher_amd import _lib, synth
+    k = 21
+    s = synth.iid(6_000_000, 41)
+    s[3_000_001] = 0
+    buf = s.tobytes()
+    pre = buf[:3_000_001]
+    oi = O.OracleIndex(pre, k)
+    out = C.c_void_p()
+    _lib.check(_lib.lib().kmhg_build(buf, len(buf), k, 0, C.byref(out)))
+    q, h = C.c_void_p(), C.c_int64()
+    _lib.check(_lib.lib().kmhg_query_run(out, buf, len(buf), k, C.byref(q), C.byref(h)))
+    rows = np.empty(2 * h.value, np.int32)
+    _lib.check(_lib.lib().kmhg_query_fill(q, C.c_void_p(rows.ctypes.data)))
+    _lib.lib().kmhg_query_free(q)
+    want = oi.query(pre, k)
+    assert np.array_equal(rows, want)
+    _lib.lib().kmhg_free(out)
