@@ -16,6 +16,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <deque>
 #include <exception>
 #include <functional>
 #include <map>
@@ -41,8 +43,8 @@
 // KMHG_ROW_ORDER_SORT, KMHG_PACK8, KMHG_NB_ROUND, KMHG_SLICE_POISON, KMHG_TEST_REPLICA,
 // KMHG_DIGIT_STREAM, KMHG_DS_BID, KMHG_DS_U8, KMHG_DS_PACK, KMHG_BUILD_TAGS), which choose
 // between equivalent paths and change no result; fault injection (KMHG_TEST_DISORDER); and the
-// A/B-only switches (KMHG_D2H, KMHG_D2H_HUGE, KMHG_HOST_RUNS, KMHG_HOST_PAIRS, KMHG_COUNT_BID,
-// KMHG_RK_CAP, KMHG_POOL_DEPTH, KMHG_POOL_BESTFIT, KMHG_POOL_TRACE).
+// A/B-only switches (KMHG_D2H, KMHG_D2H_HUGE, KMHG_HOST_RUNS, KMHG_HOST_PAIRS, KMHG_HOST_POOL,
+// KMHG_COUNT_BID, KMHG_RK_CAP, KMHG_POOL_DEPTH, KMHG_POOL_BESTFIT, KMHG_POOL_TRACE).
 namespace kmhg {
 inline const char* test_build_knob(const char* name) {
 #ifdef KMHG_TEST_BUILD
@@ -517,6 +519,110 @@ hipStream_t lib_stream() {
   return s;
 }
 
+// Host worker pool for the host-side copies: HOST_WORKERS threads made on first use and kept,
+// so a call that splits a few MB over threads does not pay their creation and join (8 threads:
+// ~0.1-0.35 ms a round -- per 16-MB chunk of a staged copy before).  run(n, fn) runs fn(0) ..
+// fn(n - 1), the calling thread taking tasks too, and returns when all are done; calls from
+// several threads at once (a multi-device query's parts) share the workers.  No task may call
+// run() itself.  big = true (GB-scale writes: the expansions) starts fresh threads instead: the
+// kernel spreads new threads over the machine's memory controllers, while woken pool workers
+// crowd near their waker (A/B in one run, profiles/r6al_pool_ab/: config 5's run expansion 18-21 ms
+// fresh, 30-54 pooled; config 4's pair rows 108-112 fresh, 99-164 pooled).
+constexpr uint64_t HOST_BIG_BYTES = 64u << 20;
+class HostPool {
+ public:
+  static constexpr int HOST_WORKERS = 15;        // + the calling thread = 16
+  static HostPool& get() {
+    static HostPool p;
+    return p;
+  }
+  void run(int n, const std::function<void(int)>& fn, bool big = false) {
+    if (n <= 1) {
+      if (n == 1) fn(0);
+      return;
+    }
+    const char* pe = test_build_knob("KMHG_HOST_POOL");   // "0": a thread per task (A/B)
+    if (big || (pe && pe[0] == '0')) {
+      std::vector<std::thread> th;
+      for (int i = 1; i < n; ++i) th.emplace_back(fn, i);
+      fn(0);
+      for (auto& t : th) t.join();
+      return;
+    }
+    Job job{&fn, n};
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (workers_.empty()) start();
+      jobs_.push_back(&job);
+    }
+    cv_.notify_all();
+    work_on(job, false);                         // until every task is handed out
+    {
+      std::lock_guard<std::mutex> g(mu_);        // no worker takes the job from here on
+      for (auto it = jobs_.begin(); it != jobs_.end(); ++it)
+        if (*it == &job) {
+          jobs_.erase(it);
+          break;
+        }
+    }
+    std::unique_lock<std::mutex> g(job.m);       // the job lives until its last worker is out
+    job.cv.wait(g, [&] { return job.done == job.n && job.refs == 0; });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+
+ private:
+  struct Job {
+    const std::function<void(int)>* fn;
+    int n;
+    std::atomic<int> next{0};
+    int done = 0, refs = 0;                      // guarded by m (refs: workers inside)
+    std::mutex m;
+    std::condition_variable cv;
+    Job(const std::function<void(int)>* f, int count) : fn(f), n(count) {}
+  };
+  void work_on(Job& job, bool worker) {
+    int ran = 0;
+    for (int i; (i = job.next.fetch_add(1)) < job.n; ++ran) (*job.fn)(i);
+    std::lock_guard<std::mutex> g(job.m);
+    job.done += ran;
+    if (worker) --job.refs;
+    if (job.done == job.n && job.refs == 0) job.cv.notify_all();
+  }
+  void start() {
+    for (int w = 0; w < HOST_WORKERS; ++w)
+      workers_.emplace_back([this] {
+        for (;;) {
+          Job* job = nullptr;
+          {
+            std::unique_lock<std::mutex> g(mu_);
+            cv_.wait(g, [&] {
+              while (!jobs_.empty() && jobs_.front()->next.load() >= jobs_.front()->n)
+                jobs_.pop_front();                 // handed out completely
+              return stop_ || !jobs_.empty();
+            });
+            if (stop_) return;
+            job = jobs_.front();
+            std::lock_guard<std::mutex> gj(job->m);
+            ++job->refs;                           // (the caller waits for it)
+          }
+          work_on(*job, true);
+        }
+      });
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job*> jobs_;
+  std::vector<std::thread> workers_;
+  bool stop_ = false;
+};
+
 // Device -> pageable host copy for the host-pointer entry points (R matrices, numpy arrays):
 // results above D2H_STAGE_MIN go through two pinned chunks, the DMA of chunk i + 1 overlapping
 // the host copy of chunk i, which d2h_threads() threads split (they also take the destination's
@@ -537,13 +643,10 @@ static int d2h_threads() {
 static void host_copy_par(char* dst, const char* src, size_t n) {
   const int T = d2h_threads();
   const size_t stripe = ((n + T - 1) / T + 4095) & ~(size_t)4095;
-  std::vector<std::thread> th;
-  for (int t = 1; t < T; ++t) {
+  HostPool::get().run(T, [=](int t) {
     const size_t a = std::min(n, t * stripe), b = std::min(n, a + stripe);
-    if (a < b) th.emplace_back([=] { std::memcpy(dst + a, src + a, b - a); });
-  }
-  std::memcpy(dst, src, std::min(n, stripe));
-  for (auto& x : th) x.join();
+    if (a < b) std::memcpy(dst + a, src + a, b - a);
+  });
 }
 
 struct PinStage {
@@ -689,13 +792,10 @@ static void expand_runs_host(const int32_t* runs, uint64_t n, uint64_t H, int32_
       }
     }
   };
-  std::vector<std::thread> th;
-  for (int t = 1; t < T; ++t) {
+  HostPool::get().run(T, [&](int t) {
     const uint64_t a = std::min(H, t * stripe), b = std::min(H, a + stripe);
-    if (a < b) th.emplace_back(work, a, b);
-  }
-  work(0, std::min(H, stripe));
-  for (auto& x : th) x.join();
+    if (a < b) work(a, b);
+  }, H * 8 >= HOST_BIG_BYTES);
 }
 
 void rows_to_host(const int2* d_rows, uint64_t H, int32_t* dst, hipStream_t s) {
@@ -3311,13 +3411,10 @@ static void expand_pairs_host(const uint32_t* pk, const uint64_t* po, uint64_t M
       t = 0;
     }
   };
-  std::vector<std::thread> th;
-  for (int i = 1; i < T; ++i) {
+  HostPool::get().run(T, [&](int i) {
     const uint64_t a = std::min(P, i * stripe), b = std::min(P, a + stripe);
-    if (a < b) th.emplace_back(work, a, b);
-  }
-  work(0, std::min(P, stripe));
-  for (auto& x : th) x.join();
+    if (a < b) work(a, b);
+  }, P * 12 >= HOST_BIG_BYTES);
 }
 
 static void pairs_to_host(kmhg_index* idx, int32_t* out, hipStream_t s) {
