@@ -526,8 +526,8 @@ hipStream_t lib_stream() {
 // several threads at once (a multi-device query's parts) share the workers.  No task may call
 // run() itself.  big = true (GB-scale writes: the expansions) starts fresh threads instead: the
 // kernel spreads new threads over the machine's memory controllers, while woken pool workers
-// crowd near their waker (A/B in one run, profiles/r6al_pool_ab/: config 5's run expansion 18-21 ms
-// fresh, 30-54 pooled; config 4's pair rows 108-112 fresh, 99-164 pooled).
+// crowd near their waker (A/B in one run, profiles/r6al_pool_ab/: config 5's run expansion
+// 18-21 ms fresh, 30-54 pooled; config 4's pair rows 108-112 fresh, 99-164 pooled).
 constexpr uint64_t HOST_BIG_BYTES = 64u << 20;
 class HostPool {
  public:
