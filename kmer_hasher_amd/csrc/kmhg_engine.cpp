@@ -528,7 +528,8 @@ hipStream_t lib_stream() {
 // kernel spreads new threads over the machine's memory controllers, while woken pool workers
 // crowd near their waker (A/B in one run, profiles/r6al_pool_ab/: config 5's run expansion
 // 18-21 ms fresh, 30-54 pooled; config 4's pair rows 108-112 fresh, 99-164 pooled).
-constexpr uint64_t HOST_BIG_BYTES = 64u << 20;
+constexpr uint64_t HOST_BIG_BYTES = 512u << 20;   // (config 2's 80 MB of rows: pooled 0.84-0.91
+                                                  // ms, fresh 1.19-1.41; profiles/r6ak*, r6al*)
 class HostPool {
  public:
   static constexpr int HOST_WORKERS = 15;        // + the calling thread = 16
