@@ -1419,8 +1419,8 @@ void launch_fill_u64(uint64_t* p, uint64_t v, hipStream_t s) {
 // The sharded query's rows travel to the root as diagonal runs: a run is a maximal stretch of
 // consecutive rows (i, j), (i + 1, j + 1), ... -- a dot plot's diagonal -- sent as {its first
 // row's index in the rank's rows, i, j} (12 B) instead of 8 B per row.  Config 5 (B = A + 1 %
-// SNVs) has ~70 rows per run.  R_flag decides a row's start: row 0, or i / j not both one past
-// the previous row's.  Tiles of TILE rows, element e = j * BLOCK + t (lane-contiguous loads).
+// SNVs) has 133 rows per run.  run_start decides a row's start: row 0, or i / j not both one
+// past the previous row's.  Tiles of TILE rows, element e = j * BLOCK + t (lane-contiguous).
 __device__ __forceinline__ bool run_start(const int2* __restrict__ rows, uint64_t r) {
   if (r == 0) return true;
   const int2 v = rows[r], p = rows[r - 1];
