@@ -145,6 +145,15 @@ int kmhg_query_run_device(kmhg_index *idx, const void *d_seq, size_t L, int k, v
 int kmhg_query_run_device_range(kmhg_index *idx, const void *d_seq, size_t L, int k,
                                 int64_t w_begin, int64_t w_end, void *stream, kmhg_query **q,
                                 int64_t *n_rows);
+/* The same range query with its rows left as diagonal runs (the format of kmhg_rows_runs, the
+ * sharded gather's): made from the query's per-window records, the rows are never written.
+ * *n_runs >= 0: the query holds n_runs runs (kmhg_query_runs_device, 3 int32 each; rows
+ * through kmhg_runs_expand); *n_runs = -1: runs would not be smaller and it holds the rows as
+ * kmhg_query_run_device_range's do.  The rows / fill / copy entries refuse a runs query. */
+int kmhg_query_run_device_range_runs(kmhg_index *idx, const void *d_seq, size_t L, int k,
+                                     int64_t w_begin, int64_t w_end, void *stream,
+                                     kmhg_query **q, int64_t *n_rows, int64_t *n_runs);
+int kmhg_query_runs_device(kmhg_query *q, const int32_t **d_runs);   /* owned by q */
 /* seq.kmer.pos over a PART of an owner-computes build (kmhg_build_device_part), without
  * assembling the parts: every window of the query is hashed and only the windows whose k-mer
  * this part owns are probed, so the rows are those windows' rows, in window order.  With one

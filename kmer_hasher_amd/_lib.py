@@ -63,6 +63,9 @@ _PROTOS = {
                                               vp, C.POINTER(vp), i64p]),
     "kmhg_query_run_device_part": (C.c_int, [vp, vp, C.c_size_t, C.c_int, vp, C.POINTER(vp),
                                              i64p]),
+    "kmhg_query_run_device_range_runs": (C.c_int, [vp, vp, C.c_size_t, C.c_int, C.c_int64,
+                                                   C.c_int64, vp, vp, i64p, i64p]),
+    "kmhg_query_runs_device": (C.c_int, [vp, vp]),
     "kmhg_query_tile_offsets": (C.c_int, [vp, vp, i64p, vp]),
     "kmhg_seq_pack": (C.c_int, [vp, C.c_int64, vp, vp, vp]),
     "kmhg_seq_unpack": (C.c_int, [vp, vp, C.c_int64, C.c_int64, C.c_int64, vp, vp]),

@@ -969,6 +969,10 @@ struct kmhg_query {
   // of each query tile (TILE windows from w0), for the root's merge of the parts' rows
   DBuf<uint64_t> tile_off;
   int64_t n_tiles = 0;
+  // a range query run for the sharded gather (kmhg_query_run_device_range_runs): its rows as
+  // n_runs diagonal runs {first row, i, j} instead of `rows` (n_runs = -1: it holds rows)
+  DBuf<int32_t> runs;
+  int64_t n_runs = -1;
 };
 
 namespace {
@@ -1750,7 +1754,8 @@ void finish_build(kmhg_index* idx) {
 // Windows [w0, w1) of the query (default: all L - kq + 1).  Rows come out ordered by window
 // end, so shards of consecutive window ranges concatenate to the unsharded result.
 kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int kq, int64_t w0,
-                         int64_t w1, hipStream_t s, bool part_query = false) {
+                         int64_t w1, hipStream_t s, bool part_query = false,
+                         bool runs_mode = false) {
   ReleaseGroup rg(s);
   if (idx->canonical) fail(KMHG_EINVAL, "External pointer has incorrect tag");
   if (idx->is_part != part_query)
@@ -1768,8 +1773,8 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
   // rows are written into a guessed capacity before the total is known (no host round trip
   // inside the query); a query with more rows than the guess -- heavy repeats -- is redone
   // by the two-pass path into an exact buffer
-  const uint64_t cap = (uint64_t)Nw + ((uint64_t)Nw >> 3) + 64;
-  q->rows.reset(cap);
+  uint64_t cap = (uint64_t)Nw + ((uint64_t)Nw >> 3) + 64;
+  if (!runs_mode) q->rows.reset(cap);
   // probe / scan / emit.  (A one-pass probe + look-back + emit was measured slower and removed
   // in round 4: config 2 0.403 against 0.365 ms; re-measured round 3 with the diagonal path,
   // self query 94 -> 53 Gbp/s -- a tile that has probed waits for its predecessors' totals
@@ -1831,6 +1836,31 @@ kmhg_query* query_device(kmhg_index* idx, const uint8_t* d_seq, int64_t L, int k
                             tile_row0, s, diag ? idx->diag_view() : DiagIdx{nullptr, nullptr, 0},
                             diag && tags_on() ? idx->ptag.p : nullptr, elist.p + nt));
   LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(tile_row0, nt, total, tiles.p + nt, s));
+  if (runs_mode) {
+    // the rows as diagonal runs, made from the window records (k_qruns_*); rows written only
+    // when runs would not be smaller (12 B per run against 8 B per row)
+    DBuf<uint64_t> rtiles((size_t)nt + scan_u64_scratch(nt), s);
+    PinnedRec hrec2 = PinnedPool::get().take();
+    GiveBack give_back2{hrec2, s};
+    uint64_t* n_runs = &hrec2.meta->n_kmers;
+    LAUNCH("k_qruns_count", s, launch_qruns_count(qrec.p, qmulti.p, (uint64_t)Nw, rtiles.p, s));
+    LAUNCH("k_scan_tiles_u64", s, launch_scan_u64(rtiles.p, nt, n_runs, rtiles.p + nt, s));
+    HIPC(hipStreamSynchronize(s));
+    H = __atomic_load_n(total, __ATOMIC_ACQUIRE);
+    const uint64_t NR = __atomic_load_n(n_runs, __ATOMIC_ACQUIRE);
+    q->H = (int64_t)H;
+    if (H > (uint64_t)INT32_MAX) fail(KMHG_EOVERFLOW, "result has more than 2^31-1 rows");
+    if (H && 3 * NR < 2 * H) {
+      q->runs.reset(3 * NR);
+      q->n_runs = (int64_t)NR;
+      LAUNCH("k_qruns_emit", s,
+             launch_qruns_emit(qrec.p, qmulti.p, idx->positions.p, (uint64_t)Nw, w0, kq,
+                               tile_row0, rtiles.p, NR, q->runs.p, s));
+      return q.release();
+    }
+    cap = std::max<uint64_t>(H, 1);              // the rows, into an exact buffer
+    q->rows.reset(cap);
+  }
   LAUNCH("k_query_emit", s,
          launch_query_emit(qrec.p, qmulti.p, Nw, w0, kq, idx->positions.p, tile_row0, q->rows.p, cap,
                            elist.p, elist.p + nt, true, s));
@@ -3541,6 +3571,30 @@ int kmhg_query_run_device_range(kmhg_index* idx, const void* d_seq, size_t L, in
   });
 }
 
+int kmhg_query_run_device_range_runs(kmhg_index* idx, const void* d_seq, size_t L, int k,
+                                     int64_t w_begin, int64_t w_end, void* stream,
+                                     kmhg_query** q, int64_t* n_rows, int64_t* n_runs) {
+  return guarded([&] {
+    if (!idx || !d_seq || !q) fail(KMHG_EINVAL, "null argument");
+    check_query_args(L, k);
+    const int64_t Nw = (int64_t)L - k + 1;
+    if (w_begin < 0 || w_end > Nw || w_begin > w_end) fail(KMHG_EINVAL, "window range out of bounds");
+    DeviceGuard g(idx->device);
+    hipStream_t s = (hipStream_t)stream;
+    *q = query_device(idx, (const uint8_t*)d_seq, (int64_t)L, k, w_begin, w_end, s, false, true);
+    if (n_rows) *n_rows = (*q)->H;
+    if (n_runs) *n_runs = (*q)->n_runs;
+  });
+}
+
+int kmhg_query_runs_device(kmhg_query* q, const int32_t** d_runs) {
+  return guarded([&] {
+    if (!q || !d_runs) fail(KMHG_EINVAL, "null argument");
+    if (q->n_runs < 0) fail(KMHG_EINVAL, "the query holds rows, not runs");
+    *d_runs = q->runs.p;
+  });
+}
+
 int kmhg_query_run_device_part(kmhg_index* part, const void* d_seq, size_t L, int k,
                                void* stream, kmhg_query** q, int64_t* n_rows) {
   return guarded([&] {
@@ -3666,6 +3720,7 @@ int kmhg_runs_expand(const void* d_runs, int64_t n_runs, int64_t n_rows, void* d
 int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
   return guarded([&] {
     if (!q) fail(KMHG_EINVAL, "null query");
+    if (q->n_runs >= 0) fail(KMHG_EINVAL, "the query holds runs (kmhg_query_runs_device)");
     if (!q->H) return;
     if (!rows) fail(KMHG_EINVAL, "null output");
     if (!q->parts.empty() && !q->gathered) {   // every part straight into its rows, in parallel
@@ -3697,6 +3752,7 @@ int kmhg_query_fill(kmhg_query* q, int32_t* rows) {
 int kmhg_query_rows_device(kmhg_query* q, const int32_t** d_rows) {
   return guarded([&] {
     if (!q || !d_rows) fail(KMHG_EINVAL, "null argument");
+    if (q->n_runs >= 0) fail(KMHG_EINVAL, "the query holds runs (kmhg_query_runs_device)");
     gather_parts(q);
     *d_rows = reinterpret_cast<const int32_t*>(q->rows.p);
   });
@@ -3705,6 +3761,7 @@ int kmhg_query_rows_device(kmhg_query* q, const int32_t** d_rows) {
 int kmhg_query_copy_device(kmhg_query* q, void* d_dst, void* stream) {
   return guarded([&] {
     if (!q) fail(KMHG_EINVAL, "null query");
+    if (q->n_runs >= 0) fail(KMHG_EINVAL, "the query holds runs (kmhg_query_runs_device)");
     if (!q->H) return;
     if (!d_dst) fail(KMHG_EINVAL, "null output");
     DeviceGuard g(q->device);

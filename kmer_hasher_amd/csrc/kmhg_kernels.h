@@ -112,6 +112,13 @@ void launch_merge_part_rows(const int2* rows, const uint64_t* seg_base, const ui
                             uint32_t n_parts, uint32_t nt, int kq, int64_t w0, int2* out,
                             hipStream_t s);
 void launch_fill_u64(uint64_t* p, uint64_t v, hipStream_t s);
+// a range query's rows as diagonal runs straight from its per-window records: run starts per
+// query tile (scanned like the rows' tile totals), then the runs at their tile offsets
+void launch_qruns_count(const uint32_t* qrec, const uint2* qmulti, uint64_t Nw,
+                        uint64_t* tile_cnt, hipStream_t s);
+void launch_qruns_emit(const uint32_t* qrec, const uint2* qmulti, const int32_t* positions,
+                       uint64_t Nw, int64_t w0, int kq, const uint64_t* tile_row0,
+                       const uint64_t* tile_run0, uint64_t n_runs, int32_t* runs, hipStream_t s);
 // a sequence as 2-bit codes + N flags, 16 chars per u32 / u16 word (kmhg_seq_pack /
 // kmhg_seq_unpack: C1 transfers); unpack writes chars [a, b) from the words held from w0 on
 void launch_seq_pack(const uint8_t* seq, int64_t L, uint32_t* code, uint16_t* nbit,

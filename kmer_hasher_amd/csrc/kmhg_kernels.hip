@@ -1613,6 +1613,129 @@ void launch_seq_unpack(const uint32_t* code, const uint16_t* nbit, uint64_t w0, 
                      s, code, nbit, w0, a, b, seq);
 }
 
+// ---------------------------------------------------------------- a query's rows as runs
+// A range query whose rows leave the device only as diagonal runs (the senders of the sharded
+// query's gather, kmhg_query_run_device_range_runs) makes the runs from its per-window records
+// (qrec / qmulti) and never writes the rows.  The row of a single-hit window w continues the
+// previous row's run when window w - 1 is a single hit one index position earlier; every row of
+// a multi-hit window is a run of its own (its rows share i).  That is a valid run encoding, not
+// always the maximal one (a single hit right after a multi-hit window starts a run even where
+// it extends one): kmhg_runs_expand gives the query's rows either way.  Thread t takes the 8
+// consecutive windows [8 t, 8 t + 8) of a TILE-window tile (window order = thread order).
+struct QRun { uint32_t n, st; };   // a window's rows, and how many of them start a run
+__device__ __forceinline__ QRun qrun_window(uint32_t rec, uint32_t prev, const uint2* qmulti,
+                                            uint64_t w) {
+  if (rec == 0) return {0u, 0u};
+  if (rec == QREC_MULTI) {
+    const uint32_t m = qmulti[w].x;
+    return {m, m};
+  }
+  return {1u, (prev != 0 && prev != QREC_MULTI && prev + 1u == rec) ? 0u : 1u};
+}
+
+// a thread's 8 window records: two 16-B loads (wa is a multiple of 8 windows and qrec starts
+// 256-B aligned), element loads at the range's end.  (Element loads throughout, lanes 32 B
+// apart, ran both kernels at ~2 TB/s.)
+static_assert(WPT == 8, "load_rec8 reads 8 records per thread");
+__device__ __forceinline__ void load_rec8(const uint32_t* __restrict__ qrec, uint64_t wa,
+                                          uint64_t Nw, uint32_t (&rec)[WPT]) {
+  if (wa + WPT <= Nw) {
+    const uint4 a = *reinterpret_cast<const uint4*>(qrec + wa);
+    const uint4 b = *reinterpret_cast<const uint4*>(qrec + wa + 4);
+    rec[0] = a.x; rec[1] = a.y; rec[2] = a.z; rec[3] = a.w;
+    rec[4] = b.x; rec[5] = b.y; rec[6] = b.z; rec[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) rec[j] = wa + j < Nw ? qrec[wa + j] : 0u;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK)
+k_qruns_count(const uint32_t* __restrict__ qrec, const uint2* __restrict__ qmulti, uint64_t Nw,
+              uint64_t* __restrict__ tile_cnt) {
+  __shared__ uint64_t sh[8];
+  const uint64_t wa = (uint64_t)blockIdx.x * TILE + WPT * threadIdx.x;
+  uint32_t prev = wa > 0 && wa - 1 < Nw ? qrec[wa - 1] : 0u;
+  uint32_t rec[WPT];
+  load_rec8(qrec, wa, Nw, rec);
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    c += qrun_window(rec[j], prev, qmulti, wa + j).st;
+    prev = rec[j];
+  }
+  uint64_t tot;
+  block_excl_scan(c, sh, tot);
+  if (threadIdx.x == 0) tile_cnt[blockIdx.x] = tot;
+}
+
+// (the per-window counts are recomputed from rec[] in the write loop rather than kept in arrays
+// across the scans: the arrays version came out of the compiler with wrong row counts on gfx950)
+__global__ void __launch_bounds__(BLOCK)
+k_qruns_emit(const uint32_t* __restrict__ qrec, const uint2* __restrict__ qmulti,
+             const int32_t* __restrict__ positions, uint64_t Nw, int64_t w0, int kq,
+             const uint64_t* __restrict__ tile_row0, const uint64_t* __restrict__ tile_run0,
+             uint64_t n_runs, int32_t* __restrict__ runs) {
+  __shared__ uint64_t sh[8];
+  // the records' loads go out first; the tile offsets (scalar loads) resolve meanwhile
+  const uint64_t wa = (uint64_t)blockIdx.x * TILE + WPT * threadIdx.x;
+  const uint32_t prev0 = wa > 0 && wa - 1 < Nw ? qrec[wa - 1] : 0u;
+  uint32_t rec[WPT];
+  load_rec8(qrec, wa, Nw, rec);
+  const uint64_t q0 = tile_run0[blockIdx.x];
+  const uint64_t row0 = tile_row0[blockIdx.x];
+  if (q0 == (blockIdx.x + 1 < gridDim.x ? tile_run0[blockIdx.x + 1] : n_runs)) return;  // no run starts here
+  uint64_t nr = 0, ns = 0;
+  uint32_t prev = prev0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const QRun x = qrun_window(rec[j], prev, qmulti, wa + j);
+    nr += x.n;
+    ns += x.st;
+    prev = rec[j];
+  }
+  // one scan for both prefixes: rows in the high half, run starts (<= rows) in the low half --
+  // the host emits runs only for H <= 2^31 - 1 rows, so neither half carries over
+  uint64_t tot;
+  const uint64_t ex = block_excl_scan((nr << 32) | ns, sh, tot);
+  uint64_t r = row0 + (ex >> 32);
+  uint64_t q = q0 + (ex & 0xffffffffull);
+  prev = prev0;
+#pragma unroll
+  for (int j = 0; j < WPT; ++j) {
+    const uint64_t w = wa + j;
+    const QRun x = qrun_window(rec[j], prev, qmulti, w);
+    prev = rec[j];
+    if (!x.n) continue;
+    const int32_t i = (int32_t)(w0 + (int64_t)w + kq);
+    if (rec[j] != QREC_MULTI) {
+      if (x.st) {
+        int32_t* o = runs + 3 * q++;
+        o[0] = (int32_t)r; o[1] = i; o[2] = (int32_t)rec[j];
+      }
+      ++r;
+    } else {
+      const uint32_t first = qmulti[w].y;
+      for (uint32_t t = 0; t < x.n; ++t, ++r) {
+        int32_t* o = runs + 3 * q++;
+        o[0] = (int32_t)r; o[1] = i; o[2] = positions[first + t];
+      }
+    }
+  }
+}
+
+void launch_qruns_count(const uint32_t* qrec, const uint2* qmulti, uint64_t Nw,
+                        uint64_t* tile_cnt, hipStream_t s) {
+  hipLaunchKernelGGL(k_qruns_count, dim3((unsigned)((Nw + TILE - 1) / TILE)), dim3(BLOCK), 0, s,
+                     qrec, qmulti, Nw, tile_cnt);
+}
+void launch_qruns_emit(const uint32_t* qrec, const uint2* qmulti, const int32_t* positions,
+                       uint64_t Nw, int64_t w0, int kq, const uint64_t* tile_row0,
+                       const uint64_t* tile_run0, uint64_t n_runs, int32_t* runs, hipStream_t s) {
+  hipLaunchKernelGGL(k_qruns_emit, dim3((unsigned)((Nw + TILE - 1) / TILE)), dim3(BLOCK), 0, s,
+                     qrec, qmulti, positions, Nw, w0, kq, tile_row0, tile_run0, n_runs, runs);
+}
+
 void launch_runs_count(const int2* rows, uint64_t n, uint64_t* tile_cnt, hipStream_t s) {
   hipLaunchKernelGGL(k_runs_count, dim3((unsigned)((n + TILE - 1) / TILE)), dim3(BLOCK), 0, s,
                      rows, n, tile_cnt);

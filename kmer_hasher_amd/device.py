@@ -132,6 +132,23 @@ class DeviceIndex:
                 C.byref(q), C.byref(h)))
         return DeviceQuery(q.value, h.value, seq.device)
 
+    def query_range_runs(self, seq: torch.Tensor, k: int, w0: int, w1: int, stream=None):
+        """Windows [w0, w1) with the rows left as diagonal runs
+        (kmhg_query_run_device_range_runs): ('runs', (n_runs, 3) int32 tensor, H), or
+        ('rows', (H, 2) int32 tensor, H) where runs would not be smaller.  Either tensor owns
+        the query."""
+        _check_seq(seq)
+        q = C.c_void_p()
+        h, nr = C.c_int64(), C.c_int64()
+        with torch.cuda.device(seq.device):
+            _lib.check(_lib.lib().kmhg_query_run_device_range_runs(
+                self._h, C.c_void_p(seq.data_ptr()), seq.numel(), k, w0, w1, _stream_ptr(stream),
+                C.byref(q), C.byref(h), C.byref(nr)))
+        dq = DeviceQuery(q.value, h.value, seq.device)
+        if nr.value < 0:
+            return "rows", dq.rows_view(), h.value
+        return "runs", dq.runs_view(nr.value), h.value
+
     def positions(self, opt: int, stream=None) -> dict:
         """kmer.pos into device tensors: {'kmer': uint8 (U, k+1), 'pos': int32 (N, 2),
         'pair.pos': int32 (P, 3), 'count': int32 (U,)} for the requested bits."""
@@ -390,6 +407,15 @@ class DeviceQuery:
         _lib.check(_lib.lib().kmhg_query_rows_device(self._h, C.byref(d)))
         return torch.as_tensor(_RowsBuffer(self, d.value))   # on the rows' own device
 
+    def runs_view(self, n_runs: int) -> torch.Tensor:
+        """The (n_runs, 3) int32 runs of a runs query (kmhg_query_runs_device), as a tensor that
+        owns this query (rows_view's contract)."""
+        if not n_runs:
+            return torch.empty((0, 3), dtype=torch.int32, device=self.device)
+        d = C.c_void_p()
+        _lib.check(_lib.lib().kmhg_query_runs_device(self._h, C.byref(d)))
+        return torch.as_tensor(_RowsBuffer(self, d.value, (n_runs, 3)))
+
     def free(self):
         if self._h:
             _lib.lib().kmhg_query_free(self._h)
@@ -406,9 +432,9 @@ class _RowsBuffer:
     """__cuda_array_interface__ of a query's device rows; torch keeps this object (and so the
     query) alive for as long as the tensor made from it."""
 
-    def __init__(self, q: DeviceQuery, ptr: int):
+    def __init__(self, q: DeviceQuery, ptr: int, shape: tuple | None = None):
         self.q = q
-        self.__cuda_array_interface__ = {"shape": (q.n_rows, 2), "typestr": "<i4",
+        self.__cuda_array_interface__ = {"shape": shape or (q.n_rows, 2), "typestr": "<i4",
                                          "data": (ptr, False), "version": 3, "strides": None,
                                          "stream": None}
 

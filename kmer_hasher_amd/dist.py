@@ -54,25 +54,34 @@ def broadcast_buffers(meta: torch.Tensor | None, bufs: list[torch.Tensor] | None
     return m, bufs
 
 
-def gather_rows(local: torch.Tensor, dst: int = 0, group=None, codec=None) -> torch.Tensor | None:
+def gather_rows(local, dst: int = 0, group=None, codec=None) -> torch.Tensor | None:
     """Concatenate every rank's (h_r, 2) int32 rows on `dst` in rank order.
 
     codec: rows travel as diagonal runs where that is smaller ("Rows as diagonal
     runs"): codec.encode(rows) -> an (n, 3) int32 runs tensor or None (send the rows), and
     codec.decode(runs, h, out) on `dst` writes the h rows into `out`.  A dot plot's rows are
-    long diagonals (config 5: 133 rows per 12-B run), so the link carries ~1/89 of the bytes."""
+    long diagonals (config 5: 133 rows per 12-B run), so the link carries ~1/89 of the bytes.
+    `local` may also come encoded already, as ('runs', (n, 3) runs, h) or ('rows', rows, h) (a
+    sender's HipQueryEngine.query_range_runs, whose rows were never written)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    dev = local.device
-    runs = codec.encode(local) if codec is not None and rank != dst and local.shape[0] else None
-    cnt = torch.tensor([local.shape[0], -1 if runs is None else runs.shape[0]], dtype=torch.int64,
+    if isinstance(local, tuple):
+        kind, t, h_local = local
+        runs = t if kind == "runs" else None
+        local = t if kind == "rows" else None
+        dev = t.device
+    else:
+        h_local = local.shape[0]
+        dev = local.device
+        runs = codec.encode(local) if codec is not None and rank != dst and h_local else None
+    cnt = torch.tensor([h_local, -1 if runs is None else runs.shape[0]], dtype=torch.int64,
                        device=dev)
     metas = [torch.zeros(2, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(metas, cnt, group=group)
     counts = [int(m[0].item()) for m in metas]
     n_runs = [int(m[1].item()) for m in metas]
     if rank == dst:
-        if world == 1:
+        if world == 1 and local is not None:
             return local                     # the rows are already where they belong
         out = torch.empty((sum(counts), 2), dtype=torch.int32, device=dev)
         offs = [0]
@@ -83,7 +92,10 @@ def gather_rows(local: torch.Tensor, dst: int = 0, group=None, codec=None) -> to
                 for r in range(world) if r != dst and counts[r] and n_runs[r] >= 0}
         works = p2p([("recv", bufs[r] if r in bufs else out[offs[r]:offs[r + 1]], r)
                      for r in range(world) if r != dst and counts[r]], group, wait=False)
-        out[offs[rank]:offs[rank + 1]] = local
+        if local is not None:
+            out[offs[rank]:offs[rank + 1]] = local
+        elif counts[rank]:
+            codec.decode(runs, counts[rank], out[offs[rank]:offs[rank + 1]])
         p2p_wait(works)
         for r, b in bufs.items():
             codec.decode(b, counts[r], out[offs[r]:offs[r + 1]])
@@ -370,9 +382,12 @@ def sharded_query(engine, seq: torch.Tensor | None, k: int, dst: int = 0, group=
     t1 = mark()
     n_windows = max(0, seq.numel() - k + 1)
     w0, w1 = shard_ranges(n_windows, world)[rank]
-    local = engine.query_range(seq, k, w0, w1)
-    t2 = mark()
     codec = getattr(engine, "codec", None)
+    if sink is None and rank != dst and codec is not None and hasattr(engine, "query_range_runs"):
+        local = engine.query_range_runs(seq, k, w0, w1)    # a sender: its runs, no rows
+    else:
+        local = engine.query_range(seq, k, w0, w1)
+    t2 = mark()
     rows = gather_rows(local, dst, group, codec) if sink is None \
         else deliver_rows_host(local, sink, group, codec)
     t3 = mark()
@@ -537,6 +552,11 @@ class HipQueryEngine:
         # the rows stay where the emit kernel wrote them (a 3 GB device copy per query at
         # config 5 otherwise); the tensor owns the query
         return self.index.query_range(seq, k, w0, w1).rows_view()
+
+    def query_range_runs(self, seq: torch.Tensor, k: int, w0: int, w1: int):
+        """A sender's range of the gather: ('runs', runs, H) made from the query's window
+        records without writing its rows, or ('rows', rows, H)."""
+        return self.index.query_range_runs(seq, k, w0, w1)
 
 
 def broadcast_index(index, device: torch.device, src: int = 0, group=None):

@@ -30,7 +30,7 @@ class _HostRows:
         return self.eng.query_range(seq, k, w0, w1).cpu()
 
 
-def _worker(rank, world, port, seq_bytes, k_index, kq, out_q):
+def _worker(rank, world, port, seq_bytes, k_index, kq, out_q, device_rows=False):
     import torch
     import torch.distributed as dist
     from kmer_hasher_amd import dist as kd
@@ -44,23 +44,33 @@ def _worker(rank, world, port, seq_bytes, k_index, kq, out_q):
         built = DeviceIndex.build(seq, k_index) if rank == 0 else None
         idx = kd.broadcast_index(built, dev, src=0)
         info = idx.info()
-        rows = kd.sharded_query(_HostRows(kd.HipQueryEngine(idx)), seq, kq, dst=0)
+        eng = kd.HipQueryEngine(idx)
+        # device_rows: the engine itself, so the sender's rows leave as runs made from its
+        # window records (query_range_runs) or as rows where runs would not be smaller
+        rows = kd.sharded_query(eng if device_rows else _HostRows(eng), seq, kq, dst=0)
         torch.cuda.synchronize()
         if rank == 0:
             out_q.put(((info["n_kmers"], info["n_positions"]),
-                       rows.numpy().reshape(-1).tolist()))
+                       rows.cpu().numpy().reshape(-1).tolist()))
         dist.barrier()
         idx.free()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,k_index,kq", [(2, 31, 31), (2, 21, 19)])
-def test_two_ranks_one_gpu_sharded_query(gpu, world, k_index, kq):
+@pytest.mark.parametrize("world,k_index,kq,seq_kind,device_rows",
+                         [(2, 31, 31, "repeats", False), (2, 21, 19, "repeats", False),
+                          (2, 31, 31, "repeats", True), (3, 21, 21, "dups", True)])
+def test_two_ranks_one_gpu_sharded_query(gpu, world, k_index, kq, seq_kind, device_rows):
     import torch.multiprocessing as mp
     from kmer_hasher_amd import synth
     from oracle import oracle as O
-    s = synth.add_n_runs(synth.repeat_rich(120_000, 5, n_gap_every=9_001), 0.005, 3)
+    if seq_kind == "repeats":
+        s = synth.add_n_runs(synth.repeat_rich(120_000, 5, n_gap_every=9_001), 0.005, 3)
+    else:                               # mostly unique, a few duplicated stretches
+        s = synth.add_n_runs(synth.iid(120_000, 5), 0.002, 3)
+        s[70_000:71_500] = s[10_000:11_500]
+        s[90_000:90_400] = s[10_200:10_600]
     s[-k_index - 2] = ord("N")          # an end-drop case in the last shard
     seq_bytes = s.tobytes()
     oi = O.OracleIndex(seq_bytes, k_index)
@@ -68,7 +78,8 @@ def test_two_ranks_one_gpu_sharded_query(gpu, world, k_index, kq):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, seq_bytes, k_index, kq, q))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, seq_bytes, k_index, kq, q, device_rows))
              for r in range(world)]
     for p in procs:
         p.start()

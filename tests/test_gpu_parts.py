@@ -205,3 +205,40 @@ def test_seq_pack_unpack_vs_reference(gpu):
                 want = np.full(L + 16, 7, np.uint8)
                 runs_ref.seq_unpack(rc[w0:], rn[w0:], w0, a, b, want)
                 assert np.array_equal(out.cpu().numpy(), want), (L, off, a, b)
+
+
+@pytest.mark.parametrize("case", ["self", "related", "repeats", "dups"])
+def test_query_range_runs_expand_to_rows(gpu, case):
+    """kmhg_query_run_device_range_runs (a sharded-query sender's runs, made from the window
+    records without writing rows) expands to exactly kmhg_query_run_device_range's rows, for
+    ragged window ranges (a range starting mid-tile, one ending at the sequence end, an empty
+    one); repeat-rich rows come back as rows (runs would not be smaller); duplicated stretches
+    put multi-hit windows (a run per row) among the diagonals."""
+    import torch
+    from kmer_hasher_amd import synth
+    from kmer_hasher_amd.device import DeviceIndex, runs_expand
+    k = 21
+    a = synth.repeat_rich(400_000, 5, n_gap_every=40_001) if case == "repeats" else \
+        synth.add_n_runs(synth.iid(400_000, 31), 0.001, 4)
+    if case == "dups":                  # multi-hit windows among long diagonals
+        a[200_000:203_000] = a[1_000:4_000]
+        a[300_000:300_500] = a[1_200:1_700]
+    b = synth.derived(a, 7, 0.01, 3) if case == "related" else a
+    ta, tb = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    idx = DeviceIndex.build(ta, k)
+    nw = b.size - k + 1
+    kinds = set()
+    for w0, w1 in [(0, nw), (1_000, 250_000), (123_457, nw), (5_000, 5_000), (nw - 3, nw)]:
+        want = idx.query_range(tb, k, w0, w1).rows().cpu().numpy()
+        kind, t, h = idx.query_range_runs(tb, k, w0, w1)
+        kinds.add(kind)
+        assert h == want.shape[0], (w0, w1)
+        if kind == "runs":
+            out = torch.empty((h, 2), dtype=torch.int32, device="cuda")
+            runs_expand(t, h, out)
+            got = out.cpu().numpy()
+        else:
+            got = t.cpu().numpy()
+        assert np.array_equal(got, want), (case, w0, w1)
+    idx.free()
+    assert "runs" in kinds if case != "repeats" else True
